@@ -1,0 +1,207 @@
+/*
+ * ptsharp_hip.h — C-ABI of libptsharp_hip.so, the MI355X (gfx950) render hot path
+ * that drops in for PTSharp's CPU `Renderer` (reference: akav/PTSharp).
+ *
+ * Boundary.  The C# side keeps scene construction (Example.*,
+ * IShape/Material/Camera/Scene objects) and the `Buffer` output; it flattens the
+ * scene once and calls these entry points through P/Invoke, following the same
+ * create / commit / execute / release lifecycle and out-string error convention
+ * the reference already uses for its only other native library, OIDN
+ * (PTSharpCore/OIDN.cs:43-95, used at Renderer.cs:614-677).
+ *
+ * Which reference interface each entry point replaces:
+ *   pt_create          Renderer.NewRenderer(scene,camera,sampler,w,h,mt)   Renderer.cs:35-56
+ *                      (+ new Buffer(w,h)                                  Buffer.cs:67-80)
+ *   pt_upload_scene    Scene.Compile() → Tree.NewTree / Mesh.Compile        Scene.cs:48-68, Tree.cs:22-29, Mesh.cs:45-57
+ *                      (lights registered as in Scene.Add                  Scene.cs:29-38)
+ *   pt_render_pass     one Renderer.RenderParallel() pass                  Renderer.cs:199-338
+ *                      = spp × Camera.CastRay → DefaultSampler.Sample      Camera.cs:98-119, Sampler.cs:40-145,191-296
+ *                        → Scene.Intersect → Tree/IShape.Intersect        Scene.cs:75-79, Tree.cs:31-128
+ *                        → Buffer.AddSample (Welford)                     Buffer.cs:33-44,94-97
+ *   pt_read_buffer     reading Renderer.PBuffer pixels {Samples, M, V}     Buffer.cs:18-58, Renderer.cs:20
+ *   pt_reset_buffer    Renderer.PBuffer = new Buffer(w,h)                  Renderer.cs:41
+ *   pt_stats           Scene.rays (Interlocked counter, never printed)     Scene.cs:70-79
+ *                      + the "time elapsed" stopwatch                      Renderer.cs:212-213,470
+ *   pt_last_error      oidnGetDeviceError(device, out msg)                 OIDN.cs:85-86
+ *   pt_destroy         oidnReleaseDevice                                   OIDN.cs:55-56
+ *   pt_comm_*          (new) Buffer gather across GPUs over RCCL/xGMI      SURVEY.md §8e
+ *
+ * Conventions: every function returns PT_OK (0) or a negative pt_status; the
+ * detail string of the last failure on the calling thread is pt_last_error().
+ * All structs are blittable POD (C# [StructLayout(LayoutKind.Sequential)]).
+ * Geometry is float (the reference stores Vector as System.Numerics.Vector3,
+ * Vector.cs:201), material/colour/camera scalars are double (Colour.cs:10-12,
+ * Camera.cs:12-14).  Host arrays are caller-owned and are copied during the call.
+ * A context is used by one host thread at a time; contexts are independent.
+ */
+#ifndef PTSHARP_HIP_H
+#define PTSHARP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+typedef enum pt_status {
+    PT_OK = 0,
+    PT_ERR_INVALID_ARG = -1,
+    PT_ERR_HIP = -2,          /* a HIP runtime call failed (detail in pt_last_error) */
+    PT_ERR_NO_SCENE = -3,     /* pt_render_pass before pt_upload_scene */
+    PT_ERR_UNSUPPORTED = -4,  /* a shape/material feature the GPU path does not cover */
+    PT_ERR_OUT_OF_MEMORY = -5,
+    PT_ERR_RCCL = -6,
+    PT_ERR_NO_DEVICE = -7
+} pt_status;
+
+/* Shape kinds in Scene.Shapes order (Scene.cs:19,29-38). */
+typedef enum pt_shape_kind {
+    PT_SHAPE_SPHERE = 0,    /* Sphere.cs   */
+    PT_SHAPE_CUBE = 1,      /* Cube.cs     */
+    PT_SHAPE_PLANE = 2,     /* Plane.cs    */
+    PT_SHAPE_TRIANGLE = 3,  /* Triangle.cs, added directly to the scene (a boxed struct) */
+    PT_SHAPE_MESH = 4       /* Mesh.cs, a range of triangles with its own tree */
+} pt_shape_kind;
+
+/* Material (Material.cs:8-62); textures are not part of the GPU path (PT_ERR_UNSUPPORTED). */
+typedef struct pt_material {
+    double color[3];      /* Colour Color            */
+    double emittance;     /* Emittance               */
+    double index;         /* Index (IOR)             */
+    double gloss;         /* Gloss (radians)         */
+    double tint;          /* Tint                    */
+    double reflectivity;  /* Reflectivity (<0: Fresnel) */
+    int32_t transparent;  /* Transparent             */
+    int32_t _pad;
+} pt_material;
+
+/* Flattened Scene.  Triangle arrays hold every triangle: directly-added ones
+ * (shape_kind TRIANGLE, shape_index = triangle index) and mesh triangles
+ * (mesh_first/mesh_count ranges).  Per-element arrays are [n][3] row-major. */
+typedef struct pt_scene_desc {
+    int32_t num_materials;
+    const pt_material* materials;
+
+    int32_t num_shapes;
+    const int32_t* shape_kind;    /* pt_shape_kind, Scene.Shapes order */
+    const int32_t* shape_index;   /* index into the per-kind arrays    */
+
+    int32_t num_spheres;
+    const float* sphere_center;   /* [n][3]  Sphere.Center (Vector) */
+    const double* sphere_radius;  /* [n]     Sphere.Radius (double) */
+    const int32_t* sphere_material;
+
+    int32_t num_cubes;
+    const float* cube_min;        /* [n][3] */
+    const float* cube_max;        /* [n][3] */
+    const int32_t* cube_material;
+
+    int32_t num_planes;
+    const float* plane_point;     /* [n][3] */
+    const float* plane_normal;    /* [n][3], already normalised as Plane.NewPlane does */
+    const int32_t* plane_material;
+
+    int32_t num_triangles;
+    const float* tri_v1;          /* [n][3] V1,V2,V3 */
+    const float* tri_v2;
+    const float* tri_v3;
+    const float* tri_n1;          /* [n][3] N1,N2,N3 (after FixNormals / SmoothNormals) */
+    const float* tri_n2;
+    const float* tri_n3;
+    const int32_t* tri_material;
+
+    int32_t num_meshes;
+    const int32_t* mesh_first;    /* first triangle of each mesh */
+    const int32_t* mesh_count;
+
+    double env_color[3];          /* Scene.Color (Scene.cs:25), returned on a miss */
+} pt_scene_desc;
+
+/* Camera struct fields (Camera.cs:11-14) as produced by Camera.LookAt/SetFocus. */
+typedef struct pt_camera {
+    float p[3], u[3], v[3], w[3];
+    double m;
+    double focal_distance;
+    double aperture_radius;
+} pt_camera;
+
+typedef enum pt_light_mode { PT_LIGHT_RANDOM = 0, PT_LIGHT_ALL = 1 } pt_light_mode;        /* LightMode.cs */
+typedef enum pt_specular_mode { PT_SPEC_NAIVE = 0, PT_SPEC_FIRST = 1, PT_SPEC_ALL = 2 } pt_specular_mode; /* SpecularMode.cs */
+
+/* DefaultSampler parameters (Sampler.cs:13-18).  FirstHitSamples/MaxBounces/
+ * DirectLighting/SoftShadows are private in C#, so the drop-in passes them explicitly. */
+typedef struct pt_sampler {
+    int32_t first_hit_samples;
+    int32_t max_bounces;
+    int32_t direct_lighting;
+    int32_t soft_shadows;
+    int32_t light_mode;      /* pt_light_mode    */
+    int32_t specular_mode;   /* pt_specular_mode */
+} pt_sampler;
+
+/* One render pass (one RenderParallel call).  Random.Shared is replaced by a
+ * counter-based stream keyed (seed, pass_index, pixel, sample, path node, dim). */
+typedef struct pt_pass_params {
+    int32_t spp;             /* Renderer.SamplesPerPixel                         */
+    int32_t stratified;      /* Renderer.StratifiedSampling (Renderer.cs:231-253) */
+    uint64_t seed;
+    uint32_t pass_index;     /* IterativeRender iteration i (Renderer.cs:709)    */
+    int32_t num_tiles;       /* 0 = whole image; else render only these 32x32 tiles */
+    const int32_t* tiles;    /* tile id = ty * ceil(W/32) + tx                   */
+} pt_pass_params;
+
+typedef struct pt_device_opts {
+    int32_t device;          /* HIP device ordinal */
+    int32_t width;
+    int32_t height;
+} pt_device_opts;
+
+typedef struct pt_stats {
+    uint64_t rays;           /* Scene.Intersect calls, last pass (Scene.cs:77) */
+    uint64_t rays_total;     /* since pt_create / pt_reset_buffer             */
+    double last_pass_ms;     /* device time of the last pass (hipEvent)       */
+    double total_ms;
+    uint64_t bvh_nodes;      /* acceleration structure size                   */
+    uint64_t bvh_bytes;
+    double build_ms;         /* host BVH build time of the last upload        */
+    uint64_t passes;
+} pt_stats;
+
+int pt_get_version(void);
+int pt_device_count(int32_t* out_count);
+int pt_create(const pt_device_opts* opts, void** out_ctx);
+int pt_upload_scene(void* ctx, const pt_scene_desc* scene);
+int pt_render_pass(void* ctx, const pt_camera* camera, const pt_sampler* sampler,
+                   const pt_pass_params* pass);
+int pt_synchronize(void* ctx);
+int pt_reset_buffer(void* ctx);
+/* Welford state of every pixel, row-major: M,V [H*W][3] (Colour, double), N [H*W]. */
+int pt_read_buffer(void* ctx, double* out_m, double* out_v, int32_t* out_n);
+int pt_stats_get(void* ctx, pt_stats* out_stats);
+const char* pt_last_error(void);
+void pt_destroy(void* ctx);
+
+/* Multi-GPU: one context per GPU (one process per GPU, or one thread per GPU).
+ * Rank 0 creates the id, every rank joins, pt_comm_gather sums the disjoint
+ * per-rank tile buffers into rank `root` (grouped RCCL send/recv over xGMI). */
+int pt_comm_unique_id(uint8_t out_id[128]);
+int pt_comm_init(void* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+int pt_comm_gather(void* ctx, int32_t root);
+int pt_comm_destroy(void* ctx);
+
+/* Instrumentation (bench / roofline): last pass' traversal counters, summed. */
+typedef struct pt_trace_counters {
+    uint64_t rays;
+    uint64_t nodes_visited;   /* BVH child-pair fetches (64 B each)            */
+    uint64_t prims_tested;    /* triangle/sphere/cube records tested (48 B)     */
+    uint64_t shading_fetches; /* closest-hit shading records (40 B)            */
+} pt_trace_counters;
+int pt_render_pass_counted(void* ctx, const pt_camera* camera, const pt_sampler* sampler,
+                           const pt_pass_params* pass, pt_trace_counters* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTSHARP_HIP_H */

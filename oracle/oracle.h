@@ -1,0 +1,105 @@
+/*
+ * oracle.h — CPU restatement of PTSharp's render hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load liboracle.so, and only as the checker / CPU baseline.
+ * The product (libptsharp_hip.so, ptsharp_amd/) never links or calls it.
+ *
+ * Parity status: UNPINNED against the reference itself — PTSharp is C#/.NET 9
+ * (no dotnet/mono in this image), ships no tests, fixtures or
+ * golden images, and draws every random number from the unseedable
+ * Random.Shared.  The restatement is pinned instead by analytic known-answer
+ * tests derived from the reference's semantics (tests/test_oracle.py) and by
+ * the golden fixtures it generates (tests/golden/, generating script committed).
+ *
+ * The scene/camera/sampler/pass structs have the same layout as the product's
+ * C-ABI (include/ptsharp_hip.h) so one host-side flattening feeds both.
+ */
+#ifndef PT_ORACLE_H
+#define PT_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_material {
+    double color[3];
+    double emittance, index, gloss, tint, reflectivity;
+    int32_t transparent, _pad;
+} or_material;
+
+typedef struct or_scene_desc {
+    int32_t num_materials; const or_material* materials;
+    int32_t num_shapes; const int32_t* shape_kind; const int32_t* shape_index;
+    int32_t num_spheres; const float* sphere_center; const double* sphere_radius; const int32_t* sphere_material;
+    int32_t num_cubes; const float* cube_min; const float* cube_max; const int32_t* cube_material;
+    int32_t num_planes; const float* plane_point; const float* plane_normal; const int32_t* plane_material;
+    int32_t num_triangles;
+    const float *tri_v1, *tri_v2, *tri_v3, *tri_n1, *tri_n2, *tri_n3;
+    const int32_t* tri_material;
+    int32_t num_meshes; const int32_t* mesh_first; const int32_t* mesh_count;
+    double env_color[3];
+} or_scene_desc;
+
+typedef struct or_camera {
+    float p[3], u[3], v[3], w[3];
+    double m, focal_distance, aperture_radius;
+} or_camera;
+
+typedef struct or_sampler {
+    int32_t first_hit_samples, max_bounces, direct_lighting, soft_shadows, light_mode, specular_mode;
+} or_sampler;
+
+typedef struct or_pass_params {
+    int32_t spp, stratified;
+    uint64_t seed;
+    uint32_t pass_index;
+    int32_t num_tiles;
+    const int32_t* tiles;
+} or_pass_params;
+
+/* Build the scene (k-d trees as Scene.Compile/Tree.NewTree do).  Returns NULL on error. */
+void* or_scene_create(const or_scene_desc* desc);
+void or_scene_destroy(void* scene);
+/* Number of k-d tree nodes (top-level + per-mesh trees). */
+int64_t or_scene_tree_nodes(void* scene);
+
+/* One RenderParallel pass into caller-owned Welford arrays (M,V: [H*W][3], N: [H*W]).
+ * brute_force != 0 replaces the k-d tree by a linear nearest-hit loop.
+ * num_threads <= 0: all hardware threads.  Returns Scene.Intersect calls. */
+int64_t or_render_pass(void* scene, int32_t width, int32_t height, const or_camera* cam,
+                       const or_sampler* smp, const or_pass_params* pass,
+                       double* m, double* v, int32_t* n, int32_t num_threads, int32_t brute_force);
+
+/* Render only pixels [pix_begin, pix_end) in row-major order (CPU-baseline sampling). */
+int64_t or_render_pixels(void* scene, int32_t width, int32_t height, const or_camera* cam,
+                         const or_sampler* smp, const or_pass_params* pass,
+                         int64_t pix_begin, int64_t pix_end, int64_t pix_stride,
+                         double* m, double* v, int32_t* n, int32_t num_threads);
+
+/* Known-answer helpers. */
+/* Nearest hit: returns t (1e9 = miss), writes hit kind (-1 none) and index. */
+double or_intersect(void* scene, const float origin[3], const float dir[3], int32_t brute_force,
+                    int32_t* out_kind, int32_t* out_index);
+/* Full Hit.Info: position, normal (after flip), inside flag, material id. */
+int32_t or_hit_info(void* scene, const float origin[3], const float dir[3],
+                    float out_pos[3], float out_normal[3], int32_t* out_inside, int32_t* out_mat);
+void or_cast_ray(const or_camera* cam, int32_t x, int32_t y, int32_t w, int32_t h,
+                 double u, double v, uint64_t key, float out_origin[3], float out_dir[3]);
+/* Primitive-level intersect on a standalone primitive (kind 0..3), for KAT tables. */
+double or_prim_intersect(int32_t kind, const float* a, const float* b, const float* c, double radius,
+                         const float origin[3], const float dir[3]);
+void or_prim_normal(int32_t kind, const float* a, const float* b, const float* c,
+                    const float* n1, const float* n2, const float* n3,
+                    const float pos[3], float out_normal[3]);
+
+/* Counter-based RNG that replaces Random.Shared (spec in DESIGN.md §RNG). */
+uint64_t or_camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample);
+uint64_t or_child_key(uint64_t key, uint32_t child);
+uint64_t or_light_key(uint64_t key, uint32_t light);
+double or_draw(uint64_t key, uint32_t dim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

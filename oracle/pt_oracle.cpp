@@ -1,0 +1,962 @@
+// pt_oracle.cpp — CPU restatement of PTSharp's per-pixel render hot path.
+//
+// TEST INFRASTRUCTURE ONLY (see oracle.h).  Parity against the C# reference is
+// UNPINNED (no runnable reference, no reference fixtures); this
+// file restates the reference line by line and is pinned by analytic KATs.
+//
+// Numeric model: PTSharp's Vector stores a
+// System.Numerics.Vector3 (fp32) behind double accessors (Vector.cs:201-234),
+// so every Add/Sub/Mul/Div re-rounds to fp32 (equivalent to an fp32 op),
+// MulScalar(double) is float(double(x)*s) (Vector.cs:435), Dot/Length/Cross/
+// Normalize are fp32 Vector3 ops (Vector.cs:356,372,384,391); scalars (t, det,
+// Fresnel, trig) are fp64; Colour is fp64 (Colour.cs:10-12).  Build with
+// -ffp-contract=off so no FMA contraction changes the rounding sequence.
+//
+// Only deliberate deviation: Random.Shared is replaced by the counter-based
+// stream below (keys documented in DESIGN.md §RNG); the GPU kernels use the
+// identical stream, so GPU-vs-oracle is a same-seed comparison.
+#include "oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------- constants
+const double EPS = 1e-9;            // Util.EPS  (Util.cs:11)
+const double HIT_INF = (double)1e9f;  // Hit.INF = 1e9F (Hit.cs:6)
+const double PI = 3.14159265358979323846;  // Math.PI
+
+// ---------------------------------------------------------------- RNG
+inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27; x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+inline uint64_t camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
+    uint64_t k = mix64(seed + 0x243F6A8885A308D3ull);
+    k = mix64(k ^ ((uint64_t)pass + 0x13198A2E03707344ull));
+    k = mix64(k ^ (pixel + 0xA4093822299F31D0ull));
+    return mix64(k ^ ((uint64_t)sample + 0x082EFA98EC4E6C89ull));
+}
+inline uint64_t child_key(uint64_t k, uint32_t c) { return mix64(k ^ ((uint64_t)c + 0x452821E638D01377ull)); }
+inline uint64_t light_key(uint64_t k, uint32_t i) { return mix64(k ^ ((uint64_t)i + 0xBE5466CF34E90C6Cull)); }
+// Random.Shared.NextDouble(): 53 random bits in [0,1).
+inline double draw(uint64_t k, uint32_t dim) {
+    return (double)(mix64(k + (uint64_t)(dim + 1) * 0x9E3779B97F4A7C15ull) >> 11) * (1.0 / 9007199254740992.0);
+}
+// Draw slots per child edge.
+enum { D_STRATUM_U = 0, D_STRATUM_V = 1, D_REFLECT = 2, D_RUV_Z = 3, D_RUV_A = 4,
+       D_LIGHT = 5, D_SS_RUV_Z = 6, D_SS_RUV_A = 7, D_SS_XY = 8 };
+// Camera-key slots.
+enum { D_JX = 0, D_JY = 1, D_LENS_ANGLE = 2, D_LENS_RADIUS = 3 };
+
+// ---------------------------------------------------------------- .NET Math.Min/Max (double)
+inline double net_max(double a, double b) {
+    if (a != b) { if (!std::isnan(a)) return b < a ? a : b; return a; }
+    return std::signbit(b) ? a : b;
+}
+inline double net_min(double a, double b) {
+    if (a != b) { if (!std::isnan(a)) return a < b ? a : b; return a; }
+    return std::signbit(a) ? a : b;
+}
+
+// ---------------------------------------------------------------- Vector (Vector.cs:193-543)
+struct V { float x, y, z; };
+inline V vmk(double x, double y, double z) { return V{(float)x, (float)y, (float)z}; }
+inline V vadd(V a, V b) { return V{a.x + b.x, a.y + b.y, a.z + b.z}; }   // Vector.Add  :408
+inline V vsub(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }   // Vector.Sub  :411
+inline V vmul(V a, V b) { return V{a.x * b.x, a.y * b.y, a.z * b.z}; }   // Vector.Mul  :414
+inline V vdiv(V a, V b) { return V{a.x / b.x, a.y / b.y, a.z / b.z}; }   // Vector.Div  :417
+inline V vmuls(V a, double s) {                                          // MulScalar   :435
+    return V{(float)((double)a.x * s), (float)((double)a.y * s), (float)((double)a.z * s)};
+}
+inline float dotf(V a, V b) {                                            // Vector3.Dot
+    float xx = a.x * b.x, yy = a.y * b.y, zz = a.z * b.z;
+    float s = xx + yy;
+    return s + zz;
+}
+inline double vdot(V a, V b) { return (double)dotf(a, b); }              // Vector.Dot  :370
+inline V vcross(V a, V b) {                                              // Vector3.Cross
+    float x1 = a.y * b.z, x2 = a.z * b.y;
+    float y1 = a.z * b.x, y2 = a.x * b.z;
+    float z1 = a.x * b.y, z2 = a.y * b.x;
+    return V{x1 - x2, y1 - y2, z1 - z2};
+}
+inline float lenf(V a) { return std::sqrt(dotf(a, a)); }                 // Vector3.Length
+inline double vlen(V a) { return (double)lenf(a); }
+inline V vnorm(V a) { float l = lenf(a); return V{a.x / l, a.y / l, a.z / l}; }  // Vector3.Normalize
+inline V vneg(V a) { return V{-a.x, -a.y, -a.z}; }                       // Negate :396
+inline V vmin(V a, V b) { return vmk(net_min(a.x, b.x), net_min(a.y, b.y), net_min(a.z, b.z)); }
+inline V vmax(V a, V b) { return vmk(net_max(a.x, b.x), net_max(a.y, b.y), net_max(a.z, b.z)); }
+inline V vzero() { return V{0.f, 0.f, 0.f}; }
+inline V vload(const float* p) { return V{p[0], p[1], p[2]}; }
+
+// Vector.RandomUnitVector (Vector.cs:339-347)
+inline V random_unit_vector(uint64_t key, uint32_t dz, uint32_t da) {
+    double z = draw(key, dz) * 2.0 - 1.0;
+    double a = draw(key, da) * 2.0 * PI;
+    double r = std::sqrt(1.0 - z * z);
+    double x = std::sin(a);
+    double y = std::cos(a);
+    return vmk(r * x, r * y, z);
+}
+// Vector.Reflect (Vector.cs:497): this = normal
+inline V vreflect(V n, V i) { return vsub(i, vmuls(n, 2 * vdot(n, i))); }
+// Vector.Refract (Vector.cs:500-514)
+inline V vrefract(V n, V i, double n1, double n2) {
+    double nr = n1 / n2;
+    double cosI = -vdot(n, i);
+    double sinT2 = nr * nr * (1 - cosI * cosI);
+    if (sinT2 > 1) return vzero();
+    double cosT = std::sqrt(1 - sinT2);
+    return vadd(vmuls(i, nr), vmuls(n, nr * cosI - cosT));
+}
+// Vector.Reflectance (Vector.cs:517-536)
+inline double vreflectance(V n, V i, double n1, double n2) {
+    double nr2 = (n1 * n1) / (n2 * n2);
+    double cosI = -vdot(n, i);
+    double sinT2 = nr2 * (1 - cosI * cosI);
+    if (sinT2 > 1) return 1;
+    double cosT = std::sqrt(1 - sinT2);
+    double cosI_n1 = n1 * cosI;
+    double cosT_n2 = n2 * cosT;
+    double rOrth = (cosI_n1 - cosT_n2) / (cosI_n1 + cosT_n2);
+    double rPar = (cosT_n2 - cosI_n1) / (cosT_n2 + cosI_n1);
+    return (rOrth * rOrth + rPar * rPar) / 2;
+}
+
+// ---------------------------------------------------------------- Colour (fp64)
+struct C { double r, g, b; };
+inline C cadd(C a, C b) { return C{a.r + b.r, a.g + b.g, a.b + b.b}; }
+inline C csub(C a, C b) { return C{a.r - b.r, a.g - b.g, a.b - b.b}; }
+inline C cmul(C a, C b) { return C{a.r * b.r, a.g * b.g, a.b * b.b}; }
+inline C cmuls(C a, double s) { return C{a.r * s, a.g * s, a.b * s}; }
+inline C cdivs(C a, double s) { return C{a.r / s, a.g / s, a.b / s}; }
+inline C cmix(C a, C b, double pct) { return cadd(cmuls(a, 1 - pct), cmuls(b, pct)); }  // Colour.Mix :219
+const C BLACK{0, 0, 0};
+
+// ---------------------------------------------------------------- Ray / Box
+struct Ray { V o, d; };
+inline V ray_position(const Ray& r, double t) { return vadd(r.o, vmuls(r.d, t)); }  // Ray.Position :19
+
+struct Box { V min, max; };
+// Box.Intersect (Box.cs:72-94)
+inline void box_intersect(const Box& b, const Ray& r, double& tmin, double& tmax) {
+    double x1 = ((double)b.min.x - (double)r.o.x) / (double)r.d.x;
+    double y1 = ((double)b.min.y - (double)r.o.y) / (double)r.d.y;
+    double z1 = ((double)b.min.z - (double)r.o.z) / (double)r.d.z;
+    double x2 = ((double)b.max.x - (double)r.o.x) / (double)r.d.x;
+    double y2 = ((double)b.max.y - (double)r.o.y) / (double)r.d.y;
+    double z2 = ((double)b.max.z - (double)r.o.z) / (double)r.d.z;
+    if (x1 > x2) std::swap(x1, x2);
+    if (y1 > y2) std::swap(y1, y2);
+    if (z1 > z2) std::swap(z1, z2);
+    tmin = net_max(net_max(x1, y1), z1);
+    tmax = net_min(net_min(x2, y2), z2);
+}
+inline Box box_extend(const Box& a, const Box& b) { return Box{vmin(a.min, b.min), vmax(a.max, b.max)}; }
+inline V box_center(const Box& b) { return vadd(b.min, vmul(vsub(b.max, b.min), vmk(0.5, 0.5, 0.5))); }  // Box.Center :318
+inline double box_outer_radius(const Box& b) { return vlen(vsub(b.min, box_center(b))); }              // :320
+
+// ---------------------------------------------------------------- scene
+enum Kind { K_SPHERE = 0, K_CUBE = 1, K_PLANE = 2, K_TRI = 3, K_MESH = 4 };
+
+struct Material {
+    C color; double emittance, index, gloss, tint, reflectivity; bool transparent;
+};
+struct Sphere { V center; double radius; int mat; Box box; };
+struct Cube { V min, max; int mat; };
+struct Plane { V point, normal; int mat; };
+struct Tri { V v1, v2, v3, n1, n2, n3; int mat; };
+struct ShapeRef { int kind; int idx; };
+
+struct Hit { double t; int kind; int idx; };  // kind: K_* of the primitive hit (mesh hits report K_TRI)
+const Hit NOHIT{HIT_INF, -1, -1};
+
+struct KdNode {
+    int axis;  // 0 none (leaf), 1 x, 2 y, 3 z  (Axis.cs)
+    double point;
+    int left, right;
+    std::vector<ShapeRef> shapes;
+};
+struct KdTree {
+    Box box;
+    std::vector<KdNode> nodes;  // nodes[0] = root
+};
+
+struct Scene {
+    std::vector<Material> mats;
+    std::vector<Sphere> spheres;
+    std::vector<Cube> cubes;
+    std::vector<Plane> planes;
+    std::vector<Tri> tris;
+    std::vector<int> mesh_first, mesh_count;
+    std::vector<KdTree> mesh_trees;
+    std::vector<ShapeRef> shapes;
+    std::vector<ShapeRef> lights;  // Scene.Lights (Scene.cs:33-37)
+    KdTree tree;
+    C env;
+};
+
+// ---------------------------------------------------------------- primitives
+// Sphere.Intersect (Sphere.cs:40-60)
+inline double sphere_t(V center, double radius, const Ray& r) {
+    V to = vsub(r.o, center);
+    double b = vdot(to, r.d);
+    double c = vdot(to, to) - radius * radius;
+    double d = b * b - c;
+    if (d > 0) {
+        d = std::sqrt(d);
+        double t1 = -b - d;
+        if (t1 > EPS) return t1;
+        double t2 = -b + d;
+        if (t2 > EPS) return t2;
+    }
+    return HIT_INF;
+}
+// Cube.Intersect (Cube.cs:35-47)
+inline double cube_t(V mn, V mx, const Ray& r) {
+    V n = vdiv(vsub(mn, r.o), r.d);
+    V f = vdiv(vsub(mx, r.o), r.d);
+    V n2 = vmin(n, f), f2 = vmax(n, f);
+    double t0 = net_max(net_max(n2.x, n2.y), n2.z);
+    double t1 = net_min(net_min(f2.x, f2.y), f2.z);
+    if (t0 > 0 && t0 < t1) return t0;
+    return HIT_INF;
+}
+// Plane.Intersect (Plane.cs:36-50)
+inline double plane_t(V point, V normal, const Ray& r) {
+    double d = vdot(normal, r.d);
+    if (std::fabs(d) < EPS) return HIT_INF;
+    V a = vsub(point, r.o);
+    double t = vdot(a, normal) / d;
+    if (t < EPS) return HIT_INF;
+    return t;
+}
+// Triangle.Intersect, Möller–Trumbore (Triangle.cs:95-124)
+inline double tri_t(V v1, V v2, V v3, const Ray& r) {
+    V e1 = vsub(v2, v1);
+    V e2 = vsub(v3, v1);
+    V h = vcross(r.d, e2);
+    double det = vdot(e1, h);
+    if (det > -EPS && det < EPS) return HIT_INF;
+    double invDet = 1.0 / det;
+    V s = vsub(r.o, v1);
+    double u = vdot(s, h) * invDet;
+    if (u < 0 || u > 1) return HIT_INF;
+    V q = vcross(s, e1);
+    double v = vdot(r.d, q) * invDet;
+    if (v < 0 || (u + v) > 1) return HIT_INF;
+    double t = vdot(e2, q) * invDet;
+    if (t < EPS) return HIT_INF;
+    return t;
+}
+// Cube.NormalAt (Cube.cs:57-69), including the EPS face-match quirk.
+inline V cube_normal(V mn, V mx, V p) {
+    if (std::fabs((double)p.x - (double)mn.x) < EPS) return vmk(-1, 0, 0);
+    if (std::fabs((double)p.x - (double)mx.x) < EPS) return vmk(1, 0, 0);
+    if (std::fabs((double)p.y - (double)mn.y) < EPS) return vmk(0, -1, 0);
+    if (std::fabs((double)p.y - (double)mx.y) < EPS) return vmk(0, 1, 0);
+    if (std::fabs((double)p.z - (double)mn.z) < EPS) return vmk(0, 0, -1);
+    if (std::fabs((double)p.z - (double)mx.z) < EPS) return vmk(0, 0, 1);
+    return vmk(0, 1, 0);
+}
+// Triangle.NormalAt via Barycentric (Triangle.cs:142-189, 208-223), no normal/bump maps.
+inline V tri_normal(const Tri& t, V p) {
+    V v0 = vsub(t.v2, t.v1);
+    V v1 = vsub(t.v3, t.v1);
+    V v2 = vsub(p, t.v1);
+    double d00 = vdot(v0, v0);
+    double d01 = vdot(v0, v1);
+    double d11 = vdot(v1, v1);
+    double d20 = vdot(v2, v0);
+    double d21 = vdot(v2, v1);
+    double d = d00 * d11 - d01 * d01;
+    double bv = (d11 * d20 - d01 * d21) / d;
+    double bw = (d00 * d21 - d01 * d20) / d;
+    double bu = 1 - bv - bw;
+    V n = vadd(vadd(vmuls(t.n1, bu), vmuls(t.n2, bv)), vmuls(t.n3, bw));
+    return vnorm(n);
+}
+
+inline Box tri_box(const Tri& t) { return Box{vmin(vmin(t.v1, t.v2), t.v3), vmax(vmax(t.v1, t.v2), t.v3)}; }
+
+Box shape_box(const Scene& s, ShapeRef r) {
+    switch (r.kind) {
+        case K_SPHERE: return s.spheres[r.idx].box;
+        case K_CUBE: return Box{s.cubes[r.idx].min, s.cubes[r.idx].max};
+        case K_PLANE: return Box{vmk(-1e9, -1e9, -1e9), vmk(1e9, 1e9, 1e9)};  // Plane.cs:31-34 (Util.INF)
+        case K_TRI: return tri_box(s.tris[r.idx]);
+        case K_MESH: {  // Mesh.BoundingBox (Mesh.cs:88-120)
+            int f = s.mesh_first[r.idx], n = s.mesh_count[r.idx];
+            V mn = s.tris[f].v1, mx = s.tris[f].v1;
+            for (int i = f; i < f + n; i++) {
+                const Tri& t = s.tris[i];
+                mn = vmin(vmin(vmin(mn, t.v1), t.v2), t.v3);
+                mx = vmax(vmax(vmax(mx, t.v1), t.v2), t.v3);
+            }
+            return Box{mn, mx};
+        }
+    }
+    return Box{vzero(), vzero()};
+}
+
+// ---------------------------------------------------------------- k-d tree build (Tree.cs:22-29,130-265)
+struct TreeBuilder {
+    const Scene& s;
+    KdTree& tree;
+    std::vector<Box> boxcache;  // by position in `all`
+    TreeBuilder(const Scene& s_, KdTree& t) : s(s_), tree(t) {}
+
+    // Box.Partition (Box.cs:96-114)
+    static void partition(const Box& b, int axis, double point, bool& l, bool& r) {
+        switch (axis) {
+            case 1: l = b.min.x <= point; r = b.max.x >= point; break;
+            case 2: l = b.min.y <= point; r = b.max.y >= point; break;
+            default: l = b.min.z <= point; r = b.max.z >= point; break;
+        }
+    }
+    static int partition_score(const std::vector<Box>& boxes, int axis, double point) {
+        int left = 0, right = 0;
+        for (const Box& b : boxes) {
+            bool l, r; partition(b, axis, point, l, r);
+            if (l) left++;
+            if (r) right++;
+        }
+        return left >= right ? left : right;
+    }
+    // Node.Median over a ConcurrentBag filled in insertion order L = [min0,max0,min1,...]:
+    // enumeration is LIFO, the count is always even (2 per shape), so the
+    // "median" is (L[n-1] + L[n]) / 2 with n = #shapes (Tree.cs:130-148, 208-226).
+    static double median(const std::vector<double>& L) {
+        if (L.empty()) return 0;
+        size_t cnt = L.size();
+        std::vector<double> R(L.rbegin(), L.rend());
+        size_t mid = cnt / 2;
+        if (cnt % 2 == 1) return R[mid];
+        return (R[cnt / 2 - 1] + R[cnt / 2]) / 2;
+    }
+    int new_node(std::vector<ShapeRef>&& shapes) {
+        KdNode n; n.axis = 0; n.point = 0; n.left = n.right = -1; n.shapes = std::move(shapes);
+        tree.nodes.push_back(std::move(n));
+        return (int)tree.nodes.size() - 1;
+    }
+    void split(int node, int depth) {  // Node.Split (Tree.cs:201-265)
+        std::vector<ShapeRef> shapes = tree.nodes[node].shapes;
+        if (shapes.size() < 8) return;
+        std::vector<Box> boxes(shapes.size());
+        std::vector<double> xs, ys, zs;
+        xs.reserve(2 * shapes.size()); ys.reserve(2 * shapes.size()); zs.reserve(2 * shapes.size());
+        for (size_t i = 0; i < shapes.size(); i++) {
+            boxes[i] = shape_box(s, shapes[i]);
+            xs.push_back(boxes[i].min.x); xs.push_back(boxes[i].max.x);
+            ys.push_back(boxes[i].min.y); ys.push_back(boxes[i].max.y);
+            zs.push_back(boxes[i].min.z); zs.push_back(boxes[i].max.z);
+        }
+        double mx = median(xs), my = median(ys), mz = median(zs);
+        int best = (int)(shapes.size() * 0.85);
+        int bestAxis = 0; double bestPoint = 0.0;
+        int sx = partition_score(boxes, 1, mx);
+        if (sx < best) { best = sx; bestAxis = 1; bestPoint = mx; }
+        int sy = partition_score(boxes, 2, my);
+        if (sy < best) { best = sy; bestAxis = 2; bestPoint = my; }
+        int sz = partition_score(boxes, 3, mz);
+        if (sz < best) { best = sz; bestAxis = 3; bestPoint = mz; }
+        if (bestAxis == 0) return;
+        // Partition into ConcurrentBags; ToArray() yields LIFO (reverse insertion) order.
+        std::vector<ShapeRef> l, r;
+        for (size_t i = 0; i < shapes.size(); i++) {
+            bool bl, br; partition(boxes[i], bestAxis, bestPoint, bl, br);
+            if (bl) l.push_back(shapes[i]);
+            if (br) r.push_back(shapes[i]);
+        }
+        std::reverse(l.begin(), l.end());
+        std::reverse(r.begin(), r.end());
+        tree.nodes[node].axis = bestAxis;
+        tree.nodes[node].point = bestPoint;
+        int li = new_node(std::move(l));
+        int ri = new_node(std::move(r));
+        tree.nodes[node].left = li;
+        tree.nodes[node].right = ri;
+        split(li, depth + 1);
+        split(ri, depth + 1);
+        tree.nodes[node].shapes.clear();
+        tree.nodes[node].shapes.shrink_to_fit();
+    }
+    void build(const std::vector<ShapeRef>& shapes) {  // Tree.NewTree (Tree.cs:22-29)
+        tree.nodes.clear();
+        if (!shapes.empty()) {
+            Box b = shape_box(s, shapes[0]);
+            for (const ShapeRef& r : shapes) b = box_extend(b, shape_box(s, r));
+            tree.box = b;
+        } else {
+            tree.box = Box{vzero(), vzero()};
+        }
+        int root = new_node(std::vector<ShapeRef>(shapes));
+        split(root, 0);
+    }
+};
+
+// ---------------------------------------------------------------- tracing
+struct Tracer {
+    const Scene& s;
+    bool brute;
+    uint64_t rays = 0;
+    Tracer(const Scene& s_, bool b) : s(s_), brute(b) {}
+
+    Hit shape_intersect(ShapeRef r, const Ray& ray) const {
+        double t = HIT_INF;
+        switch (r.kind) {
+            case K_SPHERE: t = sphere_t(s.spheres[r.idx].center, s.spheres[r.idx].radius, ray); break;
+            case K_CUBE: t = cube_t(s.cubes[r.idx].min, s.cubes[r.idx].max, ray); break;
+            case K_PLANE: t = plane_t(s.planes[r.idx].point, s.planes[r.idx].normal, ray); break;
+            case K_TRI: { const Tri& tr = s.tris[r.idx]; t = tri_t(tr.v1, tr.v2, tr.v3, ray); break; }
+            case K_MESH:
+                if (brute) {
+                    Hit h = NOHIT;
+                    int f = s.mesh_first[r.idx], n = s.mesh_count[r.idx];
+                    for (int i = f; i < f + n; i++) {
+                        const Tri& tr = s.tris[i];
+                        double tt = tri_t(tr.v1, tr.v2, tr.v3, ray);
+                        if (tt < h.t) h = Hit{tt, K_TRI, i};
+                    }
+                    return h;
+                }
+                return tree_intersect(s.mesh_trees[r.idx], ray);  // Mesh.Intersect (Mesh.cs:83-86)
+        }
+        if (t < HIT_INF) return Hit{t, r.kind, r.idx};
+        return NOHIT;
+    }
+    // Node.IntersectShapes (Tree.cs:115-128): strict '<', first shape wins ties.
+    Hit intersect_shapes(const std::vector<ShapeRef>& shapes, const Ray& ray) const {
+        Hit hit = NOHIT;
+        for (const ShapeRef& r : shapes) {
+            Hit h = shape_intersect(r, ray);
+            if (h.t < hit.t) hit = h;
+        }
+        return hit;
+    }
+    // Node.Intersect (Tree.cs:67-113)
+    Hit node_intersect(const KdTree& tr, int ni, const Ray& r, double tmin, double tmax) const {
+        const KdNode& n = tr.nodes[ni];
+        double tsplit; bool leftFirst;
+        switch (n.axis) {
+            case 0: return intersect_shapes(n.shapes, r);
+            case 1: tsplit = (n.point - (double)r.o.x) / (double)r.d.x;
+                    leftFirst = ((double)r.o.x < n.point) || ((double)r.o.x == n.point && r.d.x <= 0); break;
+            case 2: tsplit = (n.point - (double)r.o.y) / (double)r.d.y;
+                    leftFirst = ((double)r.o.y < n.point) || ((double)r.o.y == n.point && r.d.y <= 0); break;
+            default: tsplit = (n.point - (double)r.o.z) / (double)r.d.z;
+                    leftFirst = ((double)r.o.z < n.point) || ((double)r.o.z == n.point && r.d.z <= 0); break;
+        }
+        int first = leftFirst ? n.left : n.right;
+        int second = leftFirst ? n.right : n.left;
+        if (tsplit > tmax || tsplit <= 0) return node_intersect(tr, first, r, tmin, tmax);
+        if (tsplit < tmin) return node_intersect(tr, second, r, tmin, tmax);
+        Hit h1 = node_intersect(tr, first, r, tmin, tsplit);
+        if (h1.t <= tsplit) return h1;
+        Hit h2 = node_intersect(tr, second, r, tsplit, net_min(tmax, h1.t));
+        return h1.t <= h2.t ? h1 : h2;
+    }
+    // Tree.Intersect (Tree.cs:31-42)
+    Hit tree_intersect(const KdTree& tr, const Ray& r) const {
+        if (tr.nodes.empty()) return NOHIT;
+        double tmin, tmax;
+        box_intersect(tr.box, r, tmin, tmax);
+        if (tmax < tmin || tmax <= 0) return NOHIT;
+        return node_intersect(tr, 0, r, tmin, tmax);
+    }
+    // Scene.Intersect (Scene.cs:75-79): counts every call.
+    Hit intersect(const Ray& r) {
+        rays++;
+        if (brute) return intersect_shapes(s.shapes, r);
+        return tree_intersect(s.tree, r);
+    }
+};
+
+struct HitInfo { V position, normal; Ray ray; int mat; bool inside; };
+
+V shape_normal(const Scene& s, const Hit& h, V p) {
+    switch (h.kind) {
+        case K_SPHERE: return vnorm(vsub(p, s.spheres[h.idx].center));  // Sphere.NormalAt :78-81
+        case K_CUBE: return cube_normal(s.cubes[h.idx].min, s.cubes[h.idx].max, p);
+        case K_PLANE: return s.planes[h.idx].normal;                      // Plane.NormalAt :61-64
+        default: return tri_normal(s.tris[h.idx], p);
+    }
+}
+int shape_mat(const Scene& s, const Hit& h) {
+    switch (h.kind) {
+        case K_SPHERE: return s.spheres[h.idx].mat;
+        case K_CUBE: return s.cubes[h.idx].mat;
+        case K_PLANE: return s.planes[h.idx].mat;
+        default: return s.tris[h.idx].mat;
+    }
+}
+// Hit.Info (Hit.cs:26-55)
+HitInfo hit_info(const Scene& s, const Hit& h, const Ray& r) {
+    HitInfo info;
+    info.position = ray_position(r, h.t);
+    V normal = shape_normal(s, h, info.position);
+    info.mat = shape_mat(s, h);
+    info.inside = false;
+    if (vdot(normal, r.d) > 0) { normal = vneg(normal); info.inside = true; }
+    info.normal = normal;
+    info.ray = Ray{info.position, normal};
+    return info;
+}
+
+// ---------------------------------------------------------------- sampler (Sampler.cs)
+struct Sampler {
+    int fh, mb; bool dl, ss; int light_mode, spec_mode;
+};
+
+struct Integrator {
+    const Scene& s;
+    const Sampler& smp;
+    Tracer& tr;
+    Integrator(const Scene& s_, const Sampler& m, Tracer& t) : s(s_), smp(m), tr(t) {}
+
+    // Util.Cone (Util.cs:17-32)
+    V cone(V direction, double theta, double u, double v, uint64_t key) {
+        if (theta < EPS) return direction;
+        theta = theta * (1 - (2 * std::acos(u) / PI));
+        double m1 = std::sin(theta);
+        double m2 = std::cos(theta);
+        double a = v * 2 * PI;
+        V q = random_unit_vector(key, D_RUV_Z, D_RUV_A);
+        V sv = vcross(direction, q);
+        V tv = vcross(direction, sv);
+        V d = vadd(vadd(vadd(vzero(), vmuls(sv, m1 * std::cos(a))), vmuls(tv, m1 * std::sin(a))), vmuls(direction, m2));
+        return vnorm(d);
+    }
+    // Ray.WeightedBounce (Ray.cs:28-35), on the normal ray n
+    Ray weighted_bounce(const Ray& n, double u, double v, uint64_t key) {
+        double radius = std::sqrt(u);
+        double theta = 2 * PI * v;
+        V sv = vnorm(vcross(n.d, random_unit_vector(key, D_RUV_Z, D_RUV_A)));
+        V tv = vcross(n.d, sv);
+        V d = vadd(vadd(vadd(vzero(), vmuls(sv, radius * std::cos(theta))), vmuls(tv, radius * std::sin(theta))),
+                   vmuls(n.d, std::sqrt(1 - u)));
+        return Ray{n.o, d};
+    }
+    // Ray.Bounce (Ray.cs:44-85); bounce type 0 Any, 1 Diffuse, 2 Specular (BounceType.cs)
+    Ray bounce(const Ray& in, const HitInfo& info, double u, double v, int btype, uint64_t key,
+               bool& reflected, double& p) {
+        const Material& m = s.mats[info.mat];
+        const Ray& n = info.ray;
+        double n1 = 1.0, n2 = m.index;
+        if (info.inside) std::swap(n1, n2);
+        p = m.reflectivity >= 0 ? m.reflectivity : vreflectance(n.d, in.d, n1, n2);
+        bool reflect;
+        switch (btype) {
+            case 0: reflect = draw(key, D_REFLECT) < p; break;
+            case 1: reflect = false; break;
+            default: reflect = true; break;
+        }
+        if (reflect) {
+            Ray r{n.o, vreflect(n.d, in.d)};
+            reflected = true;
+            return Ray{r.o, cone(r.d, m.gloss, u, v, key)};
+        } else if (m.transparent) {
+            Ray r{n.o, vrefract(n.d, in.d, n1, n2)};
+            r.o = vadd(r.o, vmuls(r.d, 1e-4));
+            reflected = true;
+            p = 1 - p;
+            return Ray{r.o, cone(r.d, m.gloss, u, v, key)};
+        }
+        reflected = false;
+        p = 1 - p;
+        return weighted_bounce(n, u, v, key);
+    }
+    bool light_identity(ShapeRef light, const Hit& h) const {
+        // hit.Shape != light is a reference compare (Sampler.cs:264): class shapes
+        // compare equal to themselves; a struct Triangle is re-boxed per Hit, never equal.
+        if (light.kind == K_TRI || light.kind == K_MESH) return false;
+        return h.kind == light.kind && h.idx == light.idx;
+    }
+    // Sampler.sampleLight (Sampler.cs:212-296)
+    C sample_light(const Ray& n, ShapeRef light, uint64_t key) {
+        V center; double radius;
+        if (light.kind == K_SPHERE) {
+            radius = s.spheres[light.idx].radius;
+            center = s.spheres[light.idx].center;
+        } else {
+            Box b = shape_box(s, light);
+            radius = box_outer_radius(b);
+            center = box_center(b);
+        }
+        V point = center;
+        if (smp.ss) {
+            for (uint32_t k = 0; k < 256; k++) {
+                double x = draw(key, D_SS_XY + 2 * k) * 2 - 1;
+                double y = draw(key, D_SS_XY + 2 * k + 1) * 2 - 1;
+                if (x * x + y * y <= 1) {
+                    V l = vnorm(vsub(center, n.o));
+                    V u = vnorm(vcross(l, random_unit_vector(key, D_SS_RUV_Z, D_SS_RUV_A)));
+                    V v = vcross(l, u);
+                    point = vadd(vadd(center, vmuls(u, x * radius)), vmuls(v, y * radius));
+                    break;
+                }
+            }
+        }
+        V rayDirection = vnorm(vsub(point, n.o));
+        double diffuse = vdot(rayDirection, n.d);
+        if (diffuse <= 0) return BLACK;
+        Ray ray{n.o, rayDirection};
+        Hit hit = tr.intersect(ray);
+        if (!(hit.t < HIT_INF) || !light_identity(light, hit)) return BLACK;
+        double hyp = vlen(vsub(center, n.o));
+        double theta = std::asin(radius / hyp);
+        double adj = radius / std::tan(theta);
+        double d = std::cos(theta) * adj;
+        double r = std::sin(theta) * adj;
+        double coverage = (r * r) / (d * d);
+        if (hyp < radius) coverage = 1;
+        coverage = net_min(coverage, 1);
+        int mi = light.kind == K_SPHERE ? s.spheres[light.idx].mat
+               : light.kind == K_CUBE ? s.cubes[light.idx].mat
+               : light.kind == K_PLANE ? s.planes[light.idx].mat : s.tris[light.idx].mat;
+        const Material& m = s.mats[mi];
+        double mm = m.emittance * diffuse * coverage;
+        return cmuls(m.color, mm);
+    }
+    // Sampler.sampleLights (Sampler.cs:191-210)
+    C sample_lights(const Ray& n, uint64_t key) {
+        int nLights = (int)s.lights.size();
+        if (nLights == 0) return BLACK;
+        if (smp.light_mode == 1) {
+            C result{0, 0, 0};
+            for (int i = 0; i < nLights; i++) result = cadd(result, sample_light(n, s.lights[i], light_key(key, (uint32_t)i)));
+            return cdivs(result, nLights);
+        }
+        int idx = (int)(draw(key, D_LIGHT) * nLights);
+        if (idx >= nLights) idx = nLights - 1;
+        return cmuls(sample_light(n, s.lights[idx], key), (double)nLights);
+    }
+    // DefaultSampler.sample (Sampler.cs:55-145); Russian roulette is never enabled.
+    C sample(const Ray& ray, bool emission, int samples, int depth, uint64_t node) {
+        if (depth > smp.mb) return BLACK;
+        Hit hit = tr.intersect(ray);
+        if (!(hit.t < HIT_INF)) return s.env;  // sampleEnvironment (Sampler.cs:177-189), no texture
+        HitInfo info = hit_info(s, hit, ray);
+        const Material& material = s.mats[info.mat];
+        C result{0, 0, 0};
+        if (material.emittance > 0) {
+            if (smp.dl && !emission) return BLACK;
+            result = cadd(result, cmuls(material.color, material.emittance * samples));
+        }
+        int n = (int)std::sqrt((double)samples);
+        int ma, mb;
+        if (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) { ma = 1; mb = 2; }
+        else { ma = 0; mb = 0; }
+        int nm = mb - ma + 1;
+        for (int u = 0; u < n; u++) {
+            for (int v = 0; v < n; v++) {
+                for (int mode = ma; mode <= mb; mode++) {
+                    uint32_t c = (uint32_t)((u * n + v) * nm + (mode - ma));
+                    uint64_t E = child_key(node, c);
+                    double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)n;
+                    double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)n;
+                    bool reflected; double p;
+                    Ray newRay = bounce(ray, info, fu, fv, mode, E, reflected, p);
+                    if (mode == 0) p = 1;
+                    if (p > 0 && reflected) {
+                        C indirect = sample(newRay, reflected, 1, depth + 1, E);
+                        C tinted = cmix(indirect, cmul(material.color, indirect), material.tint);
+                        result = cadd(result, cmuls(tinted, p));
+                    }
+                    if (p > 0 && !reflected) {
+                        C indirect = sample(newRay, reflected, 1, depth + 1, E);
+                        C direct = BLACK;
+                        if (smp.dl) direct = sample_lights(info.ray, E);
+                        result = cadd(result, cmuls(cmul(material.color, cadd(direct, indirect)), p));
+                    }
+                }
+            }
+        }
+        return cdivs(result, (double)(n * n));
+    }
+};
+
+// Camera.CastRay (Camera.cs:98-119)
+Ray cast_ray(const or_camera& cam, int x, int y, int w, int h, double u, double v, uint64_t key) {
+    double aspect = w / (double)h;
+    double px = ((x + u - 0.5) / (w - 1.0)) * 2 - 1;
+    double py = ((y + v - 0.5) / (h - 1.0)) * 2 - 1;
+    V cu = vload(cam.u), cv = vload(cam.v), cw = vload(cam.w), cp = vload(cam.p);
+    V d = vnorm(vadd(vadd(vadd(vzero(), vmuls(cu, -px * aspect)), vmuls(cv, -py)), vmuls(cw, cam.m)));
+    V p = cp;
+    if (cam.aperture_radius > 0) {
+        V focalPoint = vadd(cp, vmuls(d, cam.focal_distance));
+        double angle = draw(key, D_LENS_ANGLE) * 2 * PI;
+        double radius = draw(key, D_LENS_RADIUS) * cam.aperture_radius;
+        p = vadd(p, vmuls(cu, std::cos(angle) * radius));
+        p = vadd(p, vmuls(cv, std::sin(angle) * radius));
+        d = vnorm(vsub(focalPoint, p));
+    }
+    return Ray{p, d};
+}
+
+// Pixel.AddSample (Buffer.cs:33-44)
+inline void welford(double* m, double* v, int32_t* n, C s) {
+    (*n)++;
+    if (*n == 1) { m[0] = s.r; m[1] = s.g; m[2] = s.b; return; }
+    C M{m[0], m[1], m[2]}, Vv{v[0], v[1], v[2]};
+    C mo = M;
+    M = cadd(M, cdivs(csub(s, M), (double)*n));
+    Vv = cadd(Vv, cmul(csub(s, mo), csub(s, M)));
+    m[0] = M.r; m[1] = M.g; m[2] = M.b;
+    v[0] = Vv.r; v[1] = Vv.g; v[2] = Vv.b;
+}
+
+Sampler make_sampler(const or_sampler* s) {
+    return Sampler{s->first_hit_samples, s->max_bounces, s->direct_lighting != 0, s->soft_shadows != 0,
+                   s->light_mode, s->specular_mode};
+}
+
+// One pixel of RenderParallel (Renderer.cs:287-310) or of the stratified path (:233-253).
+void render_pixel(Integrator& in, const or_camera& cam, int x, int y, int w, int h, const or_pass_params& pp,
+                  double* M, double* Vv, int32_t* N) {
+    uint64_t pix = (uint64_t)y * (uint64_t)w + (uint64_t)x;
+    size_t i = (size_t)pix;
+    if (pp.stratified) {
+        int sppRoot = (int)std::sqrt((double)pp.spp);
+        for (int u = 0; u < sppRoot; u++)
+            for (int v = 0; v < sppRoot; v++) {
+                uint64_t K = camera_key(pp.seed, pp.pass_index, pix, (uint32_t)(u * sppRoot + v));
+                double fu = ((double)u + 0.5) / (double)sppRoot;
+                double fv = ((double)v + 0.5) / (double)sppRoot;
+                Ray ray = cast_ray(cam, x, y, w, h, fu, fv, K);
+                C smp = in.sample(ray, true, in.smp.fh, 0, K);
+                welford(M + 3 * i, Vv + 3 * i, N + i, smp);
+            }
+        return;
+    }
+    C c{0, 0, 0};
+    for (int p = 0; p < pp.spp; p++) {
+        uint64_t K = camera_key(pp.seed, pp.pass_index, pix, (uint32_t)p);
+        double xOffset = draw(K, D_JX);
+        double yOffset = draw(K, D_JY);
+        double fu = (x + xOffset) / w;  // the jitter bug: CastRay adds x again
+        double fv = (y + yOffset) / h;
+        Ray ray = cast_ray(cam, x, y, w, h, fu, fv, K);
+        c = cadd(c, in.sample(ray, true, in.smp.fh, 0, K));
+    }
+    c = cdivs(c, (double)pp.spp);
+    welford(M + 3 * i, Vv + 3 * i, N + i, c);
+}
+
+template <class F>
+void parallel_tasks(int64_t ntasks, int nthreads, F&& fn) {
+    if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+    std::atomic<int64_t> next{0};
+    auto worker = [&](int tid) {
+        for (;;) {
+            int64_t t = next.fetch_add(1);
+            if (t >= ntasks) break;
+            fn(t, tid);
+        }
+    };
+    if (nthreads == 1) { worker(0); return; }
+    std::vector<std::thread> th;
+    for (int i = 0; i < nthreads; i++) th.emplace_back(worker, i);
+    for (auto& t : th) t.join();
+}
+
+Scene* build_scene(const or_scene_desc* d) {
+    Scene* s = new Scene();
+    for (int i = 0; i < d->num_materials; i++) {
+        const or_material& m = d->materials[i];
+        s->mats.push_back(Material{C{m.color[0], m.color[1], m.color[2]}, m.emittance, m.index, m.gloss, m.tint,
+                                   m.reflectivity, m.transparent != 0});
+    }
+    for (int i = 0; i < d->num_spheres; i++) {
+        V c = vload(d->sphere_center + 3 * i);
+        double r = d->sphere_radius[i];
+        // Sphere.NewSphere (Sphere.cs:27-33)
+        Box b{vmk((double)c.x - r, (double)c.y - r, (double)c.z - r), vmk((double)c.x + r, (double)c.y + r, (double)c.z + r)};
+        s->spheres.push_back(Sphere{c, r, d->sphere_material[i], b});
+    }
+    for (int i = 0; i < d->num_cubes; i++)
+        s->cubes.push_back(Cube{vload(d->cube_min + 3 * i), vload(d->cube_max + 3 * i), d->cube_material[i]});
+    for (int i = 0; i < d->num_planes; i++)
+        s->planes.push_back(Plane{vload(d->plane_point + 3 * i), vload(d->plane_normal + 3 * i), d->plane_material[i]});
+    for (int i = 0; i < d->num_triangles; i++)
+        s->tris.push_back(Tri{vload(d->tri_v1 + 3 * i), vload(d->tri_v2 + 3 * i), vload(d->tri_v3 + 3 * i),
+                              vload(d->tri_n1 + 3 * i), vload(d->tri_n2 + 3 * i), vload(d->tri_n3 + 3 * i),
+                              d->tri_material[i]});
+    for (int i = 0; i < d->num_meshes; i++) {
+        s->mesh_first.push_back(d->mesh_first[i]);
+        s->mesh_count.push_back(d->mesh_count[i]);
+    }
+    for (int i = 0; i < d->num_shapes; i++) {
+        ShapeRef r{d->shape_kind[i], d->shape_index[i]};
+        s->shapes.push_back(r);
+        // Scene.Add (Scene.cs:29-38): MaterialAt(new Vector()).Emittance > 0; Mesh.MaterialAt is `default`.
+        double em = 0;
+        switch (r.kind) {
+            case K_SPHERE: em = s->mats[s->spheres[r.idx].mat].emittance; break;
+            case K_CUBE: em = s->mats[s->cubes[r.idx].mat].emittance; break;
+            case K_PLANE: em = s->mats[s->planes[r.idx].mat].emittance; break;
+            case K_TRI: em = s->mats[s->tris[r.idx].mat].emittance; break;
+            default: em = 0; break;
+        }
+        if (em > 0) s->lights.push_back(r);
+    }
+    s->env = C{d->env_color[0], d->env_color[1], d->env_color[2]};
+    // Scene.Compile: each Mesh builds its own tree over its triangles, then the top-level tree.
+    s->mesh_trees.resize(s->mesh_first.size());
+    std::vector<int> mesh_ids(s->mesh_first.size());
+    for (size_t i = 0; i < mesh_ids.size(); i++) mesh_ids[i] = (int)i;
+    parallel_tasks((int64_t)mesh_ids.size(), 0, [&](int64_t mi, int) {
+        std::vector<ShapeRef> tri_refs;
+        int f = s->mesh_first[mi], n = s->mesh_count[mi];
+        for (int t = f; t < f + n; t++) tri_refs.push_back(ShapeRef{K_TRI, t});
+        TreeBuilder(*s, s->mesh_trees[mi]).build(tri_refs);
+    });
+    TreeBuilder(*s, s->tree).build(s->shapes);
+    return s;
+}
+
+}  // namespace
+
+// ====================================================================== C API
+extern "C" {
+
+void* or_scene_create(const or_scene_desc* desc) {
+    if (!desc) return nullptr;
+    return build_scene(desc);
+}
+void or_scene_destroy(void* scene) { delete (Scene*)scene; }
+int64_t or_scene_tree_nodes(void* scene) {
+    Scene* s = (Scene*)scene;
+    int64_t n = (int64_t)s->tree.nodes.size();
+    for (auto& t : s->mesh_trees) n += (int64_t)t.nodes.size();
+    return n;
+}
+
+int64_t or_render_pass(void* scene, int32_t width, int32_t height, const or_camera* cam, const or_sampler* smp,
+                       const or_pass_params* pass, double* m, double* v, int32_t* n, int32_t num_threads,
+                       int32_t brute_force) {
+    const Scene& s = *(Scene*)scene;
+    Sampler sm = make_sampler(smp);
+    // RenderParallel (Renderer.cs:257-312): 256² tiles of 32² sub-tiles; here a task is one
+    // 32² tile (tile id = ty*ceil(W/32)+tx), the same granularity as the reference's sub-tile task.
+    int tx = (width + 31) / 32, ty = (height + 31) / 32;
+    std::vector<int32_t> tiles;
+    if (pass->num_tiles > 0) tiles.assign(pass->tiles, pass->tiles + pass->num_tiles);
+    else { tiles.resize((size_t)tx * ty); for (int i = 0; i < tx * ty; i++) tiles[i] = i; }
+    int nt = num_threads <= 0 ? (int)std::max(1u, std::thread::hardware_concurrency()) : num_threads;
+    std::vector<uint64_t> rays((size_t)nt, 0);
+    parallel_tasks((int64_t)tiles.size(), nt, [&](int64_t t, int tid) {
+        int tile = tiles[(size_t)t];
+        int x0 = (tile % tx) * 32, y0 = (tile / tx) * 32;
+        Tracer tr(s, brute_force != 0);
+        Integrator in(s, sm, tr);
+        for (int y = y0; y < std::min(y0 + 32, (int)height); y++)
+            for (int x = x0; x < std::min(x0 + 32, (int)width); x++)
+                render_pixel(in, *cam, x, y, width, height, *pass, m, v, n);
+        rays[(size_t)tid] += tr.rays;
+    });
+    uint64_t total = 0;
+    for (uint64_t r : rays) total += r;
+    return (int64_t)total;
+}
+
+int64_t or_render_pixels(void* scene, int32_t width, int32_t height, const or_camera* cam, const or_sampler* smp,
+                         const or_pass_params* pass, int64_t pix_begin, int64_t pix_end, int64_t pix_stride,
+                         double* m, double* v, int32_t* n, int32_t num_threads) {
+    const Scene& s = *(Scene*)scene;
+    Sampler sm = make_sampler(smp);
+    if (pix_stride <= 0) pix_stride = 1;
+    int64_t count = (pix_end - pix_begin + pix_stride - 1) / pix_stride;
+    const int64_t chunk = 64;
+    int nt = num_threads <= 0 ? (int)std::max(1u, std::thread::hardware_concurrency()) : num_threads;
+    std::vector<uint64_t> rays((size_t)nt, 0);
+    parallel_tasks((count + chunk - 1) / chunk, nt, [&](int64_t t, int tid) {
+        Tracer tr(s, false);
+        Integrator in(s, sm, tr);
+        for (int64_t k = t * chunk; k < std::min(count, (t + 1) * chunk); k++) {
+            int64_t pix = pix_begin + k * pix_stride;
+            render_pixel(in, *cam, (int)(pix % width), (int)(pix / width), width, height, *pass, m, v, n);
+        }
+        rays[(size_t)tid] += tr.rays;
+    });
+    uint64_t total = 0;
+    for (uint64_t r : rays) total += r;
+    return (int64_t)total;
+}
+
+double or_intersect(void* scene, const float origin[3], const float dir[3], int32_t brute_force, int32_t* out_kind,
+                    int32_t* out_index) {
+    const Scene& s = *(Scene*)scene;
+    Tracer tr(s, brute_force != 0);
+    Hit h = tr.intersect(Ray{vload(origin), vload(dir)});
+    if (out_kind) *out_kind = h.kind;
+    if (out_index) *out_index = h.idx;
+    return h.t;
+}
+
+int32_t or_hit_info(void* scene, const float origin[3], const float dir[3], float out_pos[3], float out_normal[3],
+                    int32_t* out_inside, int32_t* out_mat) {
+    const Scene& s = *(Scene*)scene;
+    Tracer tr(s, false);
+    Ray r{vload(origin), vload(dir)};
+    Hit h = tr.intersect(r);
+    if (!(h.t < HIT_INF)) return 0;
+    HitInfo info = hit_info(s, h, r);
+    out_pos[0] = info.position.x; out_pos[1] = info.position.y; out_pos[2] = info.position.z;
+    out_normal[0] = info.normal.x; out_normal[1] = info.normal.y; out_normal[2] = info.normal.z;
+    *out_inside = info.inside ? 1 : 0;
+    *out_mat = info.mat;
+    return 1;
+}
+
+void or_cast_ray(const or_camera* cam, int32_t x, int32_t y, int32_t w, int32_t h, double u, double v, uint64_t key,
+                 float out_origin[3], float out_dir[3]) {
+    Ray r = cast_ray(*cam, x, y, w, h, u, v, key);
+    out_origin[0] = r.o.x; out_origin[1] = r.o.y; out_origin[2] = r.o.z;
+    out_dir[0] = r.d.x; out_dir[1] = r.d.y; out_dir[2] = r.d.z;
+}
+
+double or_prim_intersect(int32_t kind, const float* a, const float* b, const float* c, double radius,
+                         const float origin[3], const float dir[3]) {
+    Ray r{vload(origin), vload(dir)};
+    switch (kind) {
+        case K_SPHERE: return sphere_t(vload(a), radius, r);
+        case K_CUBE: return cube_t(vload(a), vload(b), r);
+        case K_PLANE: return plane_t(vload(a), vload(b), r);
+        default: return tri_t(vload(a), vload(b), vload(c), r);
+    }
+}
+
+void or_prim_normal(int32_t kind, const float* a, const float* b, const float* c, const float* n1, const float* n2,
+                    const float* n3, const float pos[3], float out_normal[3]) {
+    V p = vload(pos), n;
+    switch (kind) {
+        case K_SPHERE: n = vnorm(vsub(p, vload(a))); break;
+        case K_CUBE: n = cube_normal(vload(a), vload(b), p); break;
+        case K_PLANE: n = vload(b); break;
+        default: {
+            Tri t{vload(a), vload(b), vload(c), vload(n1), vload(n2), vload(n3), 0};
+            n = tri_normal(t, p);
+        }
+    }
+    out_normal[0] = n.x; out_normal[1] = n.y; out_normal[2] = n.z;
+}
+
+uint64_t or_camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
+    return camera_key(seed, pass, pixel, sample);
+}
+uint64_t or_child_key(uint64_t key, uint32_t child) { return child_key(key, child); }
+uint64_t or_light_key(uint64_t key, uint32_t light) { return light_key(key, light); }
+double or_draw(uint64_t key, uint32_t dim) { return draw(key, dim); }
+
+}  // extern "C"

@@ -1,0 +1,571 @@
+// pt_api.hip — C-ABI implementation of libptsharp_hip.so (include/ptsharp_hip.h).
+//
+// Host runtime around the gfx950 render kernels: scene flattening and BVH
+// build (replacing Scene.Compile / Tree.NewTree, Scene.cs:48-68), HBM-resident
+// Welford buffer (Renderer.PBuffer, Renderer.cs:20), pass launch and timing
+// (RenderParallel + its stopwatch, Renderer.cs:199-213,470), ray statistics
+// (Scene.rays, Scene.cs:70-79), and the multi-GPU Buffer gather over RCCL.
+// No exception crosses the ABI: every entry point returns a pt_status and
+// leaves a thread-local message for pt_last_error (the OIDN convention,
+// OIDN.cs:85-86).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/ptsharp_hip.h"
+#include "pt_bvh.h"
+#include "pt_math.h"
+#include "pt_scene.h"
+
+#pragma clang fp contract(off)
+
+namespace pt {
+hipError_t launch_render_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
+                              const DevBuffer& B, int num_tiles, bool count, hipStream_t stream);
+}
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define PT_HIP(call)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (call);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return fail(PT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));               \
+    } while (0)
+
+struct DeviceArray {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    void release() { if (ptr) (void)hipFree(ptr); ptr = nullptr; bytes = 0; }
+};
+
+struct Ctx {
+    int device = 0;
+    int width = 0, height = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // Welford buffer
+    double* d_m = nullptr;
+    double* d_v = nullptr;
+    int32_t* d_n = nullptr;
+    unsigned long long* d_counters = nullptr;
+    int32_t* d_tiles = nullptr;
+    int32_t tiles_cap = 0;
+    // scene
+    bool has_scene = false;
+    std::vector<DeviceArray> scene_arrays;
+    pt::DevScene S{};
+    // stats
+    pt_stats stats{};
+    // RCCL
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+template <class T>
+int upload(Ctx* c, const std::vector<T>& host, const T** out) {
+    *out = nullptr;
+    if (host.empty()) return PT_OK;
+    DeviceArray a;
+    a.bytes = host.size() * sizeof(T);
+    hipError_t e = hipMalloc(&a.ptr, a.bytes);
+    if (e != hipSuccess) return fail(PT_ERR_OUT_OF_MEMORY, std::string("hipMalloc scene: ") + hipGetErrorString(e));
+    c->scene_arrays.push_back(a);
+    PT_HIP(hipMemcpyAsync(a.ptr, host.data(), a.bytes, hipMemcpyHostToDevice, c->stream));
+    *out = (const T*)a.ptr;
+    return PT_OK;
+}
+
+void free_scene(Ctx* c) {
+    for (auto& a : c->scene_arrays) a.release();
+    c->scene_arrays.clear();
+    c->S = pt::DevScene{};
+    c->has_scene = false;
+}
+
+inline float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
+inline float u2f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+inline pt::v3 ld3(const float* p) { return pt::v3{p[0], p[1], p[2]}; }
+
+// Conservative AABB padding for the fp32 slab test (see k_render_pass).
+inline void pad_box(float* lo, float* hi) {
+    for (int k = 0; k < 3; k++) {
+        float m = std::max(std::fabs(lo[k]), std::fabs(hi[k]));
+        float e = m * 2.0e-6f + 1e-30f;
+        lo[k] = lo[k] - e;
+        hi[k] = hi[k] + e;
+    }
+}
+
+// BVH nodes → device float4 pairs with packed child / leaf refs.
+std::vector<float4> pack_nodes(const pt::BvhResult& b) {
+    std::vector<float4> out(b.nodes.size() * 2);
+    for (size_t i = 0; i < b.nodes.size(); i++) {
+        const pt::BvhNode& n = b.nodes[i];
+        uint32_t ref;
+        if (n.b == 0) ref = n.a;  // inner: left child of the pair
+        else ref = 0x80000000u | ((n.b - 1u) << 29) | (n.a & 0x1FFFFFFFu);
+        out[2 * i] = f4(n.bmin[0], n.bmin[1], n.bmin[2], u2f(ref));
+        out[2 * i + 1] = f4(n.bmax[0], n.bmax[1], n.bmax[2], 0.f);
+    }
+    return out;
+}
+
+// Box of a light shape as Box.Center / Box.OuterRadius compute it (Box.cs:316-324).
+void light_sphere_of_box(pt::v3 mn, pt::v3 mx, pt::DevLight& L) {
+    pt::v3 center = pt::add(mn, pt::mul(pt::sub(mx, mn), pt::mk(0.5, 0.5, 0.5)));
+    L.center[0] = center.x; L.center[1] = center.y; L.center[2] = center.z;
+    L.radius = (double)pt::lengthf(pt::sub(mn, center));
+}
+
+int validate_scene(const pt_scene_desc* d) {
+    if (!d) return fail(PT_ERR_INVALID_ARG, "scene is NULL");
+    if (d->num_materials <= 0 || !d->materials) return fail(PT_ERR_INVALID_ARG, "scene has no materials");
+    if (d->num_shapes < 0 || (d->num_shapes > 0 && (!d->shape_kind || !d->shape_index)))
+        return fail(PT_ERR_INVALID_ARG, "shape arrays missing");
+    auto chk_mat = [&](const int32_t* m, int n) {
+        for (int i = 0; i < n; i++) if (m[i] < 0 || m[i] >= d->num_materials) return false;
+        return true;
+    };
+    if (d->num_spheres > 0 && (!d->sphere_center || !d->sphere_radius || !d->sphere_material ||
+                               !chk_mat(d->sphere_material, d->num_spheres)))
+        return fail(PT_ERR_INVALID_ARG, "bad sphere arrays");
+    if (d->num_cubes > 0 && (!d->cube_min || !d->cube_max || !d->cube_material || !chk_mat(d->cube_material, d->num_cubes)))
+        return fail(PT_ERR_INVALID_ARG, "bad cube arrays");
+    if (d->num_planes > 0 && (!d->plane_point || !d->plane_normal || !d->plane_material ||
+                              !chk_mat(d->plane_material, d->num_planes)))
+        return fail(PT_ERR_INVALID_ARG, "bad plane arrays");
+    if (d->num_triangles > 0 && (!d->tri_v1 || !d->tri_v2 || !d->tri_v3 || !d->tri_n1 || !d->tri_n2 || !d->tri_n3 ||
+                                 !d->tri_material || !chk_mat(d->tri_material, d->num_triangles)))
+        return fail(PT_ERR_INVALID_ARG, "bad triangle arrays");
+    if (d->num_meshes > 0 && (!d->mesh_first || !d->mesh_count)) return fail(PT_ERR_INVALID_ARG, "bad mesh arrays");
+    for (int i = 0; i < d->num_shapes; i++) {
+        int k = d->shape_kind[i], j = d->shape_index[i];
+        int lim = k == PT_SHAPE_SPHERE ? d->num_spheres : k == PT_SHAPE_CUBE ? d->num_cubes
+                : k == PT_SHAPE_PLANE ? d->num_planes : k == PT_SHAPE_TRIANGLE ? d->num_triangles
+                : k == PT_SHAPE_MESH ? d->num_meshes : -1;
+        if (lim < 0) return fail(PT_ERR_UNSUPPORTED, "unsupported shape kind " + std::to_string(k));
+        if (j < 0 || j >= lim) return fail(PT_ERR_INVALID_ARG, "shape index out of range at shape " + std::to_string(i));
+        if (k == PT_SHAPE_MESH) {
+            int64_t f = d->mesh_first[j], n = d->mesh_count[j];
+            if (f < 0 || n < 0 || f + n > d->num_triangles) return fail(PT_ERR_INVALID_ARG, "mesh range out of bounds");
+        }
+    }
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pt_get_version(void) { return PT_ABI_VERSION; }
+
+const char* pt_last_error(void) { return g_last_error.c_str(); }
+
+int pt_device_count(int32_t* out_count) {
+    if (!out_count) return fail(PT_ERR_INVALID_ARG, "out_count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *out_count = 0; return fail(PT_ERR_NO_DEVICE, hipGetErrorString(e)); }
+    *out_count = n;
+    return PT_OK;
+}
+
+int pt_create(const pt_device_opts* opts, void** out_ctx) {
+    if (!opts || !out_ctx) return fail(PT_ERR_INVALID_ARG, "NULL argument");
+    *out_ctx = nullptr;
+    if (opts->width <= 1 || opts->height <= 1) return fail(PT_ERR_INVALID_ARG, "width/height must be > 1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PT_ERR_NO_DEVICE, "no HIP device");
+    if (opts->device < 0 || opts->device >= ndev) return fail(PT_ERR_INVALID_ARG, "device ordinal out of range");
+    Ctx* c = new (std::nothrow) Ctx();
+    if (!c) return fail(PT_ERR_OUT_OF_MEMORY, "context allocation");
+    c->device = opts->device;
+    c->width = opts->width;
+    c->height = opts->height;
+    auto cleanup = [&](int code) { pt_destroy(c); return code; };
+    if (hipSetDevice(c->device) != hipSuccess) return cleanup(fail(PT_ERR_HIP, "hipSetDevice"));
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(PT_ERR_HIP, "stream"));
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
+        return cleanup(fail(PT_ERR_HIP, "events"));
+    size_t P = (size_t)c->width * (size_t)c->height;
+    if (hipMalloc(&c->d_m, P * 3 * sizeof(double)) != hipSuccess || hipMalloc(&c->d_v, P * 3 * sizeof(double)) != hipSuccess ||
+        hipMalloc(&c->d_n, P * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess)
+        return cleanup(fail(PT_ERR_OUT_OF_MEMORY, "buffer allocation"));
+    int rc = pt_reset_buffer(c);
+    if (rc != PT_OK) return cleanup(rc);
+    *out_ctx = c;
+    return PT_OK;
+}
+
+int pt_reset_buffer(void* ctx) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c) return fail(PT_ERR_INVALID_ARG, "ctx is NULL");
+    PT_HIP(hipSetDevice(c->device));
+    size_t P = (size_t)c->width * (size_t)c->height;
+    PT_HIP(hipMemsetAsync(c->d_m, 0, P * 3 * sizeof(double), c->stream));
+    PT_HIP(hipMemsetAsync(c->d_v, 0, P * 3 * sizeof(double), c->stream));
+    PT_HIP(hipMemsetAsync(c->d_n, 0, P * sizeof(int32_t), c->stream));
+    PT_HIP(hipStreamSynchronize(c->stream));
+    c->stats.rays_total = 0;
+    c->stats.total_ms = 0;
+    c->stats.passes = 0;
+    return PT_OK;
+}
+
+int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c) return fail(PT_ERR_INVALID_ARG, "ctx is NULL");
+    int rc = validate_scene(d);
+    if (rc != PT_OK) return rc;
+    PT_HIP(hipSetDevice(c->device));
+    auto t0 = std::chrono::steady_clock::now();
+    free_scene(c);
+
+    std::vector<pt::DevMaterial> mats((size_t)d->num_materials);
+    for (int i = 0; i < d->num_materials; i++) {
+        const pt_material& m = d->materials[i];
+        pt::DevMaterial& o = mats[(size_t)i];
+        for (int k = 0; k < 3; k++) o.color[k] = (float)m.color[k];
+        o.emittance = (float)m.emittance;
+        o.tint = (float)m.tint;
+        o.transparent = m.transparent;
+        o.index = m.index;
+        o.gloss = m.gloss;
+        o.reflectivity = m.reflectivity;
+    }
+
+    // --- gather primitives in Scene.Shapes order
+    std::vector<int32_t> ana_kind, ana_scene;     // analytic prims (sphere, cube)
+    std::vector<int32_t> tri_src;                  // source triangle index per BVH triangle
+    std::vector<int32_t> plane_scene;
+    for (int i = 0; i < d->num_shapes; i++) {
+        int k = d->shape_kind[i], j = d->shape_index[i];
+        if (k == PT_SHAPE_SPHERE || k == PT_SHAPE_CUBE) { ana_kind.push_back(k); ana_scene.push_back(j); }
+        else if (k == PT_SHAPE_PLANE) plane_scene.push_back(j);
+        else if (k == PT_SHAPE_TRIANGLE) tri_src.push_back(j);
+        else for (int t = 0; t < d->mesh_count[j]; t++) tri_src.push_back(d->mesh_first[j] + t);
+    }
+    if ((int64_t)tri_src.size() >= (int64_t)(1u << 29) || ana_kind.size() >= (1u << 29))
+        return fail(PT_ERR_UNSUPPORTED, "more than 2^29 primitives");
+
+    // --- triangle BVH
+    const size_t nt = tri_src.size();
+    std::vector<float> bmin(nt * 3), bmax(nt * 3);
+    for (size_t i = 0; i < nt; i++) {
+        int s = tri_src[i];
+        for (int k = 0; k < 3; k++) {
+            float a = d->tri_v1[3 * s + k], b = d->tri_v2[3 * s + k], cc = d->tri_v3[3 * s + k];
+            bmin[3 * i + k] = std::fmin(std::fmin(a, b), cc);
+            bmax[3 * i + k] = std::fmax(std::fmax(a, b), cc);
+        }
+        pad_box(&bmin[3 * i], &bmax[3 * i]);
+    }
+    pt::BvhResult tb;
+    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb);
+    std::vector<float4> tri_recs(nt * 3), tri_shade(nt * 3);
+    for (size_t i = 0; i < nt; i++) {
+        int s = tri_src[tb.order[i]];
+        pt::v3 v1 = ld3(d->tri_v1 + 3 * s), v2 = ld3(d->tri_v2 + 3 * s), v3_ = ld3(d->tri_v3 + 3 * s);
+        pt::v3 e1 = pt::sub(v2, v1), e2 = pt::sub(v3_, v1);  // Triangle.cs:97-98
+        tri_recs[3 * i + 0] = f4(v1.x, v1.y, v1.z, e1.x);
+        tri_recs[3 * i + 1] = f4(e1.y, e1.z, e2.x, e2.y);
+        tri_recs[3 * i + 2] = f4(e2.z, 0.f, 0.f, 0.f);
+        const float* n1 = d->tri_n1 + 3 * s; const float* n2 = d->tri_n2 + 3 * s; const float* n3 = d->tri_n3 + 3 * s;
+        tri_shade[3 * i + 0] = f4(n1[0], n1[1], n1[2], n2[0]);
+        tri_shade[3 * i + 1] = f4(n2[1], n2[2], n3[0], n3[1]);
+        tri_shade[3 * i + 2] = f4(n3[2], u2f((uint32_t)d->tri_material[s]), 0.f, 0.f);
+    }
+    std::vector<float4> tri_nodes = pack_nodes(tb);
+
+    // --- analytic BVH (spheres, cubes)
+    const size_t na = ana_kind.size();
+    std::vector<float> amin(na * 3), amax(na * 3);
+    for (size_t i = 0; i < na; i++) {
+        int j = ana_scene[i];
+        if (ana_kind[i] == PT_SHAPE_SPHERE) {
+            double r = d->sphere_radius[j];
+            for (int k = 0; k < 3; k++) {
+                double cc = d->sphere_center[3 * j + k];
+                amin[3 * i + k] = std::nextafter((float)(cc - r), -INFINITY);
+                amax[3 * i + k] = std::nextafter((float)(cc + r), INFINITY);
+            }
+        } else {
+            for (int k = 0; k < 3; k++) { amin[3 * i + k] = d->cube_min[3 * j + k]; amax[3 * i + k] = d->cube_max[3 * j + k]; }
+        }
+        pad_box(&amin[3 * i], &amax[3 * i]);
+    }
+    pt::BvhResult ab;
+    pt::build_bvh(amin.data(), amax.data(), (int64_t)na, 0, ab);
+    std::vector<float4> ana_recs(na * 3);
+    std::vector<int32_t> ana_pos_of_scene_sphere(d->num_spheres > 0 ? d->num_spheres : 0, -1);
+    std::vector<int32_t> ana_pos_of_scene_cube(d->num_cubes > 0 ? d->num_cubes : 0, -1);
+    for (size_t i = 0; i < na; i++) {
+        size_t src = ab.order[i];
+        int j = ana_scene[src];
+        if (ana_kind[src] == PT_SHAPE_SPHERE) {
+            const float* cc = d->sphere_center + 3 * j;
+            uint64_t rb; double r = d->sphere_radius[j]; std::memcpy(&rb, &r, 8);
+            ana_recs[3 * i + 0] = f4(cc[0], cc[1], cc[2], u2f(pt::KIND_SPHERE));
+            ana_recs[3 * i + 1] = f4(0.f, 0.f, 0.f, u2f((uint32_t)j));
+            ana_recs[3 * i + 2] = f4(u2f((uint32_t)d->sphere_material[j]), u2f((uint32_t)(rb & 0xFFFFFFFFu)),
+                                     u2f((uint32_t)(rb >> 32)), 0.f);
+            if (ana_pos_of_scene_sphere[(size_t)j] < 0) ana_pos_of_scene_sphere[(size_t)j] = (int32_t)i;
+        } else {
+            const float* mn = d->cube_min + 3 * j; const float* mx = d->cube_max + 3 * j;
+            ana_recs[3 * i + 0] = f4(mn[0], mn[1], mn[2], u2f(pt::KIND_CUBE));
+            ana_recs[3 * i + 1] = f4(mx[0], mx[1], mx[2], u2f((uint32_t)j));
+            ana_recs[3 * i + 2] = f4(u2f((uint32_t)d->cube_material[j]), 0.f, 0.f, 0.f);
+            if (ana_pos_of_scene_cube[(size_t)j] < 0) ana_pos_of_scene_cube[(size_t)j] = (int32_t)i;
+        }
+    }
+    std::vector<float4> ana_nodes = pack_nodes(ab);
+
+    // --- planes
+    std::vector<float4> planes(plane_scene.size() * 2);
+    std::vector<int32_t> plane_pos_of_scene(d->num_planes > 0 ? d->num_planes : 0, -1);
+    for (size_t i = 0; i < plane_scene.size(); i++) {
+        int j = plane_scene[i];
+        const float* p = d->plane_point + 3 * j; const float* n = d->plane_normal + 3 * j;
+        planes[2 * i] = f4(p[0], p[1], p[2], u2f((uint32_t)d->plane_material[j]));
+        planes[2 * i + 1] = f4(n[0], n[1], n[2], u2f((uint32_t)j));
+        if (plane_pos_of_scene[(size_t)j] < 0) plane_pos_of_scene[(size_t)j] = (int32_t)i;
+    }
+
+    // --- lights, Scene.Add order (Scene.cs:29-38)
+    std::vector<pt::DevLight> lights;
+    for (int i = 0; i < d->num_shapes; i++) {
+        int k = d->shape_kind[i], j = d->shape_index[i];
+        int mat = k == PT_SHAPE_SPHERE ? d->sphere_material[j] : k == PT_SHAPE_CUBE ? d->cube_material[j]
+                : k == PT_SHAPE_PLANE ? d->plane_material[j] : k == PT_SHAPE_TRIANGLE ? d->tri_material[j] : -1;
+        if (mat < 0 || !(d->materials[mat].emittance > 0)) continue;  // Mesh.MaterialAt is `default` → never a light
+        pt::DevLight L{};
+        L.kind = k; L.mat = mat; L.phantom = 0;
+        if (k == PT_SHAPE_SPHERE) {
+            L.index = ana_pos_of_scene_sphere[(size_t)j];
+            const float* cc = d->sphere_center + 3 * j;
+            L.center[0] = cc[0]; L.center[1] = cc[1]; L.center[2] = cc[2];
+            L.radius = d->sphere_radius[j];
+        } else if (k == PT_SHAPE_CUBE) {
+            L.index = ana_pos_of_scene_cube[(size_t)j];
+            light_sphere_of_box(ld3(d->cube_min + 3 * j), ld3(d->cube_max + 3 * j), L);
+        } else if (k == PT_SHAPE_PLANE) {
+            L.index = plane_pos_of_scene[(size_t)j];
+            light_sphere_of_box(pt::mk(-1e9, -1e9, -1e9), pt::mk(1e9, 1e9, 1e9), L);  // Plane.BoundingBox
+        } else {  // a directly-added struct Triangle: counted as a light, never passes the identity test
+            L.index = -1; L.phantom = 1;
+            pt::v3 a = ld3(d->tri_v1 + 3 * j), b = ld3(d->tri_v2 + 3 * j), cc = ld3(d->tri_v3 + 3 * j);
+            light_sphere_of_box(pt::vmin(pt::vmin(a, b), cc), pt::vmax(pt::vmax(a, b), cc), L);
+        }
+        lights.push_back(L);
+    }
+
+    pt::DevScene S{};
+    rc = upload(c, tri_nodes, &S.tri_nodes); if (rc) return rc;
+    rc = upload(c, tri_recs, &S.tri_recs); if (rc) return rc;
+    rc = upload(c, tri_shade, &S.tri_shade); if (rc) return rc;
+    rc = upload(c, ana_nodes, &S.ana_nodes); if (rc) return rc;
+    rc = upload(c, ana_recs, &S.ana_recs); if (rc) return rc;
+    rc = upload(c, planes, &S.planes); if (rc) return rc;
+    rc = upload(c, mats, &S.mats); if (rc) return rc;
+    rc = upload(c, lights, &S.lights); if (rc) return rc;
+    S.tri_num_nodes = (int32_t)tb.nodes.size();
+    S.ana_num_nodes = (int32_t)ab.nodes.size();
+    S.num_planes = (int32_t)plane_scene.size();
+    S.num_lights = (int32_t)lights.size();
+    for (int k = 0; k < 3; k++) S.env[k] = (float)d->env_color[k];
+    PT_HIP(hipStreamSynchronize(c->stream));
+    c->S = S;
+    c->has_scene = true;
+    c->stats.bvh_nodes = tb.nodes.size() + ab.nodes.size();
+    c->stats.bvh_bytes = (tri_nodes.size() + ana_nodes.size()) * sizeof(float4) +
+                         (tri_recs.size() + tri_shade.size() + ana_recs.size()) * sizeof(float4);
+    c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return PT_OK;
+}
+
+static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* sampler, const pt_pass_params* pass,
+                            pt_trace_counters* counted) {
+    if (!c || !camera || !sampler || !pass) return fail(PT_ERR_INVALID_ARG, "NULL argument");
+    if (!c->has_scene) return fail(PT_ERR_NO_SCENE, "pt_render_pass before pt_upload_scene");
+    if (pass->spp <= 0) return fail(PT_ERR_INVALID_ARG, "spp must be >= 1");
+    if (sampler->first_hit_samples <= 0 || sampler->max_bounces < 0) return fail(PT_ERR_INVALID_ARG, "bad sampler");
+    if (sampler->specular_mode == PT_SPEC_ALL && sampler->max_bounces > 32)
+        return fail(PT_ERR_UNSUPPORTED, "SpecularModeAll with MaxBounces > 32");
+    if (sampler->light_mode < 0 || sampler->light_mode > 1 || sampler->specular_mode < 0 || sampler->specular_mode > 2)
+        return fail(PT_ERR_INVALID_ARG, "bad light/specular mode");
+    PT_HIP(hipSetDevice(c->device));
+    const int tiles_x = (c->width + 31) / 32, tiles_y = (c->height + 31) / 32;
+    int num_tiles = tiles_x * tiles_y;
+    const int32_t* d_tiles = nullptr;
+    if (pass->num_tiles > 0) {
+        if (!pass->tiles) return fail(PT_ERR_INVALID_ARG, "tiles is NULL");
+        for (int i = 0; i < pass->num_tiles; i++)
+            if (pass->tiles[i] < 0 || pass->tiles[i] >= tiles_x * tiles_y) return fail(PT_ERR_INVALID_ARG, "tile id out of range");
+        if (pass->num_tiles > c->tiles_cap) {
+            if (c->d_tiles) (void)hipFree(c->d_tiles);
+            c->d_tiles = nullptr;
+            PT_HIP(hipMalloc(&c->d_tiles, (size_t)pass->num_tiles * sizeof(int32_t)));
+            c->tiles_cap = pass->num_tiles;
+        }
+        PT_HIP(hipMemcpyAsync(c->d_tiles, pass->tiles, (size_t)pass->num_tiles * sizeof(int32_t), hipMemcpyHostToDevice,
+                              c->stream));
+        d_tiles = c->d_tiles;
+        num_tiles = pass->num_tiles;
+    }
+    pt::DevCamera cam;
+    std::memcpy(cam.p, camera->p, sizeof cam.p); std::memcpy(cam.u, camera->u, sizeof cam.u);
+    std::memcpy(cam.v, camera->v, sizeof cam.v); std::memcpy(cam.w, camera->w, sizeof cam.w);
+    cam.m = camera->m; cam.focal_distance = camera->focal_distance; cam.aperture_radius = camera->aperture_radius;
+    pt::DevSampler smp{sampler->first_hit_samples, sampler->max_bounces, sampler->direct_lighting, sampler->soft_shadows,
+                       sampler->light_mode, sampler->specular_mode};
+    pt::DevPass P{c->width, c->height, pass->spp, pass->stratified, pass->seed, pass->pass_index, tiles_x, d_tiles,
+                  num_tiles};
+    pt::DevBuffer B{c->d_m, c->d_v, c->d_n, c->d_counters};
+    PT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    PT_HIP(hipEventRecord(c->ev0, c->stream));
+    PT_HIP(pt::launch_render_pass(c->S, cam, smp, P, B, num_tiles, counted != nullptr, c->stream));
+    PT_HIP(hipEventRecord(c->ev1, c->stream));
+    unsigned long long ctr[8];
+    PT_HIP(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
+    PT_HIP(hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    PT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->stats.rays = ctr[0];
+    c->stats.rays_total += ctr[0];
+    c->stats.last_pass_ms = ms;
+    c->stats.total_ms += ms;
+    c->stats.passes++;
+    if (counted) {
+        counted->rays = ctr[0];
+        counted->nodes_visited = ctr[1];
+        counted->prims_tested = ctr[2];
+        counted->shading_fetches = ctr[3];
+    }
+    return PT_OK;
+}
+
+int pt_render_pass(void* ctx, const pt_camera* camera, const pt_sampler* sampler, const pt_pass_params* pass) {
+    return render_pass_impl((Ctx*)ctx, camera, sampler, pass, nullptr);
+}
+
+int pt_render_pass_counted(void* ctx, const pt_camera* camera, const pt_sampler* sampler, const pt_pass_params* pass,
+                           pt_trace_counters* out) {
+    if (!out) return fail(PT_ERR_INVALID_ARG, "out is NULL");
+    return render_pass_impl((Ctx*)ctx, camera, sampler, pass, out);
+}
+
+int pt_synchronize(void* ctx) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c) return fail(PT_ERR_INVALID_ARG, "ctx is NULL");
+    PT_HIP(hipSetDevice(c->device));
+    PT_HIP(hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_read_buffer(void* ctx, double* out_m, double* out_v, int32_t* out_n) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c) return fail(PT_ERR_INVALID_ARG, "ctx is NULL");
+    PT_HIP(hipSetDevice(c->device));
+    size_t P = (size_t)c->width * (size_t)c->height;
+    if (out_m) PT_HIP(hipMemcpyAsync(out_m, c->d_m, P * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (out_v) PT_HIP(hipMemcpyAsync(out_v, c->d_v, P * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (out_n) PT_HIP(hipMemcpyAsync(out_n, c->d_n, P * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    PT_HIP(hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_stats_get(void* ctx, pt_stats* out) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c || !out) return fail(PT_ERR_INVALID_ARG, "NULL argument");
+    *out = c->stats;
+    return PT_OK;
+}
+
+void pt_destroy(void* ctx) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    free_scene(c);
+    if (c->d_m) (void)hipFree(c->d_m);
+    if (c->d_v) (void)hipFree(c->d_v);
+    if (c->d_n) (void)hipFree(c->d_n);
+    if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->d_tiles) (void)hipFree(c->d_tiles);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// ------------------------------------------------------------------ RCCL
+int pt_comm_unique_id(uint8_t out_id[128]) {
+    if (!out_id) return fail(PT_ERR_INVALID_ARG, "out_id is NULL");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(PT_ERR_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(out_id, &id, 128);
+    return PT_OK;
+}
+
+int pt_comm_init(void* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(PT_ERR_INVALID_ARG, "bad comm arguments");
+    PT_HIP(hipSetDevice(c->device));
+    if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+    if (r != ncclSuccess) return fail(PT_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    c->nranks = nranks;
+    c->rank = rank;
+    return PT_OK;
+}
+
+// Every rank rendered a disjoint tile set into a zero-initialised full-frame
+// buffer, so a sum-reduce onto `root` is the gather.
+int pt_comm_gather(void* ctx, int32_t root) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c) return fail(PT_ERR_INVALID_ARG, "ctx is NULL");
+    if (!c->comm) return fail(PT_ERR_RCCL, "pt_comm_init not called");
+    if (root < 0 || root >= c->nranks) return fail(PT_ERR_INVALID_ARG, "root out of range");
+    PT_HIP(hipSetDevice(c->device));
+    size_t P = (size_t)c->width * (size_t)c->height;
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) r = ncclReduce(c->d_m, c->d_m, P * 3, ncclFloat64, ncclSum, root, c->comm, c->stream);
+    if (r == ncclSuccess) r = ncclReduce(c->d_v, c->d_v, P * 3, ncclFloat64, ncclSum, root, c->comm, c->stream);
+    if (r == ncclSuccess) r = ncclReduce(c->d_n, c->d_n, P, ncclInt32, ncclSum, root, c->comm, c->stream);
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return fail(PT_ERR_RCCL, std::string("ncclReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    PT_HIP(hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_comm_destroy(void* ctx) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c) return fail(PT_ERR_INVALID_ARG, "ctx is NULL");
+    if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    c->nranks = 1; c->rank = 0;
+    return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,209 @@
+// pt_math.h — numeric core of the render path, shared by the gfx950 kernels and
+// the host-side scene preparation.
+//
+// PTSharp's Vector keeps a System.Numerics.Vector3 (fp32) behind double
+// accessors (PTSharpCore/Vector.cs:201-234): Add/Sub/Mul/Div round to fp32 after
+// every operation, MulScalar(double) is float(double(x)*s) (Vector.cs:435), and
+// Dot/Cross/Length/Normalize are fp32 Vector3 operations (Vector.cs:356-393).
+// Scalars that the reference keeps in double (ray t, det, Fresnel terms, trig)
+// stay double here so hit positions and branch decisions reproduce the same
+// rounding sequence.  Everything is compiled with -ffp-contract=off.
+#pragma once
+#include <stdint.h>
+#include <math.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define PT_HD __host__ __device__ __forceinline__
+#else
+#define PT_HD inline
+#endif
+
+#pragma clang fp contract(off)
+
+namespace pt {
+
+constexpr double kEps = 1e-9;                 // Util.EPS (Util.cs:11)
+constexpr double kHitInf = 1000000000.0;      // Hit.INF = 1e9F (Hit.cs:6)
+constexpr double kPi = 3.14159265358979323846;
+
+struct v3 { float x, y, z; };
+
+PT_HD v3 mk(double x, double y, double z) { return v3{(float)x, (float)y, (float)z}; }
+PT_HD v3 add(v3 a, v3 b) { return v3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+PT_HD v3 sub(v3 a, v3 b) { return v3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+PT_HD v3 mul(v3 a, v3 b) { return v3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+PT_HD v3 divv(v3 a, v3 b) { return v3{a.x / b.x, a.y / b.y, a.z / b.z}; }
+PT_HD v3 muls(v3 a, double s) {
+    return v3{(float)((double)a.x * s), (float)((double)a.y * s), (float)((double)a.z * s)};
+}
+PT_HD float dotf(v3 a, v3 b) {
+    float xx = a.x * b.x;
+    float yy = a.y * b.y;
+    float zz = a.z * b.z;
+    float s = xx + yy;
+    return s + zz;
+}
+PT_HD double dot(v3 a, v3 b) { return (double)dotf(a, b); }
+PT_HD v3 cross(v3 a, v3 b) {
+    float x1 = a.y * b.z, x2 = a.z * b.y;
+    float y1 = a.z * b.x, y2 = a.x * b.z;
+    float z1 = a.x * b.y, z2 = a.y * b.x;
+    return v3{x1 - x2, y1 - y2, z1 - z2};
+}
+PT_HD float lengthf(v3 a) { return sqrtf(dotf(a, a)); }
+PT_HD v3 normalize(v3 a) {
+    float l = lengthf(a);
+    return v3{a.x / l, a.y / l, a.z / l};
+}
+PT_HD v3 neg(v3 a) { return v3{-a.x, -a.y, -a.z}; }
+PT_HD v3 zero3() { return v3{0.f, 0.f, 0.f}; }
+
+// .NET Math.Max / Math.Min on double (NaN-propagating, -0 < +0).
+PT_HD double net_max(double a, double b) {
+    if (a != b) { if (!(a != a)) return b < a ? a : b; return a; }
+    return signbit(b) ? a : b;
+}
+PT_HD double net_min(double a, double b) {
+    if (a != b) { if (!(a != a)) return a < b ? a : b; return a; }
+    return signbit(a) ? a : b;
+}
+PT_HD v3 vmin(v3 a, v3 b) { return mk(net_min(a.x, b.x), net_min(a.y, b.y), net_min(a.z, b.z)); }
+PT_HD v3 vmax(v3 a, v3 b) { return mk(net_max(a.x, b.x), net_max(a.y, b.y), net_max(a.z, b.z)); }
+
+// ------------------------------------------------------------------ RNG
+// Counter-based replacement for Random.Shared.  A draw is a
+// pure function of (key, dim), so the GPU's iterative path order and the
+// recursive CPU order consume identical numbers.
+PT_HD uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27; x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+PT_HD uint64_t camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {
+    uint64_t k = mix64(seed + 0x243F6A8885A308D3ull);
+    k = mix64(k ^ ((uint64_t)pass + 0x13198A2E03707344ull));
+    k = mix64(k ^ (pixel + 0xA4093822299F31D0ull));
+    return mix64(k ^ ((uint64_t)sample + 0x082EFA98EC4E6C89ull));
+}
+PT_HD uint64_t child_key(uint64_t k, uint32_t c) { return mix64(k ^ ((uint64_t)c + 0x452821E638D01377ull)); }
+PT_HD uint64_t light_key(uint64_t k, uint32_t i) { return mix64(k ^ ((uint64_t)i + 0xBE5466CF34E90C6Cull)); }
+PT_HD double draw(uint64_t k, uint32_t dim) {
+    return (double)(mix64(k + (uint64_t)(dim + 1) * 0x9E3779B97F4A7C15ull) >> 11) * (1.0 / 9007199254740992.0);
+}
+enum : uint32_t { D_STRATUM_U = 0, D_STRATUM_V = 1, D_REFLECT = 2, D_RUV_Z = 3, D_RUV_A = 4,
+                  D_LIGHT = 5, D_SS_RUV_Z = 6, D_SS_RUV_A = 7, D_SS_XY = 8 };
+enum : uint32_t { D_JX = 0, D_JY = 1, D_LENS_ANGLE = 2, D_LENS_RADIUS = 3 };
+
+// Vector.RandomUnitVector (Vector.cs:339-347)
+PT_HD v3 random_unit_vector(uint64_t key, uint32_t dz, uint32_t da) {
+    double z = draw(key, dz) * 2.0 - 1.0;
+    double a = draw(key, da) * 2.0 * kPi;
+    double r = sqrt(1.0 - z * z);
+    double x = sin(a);
+    double y = cos(a);
+    return mk(r * x, r * y, z);
+}
+// Vector.Reflect / Refract / Reflectance with `this` = the surface normal (Vector.cs:497-536)
+PT_HD v3 reflect(v3 n, v3 i) { return sub(i, muls(n, 2 * dot(n, i))); }
+PT_HD v3 refract(v3 n, v3 i, double n1, double n2) {
+    double nr = n1 / n2;
+    double cosI = -dot(n, i);
+    double sinT2 = nr * nr * (1 - cosI * cosI);
+    if (sinT2 > 1) return zero3();
+    double cosT = sqrt(1 - sinT2);
+    return add(muls(i, nr), muls(n, nr * cosI - cosT));
+}
+PT_HD double reflectance(v3 n, v3 i, double n1, double n2) {
+    double nr2 = (n1 * n1) / (n2 * n2);
+    double cosI = -dot(n, i);
+    double sinT2 = nr2 * (1 - cosI * cosI);
+    if (sinT2 > 1) return 1;
+    double cosT = sqrt(1 - sinT2);
+    double cosI_n1 = n1 * cosI;
+    double cosT_n2 = n2 * cosT;
+    double rOrth = (cosI_n1 - cosT_n2) / (cosI_n1 + cosT_n2);
+    double rPar = (cosT_n2 - cosI_n1) / (cosT_n2 + cosI_n1);
+    return (rOrth * rOrth + rPar * rPar) / 2;
+}
+
+// ------------------------------------------------------------------ primitives
+// Sphere.Intersect (Sphere.cs:40-60)
+PT_HD double isect_sphere(v3 center, double radius, v3 o, v3 d) {
+    v3 to = sub(o, center);
+    double b = dot(to, d);
+    double c = dot(to, to) - radius * radius;
+    double disc = b * b - c;
+    if (disc > 0) {
+        disc = sqrt(disc);
+        double t1 = -b - disc;
+        if (t1 > kEps) return t1;
+        double t2 = -b + disc;
+        if (t2 > kEps) return t2;
+    }
+    return kHitInf;
+}
+// Cube.Intersect (Cube.cs:35-47): entry face only.
+PT_HD double isect_cube(v3 mn, v3 mx, v3 o, v3 d) {
+    v3 n = divv(sub(mn, o), d);
+    v3 f = divv(sub(mx, o), d);
+    v3 n2 = vmin(n, f), f2 = vmax(n, f);
+    double t0 = net_max(net_max(n2.x, n2.y), n2.z);
+    double t1 = net_min(net_min(f2.x, f2.y), f2.z);
+    if (t0 > 0 && t0 < t1) return t0;
+    return kHitInf;
+}
+// Plane.Intersect (Plane.cs:36-50)
+PT_HD double isect_plane(v3 point, v3 normal, v3 o, v3 d) {
+    double dd = dot(normal, d);
+    if (fabs(dd) < kEps) return kHitInf;
+    v3 a = sub(point, o);
+    double t = dot(a, normal) / dd;
+    if (t < kEps) return kHitInf;
+    return t;
+}
+// Triangle.Intersect, Möller–Trumbore (Triangle.cs:95-124) on precomputed
+// e1 = V2-V1, e2 = V3-V1 (bit-identical to the per-call Sub in the reference).
+PT_HD double isect_tri(v3 v1, v3 e1, v3 e2, v3 o, v3 d) {
+    v3 h = cross(d, e2);
+    double det = dot(e1, h);
+    if (det > -kEps && det < kEps) return kHitInf;
+    double invDet = 1.0 / det;
+    v3 s = sub(o, v1);
+    double u = dot(s, h) * invDet;
+    if (u < 0 || u > 1) return kHitInf;
+    v3 q = cross(s, e1);
+    double v = dot(d, q) * invDet;
+    if (v < 0 || (u + v) > 1) return kHitInf;
+    double t = dot(e2, q) * invDet;
+    if (t < kEps) return kHitInf;
+    return t;
+}
+// Cube.NormalAt (Cube.cs:57-69) with the |p - face| < EPS quirk.
+PT_HD v3 cube_normal(v3 mn, v3 mx, v3 p) {
+    if (fabs((double)p.x - (double)mn.x) < kEps) return mk(-1, 0, 0);
+    if (fabs((double)p.x - (double)mx.x) < kEps) return mk(1, 0, 0);
+    if (fabs((double)p.y - (double)mn.y) < kEps) return mk(0, -1, 0);
+    if (fabs((double)p.y - (double)mx.y) < kEps) return mk(0, 1, 0);
+    if (fabs((double)p.z - (double)mn.z) < kEps) return mk(0, 0, -1);
+    if (fabs((double)p.z - (double)mx.z) < kEps) return mk(0, 0, 1);
+    return mk(0, 1, 0);
+}
+// Triangle.NormalAt via Barycentric (Triangle.cs:142-189, 208-223).
+PT_HD v3 tri_normal(v3 v1, v3 e1, v3 e2, v3 n1, v3 n2, v3 n3, v3 p) {
+    v3 w2 = sub(p, v1);
+    double d00 = dot(e1, e1);
+    double d01 = dot(e1, e2);
+    double d11 = dot(e2, e2);
+    double d20 = dot(w2, e1);
+    double d21 = dot(w2, e2);
+    double den = d00 * d11 - d01 * d01;
+    double bv = (d11 * d20 - d01 * d21) / den;
+    double bw = (d00 * d21 - d01 * d20) / den;
+    double bu = 1 - bv - bw;
+    v3 n = add(add(muls(n1, bu), muls(n2, bv)), muls(n3, bw));
+    return normalize(n);
+}
+
+}  // namespace pt

@@ -1,0 +1,84 @@
+// pt_scene.h — device-resident scene layout (HBM) shared by the host runtime
+// and the gfx950 kernels.
+//
+// Hot / cold split: traversal touches only node pairs (64 B) and primitive
+// records (48 B, three 16-B loads from one line); shading data (normals,
+// material id: 48 B) is fetched once per closest hit.  Everything is laid out as
+// arrays of float4 so every lane issues dwordx4 loads.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+namespace pt {
+
+enum PrimKind : int32_t { KIND_SPHERE = 0, KIND_CUBE = 1, KIND_PLANE = 2, KIND_TRI = 3, KIND_MESH = 4 };
+
+// Material (Material.cs:8-62); colour terms in fp32 (they never feed a branch),
+// the terms that feed Fresnel / cone / branch decisions stay fp64.
+struct DevMaterial {
+    float color[3];
+    float emittance;
+    float tint;
+    int32_t transparent;
+    double index;
+    double gloss;
+    double reflectivity;
+};
+
+// Scene.Lights entry (Scene.cs:33-37) with the centre/radius sampleLight derives
+// (Sampler.cs:218-234), precomputed on the host with the same fp32 ops.
+struct DevLight {
+    int32_t kind;        // KIND_SPHERE / KIND_CUBE / KIND_PLANE / KIND_TRI
+    int32_t index;       // scene index of that kind (identity test, Sampler.cs:264)
+    int32_t mat;
+    int32_t phantom;     // struct Triangle light: identity never matches (boxing)
+    float center[3];
+    float _pad;
+    double radius;
+};
+
+struct DevScene {
+    // triangle BVH (world-space mesh + directly-added triangles)
+    const float4* tri_nodes;   // 2 float4 per node (pt::BvhNode)
+    int32_t tri_num_nodes;
+    const float4* tri_recs;    // 3 float4 per triangle: {v1.xyz,e1.x} {e1.yz,e2.xy} {e2.z,-,-,-}
+    const float4* tri_shade;   // 3 float4 per triangle: {n1.xyz,n2.x} {n2.yz,n3.xy} {n3.z,mat,-,-}
+    // analytic BVH (spheres, cubes)
+    const float4* ana_nodes;
+    int32_t ana_num_nodes;
+    const float4* ana_recs;    // 3 float4: {a.xyz,kind} {b.xyz,scene index} {mat, radius(double), -}
+    // planes (unbounded: tested outside the BVHs)
+    const float4* planes;      // 2 float4: {point.xyz, mat} {normal.xyz, scene index}
+    int32_t num_planes;
+    const DevMaterial* mats;
+    const DevLight* lights;
+    int32_t num_lights;
+    float env[3];
+};
+
+struct DevCamera {
+    float p[3], u[3], v[3], w[3];
+    double m, focal_distance, aperture_radius;
+};
+
+struct DevSampler {
+    int32_t fh, mb, dl, ss, light_mode, spec_mode;
+};
+
+struct DevPass {
+    int32_t width, height, spp, stratified;
+    uint64_t seed;
+    uint32_t pass_index;
+    int32_t tiles_x;           // ceil(W/32)
+    const int32_t* tiles;      // nullptr: tile = blockIdx.x / 4
+    int32_t num_tiles;
+};
+
+struct DevBuffer {
+    double* m;                 // [P][3] Welford mean   (Pixel.M, Buffer.cs:21)
+    double* v;                 // [P][3] Welford M2     (Pixel.V, Buffer.cs:22)
+    int32_t* n;                // [P]    sample count   (Pixel.Samples)
+    unsigned long long* counters;  // [0] rays, [1] nodes, [2] prims, [3] shading fetches
+};
+
+}  // namespace pt

@@ -1,0 +1,443 @@
+"""Host-side mirror of PTSharp's plugin surface for the render path: Material,
+the IShape kinds the GPU path covers (Sphere, Cube, Plane, Triangle, Mesh),
+Scene, Camera and DefaultSampler (PTSharpCore/Material.cs, Sphere.cs, Cube.cs,
+Plane.cs, Triangle.cs, Mesh.cs, Scene.cs, Camera.cs, Sampler.cs).
+
+`Scene.flatten()` produces the caller-owned arrays of pt_scene_desc
+(include/ptsharp_hip.h) — the same flattening the C# HipRenderer performs with
+a type switch over Scene.Shapes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field, replace
+from enum import IntEnum
+
+import numpy as np
+
+from . import _abi
+from .geometry import Box, Colour, Matrix, Vector, cross_rows, dot_rows, normalize_rows
+
+
+class LightMode(IntEnum):          # LightMode.cs
+    LightModeRandom = 0
+    LightModeAll = 1
+
+
+class SpecularMode(IntEnum):       # SpecularMode.cs
+    SpecularModeNaive = 0
+    SpecularModeFirst = 1
+    SpecularModeAll = 2
+
+
+@dataclass(frozen=True)
+class Material:
+    """PTSharpCore.Material (Material.cs:8-62); texture maps are not on the GPU path."""
+    Color: Colour = field(default_factory=lambda: Colour(0, 0, 0))
+    BumpMultiplier: float = 0.0
+    Emittance: float = 0.0
+    Index: float = 0.0
+    Gloss: float = 0.0
+    Tint: float = 0.0
+    Reflectivity: float = 0.0
+    Transparent: bool = False
+    Texture: object = None
+
+    def key(self):
+        return (self.Color.r, self.Color.g, self.Color.b, self.Emittance, self.Index, self.Gloss, self.Tint,
+                self.Reflectivity, bool(self.Transparent))
+
+    # factories (Material.cs:64-97)
+    @staticmethod
+    def DiffuseMaterial(color: Colour) -> "Material":
+        return Material(color, 1, 0, 1, 0, 0, -1, False)
+
+    @staticmethod
+    def SpecularMaterial(color: Colour, index: float) -> "Material":
+        return Material(color, 1, 0, index, 0, 0, -1, False)
+
+    @staticmethod
+    def GlossyMaterial(color: Colour, index: float, gloss: float) -> "Material":
+        return Material(color, 1, 0, index, gloss, 0, -1, False)
+
+    @staticmethod
+    def ClearMaterial(index: float, gloss: float) -> "Material":
+        return Material(Colour(0, 0, 0), 1, 0, index, gloss, 0, -1, True)
+
+    @staticmethod
+    def TransparentMaterial(color: Colour, index: float, gloss: float, tint: float) -> "Material":
+        return Material(color, 1, 0, index, gloss, tint, -1, True)
+
+    @staticmethod
+    def MetallicMaterial(color: Colour, gloss: float, tint: float) -> "Material":
+        return Material(color, 1, 0, 1, gloss, tint, 1, False)
+
+    @staticmethod
+    def LightMaterial(color: Colour, emittance: float) -> "Material":
+        return Material(color, 1, emittance, 1, 0, 0, -1, False)
+
+    def with_(self, **kw) -> "Material":
+        return replace(self, **kw)
+
+
+DEFAULT_MATERIAL = Material()  # `new Material()` / `default` (Mesh.MaterialAt, Mesh.cs:132-135)
+
+
+class Sphere:
+    """PTSharpCore.Sphere (Sphere.cs)."""
+
+    def __init__(self, center: Vector, radius: float, material: Material):
+        self.Center, self.Radius, self.Material = center, float(radius), material
+
+    @staticmethod
+    def NewSphere(center: Vector, radius: float, material: Material) -> "Sphere":
+        return Sphere(center, radius, material)
+
+    def BoundingBox(self) -> Box:
+        c, r = self.Center, self.Radius
+        return Box(Vector(c.X - r, c.Y - r, c.Z - r), Vector(c.X + r, c.Y + r, c.Z + r))
+
+    def MaterialAt(self, p=None) -> Material:
+        return self.Material
+
+
+class Cube:
+    """PTSharpCore.Cube (Cube.cs)."""
+
+    def __init__(self, mn: Vector, mx: Vector, material: Material):
+        self.Min, self.Max, self.Material = mn, mx, material
+
+    @staticmethod
+    def NewCube(mn: Vector, mx: Vector, material: Material) -> "Cube":
+        return Cube(mn, mx, material)
+
+    def BoundingBox(self) -> Box:
+        return Box(self.Min, self.Max)
+
+    def MaterialAt(self, p=None) -> Material:
+        return self.Material
+
+
+class Plane:
+    """PTSharpCore.Plane (Plane.cs); NewPlane normalises the normal."""
+
+    def __init__(self, point: Vector, normal: Vector, material: Material):
+        self.Point, self.Normal, self.Material = point, normal, material
+
+    @staticmethod
+    def NewPlane(point: Vector, normal: Vector, material: Material) -> "Plane":
+        return Plane(point, normal.Normalize(), material)
+
+    def BoundingBox(self) -> Box:
+        return Box(Vector(-1e9, -1e9, -1e9), Vector(1e9, 1e9, 1e9))
+
+    def MaterialAt(self, p=None) -> Material:
+        return self.Material
+
+
+class Triangle:
+    """PTSharpCore.Triangle (Triangle.cs), a struct: added to a Scene directly it
+    is boxed, so as a light it never passes Sampler's identity test."""
+
+    def __init__(self, v1: Vector, v2: Vector, v3: Vector, n1: Vector = None, n2: Vector = None, n3: Vector = None,
+                 material: Material = DEFAULT_MATERIAL):
+        self.V1, self.V2, self.V3 = v1, v2, v3
+        self.N1 = n1 if n1 is not None else Vector()
+        self.N2 = n2 if n2 is not None else Vector()
+        self.N3 = n3 if n3 is not None else Vector()
+        self.Material = material
+
+    @staticmethod
+    def NewTriangle(v1, v2, v3, t1=None, t2=None, t3=None, material: Material = DEFAULT_MATERIAL) -> "Triangle":
+        t = Triangle(v1, v2, v3, material=material)
+        t.FixNormals()
+        return t
+
+    def Normal(self) -> Vector:
+        e1 = self.V2.Sub(self.V1)
+        e2 = self.V3.Sub(self.V1)
+        return e1.Cross(e2).Normalize()
+
+    def FixNormals(self) -> None:  # Triangle.cs:224-237
+        n = self.Normal()
+        z = Vector()
+        if self.N1 == z:
+            self.N1 = n
+        if self.N2 == z:
+            self.N2 = n
+        if self.N3 == z:
+            self.N3 = n
+
+    def BoundingBox(self) -> Box:
+        return Box(self.V1.Min(self.V2).Min(self.V3), self.V1.Max(self.V2).Max(self.V3))
+
+    def MaterialAt(self, p=None) -> Material:
+        return self.Material
+
+
+def fix_normals_arrays(v1, v2, v3, n1, n2, n3):
+    """Triangle.FixNormals over arrays: zero normals take the face normal."""
+    face = normalize_rows(cross_rows((v2 - v1).astype(np.float32), (v3 - v1).astype(np.float32)))
+    out = []
+    for n in (n1, n2, n3):
+        n = n.copy()
+        z = np.all(n == 0, axis=1)
+        n[z] = face[z]
+        out.append(n)
+    return out
+
+
+class Mesh:
+    """PTSharpCore.Mesh (Mesh.cs): a triangle container held as [n,3] float32 arrays
+    plus a per-triangle material index into `materials`."""
+
+    def __init__(self, v1, v2, v3, n1, n2, n3, mat_index=None, materials=None):
+        self.v1, self.v2, self.v3 = (np.ascontiguousarray(a, dtype=np.float32) for a in (v1, v2, v3))
+        self.n1, self.n2, self.n3 = (np.ascontiguousarray(a, dtype=np.float32) for a in (n1, n2, n3))
+        n = len(self.v1)
+        self.mat_index = np.zeros(n, np.int32) if mat_index is None else np.asarray(mat_index, np.int32)
+        self.materials = list(materials) if materials else [DEFAULT_MATERIAL]
+
+    @staticmethod
+    def NewMesh(triangles) -> "Mesh":
+        mats, idx = [], []
+        for t in triangles:
+            if t.Material not in mats:
+                mats.append(t.Material)
+            idx.append(mats.index(t.Material))
+        arr = lambda name: np.array([getattr(t, name).f32() for t in triangles], dtype=np.float32).reshape(-1, 3)
+        return Mesh(arr("V1"), arr("V2"), arr("V3"), arr("N1"), arr("N2"), arr("N3"), idx, mats)
+
+    def __len__(self):
+        return len(self.v1)
+
+    def copy(self) -> "Mesh":
+        return Mesh(self.v1.copy(), self.v2.copy(), self.v3.copy(), self.n1.copy(), self.n2.copy(), self.n3.copy(),
+                    self.mat_index.copy(), list(self.materials))
+
+    def MaterialAt(self, p=None) -> Material:
+        return DEFAULT_MATERIAL
+
+    def SetMaterial(self, material: Material) -> None:
+        self.materials = [material]
+        self.mat_index = np.zeros(len(self), np.int32)
+
+    def BoundingBox(self) -> Box:
+        """Mesh.BoundingBox (Mesh.cs:88-120): component-wise min/max over V1,V2,V3."""
+        allv = np.concatenate([self.v1, self.v2, self.v3])
+        return Box(Vector(*allv.min(axis=0)), Vector(*allv.max(axis=0)))
+
+    def Transform(self, matrix: Matrix) -> None:
+        """Mesh.Transform (Mesh.cs:254-274)."""
+        self.v1 = matrix.MulPosition_arrays(self.v1)
+        self.v2 = matrix.MulPosition_arrays(self.v2)
+        self.v3 = matrix.MulPosition_arrays(self.v3)
+        self.n1 = matrix.MulDirection_arrays(self.n1)
+        self.n2 = matrix.MulDirection_arrays(self.n2)
+        self.n3 = matrix.MulDirection_arrays(self.n3)
+
+    def FitInside(self, box: Box, anchor: Vector) -> None:
+        """Mesh.FitInside (Mesh.cs:243-252)."""
+        bb = self.BoundingBox()
+        scale = box.Size().Div(bb.Size()).MinComponent()
+        extra = box.Size().Sub(bb.Size().MulScalar(scale))
+        matrix = Matrix.Identity()
+        matrix = Matrix.TranslateM(bb.Min.Negate()).Mul(matrix)
+        matrix = Matrix.ScaleM(Vector(scale, scale, scale)).Mul(matrix)
+        matrix = Matrix.TranslateM(box.Min.Add(extra.Mul(anchor))).Mul(matrix)
+        self.Transform(matrix)
+
+    def MoveTo(self, position: Vector, anchor: Vector) -> None:
+        m = Matrix.TranslateM(position.Sub(self.BoundingBox().Anchor(anchor)))
+        self.Transform(m)
+
+    def SmoothNormals(self) -> None:
+        """Mesh.SmoothNormals (Mesh.cs:191-229): per distinct vertex, the fp32 sum of the
+        corner normals in triangle order (V1,V2,V3 of each triangle), normalised."""
+        n = len(self)
+        if n == 0:
+            return
+        verts = np.stack([self.v1, self.v2, self.v3], axis=1).reshape(-1, 3) + np.float32(0.0)  # -0 → +0
+        norms = np.stack([self.n1, self.n2, self.n3], axis=1).reshape(-1, 3)
+        _, inv = np.unique(verts, axis=0, return_inverse=True)
+        inv = inv.reshape(-1)
+        acc = np.zeros((inv.max() + 1, 3), np.float32)
+        for k in range(3):  # sequential fp32 accumulation in reference order
+            np.add.at(acc[:, k], inv, norms[:, k])
+        unit = normalize_rows(acc)
+        sm = unit[inv].reshape(n, 3, 3)
+        self.n1, self.n2, self.n3 = (np.ascontiguousarray(sm[:, k]) for k in range(3))
+
+
+class Scene:
+    """PTSharpCore.Scene (Scene.cs).  Shapes keep insertion order; emissive
+    shapes are registered as lights exactly as Scene.Add does (Scene.cs:29-38)."""
+
+    def __init__(self):
+        self.Shapes: list = []
+        self.Lights: list = []
+        self.Color = Colour()
+        self._flat = None
+
+    def Add(self, shape) -> None:
+        if isinstance(shape, Mesh):
+            shape = shape.copy()  # Mesh is a struct: Scene.Add stores a boxed copy
+        self.Shapes.append(shape)
+        if shape.MaterialAt().Emittance > 0:
+            self.Lights.append(shape)
+        self._flat = None
+
+    def AddRange(self, shapes) -> None:
+        for s in shapes:
+            self.Add(s)
+
+    def Compile(self):
+        if self._flat is None:
+            self._flat = FlatScene(self)
+        return self._flat
+
+
+class FlatScene:
+    """Caller-owned arrays for pt_scene_desc, plus the ctypes struct pointing at them."""
+
+    def __init__(self, scene: Scene):
+        mats, mat_ids = [], {}
+
+        def mid(m: Material) -> int:
+            k = m.key()
+            if k not in mat_ids:
+                mat_ids[k] = len(mats)
+                mats.append(m)
+            return mat_ids[k]
+
+        kinds, idxs = [], []
+        sph_c, sph_r, sph_m = [], [], []
+        cub_a, cub_b, cub_m = [], [], []
+        pl_p, pl_n, pl_m = [], [], []
+        tri_parts = []  # list of (v1,v2,v3,n1,n2,n3,mat)
+        ntri = 0
+        mesh_first, mesh_count = [], []
+        for s in scene.Shapes:
+            if isinstance(s, Sphere):
+                kinds.append(_abi.SHAPE_SPHERE); idxs.append(len(sph_r))
+                sph_c.append(s.Center.f32()); sph_r.append(s.Radius); sph_m.append(mid(s.Material))
+            elif isinstance(s, Cube):
+                kinds.append(_abi.SHAPE_CUBE); idxs.append(len(cub_m))
+                cub_a.append(s.Min.f32()); cub_b.append(s.Max.f32()); cub_m.append(mid(s.Material))
+            elif isinstance(s, Plane):
+                kinds.append(_abi.SHAPE_PLANE); idxs.append(len(pl_m))
+                pl_p.append(s.Point.f32()); pl_n.append(s.Normal.f32()); pl_m.append(mid(s.Material))
+            elif isinstance(s, Triangle):
+                kinds.append(_abi.SHAPE_TRIANGLE); idxs.append(ntri)
+                tri_parts.append(tuple(np.array([getattr(s, a).f32()], np.float32)
+                                       for a in ("V1", "V2", "V3", "N1", "N2", "N3"))
+                                 + (np.array([mid(s.Material)], np.int32),))
+                ntri += 1
+            elif isinstance(s, Mesh):
+                kinds.append(_abi.SHAPE_MESH); idxs.append(len(mesh_first))
+                remap = np.array([mid(m) for m in s.materials], np.int32)
+                tri_parts.append((s.v1, s.v2, s.v3, s.n1, s.n2, s.n3, remap[s.mat_index]))
+                mesh_first.append(ntri); mesh_count.append(len(s))
+                ntri += len(s)
+            else:
+                raise _abi.PTError(_abi.PT_ERR_UNSUPPORTED, "Scene.flatten",
+                                   f"shape type {type(s).__name__} is not on the GPU path")
+        if not mats:
+            mid(DEFAULT_MATERIAL)
+        self.materials = (_abi.pt_material * len(mats))()
+        for i, m in enumerate(mats):
+            self.materials[i] = _abi.pt_material((C.c_double * 3)(m.Color.r, m.Color.g, m.Color.b), m.Emittance,
+                                                 m.Index, m.Gloss, m.Tint, m.Reflectivity, int(bool(m.Transparent)), 0)
+        self.material_list = mats
+        f3 = lambda L: np.ascontiguousarray(np.array(L, np.float32).reshape(-1, 3))
+        i32 = lambda L: np.ascontiguousarray(np.array(L, np.int32).reshape(-1))
+        self.shape_kind, self.shape_index = i32(kinds), i32(idxs)
+        self.sphere_center, self.sphere_radius, self.sphere_material = f3(sph_c), np.array(sph_r, np.float64), i32(sph_m)
+        self.cube_min, self.cube_max, self.cube_material = f3(cub_a), f3(cub_b), i32(cub_m)
+        self.plane_point, self.plane_normal, self.plane_material = f3(pl_p), f3(pl_n), i32(pl_m)
+        if tri_parts:
+            cat = [np.ascontiguousarray(np.concatenate([p[k] for p in tri_parts])) for k in range(7)]
+        else:
+            cat = [np.zeros((0, 3), np.float32)] * 6 + [np.zeros(0, np.int32)]
+        (self.tri_v1, self.tri_v2, self.tri_v3, self.tri_n1, self.tri_n2, self.tri_n3) = cat[:6]
+        self.tri_material = cat[6].astype(np.int32)
+        self.mesh_first, self.mesh_count = i32(mesh_first), i32(mesh_count)
+        self.env = scene.Color.tuple()
+        self.desc = self._make_desc(_abi.pt_scene_desc)
+
+    def _make_desc(self, cls):
+        P = lambda a, t: a.ctypes.data_as(C.POINTER(t)) if a.size else C.POINTER(t)()
+        fl, db, it = C.c_float, C.c_double, C.c_int32
+        return cls(len(self.material_list), C.cast(self.materials, C.POINTER(_abi.pt_material)),
+                   len(self.shape_kind), P(self.shape_kind, it), P(self.shape_index, it),
+                   len(self.sphere_radius), P(self.sphere_center, fl), P(self.sphere_radius, db),
+                   P(self.sphere_material, it),
+                   len(self.cube_material), P(self.cube_min, fl), P(self.cube_max, fl), P(self.cube_material, it),
+                   len(self.plane_material), P(self.plane_point, fl), P(self.plane_normal, fl),
+                   P(self.plane_material, it),
+                   len(self.tri_material), P(self.tri_v1, fl), P(self.tri_v2, fl), P(self.tri_v3, fl),
+                   P(self.tri_n1, fl), P(self.tri_n2, fl), P(self.tri_n3, fl), P(self.tri_material, it),
+                   len(self.mesh_first), P(self.mesh_first, it), P(self.mesh_count, it),
+                   (C.c_double * 3)(*self.env))
+
+    @property
+    def num_triangles(self) -> int:
+        return len(self.tri_material)
+
+
+class Camera:
+    """PTSharpCore.Camera (Camera.cs): LookAt + SetFocus."""
+
+    def __init__(self):
+        self.p = self.u = self.v = self.w = Vector()
+        self.m = 0.0
+        self.focalDistance = 0.0
+        self.apertureRadius = 0.0
+        self.fovy = 0.0
+
+    @staticmethod
+    def LookAt(eye: Vector, center: Vector, up: Vector, fovy: float) -> "Camera":
+        c = Camera()
+        c.fovy = fovy
+        c.p = eye
+        c.w = center.Sub(eye).Normalize()
+        c.u = up.Cross(c.w).Normalize()
+        c.v = c.w.Cross(c.u).Normalize()
+        c.m = 1 / math.tan(fovy * math.pi / 360)
+        return c
+
+    def SetFocus(self, focalPoint: Vector, apertureRadius: float) -> None:
+        self.focalDistance = focalPoint.Sub(self.p).Length()
+        self.apertureRadius = apertureRadius
+
+    def to_c(self, cls=_abi.pt_camera):
+        a = lambda v: (C.c_float * 3)(*v.f32())
+        return cls(a(self.p), a(self.u), a(self.v), a(self.w), self.m, self.focalDistance, self.apertureRadius)
+
+
+class DefaultSampler:
+    """PTSharpCore.DefaultSampler (Sampler.cs:10-145)."""
+
+    def __init__(self, fh: int, mb: int, dl: bool, ss: bool, lm: LightMode, sm: SpecularMode):
+        self.FirstHitSamples, self.MaxBounces = int(fh), int(mb)
+        self.DirectLighting, self.SoftShadows = bool(dl), bool(ss)
+        self.LightMode, self.SpecularMode = LightMode(lm), SpecularMode(sm)
+
+    @staticmethod
+    def NewSampler(firstHitSamples: int, maxBounces: int) -> "DefaultSampler":
+        return DefaultSampler(firstHitSamples, maxBounces, True, True, LightMode.LightModeRandom,
+                              SpecularMode.SpecularModeNaive)
+
+    def NewDirectSampler(self) -> "DefaultSampler":
+        return DefaultSampler(1, 0, True, False, LightMode.LightModeAll, SpecularMode.SpecularModeAll)
+
+    def SetSpecularMode(self, s: SpecularMode) -> None:
+        self.SpecularMode = SpecularMode(s)
+
+    def SetLightMode(self, l: LightMode) -> None:
+        self.LightMode = LightMode(l)
+
+    def to_c(self, cls=_abi.pt_sampler):
+        return cls(self.FirstHitSamples, self.MaxBounces, int(self.DirectLighting), int(self.SoftShadows),
+                   int(self.LightMode), int(self.SpecularMode))

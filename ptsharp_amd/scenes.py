@@ -1,0 +1,175 @@
+"""Scenes for the BASELINE.json configs, built through the mirrored API exactly
+as PTSharpCore/Example.cs builds them.  No model assets ship with the reference
+(SURVEY.md fact 6), so meshes come from a seeded generator.
+
+  gopher3          Example.gopher (Example.cs:1542-1564) with the OBJ mesh replaced
+                   by two spheres                       → C1, C2
+  bunny_frame(n)   Example.bunny (Example.cs:1084-1102) with a seeded displaced
+                   sphere of ~n triangles in place of models/bunny.obj  → C3 (70k), C4 (1M)
+  materialspheres  Example.materialspheres (Example.cs:1204-1227)
+  simplesphere     Example.simplesphere (Example.cs:1670-1697)
+  example1         Example.example1 (Example.cs:341-359), no adaptive/firefly passes
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .geometry import Box, Colour, Util, Vector
+from .scene import Camera, Cube, DefaultSampler, Material, Mesh, Plane, Scene, SpecularMode, Sphere
+
+F = lambda x: float(np.float32(x))  # C# float literal (e.g. 0.75F)
+
+
+def gopher3():
+    scene = Scene()
+    wall = Material.GlossyMaterial(Colour.HexColor(0xFCFAE1), 1.5, Util.Radians(10))
+    light = Material.LightMaterial(Colour.White, 80)
+    scene.Add(Cube.NewCube(Vector(-10, -1, -10), Vector(-2, 10, 10), wall))
+    scene.Add(Cube.NewCube(Vector(-10, -1, -10), Vector(10, 0, 10), wall))
+    scene.Add(Sphere.NewSphere(Vector(4, 10, 1), 1, light))
+    scene.Add(Sphere.NewSphere(Vector(0, 1, 0), 1, Material.GlossyMaterial(Colour.Black, 1.2, Util.Radians(30))))
+    scene.Add(Sphere.NewSphere(Vector(0, 0.5, 1.5), 0.5, Material.SpecularMaterial(Colour.HexColor(0x334D5C), 2)))
+    camera = Camera.LookAt(Vector(4, 1, 0), Vector(0, 0.9, 0), Vector(0, 1, 0), 40)
+    sampler = DefaultSampler.NewSampler(16, 16)
+    return scene, camera, sampler
+
+
+def materialspheres():
+    scene = Scene()
+    r = F(0.4)
+    scene.Add(Sphere.NewSphere(Vector(-2, r, 0), r, Material.DiffuseMaterial(Colour.HexColor(0x334D5C))))
+    scene.Add(Sphere.NewSphere(Vector(-1, r, 0), r, Material.SpecularMaterial(Colour.HexColor(0x334D5C), 2)))
+    scene.Add(Sphere.NewSphere(Vector(0, r, 0), r, Material.GlossyMaterial(Colour.HexColor(0x334D5C), 2,
+                                                                          Util.Radians(50))))
+    scene.Add(Sphere.NewSphere(Vector(1, r, 0), r, Material.TransparentMaterial(Colour.HexColor(0x334D5C), 2,
+                                                                               Util.Radians(20), 1)))
+    scene.Add(Sphere.NewSphere(Vector(2, r, 0), r, Material.ClearMaterial(2, 0)))
+    scene.Add(Sphere.NewSphere(Vector(0, F(1.5), -4), F(1.5), Material.MetallicMaterial(Colour.HexColor(0xFFFFFF), 0, 1)))
+    scene.Add(Cube.NewCube(Vector(-1000, -1, -1000), Vector(1000, 0, 1000),
+                           Material.GlossyMaterial(Colour.HexColor(0xFFFFFF), F(1.4), Util.Radians(20))))
+    scene.Add(Sphere.NewSphere(Vector(0, 5, 0), 1, Material.LightMaterial(Colour.White, 25)))
+    camera = Camera.LookAt(Vector(0, 3, 6), Vector(0, 1, 0), Vector(0, 1, 0), 30)
+    sampler = DefaultSampler.NewSampler(16, 16)
+    return scene, camera, sampler
+
+
+def simplesphere():
+    scene = Scene()
+    material = Material.DiffuseMaterial(Colour.White)
+    scene.Add(Plane.NewPlane(Vector(0, 0, 0), Vector(0, 0, 1), material))
+    scene.Add(Sphere.NewSphere(Vector(0, 0, 1), F(1.0), material))
+    scene.Add(Sphere.NewSphere(Vector(0, 0, F(5.0)), F(1.0), Material.LightMaterial(Colour.White, 8)))
+    camera = Camera.LookAt(Vector(3, 3, 3), Vector(0, 0, F(0.5)), Vector(0, 0, 1), 50)
+    sampler = DefaultSampler.NewSampler(16, 4)
+    return scene, camera, sampler
+
+
+def example1():
+    scene = Scene()
+    scene.Add(Sphere.NewSphere(Vector(1.5, 1.25, 0), 1.25, Material.SpecularMaterial(Colour.HexColor(0x004358), 1.3)))
+    scene.Add(Sphere.NewSphere(Vector(-1, 1, 2), 1, Material.SpecularMaterial(Colour.HexColor(0xFFE11A), 1.3)))
+    scene.Add(Sphere.NewSphere(Vector(-2.5, 0.75, 0), 0.75, Material.SpecularMaterial(Colour.HexColor(0xFD7400), 1.3)))
+    scene.Add(Sphere.NewSphere(Vector(-0.75, 0.5, -1), 0.5, Material.ClearMaterial(1.5, 0)))
+    scene.Add(Cube.NewCube(Vector(-10, -1, -10), Vector(10, 0, 10), Material.GlossyMaterial(Colour.White, 1.1,
+                                                                                          Util.Radians(10))))
+    scene.Add(Sphere.NewSphere(Vector(-1.5, 4, 0), 0.5, Material.LightMaterial(Colour.White, 30)))
+    camera = Camera.LookAt(Vector(0, 2, -5), Vector(0, 0.25, 3), Vector(0, 1, 0), 45)
+    camera.SetFocus(Vector(-0.75, 1, -1), 0.1)
+    sampler = DefaultSampler.NewSampler(8, 10)
+    sampler.SpecularMode = SpecularMode.SpecularModeFirst
+    return scene, camera, sampler
+
+
+def blob_mesh(n_target: int, seed: int = 1234, amplitude: float = 0.05) -> Mesh:
+    """Seeded displaced UV sphere with ~n_target triangles (fan caps + quad bands), per-vertex
+    radius 1 + amplitude·noise, zero normals (FixNormals → face normals), consistent winding."""
+    # tris = 2*ns + 2*ns*(nr-2) = 2*ns*(nr-1);  choose nr ≈ ns/2
+    ns = max(8, int(round(math.sqrt(n_target))))
+    nr = max(3, int(round(n_target / (2 * ns))) + 1)
+    rng = np.random.default_rng(seed)
+    k = 24
+    dirs = rng.normal(size=(k, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    freq = rng.uniform(2.0, 9.0, size=k)
+    phase = rng.uniform(0, 2 * math.pi, size=k)
+    amp = rng.uniform(0.3, 1.0, size=k) / freq
+
+    theta = np.pi * np.arange(1, nr) / nr
+    phi = 2 * np.pi * np.arange(ns) / ns
+    th, ph = np.meshgrid(theta, phi, indexing="ij")
+    unit = np.stack([np.sin(th) * np.cos(ph), np.cos(th), np.sin(th) * np.sin(ph)], axis=-1).reshape(-1, 3)
+    unit = np.concatenate([unit, [[0, 1, 0], [0, -1, 0]]])
+    noise = (amp[None, :] * np.sin(unit @ dirs.T * freq[None, :] + phase[None, :])).sum(axis=1)
+    noise /= np.abs(noise).max() + 1e-12
+    verts = (unit * (1.0 + amplitude * noise)[:, None]).astype(np.float32)
+    north, south = len(verts) - 2, len(verts) - 1
+    ring = lambda i, j: i * ns + (j % ns)
+    tris = []
+    j = np.arange(ns)
+    tris.append(np.stack([np.full(ns, north), ring(0, j + 1), ring(0, j)], axis=1))
+    for i in range(nr - 2):
+        a, b, c, d = ring(i, j), ring(i, j + 1), ring(i + 1, j), ring(i + 1, j + 1)
+        tris.append(np.stack([a, b, d], axis=1))
+        tris.append(np.stack([a, d, c], axis=1))
+    tris.append(np.stack([np.full(ns, south), ring(nr - 2, j), ring(nr - 2, j + 1)], axis=1))
+    t = np.concatenate(tris)
+    z = np.zeros((len(t), 3), np.float32)
+    m = Mesh(verts[t[:, 0]], verts[t[:, 1]], verts[t[:, 2]], z, z, z)
+    from .scene import fix_normals_arrays
+    m.n1, m.n2, m.n3 = fix_normals_arrays(m.v1, m.v2, m.v3, m.n1, m.n2, m.n3)
+    return m
+
+
+def bunny_frame(n_tris: int = 69_451, seed: int = 1234, mesh: Mesh = None):
+    """Example.bunny's scene around a synthetic mesh (SURVEY.md §8d mesh70k / mesh1M)."""
+    scene = Scene()
+    material = Material.GlossyMaterial(Colour.HexColor(0xF2EBC7), F(1.5), Util.Radians(0))
+    if mesh is None:
+        mesh = blob_mesh(n_tris, seed)
+    mesh.SetMaterial(material)
+    mesh.SmoothNormals()
+    mesh.FitInside(Box(Vector(-1, 0, -1), Vector(1, 2, 1)), Vector(F(0.5), 0, F(0.5)))
+    scene.Add(mesh)
+    floor = Material.GlossyMaterial(Colour.HexColor(0x33332D), F(1.2), Util.Radians(20))
+    scene.Add(Cube.NewCube(Vector(-10000, -10000, -10000), Vector(10000, 0, 10000), floor))
+    scene.Add(Sphere.NewSphere(Vector(0, 5, 0), 1, Material.LightMaterial(Colour.White, 10)))
+    scene.Add(Sphere.NewSphere(Vector(4, 5, 4), 1, Material.LightMaterial(Colour.White, 10)))
+    camera = Camera.LookAt(Vector(-1, 2, 3), Vector(0, F(0.75), 0), Vector(0, 1, 0), 50)
+    sampler = DefaultSampler.NewSampler(4, 4)
+    sampler.SetSpecularMode(SpecularMode.SpecularModeFirst)
+    return scene, camera, sampler
+
+
+def furnace(albedo: float = 0.5):
+    """Analytic 'floor furnace' (SURVEY.md §4): a huge diffuse cube seen from above, scene.Color = 1,
+    no lights → every floor pixel is exactly `albedo`, every sky pixel exactly 1."""
+    scene = Scene()
+    scene.Color = Colour(1, 1, 1)
+    scene.Add(Cube.NewCube(Vector(-1000, -1, -1000), Vector(1000, 0, 1000),
+                           Material.DiffuseMaterial(Colour(albedo, albedo, albedo))))
+    camera = Camera.LookAt(Vector(0, 2, 3), Vector(0, 1.5, 0), Vector(0, 1, 0), 60)
+    sampler = DefaultSampler.NewSampler(4, 4)
+    return scene, camera, sampler
+
+
+def emitter(fh: int = 16):
+    """A lone light sphere in a black environment: a camera hit returns Color·Emittance·FH/⌊√FH⌋²."""
+    scene = Scene()
+    scene.Add(Sphere.NewSphere(Vector(0, 0, 0), 1, Material.LightMaterial(Colour(0.25, 0.5, 1.0), 2)))
+    camera = Camera.LookAt(Vector(0, 0, 4), Vector(0, 0, 0), Vector(0, 1, 0), 40)
+    sampler = DefaultSampler.NewSampler(fh, 4)
+    return scene, camera, sampler
+
+
+SCENES = {
+    "gopher3": gopher3,
+    "materialspheres": materialspheres,
+    "simplesphere": simplesphere,
+    "example1": example1,
+    "bunny70k": lambda: bunny_frame(69_451),
+    "mesh1m": lambda: bunny_frame(1_000_000),
+    "furnace": furnace,
+    "emitter": emitter,
+}

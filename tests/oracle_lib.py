@@ -1,0 +1,136 @@
+"""ctypes wrapper of oracle/_build/liboracle.so — the CPU restatement used as the
+parity checker and as bench.py's cpu_baseline.  TEST INFRASTRUCTURE ONLY: only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load it.
+
+The oracle's structs share the C-ABI layouts of include/ptsharp_hip.h, so the
+product's host-side flattening (ptsharp_amd.scene.FlatScene) feeds both.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from ptsharp_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+
+_lib = None
+
+
+def build_oracle() -> str:
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    return ORACLE_SO
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        L = C.CDLL(build_oracle())
+        vp, f3, i32p = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int32)
+        dp = C.POINTER(C.c_double)
+        L.or_scene_create.restype = vp
+        L.or_scene_create.argtypes = [C.POINTER(_abi.pt_scene_desc)]
+        L.or_scene_destroy.argtypes = [vp]
+        L.or_scene_tree_nodes.restype = C.c_int64
+        L.or_scene_tree_nodes.argtypes = [vp]
+        L.or_render_pass.restype = C.c_int64
+        L.or_render_pass.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(_abi.pt_camera), C.POINTER(_abi.pt_sampler),
+                                     C.POINTER(_abi.pt_pass_params), dp, dp, i32p, C.c_int32, C.c_int32]
+        L.or_render_pixels.restype = C.c_int64
+        L.or_render_pixels.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(_abi.pt_camera), C.POINTER(_abi.pt_sampler),
+                                       C.POINTER(_abi.pt_pass_params), C.c_int64, C.c_int64, C.c_int64, dp, dp, i32p,
+                                       C.c_int32]
+        L.or_intersect.restype = C.c_double
+        L.or_intersect.argtypes = [vp, f3, f3, C.c_int32, i32p, i32p]
+        L.or_hit_info.restype = C.c_int32
+        L.or_hit_info.argtypes = [vp, f3, f3, f3, f3, i32p, i32p]
+        L.or_cast_ray.argtypes = [C.POINTER(_abi.pt_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_double,
+                                  C.c_double, C.c_uint64, f3, f3]
+        L.or_prim_intersect.restype = C.c_double
+        L.or_prim_intersect.argtypes = [C.c_int32, f3, f3, f3, C.c_double, f3, f3]
+        L.or_prim_normal.argtypes = [C.c_int32, f3, f3, f3, f3, f3, f3, f3, f3]
+        L.or_camera_key.restype = C.c_uint64
+        L.or_camera_key.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]
+        L.or_child_key.restype = C.c_uint64
+        L.or_child_key.argtypes = [C.c_uint64, C.c_uint32]
+        L.or_light_key.restype = C.c_uint64
+        L.or_light_key.argtypes = [C.c_uint64, C.c_uint32]
+        L.or_draw.restype = C.c_double
+        L.or_draw.argtypes = [C.c_uint64, C.c_uint32]
+        _lib = L
+    return _lib
+
+
+def f3(v) -> C.Array:
+    return (C.c_float * 3)(*[float(np.float32(x)) for x in v])
+
+
+class OracleScene:
+    def __init__(self, scene):
+        self.flat = scene.Compile()
+        self.h = lib().or_scene_create(C.byref(self.flat.desc))
+        if not self.h:
+            raise RuntimeError("or_scene_create failed")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_scene_destroy(self.h)
+            self.h = None
+
+    def intersect(self, origin, direction, brute=False):
+        k, i = C.c_int32(), C.c_int32()
+        t = lib().or_intersect(self.h, f3(origin), f3(direction), int(brute), C.byref(k), C.byref(i))
+        return t, k.value, i.value
+
+    def tree_nodes(self) -> int:
+        return lib().or_scene_tree_nodes(self.h)
+
+
+def pass_params(spp, seed=0, pass_index=1, stratified=False, tiles=None):
+    keep = None
+    if tiles is not None:
+        keep = np.ascontiguousarray(tiles, np.int32)
+    pp = _abi.pt_pass_params(spp, int(stratified), seed, pass_index, 0 if keep is None else len(keep),
+                             C.POINTER(C.c_int32)() if keep is None else keep.ctypes.data_as(C.POINTER(C.c_int32)))
+    pp._keep = keep
+    return pp
+
+
+class OracleBuffer:
+    def __init__(self, w, h):
+        self.W, self.H = w, h
+        self.M = np.zeros((h, w, 3), np.float64)
+        self.V = np.zeros((h, w, 3), np.float64)
+        self.N = np.zeros((h, w), np.int32)
+
+    def ptrs(self):
+        return (self.M.ctypes.data_as(C.POINTER(C.c_double)), self.V.ctypes.data_as(C.POINTER(C.c_double)),
+                self.N.ctypes.data_as(C.POINTER(C.c_int32)))
+
+
+def render(oscene: OracleScene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None,
+           threads=0, brute=False, buf: OracleBuffer = None, first_pass=1):
+    """IterativeRender-equivalent on the oracle: `passes` RenderParallel calls."""
+    buf = buf or OracleBuffer(w, h)
+    cam, smp = camera.to_c(), sampler.to_c()
+    rays = 0
+    for p in range(first_pass, first_pass + passes):
+        pp = pass_params(spp, seed, p, stratified, tiles)
+        rays += lib().or_render_pass(oscene.h, w, h, C.byref(cam), C.byref(smp), C.byref(pp), *buf.ptrs(), threads,
+                                     int(brute))
+    return buf, rays
+
+
+def render_pixels(oscene: OracleScene, camera, sampler, w, h, spp, pix_begin, pix_end, pix_stride=1, seed=0,
+                  pass_index=1, threads=0, buf: OracleBuffer = None):
+    buf = buf or OracleBuffer(w, h)
+    cam, smp = camera.to_c(), sampler.to_c()
+    pp = pass_params(spp, seed, pass_index)
+    rays = lib().or_render_pixels(oscene.h, w, h, C.byref(cam), C.byref(smp), C.byref(pp), pix_begin, pix_end,
+                                  pix_stride, *buf.ptrs(), threads)
+    return buf, rays

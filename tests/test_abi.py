@@ -1,0 +1,90 @@
+"""The C-ABI library loads and exports every symbol include/ptsharp_hip.h declares;
+argument validation and error reporting work without a GPU (no compute calls)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from ptsharp_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ptsharp_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pt_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for n in ["pt_create", "pt_upload_scene", "pt_render_pass", "pt_read_buffer", "pt_stats_get", "pt_last_error",
+              "pt_destroy", "pt_comm_unique_id", "pt_comm_init", "pt_comm_gather"]:
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.load_library()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert set(declared_functions()) == set(_abi.SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    for name in declared_functions():
+        assert re.search(rf"\bT {name}\b", out), f"{name} not exported with C linkage"
+
+
+def test_version():
+    assert _abi.load_library().pt_get_version() == 1
+
+
+def test_struct_layouts_match_header():
+    # sizes computed by hand from the C declarations (x86-64 SysV alignment)
+    assert C.sizeof(_abi.pt_material) == 8 * 8 + 8
+    assert C.sizeof(_abi.pt_camera) == 12 * 4 + 3 * 8
+    assert C.sizeof(_abi.pt_sampler) == 24
+    assert C.sizeof(_abi.pt_pass_params) == 4 + 4 + 8 + 4 + 4 + 8
+    assert C.sizeof(_abi.pt_stats) == 8 * 8
+    assert C.sizeof(_abi.pt_trace_counters) == 32
+    assert _abi.pt_scene_desc.env_color.offset % 8 == 0
+
+
+def test_null_arguments_rejected_with_message():
+    lib = _abi.load_library()
+    assert lib.pt_create(None, None) == _abi.PT_ERR_INVALID_ARG
+    assert b"NULL" in lib.pt_last_error()
+    assert lib.pt_upload_scene(None, None) == _abi.PT_ERR_INVALID_ARG
+    assert lib.pt_render_pass(None, None, None, None) == _abi.PT_ERR_INVALID_ARG
+    assert lib.pt_read_buffer(None, None, None, None) == _abi.PT_ERR_INVALID_ARG
+    assert lib.pt_stats_get(None, None) == _abi.PT_ERR_INVALID_ARG
+    assert lib.pt_comm_gather(None, 0) == _abi.PT_ERR_INVALID_ARG
+    lib.pt_destroy(None)  # no-op
+
+
+def test_bad_dimensions_rejected():
+    lib = _abi.load_library()
+    ctx = C.c_void_p()
+    opts = _abi.pt_device_opts(0, 1, 1)
+    assert lib.pt_create(C.byref(opts), C.byref(ctx)) == _abi.PT_ERR_INVALID_ARG
+    assert not ctx.value
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU present")
+def test_no_device_reports_error_not_fallback():
+    lib = _abi.load_library()
+    ctx = C.c_void_p()
+    opts = _abi.pt_device_opts(0, 64, 64)
+    rc = lib.pt_create(C.byref(opts), C.byref(ctx))
+    assert rc in (_abi.PT_ERR_NO_DEVICE, _abi.PT_ERR_HIP)
+    assert lib.pt_last_error()
+    from ptsharp_amd import Renderer, scenes
+    s, c, smp = scenes.furnace()
+    with pytest.raises(_abi.PTError):
+        Renderer.NewRenderer(s, c, smp, 64, 64, True)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(ImportError):
+        _abi.load_library(str(tmp_path / "missing.so"))

@@ -1,0 +1,261 @@
+"""Known-answer tests that pin the CPU oracle to the reference's semantics.
+
+The reference ships no tests or fixtures, so these KATs are
+derived from its code: primitive intersect edge cases (Triangle.cs:95-124,
+Sphere.cs:40-60, Cube.cs:35-47, Plane.cs:36-50), the Cube normal quirk
+(Cube.cs:57-69), the camera-ray jitter bug (Renderer.cs:301 + Camera.cs:101),
+the analytic furnace / emitter images, and k-d tree ≡ brute force.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from ptsharp_amd import Camera, Colour, Cube, DefaultSampler, Material, Scene, Sphere, Vector, scenes
+
+L = O.lib
+
+
+def prim_t(kind, a, b=(0, 0, 0), c=(0, 0, 0), radius=0.0, o=(0, 0, 0), d=(0, 0, 1)):
+    return L().or_prim_intersect(kind, O.f3(a), O.f3(b), O.f3(c), radius, O.f3(o), O.f3(d))
+
+
+MISS = float(np.float32(1e9))
+
+
+class TestTriangle:
+    V1, V2, V3 = (0, 0, 0), (1, 0, 0), (0, 1, 0)
+
+    def t(self, o, d):
+        return prim_t(3, self.V1, self.V2, self.V3, o=o, d=d)
+
+    def test_hit_center(self):
+        assert self.t((0.25, 0.25, -1), (0, 0, 1)) == 1.0
+
+    def test_parallel_det_rejected(self):
+        assert self.t((0.25, 0.25, -1), (1, 0, 0)) == MISS  # |det| < EPS
+
+    def test_u_out_of_range(self):
+        assert self.t((-0.1, 0.25, -1), (0, 0, 1)) == MISS
+        assert self.t((1.1, -0.05, -1), (0, 0, 1)) == MISS
+
+    def test_v_and_sum_bounds(self):
+        assert self.t((0.25, -0.1, -1), (0, 0, 1)) == MISS
+        assert self.t((0.6, 0.6, -1), (0, 0, 1)) == MISS
+
+    def test_edges_inclusive(self):
+        # u = 0 and u + v = 1 exactly are accepted (strict < 0 and > 1 tests)
+        assert self.t((0.0, 0.5, -1), (0, 0, 1)) == 1.0
+        assert self.t((0.5, 0.5, -1), (0, 0, 1)) == 1.0
+
+    def test_behind_rejected(self):
+        assert self.t((0.25, 0.25, 1), (0, 0, 1)) == MISS  # t < EPS
+
+    def test_backface_hits(self):
+        assert self.t((0.25, 0.25, 1), (0, 0, -1)) == 1.0  # no culling
+
+
+class TestSphere:
+    def test_outside_near_root(self):
+        assert prim_t(0, (0, 0, 5), radius=1.0) == 4.0
+
+    def test_inside_far_root(self):
+        assert prim_t(0, (0, 0, 0), radius=1.0, o=(0, 0, 0)) == 1.0
+
+    def test_tangent_miss(self):
+        # d = b² - c = 0 is not > 0
+        assert prim_t(0, (1, 0, 5), radius=1.0) == MISS
+
+    def test_behind(self):
+        assert prim_t(0, (0, 0, -5), radius=1.0) == MISS
+
+
+class TestCube:
+    def test_entry_face(self):
+        assert prim_t(1, (-1, -1, 2), (1, 1, 3)) == 2.0
+
+    def test_inside_no_hit(self):
+        # only t0 > 0 && t0 < t1 counts: from inside t0 < 0
+        assert prim_t(1, (-1, -1, -1), (1, 1, 1)) == MISS
+
+    def test_miss(self):
+        assert prim_t(1, (2, 2, 2), (3, 3, 3)) == MISS
+
+
+class TestPlane:
+    def test_hit(self):
+        assert prim_t(2, (0, 0, 3), (0, 0, 1)) == 3.0
+
+    def test_parallel(self):
+        assert prim_t(2, (0, 0, 3), (1, 0, 0)) == MISS
+
+    def test_behind(self):
+        assert prim_t(2, (0, 0, -3), (0, 0, 1)) == MISS
+
+
+def normal(kind, a, b, pos, c=(0, 0, 0), n1=(0, 0, 0), n2=(0, 0, 0), n3=(0, 0, 0)):
+    out = (C.c_float * 3)()
+    L().or_prim_normal(kind, O.f3(a), O.f3(b), O.f3(c), O.f3(n1), O.f3(n2), O.f3(n3), O.f3(pos), out)
+    return tuple(out)
+
+
+class TestNormals:
+    def test_cube_faces(self):
+        mn, mx = (-1, -1, -1), (1, 1, 1)
+        assert normal(1, mn, mx, (-1, 0.3, 0.2)) == (-1, 0, 0)
+        assert normal(1, mn, mx, (1, 0.3, 0.2)) == (1, 0, 0)
+        assert normal(1, mn, mx, (0.1, -1, 0.2)) == (0, -1, 0)
+        assert normal(1, mn, mx, (0.1, 0.3, 1)) == (0, 0, 1)
+
+    def test_cube_quirk_default_up(self):
+        # |p - face| >= 1e-9 everywhere → (0,1,0) regardless of the face (Cube.cs:67)
+        p = (float(np.nextafter(np.float32(-1), np.float32(0))), 0.3, 0.2)
+        assert normal(1, (-1, -1, -1), (1, 1, 1), p) == (0, 1, 0)
+
+    def test_sphere(self):
+        assert normal(0, (0, 0, 0), (0, 0, 0), (0, 2, 0)) == (0, 1, 0)
+
+    def test_triangle_barycentric(self):
+        n = normal(3, (0, 0, 0), (1, 0, 0), (0.25, 0.25, 0), c=(0, 1, 0), n1=(0, 0, 1), n2=(0, 0, 1), n3=(0, 0, 1))
+        assert n == (0, 0, 1)
+        n = normal(3, (0, 0, 0), (1, 0, 0), (1, 0, 0), c=(0, 1, 0), n1=(0, 0, 1), n2=(1, 0, 0), n3=(0, 0, 1))
+        assert np.allclose(n, (1, 0, 0), atol=1e-6)
+
+
+class TestRNG:
+    def test_range_and_determinism(self):
+        k = L().or_camera_key(7, 1, 12345, 3)
+        xs = [L().or_draw(k, d) for d in range(2000)]
+        assert all(0.0 <= x < 1.0 for x in xs)
+        assert xs == [L().or_draw(k, d) for d in range(2000)]
+        assert abs(np.mean(xs) - 0.5) < 0.02
+        assert abs(np.var(xs) - 1 / 12) < 0.01
+
+    def test_keys_distinct(self):
+        keys = {L().or_camera_key(0, p, px, s) for p in range(3) for px in range(50) for s in range(4)}
+        assert len(keys) == 600
+        ck = {L().or_child_key(123, c) for c in range(1000)} | {L().or_light_key(123, c) for c in range(1000)}
+        assert len(ck) == 2000
+
+    def test_53_bit_resolution(self):
+        k = L().or_camera_key(1, 1, 1, 1)
+        x = L().or_draw(k, 0)
+        assert x * 2**53 == math.floor(x * 2**53)
+
+
+class TestCamera:
+    def test_castray_center_and_jitter_bug(self):
+        cam = Camera.LookAt(Vector(0, 0, 5), Vector(0, 0, 0), Vector(0, 1, 0), 60)
+        o, d = (C.c_float * 3)(), (C.c_float * 3)()
+        w = h = 101
+        # RenderParallel passes fu = (x + ξ)/w; CastRay adds x again.
+        x = y = 10
+        L().or_cast_ray(C.byref(cam.to_c()), x, y, w, h, (x + 0.5) / w, (y + 0.5) / h, 0, o, d)
+        # px = ((x + u - 0.5)/(w - 1))·2 - 1 with u = (x+0.5)/w (bugged) vs u = 0.5 (intended)
+        px = ((x + (x + 0.5) / w - 0.5) / (w - 1.0)) * 2 - 1
+        px_fixed = ((x + 0.5 - 0.5) / (w - 1.0)) * 2 - 1
+        assert abs(px - px_fixed) > 1e-3
+        assert tuple(o) == (0.0, 0.0, 5.0)
+        # d = normalize(-px·aspect·U - py·V + m·W), U = (-1,0,0), V = (0,1,0): d.x ∝ px, d.y ∝ -py
+        dx = float(d[0])
+        assert np.isclose(dx, px / math.sqrt(px * px * 2 + cam.m ** 2), rtol=1e-5)
+        assert not np.isclose(dx, px_fixed / math.sqrt(px_fixed ** 2 * 2 + cam.m ** 2), rtol=1e-5)
+
+    def test_aperture_changes_origin(self):
+        cam = Camera.LookAt(Vector(0, 0, 5), Vector(0, 0, 0), Vector(0, 1, 0), 60)
+        cam.SetFocus(Vector(0, 0, 0), 0.2)
+        o, d = (C.c_float * 3)(), (C.c_float * 3)()
+        L().or_cast_ray(C.byref(cam.to_c()), 10, 10, 64, 64, 0.3, 0.3, 99, o, d)
+        assert np.hypot(o[0], o[1]) <= 0.2 + 1e-6 and o[2] == 5.0
+
+
+def test_furnace_exact():
+    s, c, smp = scenes.furnace(0.5)
+    buf, rays = O.render(O.OracleScene(s), c, smp, 48, 32, spp=2, passes=3, seed=1)
+    assert set(np.unique(buf.M)) == {0.5, 1.0}
+    assert (buf.N == 3).all()
+    assert (buf.V == 0).all()
+
+
+@pytest.mark.parametrize("fh", [1, 4, 8, 16])
+def test_emitter_exact(fh):
+    s, c, smp = scenes.emitter(fh)
+    buf, _ = O.render(O.OracleScene(s), c, smp, 40, 32, spp=1, seed=2)
+    n = int(math.sqrt(fh))
+    vals = {tuple(v) for v in buf.M.reshape(-1, 3)}
+    assert vals == {(0.0, 0.0, 0.0), tuple(np.array([0.25, 0.5, 1.0]) * 2 * fh / (n * n))}
+
+
+@pytest.mark.parametrize("name", ["gopher3", "materialspheres", "simplesphere", "example1"])
+def test_kdtree_equals_brute_force(name):
+    s, c, smp = scenes.SCENES[name]()
+    smp.MaxBounces = 3
+    os_ = O.OracleScene(s)
+    a, ra = O.render(os_, c, smp, 40, 30, spp=1, seed=4)
+    b, rb = O.render(os_, c, smp, 40, 30, spp=1, seed=4, brute=True)
+    assert ra == rb
+    assert np.array_equal(a.M, b.M)
+
+
+def test_kdtree_equals_brute_force_mesh_rays():
+    s, c, smp = scenes.bunny_frame(3000, seed=3)
+    os_ = O.OracleScene(s)
+    rng = np.random.default_rng(0)
+    for _ in range(400):
+        o = rng.uniform(-2, 3, 3)
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        assert os_.intersect(o, d) == os_.intersect(o, d, brute=True)
+
+
+def test_welford_matches_mean_var():
+    s, c, smp = scenes.simplesphere()
+    smp.MaxBounces = 2
+    buf, _ = O.render(O.OracleScene(s), c, smp, 16, 12, spp=1, passes=6, seed=5)
+    # recompute each pass independently and compare mean / unbiased variance
+    os_ = O.OracleScene(s)
+    samples = []
+    for p in range(1, 7):
+        b, _ = O.render(os_, c, smp, 16, 12, spp=1, passes=1, seed=5, first_pass=p)
+        samples.append(b.M)
+    S = np.stack(samples)
+    assert np.allclose(buf.M, S.mean(axis=0), rtol=1e-12, atol=1e-12)
+    assert np.allclose(buf.V / 5, S.var(axis=0, ddof=1), rtol=1e-9, atol=1e-12)
+
+
+def test_tiles_partition_bit_identical():
+    from ptsharp_amd import tiles_for_rank
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 3
+    os_ = O.OracleScene(s)
+    w, h = 70, 40
+    full, rf = O.render(os_, c, smp, w, h, spp=1, seed=8)
+    parts = [O.render(os_, c, smp, w, h, spp=1, seed=8, tiles=tiles_for_rank(w, h, r, 3)) for r in range(3)]
+    assert sum(p[1] for p in parts) == rf
+    assert np.array_equal(sum(p[0].M for p in parts), full.M)
+    assert np.array_equal(sum(p[0].N for p in parts), full.N)
+
+
+def test_light_identity_struct_triangle_never_lights():
+    """A directly-added emissive Triangle is in Scene.Lights but never passes hit.Shape != light."""
+    from ptsharp_amd import Triangle
+    s = Scene()
+    s.Add(Cube.NewCube(Vector(-5, -1, -5), Vector(5, 0, 5), Material.DiffuseMaterial(Colour(0.8, 0.8, 0.8))))
+    tri = Triangle.NewTriangle(Vector(-1, 2, -1), Vector(1, 2, -1), Vector(0, 2, 1),
+                               material=Material.LightMaterial(Colour.White, 10))
+    s.Add(tri)
+    assert len(s.Lights) == 1
+    c = Camera.LookAt(Vector(0, 1, 4), Vector(0, 0, 0), Vector(0, 1, 0), 50)
+    smp = DefaultSampler.NewSampler(1, 0)   # no bounces: floor colour is direct light only
+    buf, _ = O.render(O.OracleScene(s), c, smp, 32, 24, spp=1, seed=1)
+    floor = buf.M[buf.N > 0]
+    lit = (floor > 0).any(axis=1)
+    # the only non-zero pixels are the (emissive) triangle seen by the camera
+    assert lit.sum() < floor.shape[0] * 0.5
+    s2 = Scene()
+    s2.Add(Cube.NewCube(Vector(-5, -1, -5), Vector(5, 0, 5), Material.DiffuseMaterial(Colour(0.8, 0.8, 0.8))))
+    s2.Add(Sphere.NewSphere(Vector(0, 2, 0), 0.5, Material.LightMaterial(Colour.White, 10)))
+    buf2, _ = O.render(O.OracleScene(s2), c, smp, 32, 24, spp=1, seed=1)
+    assert (buf2.M > 0).any(axis=2).mean() > 0.5  # a sphere light does light the floor
