@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     p.add_argument("--no-parity", action="store_true")
+    p.add_argument("--engine", choices=["auto", "mega", "wave"], default="auto")
     p.add_argument("--json-out", default=None)
     return p.parse_args()
 
@@ -74,6 +75,7 @@ def main():
     r = Renderer.NewRenderer(scene, camera, sampler, W, H, True, device=local)
     r.SamplesPerPixel = a.spp
     r.Seed = a.seed
+    r.Engine = {"auto": 0, "mega": 1, "wave": 2}[a.engine]
     if world > 1:
         r.Tiles = tiles_for_rank(W, H, rank, world)
         obj = [Renderer.CommUniqueId() if rank == 0 else None]
@@ -151,7 +153,7 @@ def main():
             "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}",
             "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
             "rays_per_camera_sample": round(total_rays / (W * H * a.spp * a.steps), 3),
-            "scene_build_s": round(t_scene, 3), "bvh_build_ms": round(build_ms, 1), "bvh_bytes": int(bvh_bytes),
+            "engine": a.engine, "scene_build_s": round(t_scene, 3), "bvh_build_ms": round(build_ms, 1), "bvh_bytes": int(bvh_bytes),
         },
         "roofline": {
             "bound": "hbm", "kernel": "k_render_pass<false>",

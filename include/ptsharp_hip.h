@@ -150,7 +150,16 @@ typedef struct pt_pass_params {
     uint32_t pass_index;     /* IterativeRender iteration i (Renderer.cs:709)    */
     int32_t num_tiles;       /* 0 = whole image; else render only these 32x32 tiles */
     const int32_t* tiles;    /* tile id = ty * ceil(W/32) + tx                   */
+    int32_t engine;          /* pt_engine                                        */
+    int32_t _pad;
 } pt_pass_params;
+
+/* Both engines compute identical per-ray arithmetic; they differ in scheduling. */
+typedef enum pt_engine {
+    PT_ENGINE_AUTO = 0,        /* wavefront, megakernel when the queues cannot hold a useful chunk */
+    PT_ENGINE_MEGAKERNEL = 1,  /* one lane per pixel runs the whole sampler recursion */
+    PT_ENGINE_WAVEFRONT = 2    /* depth-by-depth ray queues in HBM (trace / shade / shadow kernels) */
+} pt_engine;
 
 typedef struct pt_device_opts {
     int32_t device;          /* HIP device ordinal */

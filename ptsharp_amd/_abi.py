@@ -21,6 +21,8 @@ PT_ERR_OUT_OF_MEMORY = -5
 PT_ERR_RCCL = -6
 PT_ERR_NO_DEVICE = -7
 
+ENGINE_AUTO, ENGINE_MEGAKERNEL, ENGINE_WAVEFRONT = 0, 1, 2
+
 SHAPE_SPHERE, SHAPE_CUBE, SHAPE_PLANE, SHAPE_TRIANGLE, SHAPE_MESH = 0, 1, 2, 3, 4
 
 _f = C.POINTER(C.c_float)
@@ -60,7 +62,7 @@ class pt_sampler(C.Structure):
 
 class pt_pass_params(C.Structure):
     _fields_ = [("spp", C.c_int32), ("stratified", C.c_int32), ("seed", C.c_uint64), ("pass_index", C.c_uint32),
-                ("num_tiles", C.c_int32), ("tiles", _i)]
+                ("num_tiles", C.c_int32), ("tiles", _i), ("engine", C.c_int32), ("_pad", C.c_int32)]
 
 
 class pt_device_opts(C.Structure):

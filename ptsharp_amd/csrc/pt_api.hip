@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -23,6 +24,7 @@
 #include "pt_bvh.h"
 #include "pt_math.h"
 #include "pt_scene.h"
+#include "pt_wavefront.h"
 
 #pragma clang fp contract(off)
 
@@ -74,7 +76,62 @@ struct Ctx {
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // wavefront queues (allocated on first use, grown on demand)
+    pt::WfQueues Q{};
+    std::vector<DeviceArray> wf_arrays;
+    uint32_t wf_cap = 0, wf_scap = 0;
+    int last_engine = 0;
 };
+
+constexpr uint32_t kWfMaxCap = 1u << 23;   // 8M rays per queue: ~1.5 GB of queues at most
+
+void free_wavefront(Ctx* c) {
+    for (auto& a : c->wf_arrays) a.release();
+    c->wf_arrays.clear();
+    c->Q = pt::WfQueues{};
+    c->wf_cap = c->wf_scap = 0;
+}
+
+template <class T>
+int wf_alloc(Ctx* c, T** out, size_t n) {
+    DeviceArray a;
+    a.bytes = n * sizeof(T);
+    hipError_t e = hipMalloc(&a.ptr, a.bytes);
+    if (e != hipSuccess) return fail(PT_ERR_OUT_OF_MEMORY, std::string("hipMalloc wavefront queues: ") + hipGetErrorString(e));
+    c->wf_arrays.push_back(a);
+    *out = (T*)a.ptr;
+    return PT_OK;
+}
+
+int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
+    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc) return PT_OK;
+    cap = std::max(cap, c->wf_cap);
+    scap = std::max(scap, c->wf_scap);
+    free_wavefront(c);
+    pt::WfQueues Q{};
+    int rc;
+    for (int q = 0; q < 2; q++) {
+        if ((rc = wf_alloc(c, &Q.q_o[q], cap))) return rc;
+        if ((rc = wf_alloc(c, &Q.q_d[q], cap))) return rc;
+        if ((rc = wf_alloc(c, &Q.q_t[q], cap))) return rc;
+        if ((rc = wf_alloc(c, &Q.q_k[q], cap))) return rc;
+    }
+    if ((rc = wf_alloc(c, &Q.hits, cap))) return rc;
+    if ((rc = wf_alloc(c, &Q.s_o, scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.s_d, scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.s_c, scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.counts, 4))) return rc;
+    size_t P = (size_t)c->width * (size_t)c->height;
+    if ((rc = wf_alloc(c, &Q.acc, P * 3))) return rc;
+    PT_HIP(hipMemsetAsync(Q.acc, 0, P * 3 * sizeof(double), c->stream));
+    PT_HIP(hipMemsetAsync(Q.counts, 0, 4 * sizeof(uint32_t), c->stream));
+    Q.cap = cap;
+    Q.s_cap = scap;
+    c->Q = Q;
+    c->wf_cap = cap;
+    c->wf_scap = scap;
+    return PT_OK;
+}
 
 template <class T>
 int upload(Ctx* c, const std::vector<T>& host, const T** out) {
@@ -437,13 +494,50 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     pt::DevPass P{c->width, c->height, pass->spp, pass->stratified, pass->seed, pass->pass_index, tiles_x, d_tiles,
                   num_tiles};
     pt::DevBuffer B{c->d_m, c->d_v, c->d_n, c->d_counters};
+    // ---- engine choice and wavefront plan
+    const int n_root = (int)std::sqrt((double)sampler->first_hit_samples);
+    const int nm_root = (sampler->specular_mode != PT_SPEC_NAIVE) ? 2 : 1;
+    const int nm = sampler->specular_mode == PT_SPEC_ALL ? 2 : 1;
+    pt::WfPlan plan{};
+    plan.root_children = (uint32_t)std::max(1, n_root * n_root * nm_root);
+    plan.children = (uint32_t)nm;
+    plan.lights_per_child = (uint32_t)(sampler->light_mode == PT_LIGHT_ALL ? std::max(1, c->S.num_lights) : 1);
+    plan.trace_blocks = 256 * 8;
+    plan.shade_blocks = 256 * 8;
+    const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp);
+    double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)
+    if (nm == 2) growth = std::ldexp(1.0, std::min(std::max(sampler->max_bounces - 1, 0), 60));
+    const double per_sample = (double)plan.root_children * growth * (double)plan.lights_per_child;
+    uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples, std::floor((double)kWfMaxCap / per_sample));
+    int engine = pass->engine;
+    if (engine == PT_ENGINE_AUTO) engine = chunk >= 4096 || chunk >= cam_samples ? PT_ENGINE_WAVEFRONT : PT_ENGINE_MEGAKERNEL;
+    if (engine == PT_ENGINE_WAVEFRONT && chunk < 1)
+        return fail(PT_ERR_UNSUPPORTED, "wavefront queues cannot hold one camera sample of this sampler (use the megakernel)");
+    if (engine != PT_ENGINE_WAVEFRONT && engine != PT_ENGINE_MEGAKERNEL) return fail(PT_ERR_INVALID_ARG, "bad engine");
+    if (engine == PT_ENGINE_WAVEFRONT) {
+        plan.chunk = chunk;
+        const double rays_needed = (double)chunk * (double)plan.root_children * growth;
+        uint32_t cap = (uint32_t)std::min<double>((double)kWfMaxCap, std::max(65536.0, std::max((double)chunk, rays_needed)));
+        uint32_t scap = (uint32_t)std::min<double>((double)kWfMaxCap, std::max(65536.0, rays_needed * plan.lights_per_child));
+        int rc = ensure_wavefront(c, cap, scap);
+        if (rc) return rc;
+    }
+    c->last_engine = engine;
     PT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
     PT_HIP(hipEventRecord(c->ev0, c->stream));
-    PT_HIP(pt::launch_render_pass(c->S, cam, smp, P, B, num_tiles, counted != nullptr, c->stream));
+    if (engine == PT_ENGINE_WAVEFRONT)
+        PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream));
+    else
+        PT_HIP(pt::launch_render_pass(c->S, cam, smp, P, B, num_tiles, counted != nullptr, c->stream));
     PT_HIP(hipEventRecord(c->ev1, c->stream));
     unsigned long long ctr[8];
     PT_HIP(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
+    if (engine == PT_ENGINE_WAVEFRONT) {
+        uint32_t flags[4];
+        PT_HIP(hipMemcpy(flags, c->Q.counts, sizeof flags, hipMemcpyDeviceToHost));
+        if (flags[3]) return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
+    }
     float ms = 0.f;
     PT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->stats.rays = ctr[0];
@@ -504,6 +598,7 @@ void pt_destroy(void* ctx) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
     free_scene(c);
+    free_wavefront(c);
     if (c->d_m) (void)hipFree(c->d_m);
     if (c->d_v) (void)hipFree(c->d_v);
     if (c->d_n) (void)hipFree(c->d_n);

@@ -1,0 +1,348 @@
+// pt_device.h — device functions shared by both render engines (the per-pixel
+// megakernel in pt_render.hip and the wavefront kernels in pt_wavefront.hip),
+// so both run bit-identical arithmetic for every Scene.Intersect, Hit.Info,
+// Ray.Bounce and sampleLight.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pt_bvh.h"
+#include "pt_math.h"
+#include "pt_scene.h"
+
+#pragma clang fp contract(off)
+
+namespace pt {
+
+struct HitRec {
+    double t;
+    int32_t kind;   // KIND_* of the primitive hit; -1 = miss
+    int32_t idx;    // record position: tri_recs / ana_recs / planes
+};
+
+struct Counters {
+    uint32_t rays, nodes, prims, shades;
+};
+
+__device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
+
+// Conservative fp32 slab test: (b - o) * (1/d) carries <= 3 ulp of relative error,
+// so the far distance is widened by 2^-21 relative; NaN slabs (o on a plane with
+// d = 0) drop out of fminf/fmaxf, which only widens the interval.
+__device__ __forceinline__ bool slab(float4 lo, float4 hi, v3 o, v3 invd, float tmax, float& tentry) {
+    float tx1 = (lo.x - o.x) * invd.x, tx2 = (hi.x - o.x) * invd.x;
+    float ty1 = (lo.y - o.y) * invd.y, ty2 = (hi.y - o.y) * invd.y;
+    float tz1 = (lo.z - o.z) * invd.z, tz2 = (hi.z - o.z) * invd.z;
+    float tn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fmaxf(fminf(tz1, tz2), 0.0f));
+    float tf = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fminf(fmaxf(tz1, tz2), tmax));
+    tentry = tn;
+    return tn <= tf * 1.0000005f;
+}
+
+// Round a hit distance up so the fp32 cull never drops an equal-t candidate.
+__device__ __forceinline__ float tmax_bound(double t) {
+    float f = (float)t;
+    return (double)f < t ? __uint_as_float(f2u(f) + 1u) : f;
+}
+
+// Intersect one record; returns t (kHitInf = miss) and the primitive kind.
+template <bool TRI>
+__device__ __forceinline__ double prim_t(const float4* __restrict__ recs, uint32_t pos, v3 o, v3 d, int32_t& kind) {
+    const float4* r = recs + 3 * (size_t)pos;
+    if (TRI) {
+        float4 a = r[0], b = r[1], c = r[2];
+        kind = KIND_TRI;
+        return isect_tri(v3{a.x, a.y, a.z}, v3{a.w, b.x, b.y}, v3{b.z, b.w, c.x}, o, d);
+    }
+    float4 a = r[0], b = r[1];
+    kind = (int32_t)f2u(a.w);
+    if (kind == KIND_SPHERE) {
+        float4 c = r[2];
+        double radius = __hiloint2double((int)f2u(c.z), (int)f2u(c.y));
+        return isect_sphere(v3{a.x, a.y, a.z}, radius, o, d);
+    }
+    return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+}
+
+// Stack-based BVH2 traversal.  A child pair is fetched together (64 B, one
+// line); the nearer child is descended, the farther pushed on the per-lane LDS
+// stack (`stack` points at this lane's column, entries STRIDE words apart).
+// Node ref (host encoding, pt_api.hip): bit31 = 0 → inner, value = index of the
+// pair's left node; bit31 = 1 → leaf, bits 29..30 = count-1, bits 0..28 = first.
+// ANY: stop at the first primitive with t < best.t (shadow visibility).
+template <bool TRI, bool COUNT, bool ANY, int STRIDE>
+__device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32_t num_nodes,
+                                         const float4* __restrict__ recs, v3 o, v3 d, v3 invd, HitRec& best,
+                                         uint32_t* __restrict__ stack, Counters& ctr) {
+    if (num_nodes <= 0) return false;
+    float4 r0 = nodes[0], r1 = nodes[1];
+    float te;
+    if (!slab(r0, r1, o, invd, tmax_bound(best.t), te)) return false;
+    uint32_t ref = f2u(r0.w);
+    int sp = 0;
+    for (;;) {
+        if (!(ref & 0x80000000u)) {
+            const float4* c = nodes + 2 * (size_t)ref;
+            float4 l0 = c[0], l1 = c[1], q0 = c[2], q1 = c[3];
+            if (COUNT) ctr.nodes++;
+            float tmax = tmax_bound(best.t);
+            float tl, tr;
+            bool hl = slab(l0, l1, o, invd, tmax, tl);
+            bool hr = slab(q0, q1, o, invd, tmax, tr);
+            if (hl && hr) {
+                uint32_t nearr = f2u(l0.w), farr = f2u(q0.w);
+                if (tr < tl) { uint32_t s = nearr; nearr = farr; farr = s; }
+                stack[sp * STRIDE] = farr;
+                sp++;
+                ref = nearr;
+                continue;
+            }
+            if (hl) { ref = f2u(l0.w); continue; }
+            if (hr) { ref = f2u(q0.w); continue; }
+        } else {
+            const uint32_t first = ref & 0x1FFFFFFFu, cnt = ((ref >> 29) & 3u) + 1u;
+            for (uint32_t k = 0; k < cnt; k++) {
+                if (COUNT) ctr.prims++;
+                int32_t kind;
+                double t = prim_t<TRI>(recs, first + k, o, d, kind);
+                if (t < best.t) {
+                    if (ANY) return true;
+                    best.t = t; best.kind = kind; best.idx = (int32_t)(first + k);
+                }
+            }
+        }
+        if (sp == 0) break;
+        sp--;
+        ref = stack[sp * STRIDE];
+    }
+    return false;
+}
+
+// Scene.Intersect (Scene.cs:75-79): closest hit over planes, analytic BVH, triangle BVH.
+template <bool COUNT, int STRIDE>
+__device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, uint32_t* stack, Counters& ctr) {
+    ctr.rays++;
+    HitRec best{kHitInf, -1, -1};
+    for (int i = 0; i < S.num_planes; i++) {
+        float4 a = S.planes[2 * i], b = S.planes[2 * i + 1];
+        double t = isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+        if (t < best.t) { best.t = t; best.kind = KIND_PLANE; best.idx = i; }
+    }
+    v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    traverse<false, COUNT, false, STRIDE>(S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
+    traverse<true, COUNT, false, STRIDE>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr);
+    return best;
+}
+
+// t of the light's own primitive along (o, d), exactly as the closest-hit query computes it.
+__device__ __forceinline__ double light_t(const DevScene& S, const DevLight& L, v3 o, v3 d) {
+    if (L.kind == KIND_PLANE) {
+        float4 a = S.planes[2 * L.index], b = S.planes[2 * L.index + 1];
+        return isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+    }
+    int32_t kind;
+    return prim_t<false>(S.ana_recs, (uint32_t)L.index, o, d, kind);
+}
+
+// Shadow visibility (Sampler.cs:261-265): the reference takes the nearest hit and
+// compares it with the light by reference.  Equivalent query: the light's own t,
+// then "is any primitive strictly nearer" (any-hit, early exit).  Counts one ray.
+template <bool COUNT, int STRIDE>
+__device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight& L, v3 o, v3 d, uint32_t* stack,
+                                              Counters& ctr) {
+    ctr.rays++;
+    if (L.phantom) {
+        // a struct Triangle light never equals the re-boxed hit shape; the reference still
+        // traces the ray, so trace it (the answer is "not visible" either way)
+        HitRec h{kHitInf, -1, -1};
+        v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        traverse<true, COUNT, true, STRIDE>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, h, stack, ctr);
+        return false;
+    }
+    double tl = light_t(S, L, o, d);
+    if (!(tl < kHitInf)) return false;
+    HitRec best{tl, -1, -1};
+    for (int i = 0; i < S.num_planes; i++) {
+        float4 a = S.planes[2 * i], b = S.planes[2 * i + 1];
+        if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
+    }
+    v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    if (traverse<false, COUNT, true, STRIDE>(S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr))
+        return false;
+    if (traverse<true, COUNT, true, STRIDE>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr))
+        return false;
+    return true;
+}
+
+struct Shade {
+    v3 pos, nrm;
+    int32_t mat;
+    int32_t inside;
+};
+
+// Hit.Info (Hit.cs:26-55): position (fp32 re-rounded), NormalAt, MaterialAt, flip.
+template <bool COUNT>
+__device__ __forceinline__ Shade hit_info(const DevScene& S, const HitRec& h, v3 o, v3 d, Counters& ctr) {
+    Shade s;
+    s.pos = add(o, muls(d, h.t));
+    v3 n;
+    if (h.kind == KIND_TRI) {
+        if (COUNT) ctr.shades++;
+        const float4* r = S.tri_recs + 3 * (size_t)h.idx;
+        const float4* q = S.tri_shade + 3 * (size_t)h.idx;
+        float4 a = r[0], b = r[1], c = r[2];
+        float4 x = q[0], y = q[1], z = q[2];
+        n = tri_normal(v3{a.x, a.y, a.z}, v3{a.w, b.x, b.y}, v3{b.z, b.w, c.x}, v3{x.x, x.y, x.z},
+                       v3{x.w, y.x, y.y}, v3{y.z, y.w, z.x}, s.pos);
+        s.mat = (int32_t)f2u(z.y);
+    } else if (h.kind == KIND_PLANE) {
+        float4 a = S.planes[2 * h.idx], b = S.planes[2 * h.idx + 1];
+        n = v3{b.x, b.y, b.z};
+        s.mat = (int32_t)f2u(a.w);
+    } else {
+        const float4* r = S.ana_recs + 3 * (size_t)h.idx;
+        float4 a = r[0], b = r[1], c = r[2];
+        if (h.kind == KIND_SPHERE) n = normalize(sub(s.pos, v3{a.x, a.y, a.z}));   // Sphere.NormalAt
+        else n = cube_normal(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, s.pos);           // Cube.NormalAt
+        s.mat = (int32_t)f2u(c.x);
+    }
+    s.inside = 0;
+    if (dot(n, d) > 0) { n = neg(n); s.inside = 1; }
+    s.nrm = n;
+    return s;
+}
+
+// Util.Cone (Util.cs:17-32)
+__device__ __forceinline__ v3 cone(v3 direction, double theta, double u, double v, uint64_t key) {
+    if (theta < kEps) return direction;
+    theta = theta * (1 - (2 * acos(u) / kPi));
+    double m1 = sin(theta);
+    double m2 = cos(theta);
+    double a = v * 2 * kPi;
+    v3 q = random_unit_vector(key, D_RUV_Z, D_RUV_A);
+    v3 s = cross(direction, q);
+    v3 t = cross(direction, s);
+    v3 dd = add(add(add(zero3(), muls(s, m1 * cos(a))), muls(t, m1 * sin(a))), muls(direction, m2));
+    return normalize(dd);
+}
+
+// Ray.Bounce (Ray.cs:44-85); btype 0 Any, 1 Diffuse, 2 Specular.  Returns the new
+// ray in (no, nd); `reflected` and `p` as the reference's tuple.
+__device__ __forceinline__ void bounce(const DevMaterial& m, const Shade& sh, v3 indir, double u, double v, int btype,
+                                       uint64_t key, v3& no, v3& nd, bool& reflected, double& p) {
+    double n1 = 1.0, n2 = m.index;
+    if (sh.inside) { double t = n1; n1 = n2; n2 = t; }
+    p = m.reflectivity >= 0 ? m.reflectivity : reflectance(sh.nrm, indir, n1, n2);
+    bool refl = btype == 2 || (btype == 0 && draw(key, D_REFLECT) < p);
+    if (refl) {
+        no = sh.pos;
+        nd = cone(reflect(sh.nrm, indir), m.gloss, u, v, key);
+        reflected = true;
+    } else if (m.transparent) {
+        v3 rd = refract(sh.nrm, indir, n1, n2);
+        no = add(sh.pos, muls(rd, 1e-4));
+        nd = cone(rd, m.gloss, u, v, key);
+        reflected = true;
+        p = 1 - p;
+    } else {
+        // Ray.WeightedBounce (Ray.cs:28-35) around the normal
+        double radius = sqrt(u);
+        double theta = 2 * kPi * v;
+        v3 s = normalize(cross(sh.nrm, random_unit_vector(key, D_RUV_Z, D_RUV_A)));
+        v3 t = cross(sh.nrm, s);
+        no = sh.pos;
+        nd = add(add(add(zero3(), muls(s, radius * cos(theta))), muls(t, radius * sin(theta))),
+                 muls(sh.nrm, sqrt(1 - u)));
+        reflected = false;
+        p = 1 - p;
+    }
+}
+
+// Sampler.sampleLight (Sampler.cs:212-296) up to the shadow query: the sampled
+// direction and the colour the light contributes if it is the nearest hit
+// (coverage depends only on the light centre/radius, so it is computed here).
+// Returns false when diffuse <= 0 (no shadow ray is cast).
+__device__ __forceinline__ bool light_setup(const DevScene& S, const DevSampler& smp, const DevLight& L, v3 o, v3 n,
+                                            uint64_t key, v3& dir, float3& contrib) {
+    v3 center{L.center[0], L.center[1], L.center[2]};
+    double radius = L.radius;
+    v3 point = center;
+    if (smp.ss) {
+        for (uint32_t k = 0; k < 256; k++) {
+            double x = draw(key, D_SS_XY + 2 * k) * 2 - 1;
+            double y = draw(key, D_SS_XY + 2 * k + 1) * 2 - 1;
+            if (x * x + y * y <= 1) {
+                v3 l = normalize(sub(center, o));
+                v3 u = normalize(cross(l, random_unit_vector(key, D_SS_RUV_Z, D_SS_RUV_A)));
+                v3 v = cross(l, u);
+                point = add(add(center, muls(u, x * radius)), muls(v, y * radius));
+                break;
+            }
+        }
+    }
+    dir = normalize(sub(point, o));
+    double diffuse = dot(dir, n);
+    if (diffuse <= 0) return false;
+    double hyp = (double)lengthf(sub(center, o));
+    double theta = asin(radius / hyp);
+    double adj = radius / tan(theta);
+    double dd = cos(theta) * adj;
+    double rr = sin(theta) * adj;
+    double coverage = (rr * rr) / (dd * dd);
+    if (hyp < radius) coverage = 1;
+    coverage = net_min(coverage, 1);
+    const DevMaterial& m = S.mats[L.mat];
+    float mm = (float)((double)m.emittance * diffuse * coverage);
+    contrib = make_float3(m.color[0] * mm, m.color[1] * mm, m.color[2] * mm);
+    return true;
+}
+
+// Camera.CastRay (Camera.cs:98-119), u/v as passed by RenderParallel (jitter bug kept).
+__device__ __forceinline__ void cast_ray(const DevCamera& cam, int x, int y, int w, int h, double u, double v,
+                                         uint64_t key, v3& o, v3& d) {
+    double aspect = w / (double)h;
+    double px = ((x + u - 0.5) / (w - 1.0)) * 2 - 1;
+    double py = ((y + v - 0.5) / (h - 1.0)) * 2 - 1;
+    v3 cu{cam.u[0], cam.u[1], cam.u[2]}, cv{cam.v[0], cam.v[1], cam.v[2]};
+    v3 cw{cam.w[0], cam.w[1], cam.w[2]}, cp{cam.p[0], cam.p[1], cam.p[2]};
+    d = normalize(add(add(add(zero3(), muls(cu, -px * aspect)), muls(cv, -py)), muls(cw, cam.m)));
+    o = cp;
+    if (cam.aperture_radius > 0) {
+        v3 focal = add(cp, muls(d, cam.focal_distance));
+        double angle = draw(key, D_LENS_ANGLE) * 2 * kPi;
+        double radius = draw(key, D_LENS_RADIUS) * cam.aperture_radius;
+        o = add(o, muls(cu, cos(angle) * radius));
+        o = add(o, muls(cv, sin(angle) * radius));
+        d = normalize(sub(focal, o));
+    }
+}
+
+// Pixel.AddSample (Buffer.cs:33-44)
+__device__ __forceinline__ void welford(const DevBuffer& B, size_t i, double r, double g, double b) {
+    int32_t n = B.n[i] + 1;
+    B.n[i] = n;
+    double* M = B.m + 3 * i;
+    double* V = B.v + 3 * i;
+    if (n == 1) { M[0] = r; M[1] = g; M[2] = b; return; }
+    double s[3] = {r, g, b};
+    for (int k = 0; k < 3; k++) {
+        double mo = M[k];
+        double mn = mo + (s[k] - mo) / (double)n;
+        V[k] = V[k] + (s[k] - mo) * (s[k] - mn);
+        M[k] = mn;
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Pixel (x, y) of slot `local` (0..1023) of a 32x32 tile: 8x8 blocks per wave,
+// 16x16 quarters, so consecutive slots are screen-space neighbours.
+__device__ __forceinline__ void tile_pixel(int tile, int local, int tiles_x, int& x, int& y) {
+    const int quarter = local >> 8, wave = (local >> 6) & 3, lane = local & 63;
+    x = (tile % tiles_x) * 32 + (quarter & 1) * 16 + (wave & 1) * 8 + (lane & 7);
+    y = (tile / tiles_x) * 32 + (quarter >> 1) * 16 + (wave >> 1) * 8 + (lane >> 3);
+}
+
+}  // namespace pt

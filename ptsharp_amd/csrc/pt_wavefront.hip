@@ -1,0 +1,322 @@
+// pt_wavefront.hip — wavefront engine for PTSharp's render hot path on gfx950.
+//
+// The per-pixel megakernel (pt_render.hip) carries the whole sampler state and
+// both traversal stacks in one kernel, which costs ~240 VGPRs (2 waves/SIMD).
+// Here the recursion of DefaultSampler.sample (Sampler.cs:55-145) is unrolled
+// by depth into queues in HBM:
+//
+//   k_wf_camera   camera samples → extension rays, depth 0      (Renderer.cs:294-305, Camera.cs:98-119)
+//   k_wf_trace    closest hit for every queued ray               (Scene.Intersect, Scene.cs:75-79)
+//   k_wf_shade    Hit.Info, emission, and every child of the vertex: Ray.Bounce →
+//                 next-depth extension ray, sampleLights → shadow ray
+//                                                                (Sampler.cs:62-131, Ray.cs:44-85)
+//   k_wf_shadow   shadow visibility (nearest-hit == light ⇔ no primitive nearer
+//                 than the light's own t: any-hit, early exit)   (Sampler.cs:255-296)
+//   k_wf_finalize per-pixel mean of the pass → Welford           (Renderer.cs:308-309, Buffer.cs:33-44)
+//
+// The traversal kernels keep only ray + stack state, so they run at the
+// occupancy the LDS stack allows.  Queue appends are wave-aggregated atomics;
+// per-pixel contributions are fp64 atomics into a frame accumulator (a path's
+// contributions are summed in a different order than the recursion, which is
+// linear, so only the last fp64 bits can differ).
+#include <hip/hip_runtime.h>
+
+#include "pt_device.h"
+#include "pt_wavefront.h"
+
+#pragma clang fp contract(off)
+
+namespace pt {
+
+constexpr int kTB = 256;   // threads per block, traversal kernels (LDS stack column stride)
+
+// Streaming (nt) accesses for queue traffic: read or written once per depth, they
+// should not displace the BVH from L2 / the Infinity Cache.
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void nt_store(float4* p, float4 v) {
+    f4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, (f4v*)p);
+}
+__device__ __forceinline__ void nt_store(uint4* p, uint4 v) {
+    u4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, (u4v*)p);
+}
+__device__ __forceinline__ void nt_store(uint64_t* p, uint64_t v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ float4 nt_load(const float4* p) {
+    f4v x = __builtin_nontemporal_load((const f4v*)p);
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ uint4 nt_load(const uint4* p) {
+    u4v x = __builtin_nontemporal_load((const u4v*)p);
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ uint64_t nt_load(const uint64_t* p) { return __builtin_nontemporal_load(p); }
+
+__device__ __forceinline__ uint32_t append(uint32_t* counter) {
+    return atomicAdd(counter, 1u);  // hipcc aggregates a uniform +1 into one atomic per wave
+}
+
+__device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, float3 thr, uint32_t pixel,
+                                          uint32_t meta, uint64_t key) {
+    nt_store(&Q.q_o[q][i], make_float4(o.x, o.y, o.z, __uint_as_float(pixel)));
+    nt_store(&Q.q_d[q][i], make_float4(d.x, d.y, d.z, __uint_as_float(meta)));
+    nt_store(&Q.q_t[q][i], make_float4(thr.x, thr.y, thr.z, 0.f));
+    nt_store(&Q.q_k[q][i], key);
+}
+
+__device__ __forceinline__ void acc_add(double* acc, uint32_t pixel, float r, float g, float b) {
+    double* a = acc + 3 * (size_t)pixel;
+    if (r != 0.f) atomicAdd(a + 0, (double)r);
+    if (g != 0.f) atomicAdd(a + 1, (double)g);
+    if (b != 0.f) atomicAdd(a + 2, (double)b);
+}
+
+// ---------------------------------------------------------------- camera
+__global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQueues Q, uint64_t begin,
+                                                   uint32_t count, int32_t spp_launch, int32_t sample_base) {
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < count; g += gridDim.x * blockDim.x) {
+        const uint64_t slot = begin + g;
+        const uint64_t pslot = slot / (uint64_t)spp_launch;
+        const int s = (int)(slot % (uint64_t)spp_launch);
+        const int tile_slot = (int)(pslot >> 10);
+        const int tile = P.tiles ? P.tiles[tile_slot] : tile_slot;
+        int x, y;
+        tile_pixel(tile, (int)(pslot & 1023), P.tiles_x, x, y);
+        if (x >= P.width || y >= P.height) continue;
+        const int w = P.width, h = P.height;
+        const uint64_t pix = (uint64_t)y * (uint64_t)w + (uint64_t)x;
+        v3 o, d;
+        uint64_t K;
+        if (P.stratified) {
+            const int sample = sample_base + s;
+            const int root = (int)sqrt((double)P.spp);
+            const int u = sample / root, v = sample % root;
+            K = camera_key(P.seed, P.pass_index, pix, (uint32_t)sample);
+            cast_ray(cam, x, y, w, h, ((double)u + 0.5) / (double)root, ((double)v + 0.5) / (double)root, K, o, d);
+        } else {
+            K = camera_key(P.seed, P.pass_index, pix, (uint32_t)s);
+            double fu = (x + draw(K, D_JX)) / w;   // RenderParallel's jitter (Renderer.cs:297-302)
+            double fv = (y + draw(K, D_JY)) / h;
+            cast_ray(cam, x, y, w, h, fu, fv, K, o, d);
+        }
+        const uint32_t i = append(&Q.counts[0]);
+        if (i >= Q.cap) { Q.counts[3] = 1; continue; }
+        ray_store(Q, 0, i, o, d, make_float3(1.f, 1.f, 1.f), (uint32_t)pix, 0u | (1u << 8), K);
+    }
+}
+
+// ---------------------------------------------------------------- closest hit
+template <bool COUNT>
+__global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+    __shared__ uint32_t s_stack[kMaxDepth * kTB];
+    uint32_t* stack = s_stack + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // the next-depth queue and the shadow queue are free now: reset them for k_wf_shade
+        Q.counts[1 - qi] = 0;
+        Q.counts[2] = 0;
+    }
+    const uint32_t n = Q.counts[qi] < Q.cap ? Q.counts[qi] : Q.cap;
+    Counters ctr{0, 0, 0, 0};
+    for (uint32_t i = blockIdx.x * kTB + threadIdx.x; i < n; i += gridDim.x * kTB) {
+        float4 a = nt_load(&Q.q_o[qi][i]);
+        float4 b = nt_load(&Q.q_d[qi][i]);
+        HitRec h = trace<COUNT, kTB>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+        unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
+        nt_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t rays = wave_sum(ctr.rays);
+    if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
+    if (COUNT) {
+        uint32_t nodes = wave_sum(ctr.nodes), prims = wave_sum(ctr.prims);
+        if (lane == 0) {
+            atomicAdd(&counters[1], (unsigned long long)nodes);
+            atomicAdd(&counters[2], (unsigned long long)prims);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- shade / bounce
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
+                                                  unsigned long long* counters) {
+    const uint32_t n = Q.counts[qi] < Q.cap ? Q.counts[qi] : Q.cap;
+    const int qo = 1 - qi;
+    Counters ctr{0, 0, 0, 0};
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        float4 ro = nt_load(&Q.q_o[qi][i]);
+        float4 rd = nt_load(&Q.q_d[qi][i]);
+        float4 rt = nt_load(&Q.q_t[qi][i]);
+        uint4 hr = nt_load(&Q.hits[i]);
+        const uint32_t pixel = __float_as_uint(ro.w);
+        const uint32_t meta = __float_as_uint(rd.w);
+        const int depth = (int)(meta & 0xFF);
+        const bool emission = (meta >> 8) & 1;
+        HitRec h;
+        h.t = __longlong_as_double((long long)(((unsigned long long)hr.y << 32) | hr.x));
+        h.kind = (int32_t)hr.z;
+        h.idx = (int32_t)hr.w;
+        const float thr[3] = {rt.x, rt.y, rt.z};
+        if (!(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67)
+            acc_add(Q.acc, pixel, thr[0] * S.env[0], thr[1] * S.env[1], thr[2] * S.env[2]);
+            continue;
+        }
+        const uint64_t node = nt_load(&Q.q_k[qi][i]);
+        const v3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z};
+        Shade sh = hit_info<COUNT>(S, h, o, d, ctr);
+        const DevMaterial& m = S.mats[sh.mat];
+        const int samples = depth == 0 ? smp.fh : 1;
+        const int nn = (int)sqrt((double)samples);
+        const float inv_n2 = 1.0f / (float)(nn * nn);
+        if (m.emittance > 0) {
+            if (smp.dl && !emission) continue;  // Sampler.cs:75-78
+            float e = (float)((double)m.emittance * samples) * inv_n2;
+            acc_add(Q.acc, pixel, thr[0] * m.color[0] * e, thr[1] * m.color[1] * e, thr[2] * m.color[2] * e);
+        }
+        const int nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
+        const int nch = nn * nn * nm;
+        const float t2[3] = {thr[0] * inv_n2, thr[1] * inv_n2, thr[2] * inv_n2};
+        const int ma = nm == 2 ? 1 : 0;
+        for (int c = 0; c < nch; c++) {
+            const int mode = ma + c % nm;
+            const int stratum = c / nm;
+            const int u = stratum / nn, v = stratum % nn;
+            const uint64_t E = child_key(node, (uint32_t)c);
+            const double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)nn;
+            const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
+            v3 no, nd;
+            bool reflected;
+            double p;
+            bounce(m, sh, d, fu, fv, mode, E, no, nd, reflected, p);
+            if (mode == 0) p = 1;
+            if (!(p > 0)) continue;
+            const float fp = (float)p;
+            float w[3];
+            if (reflected) {
+                for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * m.color[k]);
+            } else {
+                for (int k = 0; k < 3; k++) w[k] = fp * m.color[k];
+                if (smp.dl && S.num_lights > 0) {  // sampleLights (Sampler.cs:191-210)
+                    const int nl = S.num_lights;
+                    const bool all = smp.light_mode == 1;
+                    const int first = all ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
+                    const int last = all ? nl : first + 1;
+                    const float scale = all ? 1.0f / (float)nl : (float)nl;
+                    for (int li = first; li < last; li++) {
+                        const uint64_t LK = all ? light_key(E, (uint32_t)li) : E;
+                        v3 ldir;
+                        float3 lc;
+                        if (!light_setup(S, smp, S.lights[li], sh.pos, sh.nrm, LK, ldir, lc)) continue;
+                        const uint32_t si = append(&Q.counts[2]);
+                        if (si >= Q.s_cap) { Q.counts[3] = 1; continue; }
+                        nt_store(&Q.s_o[si], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
+                        nt_store(&Q.s_d[si], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float((uint32_t)li)));
+                        nt_store(&Q.s_c[si], make_float4(t2[0] * w[0] * (lc.x * scale), t2[1] * w[1] * (lc.y * scale),
+                                                                t2[2] * w[2] * (lc.z * scale), 0.f));
+                    }
+                }
+            }
+            if (depth + 1 > smp.mb) continue;  // sample() at depth > MaxBounces returns black, no Intersect
+            const uint32_t j = append(&Q.counts[qo]);
+            if (j >= Q.cap) { Q.counts[3] = 1; continue; }
+            ray_store(Q, qo, j, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
+                      (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
+        }
+    }
+    if (COUNT) {
+        uint32_t shades = wave_sum(ctr.shades);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&counters[3], (unsigned long long)shades);
+    }
+}
+
+// ---------------------------------------------------------------- shadow rays
+template <bool COUNT>
+__global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, unsigned long long* counters) {
+    __shared__ uint32_t s_stack[kMaxDepth * kTB];
+    uint32_t* stack = s_stack + threadIdx.x;
+    const uint32_t n = Q.counts[2] < Q.s_cap ? Q.counts[2] : Q.s_cap;
+    Counters ctr{0, 0, 0, 0};
+    for (uint32_t i = blockIdx.x * kTB + threadIdx.x; i < n; i += gridDim.x * kTB) {
+        float4 a = nt_load(&Q.s_o[i]);
+        float4 b = nt_load(&Q.s_d[i]);
+        const DevLight L = S.lights[__float_as_uint(b.w)];
+        if (light_visible<COUNT, kTB>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) {
+            float4 c = nt_load(&Q.s_c[i]);
+            acc_add(Q.acc, __float_as_uint(a.w), c.x, c.y, c.z);
+        }
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t rays = wave_sum(ctr.rays);
+    if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
+    if (COUNT) {
+        uint32_t nodes = wave_sum(ctr.nodes), prims = wave_sum(ctr.prims);
+        if (lane == 0) {
+            atomicAdd(&counters[1], (unsigned long long)nodes);
+            atomicAdd(&counters[2], (unsigned long long)prims);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- Welford
+__global__ __launch_bounds__(256) void k_wf_finalize(DevPass P, DevBuffer B, WfQueues Q, double inv_spp) {
+    const uint32_t total = (uint32_t)P.num_tiles * 1024u;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < total; s += gridDim.x * blockDim.x) {
+        const int tile = P.tiles ? P.tiles[s >> 10] : (int)(s >> 10);
+        int x, y;
+        tile_pixel(tile, (int)(s & 1023), P.tiles_x, x, y);
+        if (x >= P.width || y >= P.height) continue;
+        const size_t pix = (size_t)y * (size_t)P.width + (size_t)x;
+        double* a = Q.acc + 3 * pix;
+        // c /= spp (Renderer.cs:308) then Buffer.AddSample
+        welford(B, pix, a[0] * inv_spp, a[1] * inv_spp, a[2] * inv_spp);
+        a[0] = 0.0; a[1] = 0.0; a[2] = 0.0;
+    }
+}
+
+// ---------------------------------------------------------------- host driver
+static unsigned grid_for(uint64_t items, unsigned block, unsigned cap_blocks) {
+    uint64_t g = (items + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap_blocks) g = cap_blocks;
+    return (unsigned)g;
+}
+
+hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
+                          const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream) {
+    const uint64_t pix_slots = (uint64_t)P.num_tiles * 1024u;
+    const int rounds = P.stratified ? P.spp : 1;        // stratified: one Welford sample per sample index
+    const int spp_launch = P.stratified ? 1 : P.spp;
+    const double inv_spp = 1.0 / (double)spp_launch;
+    const uint64_t total = pix_slots * (uint64_t)spp_launch;
+    for (int r = 0; r < rounds; r++) {
+        for (uint64_t begin = 0; begin < total; begin += plan.chunk) {
+            const uint32_t cnt = (uint32_t)((total - begin) < plan.chunk ? (total - begin) : plan.chunk);
+            hipError_t e = hipMemsetAsync(Q.counts, 0, 4 * sizeof(uint32_t), stream);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_wf_camera, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Q, begin,
+                               cnt, spp_launch, r);
+            int qi = 0;
+            uint64_t bound = cnt;
+            for (int depth = 0; depth <= smp.mb; depth++) {
+                const unsigned tg = grid_for(bound, kTB, plan.trace_blocks);
+                if (count) hipLaunchKernelGGL(k_wf_trace<true>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+                else hipLaunchKernelGGL(k_wf_trace<false>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+                const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
+                if (count) hipLaunchKernelGGL(k_wf_shade<true>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+                else hipLaunchKernelGGL(k_wf_shade<false>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+                const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
+                const uint64_t shadows = children * (uint64_t)plan.lights_per_child;
+                const unsigned hg = grid_for(shadows, kTB, plan.trace_blocks);
+                if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, Q, B.counters);
+                else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, Q, B.counters);
+                bound = children < Q.cap ? children : Q.cap;
+                qi = 1 - qi;
+            }
+        }
+        hipLaunchKernelGGL(k_wf_finalize, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, Q, inv_spp);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace pt

@@ -121,6 +121,7 @@ class Renderer:
         self.Seed = 0            # Random.Shared is unseedable; this keys the counter-based stream
         self.Device = 0
         self.Tiles = None        # optional 32x32 tile ids this context renders (multi-GPU sharding)
+        self.Engine = _abi.ENGINE_AUTO  # scheduling only: both engines compute identical per-ray arithmetic
         self.Verbose = False
         self._ctx = None
         self._lib = None
@@ -168,7 +169,8 @@ class Renderer:
                                  C.c_uint64(self.Seed & 0xFFFFFFFFFFFFFFFF).value,
                                  int(self._pass if pass_index is None else pass_index),
                                  0 if tiles is None else len(tiles),
-                                 C.POINTER(C.c_int32)() if tiles is None else tiles.ctypes.data_as(C.POINTER(C.c_int32)))
+                                 C.POINTER(C.c_int32)() if tiles is None else tiles.ctypes.data_as(C.POINTER(C.c_int32)),
+                                 int(self.Engine))
         return pp
 
     def RenderParallel(self) -> None:
