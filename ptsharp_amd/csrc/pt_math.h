@@ -101,8 +101,8 @@ PT_HD v3 random_unit_vector(uint64_t key, uint32_t dz, uint32_t da) {
     double z = draw(key, dz) * 2.0 - 1.0;
     double a = draw(key, da) * 2.0 * kPi;
     double r = sqrt(1.0 - z * z);
-    double x = sin(a);
-    double y = cos(a);
+    double x, y;
+    sincos(a, &x, &y);
     return mk(r * x, r * y, z);
 }
 // Vector.Reflect / Refract / Reflectance with `this` = the surface normal (Vector.cs:497-536)

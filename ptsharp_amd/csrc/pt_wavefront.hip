@@ -57,6 +57,24 @@ __device__ __forceinline__ uint32_t append(uint32_t* counter) {
     return atomicAdd(counter, 1u);  // hipcc aggregates a uniform +1 into one atomic per wave
 }
 
+constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that was not cast
+
+// Reserve n slots per lane with one atomic per wave (wave prefix scan); all 64
+// lanes must be active.  Returns this lane's first slot.
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* counter, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = n;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    const uint32_t total = __shfl(x, 63, 64);
+    uint32_t base = 0;
+    if (lane == 0 && total) base = atomicAdd(counter, total);
+    base = __shfl(base, 0, 64);
+    return base + x - n;
+}
+
 __device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, float3 thr, uint32_t pixel,
                                           uint32_t meta, uint64_t key) {
     nt_store(&Q.q_o[q][i], make_float4(o.x, o.y, o.z, __uint_as_float(pixel)));
@@ -119,8 +137,9 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
     const uint32_t n = Q.counts[qi] < Q.cap ? Q.counts[qi] : Q.cap;
     Counters ctr{0, 0, 0, 0};
     for (uint32_t i = blockIdx.x * kTB + threadIdx.x; i < n; i += gridDim.x * kTB) {
-        float4 a = nt_load(&Q.q_o[qi][i]);
         float4 b = nt_load(&Q.q_d[qi][i]);
+        float4 a = nt_load(&Q.q_o[qi][i]);
+        if (__float_as_uint(b.w) == kDead) continue;
         HitRec h = trace<COUNT, kTB>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
         unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
         nt_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
@@ -138,19 +157,38 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
 }
 
 // ---------------------------------------------------------------- shade / bounce
+#ifndef PT_SHADE_WAVES
+#define PT_SHADE_WAVES 2
+#endif
+// One thread per queued ray.  Every wave reserves the queue slots of all its
+// lanes' children with ONE atomic per queue (a returning atomic on one word
+// saturates near 88 per µs on MI355X, MI355X_MICROARCH.md "dequeue"); a child
+// that turns out dead (p <= 0, a specular Any-mode child's shadow slot, light
+// below the horizon) leaves a kDead marker that the consuming kernel skips.
 template <bool COUNT>
-__global__ __launch_bounds__(256) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
-                                                  unsigned long long* counters) {
+__global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
+                                                                  unsigned long long* counters) {
     const uint32_t n = Q.counts[qi] < Q.cap ? Q.counts[qi] : Q.cap;
     const int qo = 1 - qi;
+    const int nl = S.num_lights;
+    const bool all_lights = smp.light_mode == 1;
+    const uint32_t lights_per_child = all_lights ? (uint32_t)nl : 1u;
     Counters ctr{0, 0, 0, 0};
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        float4 ro = nt_load(&Q.q_o[qi][i]);
-        float4 rd = nt_load(&Q.q_d[qi][i]);
-        float4 rt = nt_load(&Q.q_t[qi][i]);
-        uint4 hr = nt_load(&Q.hits[i]);
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {  // block-uniform
+        const uint32_t i = i0 + threadIdx.x;
+        bool alive = i < n;
+        float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, rt = ro;
+        uint4 hr = make_uint4(0, 0, 0, 0);
+        uint32_t meta = kDead;
+        if (alive) {  // all loads issued together: one memory round trip
+            rd = nt_load(&Q.q_d[qi][i]);
+            ro = nt_load(&Q.q_o[qi][i]);
+            rt = nt_load(&Q.q_t[qi][i]);
+            hr = nt_load(&Q.hits[i]);
+            meta = __float_as_uint(rd.w);
+            alive = meta != kDead;
+        }
         const uint32_t pixel = __float_as_uint(ro.w);
-        const uint32_t meta = __float_as_uint(rd.w);
         const int depth = (int)(meta & 0xFF);
         const bool emission = (meta >> 8) & 1;
         HitRec h;
@@ -158,25 +196,42 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, DevSampler smp, Wf
         h.kind = (int32_t)hr.z;
         h.idx = (int32_t)hr.w;
         const float thr[3] = {rt.x, rt.y, rt.z};
-        if (!(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67)
-            acc_add(Q.acc, pixel, thr[0] * S.env[0], thr[1] * S.env[1], thr[2] * S.env[2]);
-            continue;
-        }
-        const uint64_t node = nt_load(&Q.q_k[qi][i]);
         const v3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z};
-        Shade sh = hit_info<COUNT>(S, h, o, d, ctr);
-        const DevMaterial& m = S.mats[sh.mat];
-        const int samples = depth == 0 ? smp.fh : 1;
-        const int nn = (int)sqrt((double)samples);
-        const float inv_n2 = 1.0f / (float)(nn * nn);
-        if (m.emittance > 0) {
-            if (smp.dl && !emission) continue;  // Sampler.cs:75-78
-            float e = (float)((double)m.emittance * samples) * inv_n2;
-            acc_add(Q.acc, pixel, thr[0] * m.color[0] * e, thr[1] * m.color[1] * e, thr[2] * m.color[2] * e);
+        Shade sh{};
+        int mat = 0, nn = 1, nm = 1, nch = 0;
+        float t2[3] = {0.f, 0.f, 0.f};
+        uint64_t node = 0;
+        if (alive && !(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67)
+            acc_add(Q.acc, pixel, thr[0] * S.env[0], thr[1] * S.env[1], thr[2] * S.env[2]);
+            alive = false;
         }
-        const int nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
-        const int nch = nn * nn * nm;
-        const float t2[3] = {thr[0] * inv_n2, thr[1] * inv_n2, thr[2] * inv_n2};
+        if (alive) {
+            node = nt_load(&Q.q_k[qi][i]);
+            sh = hit_info<COUNT>(S, h, o, d, ctr);
+            mat = sh.mat;
+            const DevMaterial& m = S.mats[mat];
+            const int samples = depth == 0 ? smp.fh : 1;
+            nn = (int)sqrt((double)samples);
+            const float inv_n2 = 1.0f / (float)(nn * nn);
+            if (m.emittance > 0) {
+                if (smp.dl && !emission) {
+                    alive = false;  // Sampler.cs:75-78
+                } else {
+                    float e = (float)((double)m.emittance * samples) * inv_n2;
+                    acc_add(Q.acc, pixel, thr[0] * m.color[0] * e, thr[1] * m.color[1] * e, thr[2] * m.color[2] * e);
+                }
+            }
+            nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
+            nch = alive ? nn * nn * nm : 0;
+            for (int k = 0; k < 3; k++) t2[k] = thr[k] * inv_n2;
+        }
+        // extension-ray slots: reserved for all children at once (all 64 lanes take part);
+        // shadow rays are appended compactly (their count is known only after the bounce).
+        const uint32_t n_ext = (depth + 1 <= smp.mb) ? (uint32_t)nch : 0u;
+        const bool do_nee = smp.dl && nl > 0;
+        const uint32_t ebase = wave_reserve(&Q.counts[qo], n_ext);
+        if (ebase + n_ext > Q.cap) Q.counts[3] = 1;
+        const DevMaterial& m = S.mats[mat];
         const int ma = nm == 2 ? 1 : 0;
         for (int c = 0; c < nch; c++) {
             const int mode = ma + c % nm;
@@ -185,26 +240,25 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, DevSampler smp, Wf
             const uint64_t E = child_key(node, (uint32_t)c);
             const double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)nn;
             const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
+            const uint32_t es = ebase + (uint32_t)c;
             v3 no, nd;
             bool reflected;
             double p;
             bounce(m, sh, d, fu, fv, mode, E, no, nd, reflected, p);
             if (mode == 0) p = 1;
-            if (!(p > 0)) continue;
+            const bool live = p > 0;
             const float fp = (float)p;
             float w[3];
-            if (reflected) {
+            if (live && reflected) {
                 for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * m.color[k]);
-            } else {
+            } else if (live) {
                 for (int k = 0; k < 3; k++) w[k] = fp * m.color[k];
-                if (smp.dl && S.num_lights > 0) {  // sampleLights (Sampler.cs:191-210)
-                    const int nl = S.num_lights;
-                    const bool all = smp.light_mode == 1;
-                    const int first = all ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
-                    const int last = all ? nl : first + 1;
-                    const float scale = all ? 1.0f / (float)nl : (float)nl;
+                if (do_nee) {  // sampleLights (Sampler.cs:191-210)
+                    const int first = all_lights ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
+                    const int last = all_lights ? nl : first + 1;
+                    const float scale = all_lights ? 1.0f / (float)nl : (float)nl;
                     for (int li = first; li < last; li++) {
-                        const uint64_t LK = all ? light_key(E, (uint32_t)li) : E;
+                        const uint64_t LK = all_lights ? light_key(E, (uint32_t)li) : E;
                         v3 ldir;
                         float3 lc;
                         if (!light_setup(S, smp, S.lights[li], sh.pos, sh.nrm, LK, ldir, lc)) continue;
@@ -213,14 +267,16 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, DevSampler smp, Wf
                         nt_store(&Q.s_o[si], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
                         nt_store(&Q.s_d[si], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float((uint32_t)li)));
                         nt_store(&Q.s_c[si], make_float4(t2[0] * w[0] * (lc.x * scale), t2[1] * w[1] * (lc.y * scale),
-                                                                t2[2] * w[2] * (lc.z * scale), 0.f));
+                                                         t2[2] * w[2] * (lc.z * scale), 0.f));
                     }
                 }
             }
-            if (depth + 1 > smp.mb) continue;  // sample() at depth > MaxBounces returns black, no Intersect
-            const uint32_t j = append(&Q.counts[qo]);
-            if (j >= Q.cap) { Q.counts[3] = 1; continue; }
-            ray_store(Q, qo, j, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
+            if (n_ext == 0 || es >= Q.cap) continue;  // depth > MaxBounces: sample() returns black, no Intersect
+            if (!live) {
+                nt_store(&Q.q_d[qo][es], make_float4(0.f, 0.f, 0.f, __uint_as_float(kDead)));
+                continue;
+            }
+            ray_store(Q, qo, es, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
                       (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
         }
     }
@@ -238,8 +294,8 @@ __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, unsig
     const uint32_t n = Q.counts[2] < Q.s_cap ? Q.counts[2] : Q.s_cap;
     Counters ctr{0, 0, 0, 0};
     for (uint32_t i = blockIdx.x * kTB + threadIdx.x; i < n; i += gridDim.x * kTB) {
-        float4 a = nt_load(&Q.s_o[i]);
         float4 b = nt_load(&Q.s_d[i]);
+        float4 a = nt_load(&Q.s_o[i]);
         const DevLight L = S.lights[__float_as_uint(b.w)];
         if (light_visible<COUNT, kTB>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) {
             float4 c = nt_load(&Q.s_c[i]);
