@@ -64,7 +64,7 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    from ptsharp_amd import Renderer, scenes, tiles_for_rank
+    from ptsharp_amd import Renderer, _abi, scenes, tiles_for_rank
 
     t_scene = time.perf_counter()
     scene, camera, sampler = scenes.bunny_frame(a.tris, seed=a.seed)
@@ -87,24 +87,33 @@ def main():
 
     for _ in range(a.warmup):
         r.RenderParallel()
-    # one instrumented (untimed) pass: traversal counters → algorithmic bytes per ray
+    # one instrumented (untimed) pass: traversal counters → algorithmic bytes per ray, per kernel
     ctr = r.RenderCounted()
-    bytes_per_ray = (B_NODE * 2 * ctr.nodes_visited + B_PRIM * ctr.prims_tested + B_RAY * ctr.rays +
-                     B_SHADE * ctr.shading_fetches) / max(ctr.rays, 1)
+    ext_rays = ctr.rays - ctr.shadow_rays
+    ext_nodes = ctr.nodes_visited - ctr.shadow_nodes
+    ext_prims = ctr.prims_tested - ctr.shadow_prims
+    bytes_ext = B_NODE * 2 * ext_nodes + B_PRIM * ext_prims + B_RAY * ext_rays
+    bytes_sh = B_NODE * 2 * ctr.shadow_nodes + B_PRIM * ctr.shadow_prims + B_RAY * ctr.shadow_rays
+    bytes_all = bytes_ext + bytes_sh + B_SHADE * ctr.shading_fetches
     r.ResetBuffer()
 
-    # ---------------- timed region
+    # ---------------- timed region (per-kernel hipEvent timing on the library's stream)
+    r.Flags = _abi.PASS_KERNEL_TIMING
     if dist:
         dist.barrier()
     r.Synchronize()
     t0 = time.perf_counter()
     rays = 0
     kernel_ms = 0.0
+    kms = np.zeros(6)
+    klaunch = np.zeros(6, np.int64)
     for _ in range(a.steps):
         r.RenderParallel()
         s = r.Stats()
         rays += s.rays
         kernel_ms += s.last_pass_ms
+        kms += np.array(s.kernel_ms[:])
+        klaunch += np.array(s.kernel_launches[:])
     if world > 1:
         r.Gather(0)
     r.Synchronize()
@@ -131,9 +140,28 @@ def main():
         return
 
     value = total_rays / elapsed / 1e6
-    avg_launch_ms = kernel_ms / a.steps
-    rays_per_launch = rays / a.steps
-    achieved_gbs = bytes_per_ray * rays_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    names = ["k_wf_camera", "k_wf_trace<false>", "k_wf_shade<false>", "k_wf_shadow<false>", "k_wf_finalize",
+             "k_render_pass<false>"]
+    dom = int(np.argmax(kms))
+    # algorithmic bytes of the dominant kernel over the timed region: the counted pass' bytes per
+    # ray of that kernel's ray class × the rays it traced (same scene/seed/spp → same ray mix)
+    if dom == _abi.K_TRACE:
+        per_ray, kind_rays = bytes_ext / max(ext_rays, 1), ext_rays
+    elif dom == _abi.K_SHADOW:
+        per_ray, kind_rays = bytes_sh / max(ctr.shadow_rays, 1), ctr.shadow_rays
+    else:
+        per_ray, kind_rays = bytes_all / max(ctr.rays, 1), ctr.rays
+    frac_rays = kind_rays / max(ctr.rays, 1)
+    dom_bytes = per_ray * rays * frac_rays
+    avg_launch_ms = kms[dom] / max(klaunch[dom], 1)
+    achieved_gbs = dom_bytes / (kms[dom] * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            tj = json.load(f)
+        if tj.get("kernel") == names[dom] and tj.get("workload_tris") == a.tris:
+            traffic = round(tj["traffic_bytes_per_ray"] * rays * frac_rays / max(klaunch[dom], 1))
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -153,16 +181,24 @@ def main():
             "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}",
             "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
             "rays_per_camera_sample": round(total_rays / (W * H * a.spp * a.steps), 3),
-            "engine": a.engine, "scene_build_s": round(t_scene, 3), "bvh_build_ms": round(build_ms, 1), "bvh_bytes": int(bvh_bytes),
+            "shadow_ray_fraction": round(ctr.shadow_rays / max(ctr.rays, 1), 4),
+            "engine": a.engine, "scene_build_s": round(t_scene, 3), "bvh_build_ms": round(build_ms, 1),
+            "bvh_bytes": int(bvh_bytes),
+            "kernel_ms_per_step": {names[k]: round(kms[k] / a.steps, 3) for k in range(6) if klaunch[k]},
         },
         "roofline": {
-            "bound": "hbm", "kernel": "k_render_pass<false>",
+            "bound": "hbm", "kernel": names[dom],
             "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": None,
-            "avg_launch_ms": round(avg_launch_ms, 4), "rays_per_launch": int(rays_per_launch),
-            "bytes_per_ray": round(bytes_per_ray, 2),
-            "nodes_per_ray": round(2 * ctr.nodes_visited / max(ctr.rays, 1), 3),
-            "prims_per_ray": round(ctr.prims_tested / max(ctr.rays, 1), 3),
+            "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "avg_launch_ms": round(float(avg_launch_ms), 4), "launches": int(klaunch[dom]),
+            "bytes_per_launch": round(dom_bytes / max(klaunch[dom], 1)),
+            "bytes_per_ray": round(per_ray, 2),
+            "nodes_per_ray": round(2 * (ext_nodes if dom == _abi.K_TRACE else ctr.nodes_visited) /
+                                   max(ext_rays if dom == _abi.K_TRACE else ctr.rays, 1), 3),
+            "prims_per_ray": round((ext_prims if dom == _abi.K_TRACE else ctr.prims_tested) /
+                                   max(ext_rays if dom == _abi.K_TRACE else ctr.rays, 1), 3),
+            "all_kernels_bytes_per_ray": round(bytes_all / max(ctr.rays, 1), 2),
+            "pass_achieved_gbs": round(bytes_all / max(ctr.rays, 1) * rays / (kernel_ms * 1e-3) / 1e9, 2),
         },
     }
 
@@ -172,14 +208,14 @@ def main():
         import oracle_lib as O
         osc = O.OracleScene(scene)
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-        # probe, then size a strided pixel sample to ~cpu_seconds of CPU work at spp = 1
-        stride = 20011
+        # probe ~2k pixels, then size a strided pixel sample to ~cpu_seconds of CPU work at spp = 1
+        stride = max(1, (W * H) // 2048)
         tp = time.perf_counter()
         _, prays = O.render_pixels(osc, camera, sampler, W, H, 1, 0, W * H, stride, seed=a.seed, pass_index=1,
                                    threads=threads)
         tp = time.perf_counter() - tp
         budget = max(a.cpu_seconds, 1.0)
-        npx = max(64, min(W * H, int((W * H // stride) * budget / max(tp, 1e-3))))
+        npx = max(64, min(W * H, int(((W * H + stride - 1) // stride) * budget / max(tp, 1e-3))))
         stride = max(1, (W * H) // npx)
         tc = time.perf_counter()
         obuf, crays = O.render_pixels(osc, camera, sampler, W, H, 1, 0, W * H, stride, seed=a.seed, pass_index=1,

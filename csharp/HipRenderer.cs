@@ -1,0 +1,247 @@
+// HipRenderer.cs — drop-in for PTSharpCore.Renderer that runs the per-pixel hot
+// path on an MI355X through libptsharp_hip.so (include/ptsharp_hip.h).
+//
+// Add this file to PTSharpCore/ (same namespace).  It mirrors the reference's
+// Renderer factory and knobs (Renderer.cs:35-56), its IterativeRender contract
+// (Renderer.cs:702-765) and writes into the same static Buffer (Renderer.PBuffer,
+// Buffer.cs:60-97).  P/Invoke follows the conventions the reference already uses
+// for its only native dependency, OIDN (OIDN.cs:43-95): Cdecl, IntPtr handles,
+// create / commit / execute / release, error strings fetched after a failure.
+//
+// NOTE: this file is not compiled in this repository (no .NET SDK in the build
+// image); the same ABI is exercised from Python/ctypes by tests/test_abi.py and
+// the GPU parity suite.  Struct layouts below match ptsharp_hip.h field by field.
+using System;
+using System.Collections.Generic;
+using System.Runtime.InteropServices;
+using SkiaSharp;
+
+namespace PTSharpCore
+{
+    internal static class PtHip
+    {
+        const string Lib = "ptsharp_hip";   // libptsharp_hip.so on Linux
+
+        public const int PT_OK = 0;
+        public const int PT_ERR_UNSUPPORTED = -4;
+        public const int SHAPE_SPHERE = 0, SHAPE_CUBE = 1, SHAPE_PLANE = 2, SHAPE_TRIANGLE = 3, SHAPE_MESH = 4;
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_material
+        {
+            public double r, g, b, emittance, index, gloss, tint, reflectivity;
+            public int transparent, _pad;
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_scene_desc
+        {
+            public int num_materials; public IntPtr materials;
+            public int num_shapes; public IntPtr shape_kind; public IntPtr shape_index;
+            public int num_spheres; public IntPtr sphere_center; public IntPtr sphere_radius; public IntPtr sphere_material;
+            public int num_cubes; public IntPtr cube_min; public IntPtr cube_max; public IntPtr cube_material;
+            public int num_planes; public IntPtr plane_point; public IntPtr plane_normal; public IntPtr plane_material;
+            public int num_triangles; public IntPtr tri_v1, tri_v2, tri_v3, tri_n1, tri_n2, tri_n3; public IntPtr tri_material;
+            public int num_meshes; public IntPtr mesh_first; public IntPtr mesh_count;
+            public double env_r, env_g, env_b;
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public unsafe struct pt_camera
+        {
+            public fixed float p[3]; public fixed float u[3]; public fixed float v[3]; public fixed float w[3];
+            public double m, focal_distance, aperture_radius;
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_sampler
+        {
+            public int first_hit_samples, max_bounces, direct_lighting, soft_shadows, light_mode, specular_mode;
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_pass_params
+        {
+            public int spp, stratified;
+            public ulong seed;
+            public uint pass_index;
+            public int num_tiles;
+            public IntPtr tiles;
+            public int engine, _pad;
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_device_opts { public int device, width, height; }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_stats
+        {
+            public ulong rays, rays_total; public double last_pass_ms, total_ms;
+            public ulong bvh_nodes, bvh_bytes; public double build_ms; public ulong passes;
+        }
+
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_get_version();
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_create(ref pt_device_opts opts, out IntPtr ctx);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_upload_scene(IntPtr ctx, ref pt_scene_desc scene);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_render_pass(IntPtr ctx, ref pt_camera cam, ref pt_sampler smp, ref pt_pass_params pass);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_read_buffer(IntPtr ctx, double[] m, double[] v, int[] n);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_reset_buffer(IntPtr ctx);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_stats_get(IntPtr ctx, out pt_stats stats);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern IntPtr pt_last_error();
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern void pt_destroy(IntPtr ctx);
+
+        public static void Check(int rc, string where)
+        {
+            if (rc != PT_OK)
+                throw new InvalidOperationException($"{where} failed ({rc}): {Marshal.PtrToStringAnsi(pt_last_error())}");
+        }
+    }
+
+    /// <summary>Renderer drop-in: same factory, knobs and IterativeRender contract as Renderer.</summary>
+    class HipRenderer : IDisposable
+    {
+        Scene Scene; Camera Camera; DefaultSampler Sampler;
+        public int SamplesPerPixel = 2;           // Renderer.cs:42
+        public bool StratifiedSampling = false;   // Renderer.cs:44
+        public ulong Seed = 0;                     // Random.Shared is unseedable; this keys the GPU stream
+        IntPtr ctx;
+        int W, H, pass;
+        bool uploaded;
+        readonly List<GCHandle> pins = new();
+
+        // DefaultSampler keeps FirstHitSamples/MaxBounces/DirectLighting/SoftShadows private
+        // (Sampler.cs:13-16): the caller passes the values it constructed the sampler with.
+        int firstHit, maxBounces; bool directLighting = true, softShadows = true;
+
+        public static HipRenderer NewRenderer(Scene scene, Camera camera, DefaultSampler sampler, int firstHitSamples,
+                                              int maxBounces, int w, int h, int device = 0)
+        {
+            var r = new HipRenderer { Scene = scene, Camera = camera, Sampler = sampler, W = w, H = h,
+                                      firstHit = firstHitSamples, maxBounces = maxBounces };
+            Renderer.PBuffer = new Buffer(w, h);
+            var opts = new PtHip.pt_device_opts { device = device, width = w, height = h };
+            PtHip.Check(PtHip.pt_create(ref opts, out r.ctx), "pt_create");
+            return r;
+        }
+
+        IntPtr Pin(Array a) { var g = GCHandle.Alloc(a, GCHandleType.Pinned); pins.Add(g); return g.AddrOfPinnedObject(); }
+
+        // Flatten Scene.Shapes (Scene.cs:19) with a type switch; returns PT_ERR_UNSUPPORTED kinds as exceptions
+        // so the caller can fall back to the CPU Renderer.
+        void Upload()
+        {
+            var mats = new List<PtHip.pt_material>(); var matIds = new Dictionary<Material, int>();
+            int Mid(Material m)
+            {
+                if (m.Texture != null || m.NormalTexture != null || m.BumpTexture != null || m.GlossTexture != null)
+                    throw new NotSupportedException("textured materials are not on the GPU path");
+                if (!matIds.TryGetValue(m, out int id))
+                {
+                    id = mats.Count; matIds[m] = id;
+                    mats.Add(new PtHip.pt_material { r = m.Color.r, g = m.Color.g, b = m.Color.b, emittance = m.Emittance,
+                        index = m.Index, gloss = m.Gloss, tint = m.Tint, reflectivity = m.Reflectivity,
+                        transparent = m.Transparent ? 1 : 0 });
+                }
+                return id;
+            }
+            var kind = new List<int>(); var index = new List<int>();
+            var sc = new List<float>(); var sr = new List<double>(); var sm = new List<int>();
+            var cmin = new List<float>(); var cmax = new List<float>(); var cm = new List<int>();
+            var pp = new List<float>(); var pn = new List<float>(); var pm = new List<int>();
+            var v1 = new List<float>(); var v2 = new List<float>(); var v3 = new List<float>();
+            var n1 = new List<float>(); var n2 = new List<float>(); var n3 = new List<float>(); var tm = new List<int>();
+            var mf = new List<int>(); var mc = new List<int>();
+            void Add3(List<float> l, Vector v) { l.Add((float)v.X); l.Add((float)v.Y); l.Add((float)v.Z); }
+            void AddTri(Triangle t)
+            {
+                Add3(v1, t.V1); Add3(v2, t.V2); Add3(v3, t.V3); Add3(n1, t.N1); Add3(n2, t.N2); Add3(n3, t.N3);
+                tm.Add(Mid(t.Material));
+            }
+            foreach (var s in Scene.Shapes)
+            {
+                switch (s)
+                {
+                    case Sphere sp: kind.Add(PtHip.SHAPE_SPHERE); index.Add(sr.Count); Add3(sc, sp.Center); sr.Add(sp.Radius); sm.Add(Mid(sp.Material)); break;
+                    case Cube cu: kind.Add(PtHip.SHAPE_CUBE); index.Add(cm.Count); Add3(cmin, cu.Min); Add3(cmax, cu.Max); cm.Add(Mid(cu.Material)); break;
+                    // Plane.Point/Normal/Material are private in the reference (Plane.cs:9-11): the integration
+                    // marks them `internal`, the same visibility Sphere and Cube already use (INTEGRATION.md).
+                    case Plane pl: kind.Add(PtHip.SHAPE_PLANE); index.Add(pm.Count); Add3(pp, pl.Point); Add3(pn, pl.Normal); pm.Add(Mid(pl.Material)); break;
+                    case Triangle tr: kind.Add(PtHip.SHAPE_TRIANGLE); index.Add(tm.Count); AddTri(tr); break;
+                    case Mesh me: kind.Add(PtHip.SHAPE_MESH); index.Add(mf.Count); mf.Add(tm.Count); mc.Add(me.Triangles.Length); foreach (var t in me.Triangles) AddTri(t); break;
+                    default: throw new NotSupportedException($"{s.GetType().Name} is not on the GPU path");
+                }
+            }
+            var d = new PtHip.pt_scene_desc
+            {
+                num_materials = mats.Count, materials = Pin(mats.ToArray()),
+                num_shapes = kind.Count, shape_kind = Pin(kind.ToArray()), shape_index = Pin(index.ToArray()),
+                num_spheres = sr.Count, sphere_center = Pin(sc.ToArray()), sphere_radius = Pin(sr.ToArray()), sphere_material = Pin(sm.ToArray()),
+                num_cubes = cm.Count, cube_min = Pin(cmin.ToArray()), cube_max = Pin(cmax.ToArray()), cube_material = Pin(cm.ToArray()),
+                num_planes = pm.Count, plane_point = Pin(pp.ToArray()), plane_normal = Pin(pn.ToArray()), plane_material = Pin(pm.ToArray()),
+                num_triangles = tm.Count, tri_v1 = Pin(v1.ToArray()), tri_v2 = Pin(v2.ToArray()), tri_v3 = Pin(v3.ToArray()),
+                tri_n1 = Pin(n1.ToArray()), tri_n2 = Pin(n2.ToArray()), tri_n3 = Pin(n3.ToArray()), tri_material = Pin(tm.ToArray()),
+                num_meshes = mf.Count, mesh_first = Pin(mf.ToArray()), mesh_count = Pin(mc.ToArray()),
+                env_r = Scene.Color.r, env_g = Scene.Color.g, env_b = Scene.Color.b,
+            };
+            try { PtHip.Check(PtHip.pt_upload_scene(ctx, ref d), "pt_upload_scene"); }
+            finally { foreach (var g in pins) g.Free(); pins.Clear(); }   // arrays are copied during the call
+            uploaded = true;
+        }
+
+        unsafe PtHip.pt_camera Cam()
+        {
+            var c = new PtHip.pt_camera { m = Camera.m, focal_distance = Camera.focalDistance, aperture_radius = Camera.apertureRadius };
+            c.p[0] = (float)Camera.p.X; c.p[1] = (float)Camera.p.Y; c.p[2] = (float)Camera.p.Z;
+            c.u[0] = (float)Camera.u.X; c.u[1] = (float)Camera.u.Y; c.u[2] = (float)Camera.u.Z;
+            c.v[0] = (float)Camera.v.X; c.v[1] = (float)Camera.v.Y; c.v[2] = (float)Camera.v.Z;
+            c.w[0] = (float)Camera.w.X; c.w[1] = (float)Camera.w.Y; c.w[2] = (float)Camera.w.Z;
+            return c;
+        }
+
+        /// <summary>One Renderer.RenderParallel pass on the GPU (Renderer.cs:199-338).</summary>
+        public void RenderParallel()
+        {
+            if (!uploaded) Upload();
+            var cam = Cam();
+            var smp = new PtHip.pt_sampler { first_hit_samples = firstHit, max_bounces = maxBounces,
+                direct_lighting = directLighting ? 1 : 0, soft_shadows = softShadows ? 1 : 0,
+                light_mode = (int)Sampler.LightMode, specular_mode = (int)Sampler.SpecularMode };
+            var pass = new PtHip.pt_pass_params { spp = SamplesPerPixel, stratified = StratifiedSampling ? 1 : 0,
+                seed = Seed, pass_index = (uint)(++this.pass) };
+            PtHip.Check(PtHip.pt_render_pass(ctx, ref cam, ref smp, ref pass), "pt_render_pass");
+        }
+
+        /// <summary>Copy the HBM Welford state into Renderer.PBuffer's Pixel objects (Buffer.cs:18-58).</summary>
+        public void ReadBuffer()
+        {
+            int P = W * H;
+            var m = new double[3 * P]; var v = new double[3 * P]; var n = new int[P];
+            PtHip.Check(PtHip.pt_read_buffer(ctx, m, v, n), "pt_read_buffer");
+            for (int y = 0; y < H; y++)
+                for (int x = 0; x < W; x++)
+                {
+                    int i = y * W + x;
+                    Renderer.PBuffer.Pixels[(x, y)] = new Pixel(n[i], new Colour(m[3 * i], m[3 * i + 1], m[3 * i + 2]),
+                                                                 new Colour(v[3 * i], v[3 * i + 1], v[3 * i + 2]));
+                }
+        }
+
+        /// <summary>Renderer.IterativeRender (Renderer.cs:702-765): N passes, a PNG after each.</summary>
+        public SKBitmap IterativeRender(string pathTemplate, int iter)
+        {
+            SKBitmap colour = null;
+            for (int i = 1; i <= iter; i++)
+            {
+                Console.WriteLine("Iteration " + i + " of " + iter);
+                RenderParallel();
+                ReadBuffer();
+                colour = Renderer.PBuffer.Image(Channel.ColorChannel);
+                using var stream = System.IO.File.OpenWrite(string.Format(pathTemplate, i));
+                colour.Encode(SKEncodedImageFormat.Png, 100).SaveTo(stream);
+            }
+            return colour;
+        }
+
+        public void Dispose() { if (ctx != IntPtr.Zero) { PtHip.pt_destroy(ctx); ctx = IntPtr.Zero; } }
+    }
+}

@@ -151,8 +151,16 @@ typedef struct pt_pass_params {
     int32_t num_tiles;       /* 0 = whole image; else render only these 32x32 tiles */
     const int32_t* tiles;    /* tile id = ty * ceil(W/32) + tx                   */
     int32_t engine;          /* pt_engine                                        */
-    int32_t _pad;
+    int32_t flags;           /* PT_PASS_KERNEL_TIMING: per-kernel hipEvent timing */
 } pt_pass_params;
+
+#define PT_PASS_KERNEL_TIMING 1
+
+/* Kernel classes reported by pt_stats.kernel_ms / kernel_launches. */
+typedef enum pt_kernel_class {
+    PT_K_CAMERA = 0, PT_K_TRACE = 1, PT_K_SHADE = 2, PT_K_SHADOW = 3, PT_K_FINALIZE = 4, PT_K_MEGAKERNEL = 5,
+    PT_K_COUNT = 6
+} pt_kernel_class;
 
 /* Both engines compute identical per-ray arithmetic; they differ in scheduling. */
 typedef enum pt_engine {
@@ -176,6 +184,9 @@ typedef struct pt_stats {
     uint64_t bvh_bytes;
     double build_ms;         /* host BVH build time of the last upload        */
     uint64_t passes;
+    uint64_t shadow_rays;    /* of `rays`: shadow-visibility queries (sampleLight)     */
+    double kernel_ms[6];     /* last pass, device time per pt_kernel_class (flag PT_PASS_KERNEL_TIMING) */
+    uint32_t kernel_launches[6];
 } pt_stats;
 
 int pt_get_version(void);
@@ -202,10 +213,13 @@ int pt_comm_destroy(void* ctx);
 
 /* Instrumentation (bench / roofline): last pass' traversal counters, summed. */
 typedef struct pt_trace_counters {
-    uint64_t rays;
-    uint64_t nodes_visited;   /* BVH child-pair fetches (64 B each)            */
+    uint64_t rays;            /* all Scene.Intersect calls                     */
+    uint64_t nodes_visited;   /* BVH child-pair fetches (64 B each), all rays  */
     uint64_t prims_tested;    /* triangle/sphere/cube records tested (48 B)     */
     uint64_t shading_fetches; /* closest-hit shading records (40 B)            */
+    uint64_t shadow_rays;     /* the shadow-visibility part of the above ...   */
+    uint64_t shadow_nodes;
+    uint64_t shadow_prims;
 } pt_trace_counters;
 int pt_render_pass_counted(void* ctx, const pt_camera* camera, const pt_sampler* sampler,
                            const pt_pass_params* pass, pt_trace_counters* out);

@@ -56,7 +56,7 @@ typedef struct or_pass_params {
     uint32_t pass_index;
     int32_t num_tiles;
     const int32_t* tiles;
-    int32_t engine, _pad;   /* product-only (GPU scheduling); ignored by the oracle */
+    int32_t engine, flags;  /* product-only (GPU scheduling / timing); ignored by the oracle */
 } or_pass_params;
 
 /* Build the scene (k-d trees as Scene.Compile/Tree.NewTree do).  Returns NULL on error. */

@@ -22,6 +22,8 @@ PT_ERR_RCCL = -6
 PT_ERR_NO_DEVICE = -7
 
 ENGINE_AUTO, ENGINE_MEGAKERNEL, ENGINE_WAVEFRONT = 0, 1, 2
+PASS_KERNEL_TIMING = 1
+K_CAMERA, K_TRACE, K_SHADE, K_SHADOW, K_FINALIZE, K_MEGAKERNEL = range(6)
 
 SHAPE_SPHERE, SHAPE_CUBE, SHAPE_PLANE, SHAPE_TRIANGLE, SHAPE_MESH = 0, 1, 2, 3, 4
 
@@ -62,7 +64,7 @@ class pt_sampler(C.Structure):
 
 class pt_pass_params(C.Structure):
     _fields_ = [("spp", C.c_int32), ("stratified", C.c_int32), ("seed", C.c_uint64), ("pass_index", C.c_uint32),
-                ("num_tiles", C.c_int32), ("tiles", _i), ("engine", C.c_int32), ("_pad", C.c_int32)]
+                ("num_tiles", C.c_int32), ("tiles", _i), ("engine", C.c_int32), ("flags", C.c_int32)]
 
 
 class pt_device_opts(C.Structure):
@@ -72,12 +74,14 @@ class pt_device_opts(C.Structure):
 class pt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("rays_total", C.c_uint64), ("last_pass_ms", C.c_double),
                 ("total_ms", C.c_double), ("bvh_nodes", C.c_uint64), ("bvh_bytes", C.c_uint64),
-                ("build_ms", C.c_double), ("passes", C.c_uint64)]
+                ("build_ms", C.c_double), ("passes", C.c_uint64), ("shadow_rays", C.c_uint64),
+                ("kernel_ms", C.c_double * 6), ("kernel_launches", C.c_uint32 * 6)]
 
 
 class pt_trace_counters(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("nodes_visited", C.c_uint64), ("prims_tested", C.c_uint64),
-                ("shading_fetches", C.c_uint64)]
+                ("shading_fetches", C.c_uint64), ("shadow_rays", C.c_uint64), ("shadow_nodes", C.c_uint64),
+                ("shadow_prims", C.c_uint64)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/ptsharp_hip.h

@@ -55,6 +55,40 @@ struct DeviceArray {
     void release() { if (ptr) (void)hipFree(ptr); ptr = nullptr; bytes = 0; }
 };
 
+// hipEvent pairs around each launch of a pass (PT_PASS_KERNEL_TIMING): device
+// time per kernel class, read after the pass' final synchronisation.
+struct EventTimer : pt::LaunchTimer {
+    std::vector<hipEvent_t> pool;
+    std::vector<int> cls;
+    size_t used = 0;
+    hipStream_t stream = nullptr;
+    bool failed = false;
+    void reset(hipStream_t s) { stream = s; used = 0; cls.clear(); failed = false; }
+    void record(int c, bool is_begin) {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) { failed = true; return; }
+            pool.push_back(e);
+        }
+        if (hipEventRecord(pool[used], stream) != hipSuccess) failed = true;
+        if (is_begin) cls.push_back(c);
+        used++;
+    }
+    void begin(int c) override { record(c, true); }
+    void end(int c) override { record(c, false); }
+    hipError_t collect(double* ms, uint32_t* launches) {
+        for (size_t i = 0; i + 1 < used; i += 2) {
+            float t = 0.f;
+            hipError_t e = hipEventElapsedTime(&t, pool[i], pool[i + 1]);
+            if (e != hipSuccess) return e;
+            ms[cls[i / 2]] += t;
+            launches[cls[i / 2]]++;
+        }
+        return hipSuccess;
+    }
+    void destroy() { for (auto e : pool) (void)hipEventDestroy(e); pool.clear(); }
+};
+
 struct Ctx {
     int device = 0;
     int width = 0, height = 0;
@@ -81,6 +115,7 @@ struct Ctx {
     std::vector<DeviceArray> wf_arrays;
     uint32_t wf_cap = 0, wf_scap = 0;
     int last_engine = 0;
+    EventTimer timer;
 };
 
 constexpr uint32_t kWfMaxCap = 1u << 23;   // 8M rays per queue: ~1.5 GB of queues at most
@@ -523,13 +558,21 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         if (rc) return rc;
     }
     c->last_engine = engine;
+    const bool timing = (pass->flags & PT_PASS_KERNEL_TIMING) != 0;
+    c->timer.reset(c->stream);
     PT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    if (engine == PT_ENGINE_WAVEFRONT) PT_HIP(hipMemsetAsync(c->Q.counts + 3, 0, sizeof(uint32_t), c->stream));
     PT_HIP(hipEventRecord(c->ev0, c->stream));
-    if (engine == PT_ENGINE_WAVEFRONT)
-        PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream));
-    else
+    if (engine == PT_ENGINE_WAVEFRONT) {
+        PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream,
+                                  timing ? &c->timer : nullptr));
+    } else {
+        if (timing) c->timer.begin(PT_K_MEGAKERNEL);
         PT_HIP(pt::launch_render_pass(c->S, cam, smp, P, B, num_tiles, counted != nullptr, c->stream));
+        if (timing) c->timer.end(PT_K_MEGAKERNEL);
+    }
     PT_HIP(hipEventRecord(c->ev1, c->stream));
+    if (c->timer.failed) return fail(PT_ERR_HIP, "hipEventRecord (kernel timing) failed");
     unsigned long long ctr[8];
     PT_HIP(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
@@ -540,16 +583,24 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     }
     float ms = 0.f;
     PT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    c->stats.rays = ctr[0];
-    c->stats.rays_total += ctr[0];
+    // counters: [0..2] closest-hit rays/nodes/prims, [3] shading fetches, [4..6] shadow rays/nodes/prims
+    const uint64_t rays = ctr[0] + ctr[4];
+    c->stats.rays = rays;
+    c->stats.shadow_rays = ctr[4];
+    c->stats.rays_total += rays;
     c->stats.last_pass_ms = ms;
     c->stats.total_ms += ms;
     c->stats.passes++;
+    for (int k = 0; k < PT_K_COUNT; k++) { c->stats.kernel_ms[k] = 0.0; c->stats.kernel_launches[k] = 0; }
+    if (timing) PT_HIP(c->timer.collect(c->stats.kernel_ms, c->stats.kernel_launches));
     if (counted) {
-        counted->rays = ctr[0];
-        counted->nodes_visited = ctr[1];
-        counted->prims_tested = ctr[2];
+        counted->rays = rays;
+        counted->nodes_visited = ctr[1] + ctr[5];
+        counted->prims_tested = ctr[2] + ctr[6];
         counted->shading_fetches = ctr[3];
+        counted->shadow_rays = ctr[4];
+        counted->shadow_nodes = ctr[5];
+        counted->shadow_prims = ctr[6];
     }
     return PT_OK;
 }
@@ -604,6 +655,7 @@ void pt_destroy(void* ctx) {
     if (c->d_n) (void)hipFree(c->d_n);
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_tiles) (void)hipFree(c->d_tiles);
+    c->timer.destroy();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);

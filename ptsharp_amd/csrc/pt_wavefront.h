@@ -33,7 +33,15 @@ struct WfPlan {
     uint32_t shade_blocks;
 };
 
+// Optional per-launch timing hook (hipEvent pairs recorded around each kernel; pt_api.hip).
+struct LaunchTimer {
+    virtual void begin(int kernel_class) = 0;
+    virtual void end(int kernel_class) = 0;
+    virtual ~LaunchTimer() = default;
+};
+
 hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
-                          const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream);
+                          const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
+                          LaunchTimer* timer);
 
 }  // namespace pt

@@ -304,12 +304,12 @@ __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, unsig
     }
     const uint32_t lane = threadIdx.x & 63;
     uint32_t rays = wave_sum(ctr.rays);
-    if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
+    if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
     if (COUNT) {
         uint32_t nodes = wave_sum(ctr.nodes), prims = wave_sum(ctr.prims);
         if (lane == 0) {
-            atomicAdd(&counters[1], (unsigned long long)nodes);
-            atomicAdd(&counters[2], (unsigned long long)prims);
+            atomicAdd(&counters[5], (unsigned long long)nodes);
+            atomicAdd(&counters[6], (unsigned long long)prims);
         }
     }
 }
@@ -339,38 +339,51 @@ static unsigned grid_for(uint64_t items, unsigned block, unsigned cap_blocks) {
 }
 
 hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
-                          const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream) {
+                          const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
+                          LaunchTimer* timer) {
     const uint64_t pix_slots = (uint64_t)P.num_tiles * 1024u;
     const int rounds = P.stratified ? P.spp : 1;        // stratified: one Welford sample per sample index
     const int spp_launch = P.stratified ? 1 : P.spp;
     const double inv_spp = 1.0 / (double)spp_launch;
     const uint64_t total = pix_slots * (uint64_t)spp_launch;
+    auto begin_k = [&](int cls) { if (timer) timer->begin(cls); };
+    auto end_k = [&](int cls) { if (timer) timer->end(cls); };
     for (int r = 0; r < rounds; r++) {
         for (uint64_t begin = 0; begin < total; begin += plan.chunk) {
             const uint32_t cnt = (uint32_t)((total - begin) < plan.chunk ? (total - begin) : plan.chunk);
-            hipError_t e = hipMemsetAsync(Q.counts, 0, 4 * sizeof(uint32_t), stream);
+            hipError_t e = hipMemsetAsync(Q.counts, 0, 3 * sizeof(uint32_t), stream);
             if (e != hipSuccess) return e;
+            begin_k(0);
             hipLaunchKernelGGL(k_wf_camera, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Q, begin,
                                cnt, spp_launch, r);
+            end_k(0);
             int qi = 0;
             uint64_t bound = cnt;
             for (int depth = 0; depth <= smp.mb; depth++) {
                 const unsigned tg = grid_for(bound, kTB, plan.trace_blocks);
+                begin_k(1);
                 if (count) hipLaunchKernelGGL(k_wf_trace<true>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 else hipLaunchKernelGGL(k_wf_trace<false>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+                end_k(1);
                 const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
+                begin_k(2);
                 if (count) hipLaunchKernelGGL(k_wf_shade<true>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
                 else hipLaunchKernelGGL(k_wf_shade<false>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+                end_k(2);
                 const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
                 const uint64_t shadows = children * (uint64_t)plan.lights_per_child;
                 const unsigned hg = grid_for(shadows, kTB, plan.trace_blocks);
+                begin_k(3);
                 if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, Q, B.counters);
                 else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, Q, B.counters);
+                end_k(3);
                 bound = children < Q.cap ? children : Q.cap;
                 qi = 1 - qi;
             }
         }
+        begin_k(4);
         hipLaunchKernelGGL(k_wf_finalize, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, Q, inv_spp);
+        end_k(4);
     }
     return hipGetLastError();
 }

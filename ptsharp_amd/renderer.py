@@ -122,6 +122,7 @@ class Renderer:
         self.Device = 0
         self.Tiles = None        # optional 32x32 tile ids this context renders (multi-GPU sharding)
         self.Engine = _abi.ENGINE_AUTO  # scheduling only: both engines compute identical per-ray arithmetic
+        self.Flags = 0                  # _abi.PASS_KERNEL_TIMING: per-kernel hipEvent timing in Stats()
         self.Verbose = False
         self._ctx = None
         self._lib = None
@@ -170,7 +171,7 @@ class Renderer:
                                  int(self._pass if pass_index is None else pass_index),
                                  0 if tiles is None else len(tiles),
                                  C.POINTER(C.c_int32)() if tiles is None else tiles.ctypes.data_as(C.POINTER(C.c_int32)),
-                                 int(self.Engine))
+                                 int(self.Engine), int(self.Flags))
         return pp
 
     def RenderParallel(self) -> None:

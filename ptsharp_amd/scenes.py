@@ -103,7 +103,9 @@ def blob_mesh(n_target: int, seed: int = 1234, amplitude: float = 0.05) -> Mesh:
     unit = np.concatenate([unit, [[0, 1, 0], [0, -1, 0]]])
     noise = (amp[None, :] * np.sin(unit @ dirs.T * freq[None, :] + phase[None, :])).sum(axis=1)
     noise /= np.abs(noise).max() + 1e-12
-    verts = (unit * (1.0 + amplitude * noise)[:, None]).astype(np.float32)
+    # quantise to 2^-20 so last-ulp differences between numpy's SIMD sin/cos paths on
+    # different CPUs cannot change the mesh (fixtures are generated on one host, checked on another)
+    verts = (np.round(unit * (1.0 + amplitude * noise)[:, None] * 2.0**20) / 2.0**20).astype(np.float32)
     north, south = len(verts) - 2, len(verts) - 1
     ring = lambda i, j: i * ns + (j % ns)
     tris = []

@@ -1,0 +1,7 @@
+# GPU tests + profile (evidence) + default bench, each step time-limited
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_all.log 2>&1; echo "rc=$?" >> gpurun_out/gpu_all.log
+bash tools/gpu_profile.sh ${TAG:-r01} && \
+timeout -k 10 900 python bench.py --json-out gpurun_out/bench_default.json > gpurun_out/bench_default.log 2>&1
