@@ -152,14 +152,15 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
         if ((rc = wf_alloc(c, &Q.q_k[q], cap))) return rc;
     }
     if ((rc = wf_alloc(c, &Q.hits, cap))) return rc;
-    if ((rc = wf_alloc(c, &Q.s_o, scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.s_d, scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.s_c, scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.counts, 4))) return rc;
+    if ((rc = wf_alloc(c, &Q.n_o, scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.n_n, scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.n_w, scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.n_k, scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.counts, 8))) return rc;
     size_t P = (size_t)c->width * (size_t)c->height;
     if ((rc = wf_alloc(c, &Q.acc, P * 3))) return rc;
     PT_HIP(hipMemsetAsync(Q.acc, 0, P * 3 * sizeof(double), c->stream));
-    PT_HIP(hipMemsetAsync(Q.counts, 0, 4 * sizeof(uint32_t), c->stream));
+    PT_HIP(hipMemsetAsync(Q.counts, 0, 8 * sizeof(uint32_t), c->stream));
     Q.cap = cap;
     Q.s_cap = scap;
     c->Q = Q;
@@ -542,7 +543,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp);
     double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)
     if (nm == 2) growth = std::ldexp(1.0, std::min(std::max(sampler->max_bounces - 1, 0), 60));
-    const double per_sample = (double)plan.root_children * growth * (double)plan.lights_per_child;
+    const double per_sample = (double)plan.root_children * growth;   // NEE requests: at most one per child
     uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples, std::floor((double)kWfMaxCap / per_sample));
     int engine = pass->engine;
     if (engine == PT_ENGINE_AUTO) engine = chunk >= 4096 || chunk >= cam_samples ? PT_ENGINE_WAVEFRONT : PT_ENGINE_MEGAKERNEL;
@@ -553,7 +554,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         plan.chunk = chunk;
         const double rays_needed = (double)chunk * (double)plan.root_children * growth;
         uint32_t cap = (uint32_t)std::min<double>((double)kWfMaxCap, std::max(65536.0, std::max((double)chunk, rays_needed)));
-        uint32_t scap = (uint32_t)std::min<double>((double)kWfMaxCap, std::max(65536.0, rays_needed * plan.lights_per_child));
+        uint32_t scap = (uint32_t)std::min<double>((double)kWfMaxCap, std::max(65536.0, rays_needed));
         int rc = ensure_wavefront(c, cap, scap);
         if (rc) return rc;
     }
@@ -561,7 +562,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     const bool timing = (pass->flags & PT_PASS_KERNEL_TIMING) != 0;
     c->timer.reset(c->stream);
     PT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
-    if (engine == PT_ENGINE_WAVEFRONT) PT_HIP(hipMemsetAsync(c->Q.counts + 3, 0, sizeof(uint32_t), c->stream));
+    if (engine == PT_ENGINE_WAVEFRONT) PT_HIP(hipMemsetAsync(c->Q.counts + 4, 0, sizeof(uint32_t), c->stream));
     PT_HIP(hipEventRecord(c->ev0, c->stream));
     if (engine == PT_ENGINE_WAVEFRONT) {
         PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream,
@@ -577,9 +578,9 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     PT_HIP(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
     if (engine == PT_ENGINE_WAVEFRONT) {
-        uint32_t flags[4];
+        uint32_t flags[8];
         PT_HIP(hipMemcpy(flags, c->Q.counts, sizeof flags, hipMemcpyDeviceToHost));
-        if (flags[3]) return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
+        if (flags[4]) return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
     }
     float ms = 0.f;
     PT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));

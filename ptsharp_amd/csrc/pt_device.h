@@ -229,22 +229,37 @@ __device__ __forceinline__ v3 cone(v3 direction, double theta, double u, double 
 
 // Ray.Bounce (Ray.cs:44-85); btype 0 Any, 1 Diffuse, 2 Specular.  Returns the new
 // ray in (no, nd); `reflected` and `p` as the reference's tuple.
+__device__ __forceinline__ void bounce_dir(const DevMaterial& m, const Shade& sh, v3 indir, double u, double v, bool refl,
+                                           double n1, double n2, uint64_t key, v3& no, v3& nd);
+
+// Fresnel / fixed reflectivity of a vertex (Ray.cs:170-177): the same for every child.
+__device__ __forceinline__ double vertex_p(const DevMaterial& m, const Shade& sh, v3 indir, double& n1, double& n2) {
+    n1 = 1.0;
+    n2 = m.index;
+    if (sh.inside) { double t = n1; n1 = n2; n2 = t; }
+    return m.reflectivity >= 0 ? m.reflectivity : reflectance(sh.nrm, indir, n1, n2);
+}
+
 __device__ __forceinline__ void bounce(const DevMaterial& m, const Shade& sh, v3 indir, double u, double v, int btype,
                                        uint64_t key, v3& no, v3& nd, bool& reflected, double& p) {
-    double n1 = 1.0, n2 = m.index;
-    if (sh.inside) { double t = n1; n1 = n2; n2 = t; }
-    p = m.reflectivity >= 0 ? m.reflectivity : reflectance(sh.nrm, indir, n1, n2);
+    double n1, n2;
+    p = vertex_p(m, sh, indir, n1, n2);
     bool refl = btype == 2 || (btype == 0 && draw(key, D_REFLECT) < p);
+    bounce_dir(m, sh, indir, u, v, refl, n1, n2, key, no, nd);
+    reflected = refl || m.transparent;
+    if (!refl) p = 1 - p;
+}
+
+// The new ray of Ray.Bounce once the reflect decision is made (Ray.cs:192-205).
+__device__ __forceinline__ void bounce_dir(const DevMaterial& m, const Shade& sh, v3 indir, double u, double v, bool refl,
+                                           double n1, double n2, uint64_t key, v3& no, v3& nd) {
     if (refl) {
         no = sh.pos;
         nd = cone(reflect(sh.nrm, indir), m.gloss, u, v, key);
-        reflected = true;
     } else if (m.transparent) {
         v3 rd = refract(sh.nrm, indir, n1, n2);
         no = add(sh.pos, muls(rd, 1e-4));
         nd = cone(rd, m.gloss, u, v, key);
-        reflected = true;
-        p = 1 - p;
     } else {
         // Ray.WeightedBounce (Ray.cs:28-35) around the normal
         double radius = sqrt(u);
@@ -255,8 +270,6 @@ __device__ __forceinline__ void bounce(const DevMaterial& m, const Shade& sh, v3
         v3 t = cross(sh.nrm, s);
         no = sh.pos;
         nd = add(add(add(zero3(), muls(s, radius * ct)), muls(t, radius * st)), muls(sh.nrm, sqrt(1 - u)));
-        reflected = false;
-        p = 1 - p;
     }
 }
 

@@ -15,12 +15,14 @@ struct WfQueues {
     float4* q_t[2];      // {throughput.rgb, -}
     uint64_t* q_k[2];    // RNG node key of the vertex the ray leads to
     uint4* hits;         // {t (fp64 bits), kind, record}
-    float4* s_o;         // shadow rays: {origin.xyz, pixel}
-    float4* s_d;         // {direction.xyz, light index}
-    float4* s_c;         // {contribution if visible, -}
-    uint32_t* counts;    // [0],[1] ray queues, [2] shadow queue, [3] overflow flag
+    float4* n_o;         // NEE requests (a diffuse child's sampleLights): {position.xyz, pixel}
+    float4* n_n;         // {normal.xyz, -}
+    float4* n_w;         // {throughput·weight.rgb, -}
+    uint64_t* n_k;       // RNG key of the child edge (light choice, soft-shadow point)
+    uint32_t* counts;    // pair q = {counts[2q], counts[2q+1]}: ray queue q and the NEE requests made
+                         // with it (one packed 64-bit word, reserved together); [4] overflow flag
     uint32_t cap;        // entries per ray queue
-    uint32_t s_cap;      // shadow queue entries
+    uint32_t s_cap;      // NEE queue entries
     double* acc;         // [P][3] per-pixel sum of this pass' sample colours
 };
 
@@ -28,7 +30,7 @@ struct WfPlan {
     uint64_t chunk;            // camera samples per chunk
     uint32_t root_children;    // ⌊√FH⌋² · modes at depth 0
     uint32_t children;         // modes at depth >= 1 (1, or 2 under SpecularModeAll)
-    uint32_t lights_per_child; // 1, or #lights under LightModeAll
+    uint32_t lights_per_child; // shadow rays per NEE request: 1, or #lights under LightModeAll
     uint32_t trace_blocks;     // grid caps (grid-stride loops)
     uint32_t shade_blocks;
 };

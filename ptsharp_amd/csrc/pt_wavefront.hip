@@ -59,20 +59,44 @@ __device__ __forceinline__ uint32_t append(uint32_t* counter) {
 
 constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that was not cast
 
-// Reserve n slots per lane with one atomic per wave (wave prefix scan); all 64
-// lanes must be active.  Returns this lane's first slot.
-__device__ __forceinline__ uint32_t wave_reserve(uint32_t* counter, uint32_t n) {
-    const int lane = threadIdx.x & 63;
+__device__ __forceinline__ uint32_t wave_scan(uint32_t n, int lane) {  // inclusive
     uint32_t x = n;
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t y = __shfl_up(x, off, 64);
         if (lane >= off) x += y;
     }
-    const uint32_t total = __shfl(x, 63, 64);
-    uint32_t base = 0;
-    if (lane == 0 && total) base = atomicAdd(counter, total);
-    base = __shfl(base, 0, 64);
-    return base + x - n;
+    return x;
+}
+
+// Reserve a lane's a slots of one queue and b of another with ONE returning atomic
+// per 256-thread block: the two counters are the halves of one 64-bit word (a
+// returning atomic on one word saturates near 88 per µs on MI355X,
+// MI355X_MICROARCH.md "dequeue"; per-wave reservation made k_wf_shade wait on it).
+// Block-uniform call sites only.  Returns each lane's first slot in both queues.
+__device__ __forceinline__ void block_reserve2(unsigned long long* word, uint32_t a, uint32_t b, uint32_t& abase,
+                                               uint32_t& bbase) {
+    __shared__ uint32_t s_tot[2][4];
+    __shared__ uint32_t s_base[2][4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t xa = wave_scan(a, lane), xb = wave_scan(b, lane);
+    if (lane == 63) { s_tot[0][wid] = xa; s_tot[1][wid] = xb; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t ta = 0, tb = 0;
+        for (int w = 0; w < 4; w++) {
+            s_base[0][w] = ta; s_base[1][w] = tb;
+            ta += s_tot[0][w]; tb += s_tot[1][w];
+        }
+        unsigned long long base = 0;
+        if (ta | tb) base = atomicAdd(word, ((unsigned long long)tb << 32) | ta);
+        for (int w = 0; w < 4; w++) {
+            s_base[0][w] += (uint32_t)base;
+            s_base[1][w] += (uint32_t)(base >> 32);
+        }
+    }
+    __syncthreads();
+    abase = s_base[0][wid] + xa - a;
+    bbase = s_base[1][wid] + xb - b;
 }
 
 __device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, float3 thr, uint32_t pixel,
@@ -85,9 +109,13 @@ __device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, 
 
 __device__ __forceinline__ void acc_add(double* acc, uint32_t pixel, float r, float g, float b) {
     double* a = acc + 3 * (size_t)pixel;
+#ifdef PT_ABLATE_ACC  // timing-only build: plain (racy) adds instead of atomics
+    a[0] += r; a[1] += g; a[2] += b;
+#else
     if (r != 0.f) atomicAdd(a + 0, (double)r);
     if (g != 0.f) atomicAdd(a + 1, (double)g);
     if (b != 0.f) atomicAdd(a + 2, (double)b);
+#endif
 }
 
 // ---------------------------------------------------------------- camera
@@ -119,7 +147,7 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
             cast_ray(cam, x, y, w, h, fu, fv, K, o, d);
         }
         const uint32_t i = append(&Q.counts[0]);
-        if (i >= Q.cap) { Q.counts[3] = 1; continue; }
+        if (i >= Q.cap) { Q.counts[4] = 1; continue; }
         ray_store(Q, 0, i, o, d, make_float3(1.f, 1.f, 1.f), (uint32_t)pix, 0u | (1u << 8), K);
     }
 }
@@ -130,11 +158,11 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
     __shared__ uint32_t s_stack[kMaxDepth * kTB];
     uint32_t* stack = s_stack + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        // the next-depth queue and the shadow queue are free now: reset them for k_wf_shade
-        Q.counts[1 - qi] = 0;
-        Q.counts[2] = 0;
+        // the other pair (consumed) is free now: reset it for k_wf_shade's output
+        Q.counts[2 * (1 - qi)] = 0;
+        Q.counts[2 * (1 - qi) + 1] = 0;
     }
-    const uint32_t n = Q.counts[qi] < Q.cap ? Q.counts[qi] : Q.cap;
+    const uint32_t n = Q.counts[2 * qi] < Q.cap ? Q.counts[2 * qi] : Q.cap;
     Counters ctr{0, 0, 0, 0};
     for (uint32_t i = blockIdx.x * kTB + threadIdx.x; i < n; i += gridDim.x * kTB) {
         float4 b = nt_load(&Q.q_d[qi][i]);
@@ -160,19 +188,19 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
 #ifndef PT_SHADE_WAVES
 #define PT_SHADE_WAVES 2
 #endif
-// One thread per queued ray.  Every wave reserves the queue slots of all its
-// lanes' children with ONE atomic per queue (a returning atomic on one word
-// saturates near 88 per µs on MI355X, MI355X_MICROARCH.md "dequeue"); a child
-// that turns out dead (p <= 0, a specular Any-mode child's shadow slot, light
-// below the horizon) leaves a kDead marker that the consuming kernel skips.
+// One thread per queued ray: Hit.Info, emission, then every child of the vertex
+// (the u/v/mode loop of Sampler.cs:96-131).  Which children are reflected / live
+// depends only on the vertex' Fresnel p and one draw per Any-mode child, so each
+// lane counts its extension rays and NEE requests before computing any bounce, and
+// the wave reserves both queues with ONE atomic each (a returning atomic on one
+// word saturates near 88 per µs on MI355X, MI355X_MICROARCH.md "dequeue").  Light
+// sampling itself runs in k_wf_shadow.
 template <bool COUNT>
 __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
-    const uint32_t n = Q.counts[qi] < Q.cap ? Q.counts[qi] : Q.cap;
+    const uint32_t n = Q.counts[2 * qi] < Q.cap ? Q.counts[2 * qi] : Q.cap;
     const int qo = 1 - qi;
-    const int nl = S.num_lights;
-    const bool all_lights = smp.light_mode == 1;
-    const uint32_t lights_per_child = all_lights ? (uint32_t)nl : 1u;
+    const bool nee_on = smp.dl && S.num_lights > 0;
     Counters ctr{0, 0, 0, 0};
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {  // block-uniform
         const uint32_t i = i0 + threadIdx.x;
@@ -180,11 +208,13 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
         float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, rt = ro;
         uint4 hr = make_uint4(0, 0, 0, 0);
         uint32_t meta = kDead;
+        uint64_t node = 0;
         if (alive) {  // all loads issued together: one memory round trip
             rd = nt_load(&Q.q_d[qi][i]);
             ro = nt_load(&Q.q_o[qi][i]);
             rt = nt_load(&Q.q_t[qi][i]);
             hr = nt_load(&Q.hits[i]);
+            node = nt_load(&Q.q_k[qi][i]);
             meta = __float_as_uint(rd.w);
             alive = meta != kDead;
         }
@@ -200,13 +230,12 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
         Shade sh{};
         int mat = 0, nn = 1, nm = 1, nch = 0;
         float t2[3] = {0.f, 0.f, 0.f};
-        uint64_t node = 0;
+        double pv = 0.0, n1 = 1.0, n2 = 1.0;
         if (alive && !(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67)
             acc_add(Q.acc, pixel, thr[0] * S.env[0], thr[1] * S.env[1], thr[2] * S.env[2]);
             alive = false;
         }
         if (alive) {
-            node = nt_load(&Q.q_k[qi][i]);
             sh = hit_info<COUNT>(S, h, o, d, ctr);
             mat = sh.mat;
             const DevMaterial& m = S.mats[mat];
@@ -224,60 +253,58 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
             nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
             nch = alive ? nn * nn * nm : 0;
             for (int k = 0; k < 3; k++) t2[k] = thr[k] * inv_n2;
+            pv = vertex_p(m, sh, d, n1, n2);
         }
-        // extension-ray slots: reserved for all children at once (all 64 lanes take part);
-        // shadow rays are appended compactly (their count is known only after the bounce).
-        const uint32_t n_ext = (depth + 1 <= smp.mb) ? (uint32_t)nch : 0u;
-        const bool do_nee = smp.dl && nl > 0;
-        const uint32_t ebase = wave_reserve(&Q.counts[qo], n_ext);
-        if (ebase + n_ext > Q.cap) Q.counts[3] = 1;
         const DevMaterial& m = S.mats[mat];
         const int ma = nm == 2 ? 1 : 0;
+        const bool ext_on = depth + 1 <= smp.mb;   // deeper samples return black without an Intersect
+        // child c: mode, reflect decision, liveness (p > 0 after the Any-mode override)
+        uint32_t n_ext = 0, n_nee = 0;
         for (int c = 0; c < nch; c++) {
             const int mode = ma + c % nm;
-            const int stratum = c / nm;
-            const int u = stratum / nn, v = stratum % nn;
+            const bool refl = mode == 2 || (mode == 0 && draw(child_key(node, (uint32_t)c), D_REFLECT) < pv);
+            const bool live = mode == 0 || (refl ? pv > 0 : (1 - pv) > 0);
+            n_ext += (live && ext_on) ? 1u : 0u;
+            n_nee += (live && !refl && !m.transparent && nee_on) ? 1u : 0u;
+        }
+        uint32_t ebase, nbase;
+        block_reserve2(reinterpret_cast<unsigned long long*>(&Q.counts[2 * qo]), n_ext, n_nee, ebase, nbase);
+        if (ebase + n_ext > Q.cap || nbase + n_nee > Q.s_cap) Q.counts[4] = 1;
+        uint32_t ej = ebase, nj = nbase;
+        for (int c = 0; c < nch; c++) {
+            const int mode = ma + c % nm;
             const uint64_t E = child_key(node, (uint32_t)c);
-            const double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)nn;
-            const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
-            const uint32_t es = ebase + (uint32_t)c;
-            v3 no, nd;
-            bool reflected;
-            double p;
-            bounce(m, sh, d, fu, fv, mode, E, no, nd, reflected, p);
-            if (mode == 0) p = 1;
-            const bool live = p > 0;
-            const float fp = (float)p;
+            const bool refl = mode == 2 || (mode == 0 && draw(E, D_REFLECT) < pv);
+            const bool live = mode == 0 || (refl ? pv > 0 : (1 - pv) > 0);
+            if (!live) continue;
+            const bool reflected = refl || m.transparent;                 // specular branch (Sampler.cs:109-115)
+            const float fp = mode == 0 ? 1.0f : (float)(refl ? pv : 1 - pv);
             float w[3];
-            if (live && reflected) {
+            if (reflected) {
                 for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * m.color[k]);
-            } else if (live) {
+            } else {
                 for (int k = 0; k < 3; k++) w[k] = fp * m.color[k];
-                if (do_nee) {  // sampleLights (Sampler.cs:191-210)
-                    const int first = all_lights ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
-                    const int last = all_lights ? nl : first + 1;
-                    const float scale = all_lights ? 1.0f / (float)nl : (float)nl;
-                    for (int li = first; li < last; li++) {
-                        const uint64_t LK = all_lights ? light_key(E, (uint32_t)li) : E;
-                        v3 ldir;
-                        float3 lc;
-                        if (!light_setup(S, smp, S.lights[li], sh.pos, sh.nrm, LK, ldir, lc)) continue;
-                        const uint32_t si = append(&Q.counts[2]);
-                        if (si >= Q.s_cap) { Q.counts[3] = 1; continue; }
-                        nt_store(&Q.s_o[si], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
-                        nt_store(&Q.s_d[si], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float((uint32_t)li)));
-                        nt_store(&Q.s_c[si], make_float4(t2[0] * w[0] * (lc.x * scale), t2[1] * w[1] * (lc.y * scale),
-                                                         t2[2] * w[2] * (lc.z * scale), 0.f));
+                if (nee_on) {  // diffuse child: sampleLights from the normal ray, in k_wf_shadow
+                    if (nj < Q.s_cap) {
+                        nt_store(&Q.n_o[nj], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
+                        nt_store(&Q.n_n[nj], make_float4(sh.nrm.x, sh.nrm.y, sh.nrm.z, 0.f));
+                        nt_store(&Q.n_w[nj], make_float4(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2], 0.f));
+                        nt_store(&Q.n_k[nj], E);
                     }
+                    nj++;
                 }
             }
-            if (n_ext == 0 || es >= Q.cap) continue;  // depth > MaxBounces: sample() returns black, no Intersect
-            if (!live) {
-                nt_store(&Q.q_d[qo][es], make_float4(0.f, 0.f, 0.f, __uint_as_float(kDead)));
-                continue;
-            }
-            ray_store(Q, qo, es, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
-                      (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
+            if (!ext_on) continue;
+            const int stratum = c / nm;
+            const int u = stratum / nn, v = stratum % nn;
+            const double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)nn;
+            const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
+            v3 no, nd;
+            bounce_dir(m, sh, d, fu, fv, refl, n1, n2, E, no, nd);
+            if (ej < Q.cap)
+                ray_store(Q, qo, ej, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
+                          (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
+            ej++;
         }
     }
     if (COUNT) {
@@ -287,19 +314,34 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
 }
 
 // ---------------------------------------------------------------- shadow rays
+// One thread per NEE request: sampleLights / sampleLight (Sampler.cs:191-296) —
+// light choice, soft-shadow point, coverage — then the visibility query.
 template <bool COUNT>
-__global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, DevSampler smp, WfQueues Q, int qo,
+                                                   unsigned long long* counters) {
     __shared__ uint32_t s_stack[kMaxDepth * kTB];
     uint32_t* stack = s_stack + threadIdx.x;
-    const uint32_t n = Q.counts[2] < Q.s_cap ? Q.counts[2] : Q.s_cap;
+    const uint32_t n = Q.counts[2 * qo + 1] < Q.s_cap ? Q.counts[2 * qo + 1] : Q.s_cap;
+    const int nl = S.num_lights;
+    const bool all = smp.light_mode == 1;
     Counters ctr{0, 0, 0, 0};
     for (uint32_t i = blockIdx.x * kTB + threadIdx.x; i < n; i += gridDim.x * kTB) {
-        float4 b = nt_load(&Q.s_d[i]);
-        float4 a = nt_load(&Q.s_o[i]);
-        const DevLight L = S.lights[__float_as_uint(b.w)];
-        if (light_visible<COUNT, kTB>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) {
-            float4 c = nt_load(&Q.s_c[i]);
-            acc_add(Q.acc, __float_as_uint(a.w), c.x, c.y, c.z);
+        const float4 a = nt_load(&Q.n_o[i]);
+        const float4 b = nt_load(&Q.n_n[i]);
+        const float4 wt = nt_load(&Q.n_w[i]);
+        const uint64_t E = nt_load(&Q.n_k[i]);
+        const v3 o{a.x, a.y, a.z}, nrm{b.x, b.y, b.z};
+        const int first = all ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
+        const int last = all ? nl : first + 1;
+        const float scale = all ? 1.0f / (float)nl : (float)nl;
+        for (int li = first; li < last; li++) {
+            const DevLight L = S.lights[li];
+            v3 ldir;
+            float3 lc;
+            if (!light_setup(S, smp, L, o, nrm, all ? light_key(E, (uint32_t)li) : E, ldir, lc)) continue;
+            if (light_visible<COUNT, kTB>(S, L, o, ldir, stack, ctr))
+                acc_add(Q.acc, __float_as_uint(a.w), wt.x * (lc.x * scale), wt.y * (lc.y * scale),
+                        wt.z * (lc.z * scale));
         }
     }
     const uint32_t lane = threadIdx.x & 63;
@@ -351,7 +393,7 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     for (int r = 0; r < rounds; r++) {
         for (uint64_t begin = 0; begin < total; begin += plan.chunk) {
             const uint32_t cnt = (uint32_t)((total - begin) < plan.chunk ? (total - begin) : plan.chunk);
-            hipError_t e = hipMemsetAsync(Q.counts, 0, 3 * sizeof(uint32_t), stream);
+            hipError_t e = hipMemsetAsync(Q.counts, 0, 4 * sizeof(uint32_t), stream);
             if (e != hipSuccess) return e;
             begin_k(0);
             hipLaunchKernelGGL(k_wf_camera, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Q, begin,
@@ -371,11 +413,10 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
                 else hipLaunchKernelGGL(k_wf_shade<false>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
                 end_k(2);
                 const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
-                const uint64_t shadows = children * (uint64_t)plan.lights_per_child;
-                const unsigned hg = grid_for(shadows, kTB, plan.trace_blocks);
+                const unsigned hg = grid_for(children, kTB, plan.trace_blocks);
                 begin_k(3);
-                if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, Q, B.counters);
-                else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, Q, B.counters);
+                if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
+                else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
                 end_k(3);
                 bound = children < Q.cap ? children : Q.cap;
                 qi = 1 - qi;
