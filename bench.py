@@ -30,10 +30,11 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/s (rays×bounces/s) at 1920×1080×1024spp; PSNR vs C# ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
 
-# Algorithmic bytes per unit: per ray 32 B per BVH node tested,
-# 36 B per primitive tested (v0, e1, e2), 28 B ray in + 16 B hit out, and 40 B
-# (three normals + material id) per closest-hit shading fetch.
-B_NODE, B_PRIM, B_RAY, B_SHADE = 32, 36, 28 + 16, 40
+# Algorithmic bytes per unit: per ray 112 B per 4-wide BVH node
+# fetched (four child boxes of 24 B + four 4-B child refs), 36 B per primitive
+# tested (v0, e1, e2), 28 B ray in + 16 B hit out, and 40 B (three normals +
+# material id) per closest-hit shading fetch.
+B_NODE, B_PRIM, B_RAY, B_SHADE = 112, 36, 28 + 16, 40
 
 
 def parse():
@@ -92,8 +93,8 @@ def main():
     ext_rays = ctr.rays - ctr.shadow_rays
     ext_nodes = ctr.nodes_visited - ctr.shadow_nodes
     ext_prims = ctr.prims_tested - ctr.shadow_prims
-    bytes_ext = B_NODE * 2 * ext_nodes + B_PRIM * ext_prims + B_RAY * ext_rays
-    bytes_sh = B_NODE * 2 * ctr.shadow_nodes + B_PRIM * ctr.shadow_prims + B_RAY * ctr.shadow_rays
+    bytes_ext = B_NODE * ext_nodes + B_PRIM * ext_prims + B_RAY * ext_rays
+    bytes_sh = B_NODE * ctr.shadow_nodes + B_PRIM * ctr.shadow_prims + B_RAY * ctr.shadow_rays
     bytes_all = bytes_ext + bytes_sh + B_SHADE * ctr.shading_fetches
     r.ResetBuffer()
 
@@ -193,7 +194,7 @@ def main():
             "avg_launch_ms": round(float(avg_launch_ms), 4), "launches": int(klaunch[dom]),
             "bytes_per_launch": round(dom_bytes / max(klaunch[dom], 1)),
             "bytes_per_ray": round(per_ray, 2),
-            "nodes_per_ray": round(2 * (ext_nodes if dom == _abi.K_TRACE else ctr.nodes_visited) /
+            "nodes_per_ray": round((ext_nodes if dom == _abi.K_TRACE else ctr.nodes_visited) /
                                    max(ext_rays if dom == _abi.K_TRACE else ctr.rays, 1), 3),
             "prims_per_ray": round((ext_prims if dom == _abi.K_TRACE else ctr.prims_tested) /
                                    max(ext_rays if dom == _abi.K_TRACE else ctr.rays, 1), 3),

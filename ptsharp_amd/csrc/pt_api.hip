@@ -204,18 +204,16 @@ inline void pad_box(float* lo, float* hi) {
     }
 }
 
-// BVH nodes → device float4 pairs with packed child / leaf refs.
-std::vector<float4> pack_nodes(const pt::BvhResult& b) {
-    std::vector<float4> out(b.nodes.size() * 2);
-    for (size_t i = 0; i < b.nodes.size(); i++) {
-        const pt::BvhNode& n = b.nodes[i];
-        uint32_t ref;
-        if (n.b == 0) ref = n.a;  // inner: left child of the pair
-        else ref = 0x80000000u | ((n.b - 1u) << 29) | (n.a & 0x1FFFFFFFu);
-        out[2 * i] = f4(n.bmin[0], n.bmin[1], n.bmin[2], u2f(ref));
-        out[2 * i + 1] = f4(n.bmax[0], n.bmax[1], n.bmax[2], 0.f);
-    }
-    return out;
+// BVH2 → 4-wide nodes (pt_bvh.h collapse_bvh4) as device float4 rows.  The
+// collapse keeps every path's pushes within the kMaxDepth-entry LDS stack.
+int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_nodes) {
+    pt::Bvh4Result r;
+    pt::collapse_bvh4(b, pt::kMaxDepth, r);
+    if (r.stack_need > pt::kMaxDepth) return fail(PT_ERR_UNSUPPORTED, "BVH4 traversal stack bound exceeded");
+    out.resize(r.words.size() / 4);
+    std::memcpy(out.data(), r.words.data(), r.words.size() * sizeof(uint32_t));
+    num_nodes = (int32_t)r.nodes();
+    return PT_OK;
 }
 
 // Box of a light shape as Box.Center / Box.OuterRadius compute it (Box.cs:316-324).
@@ -384,7 +382,9 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         tri_shade[3 * i + 1] = f4(n2[1], n2[2], n3[0], n3[1]);
         tri_shade[3 * i + 2] = f4(n3[2], u2f((uint32_t)d->tri_material[s]), 0.f, 0.f);
     }
-    std::vector<float4> tri_nodes = pack_nodes(tb);
+    std::vector<float4> tri_nodes;
+    int32_t tri_num_nodes = 0;
+    if ((rc = pack_nodes(tb, tri_nodes, tri_num_nodes))) return rc;
 
     // --- analytic BVH (spheres, cubes)
     const size_t na = ana_kind.size();
@@ -427,7 +427,9 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
             if (ana_pos_of_scene_cube[(size_t)j] < 0) ana_pos_of_scene_cube[(size_t)j] = (int32_t)i;
         }
     }
-    std::vector<float4> ana_nodes = pack_nodes(ab);
+    std::vector<float4> ana_nodes;
+    int32_t ana_num_nodes = 0;
+    if ((rc = pack_nodes(ab, ana_nodes, ana_num_nodes))) return rc;
 
     // --- planes
     std::vector<float4> planes(plane_scene.size() * 2);
@@ -477,15 +479,15 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, planes, &S.planes); if (rc) return rc;
     rc = upload(c, mats, &S.mats); if (rc) return rc;
     rc = upload(c, lights, &S.lights); if (rc) return rc;
-    S.tri_num_nodes = (int32_t)tb.nodes.size();
-    S.ana_num_nodes = (int32_t)ab.nodes.size();
+    S.tri_num_nodes = tri_num_nodes;
+    S.ana_num_nodes = ana_num_nodes;
     S.num_planes = (int32_t)plane_scene.size();
     S.num_lights = (int32_t)lights.size();
     for (int k = 0; k < 3; k++) S.env[k] = (float)d->env_color[k];
     PT_HIP(hipStreamSynchronize(c->stream));
     c->S = S;
     c->has_scene = true;
-    c->stats.bvh_nodes = tb.nodes.size() + ab.nodes.size();
+    c->stats.bvh_nodes = (uint64_t)tri_num_nodes + (uint64_t)ana_num_nodes;
     c->stats.bvh_bytes = (tri_nodes.size() + ana_nodes.size()) * sizeof(float4) +
                          (tri_recs.size() + tri_shade.size() + ana_recs.size()) * sizeof(float4);
     c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

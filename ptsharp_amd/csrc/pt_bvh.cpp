@@ -174,4 +174,94 @@ void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int thre
     out.leaves = b.leaves.load();
 }
 
+namespace {
+
+struct Collapser {
+    const std::vector<BvhNode>& n2;
+    Bvh4Result& out;
+    int budget;
+    std::vector<int> height;  // BVH2 stack need below a node (leaf: 0)
+
+    bool is_leaf(uint32_t i) const { return n2[i].b != 0; }
+    float area(uint32_t i) const {
+        const BvhNode& n = n2[i];
+        float dx = n.bmax[0] - n.bmin[0], dy = n.bmax[1] - n.bmin[1], dz = n.bmax[2] - n.bmin[2];
+        return dx * dy + dy * dz + dz * dx;
+    }
+    int fill_height(uint32_t i) {
+        if (is_leaf(i)) return height[i] = 0;
+        int l = fill_height(n2[i].a), r = fill_height(n2[i].a + 1);
+        return height[i] = 1 + std::max(l, r);
+    }
+    uint32_t ref_of(uint32_t i, uint32_t node4_of_inner) const {
+        if (is_leaf(i)) return 0x80000000u | ((n2[i].b - 1u) << 29) | (n2[i].a & 0x1FFFFFFFu);
+        return node4_of_inner;
+    }
+    uint32_t alloc() {
+        out.words.resize(out.words.size() + kNode4Words, 0u);
+        return (uint32_t)(out.nodes() - 1);
+    }
+    // children set of BVH4 node `at` built from BVH2 subtree `C` (initial set), ancestors pushed A
+    void emit(uint32_t at, std::vector<uint32_t> C, int A, int depth) {
+        out.depth = std::max(out.depth, depth);
+        for (;;) {
+            if (C.size() >= 4) break;
+            // expand the largest inner child whose expansion keeps the stack budget
+            int pick = -1;
+            float best = -1.f;
+            for (size_t k = 0; k < C.size(); k++) {
+                if (is_leaf(C[k])) continue;
+                int maxh = 0;
+                for (size_t j = 0; j < C.size(); j++)
+                    if (j != k) maxh = std::max(maxh, height[C[j]]);
+                maxh = std::max(maxh, std::max(height[n2[C[k]].a], height[n2[C[k]].a + 1]));
+                if (A + (int)C.size() + maxh > budget) continue;   // |C'| - 1 = |C|
+                float a = area(C[k]);
+                if (a > best) { best = a; pick = (int)k; }
+            }
+            if (pick < 0) break;
+            uint32_t e = C[(size_t)pick];
+            C[(size_t)pick] = n2[e].a;
+            C.push_back(n2[e].a + 1);
+        }
+        const int pushed = A + (int)C.size() - 1;
+        out.stack_need = std::max(out.stack_need, pushed);
+        out.children += (int64_t)C.size();
+        uint32_t refs[4] = {kEmpty4, kEmpty4, kEmpty4, kEmpty4};
+        std::vector<std::pair<uint32_t, uint32_t>> inner;  // (bvh2 node, bvh4 node)
+        for (size_t k = 0; k < C.size(); k++) {
+            uint32_t node4 = 0;
+            if (!is_leaf(C[k])) { node4 = alloc(); inner.emplace_back(C[k], node4); }
+            refs[k] = ref_of(C[k], node4);
+        }
+        uint32_t* w = &out.words[(size_t)at * kNode4Words];
+        for (size_t k = 0; k < 4; k++) {
+            float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
+            if (k < C.size())
+                for (int ax = 0; ax < 3; ax++) { lo[ax] = n2[C[k]].bmin[ax]; hi[ax] = n2[C[k]].bmax[ax]; }
+            for (int ax = 0; ax < 3; ax++) {
+                std::memcpy(&w[8 * ax + k], &lo[ax], 4);
+                std::memcpy(&w[8 * ax + 4 + k], &hi[ax], 4);
+            }
+            w[24 + k] = refs[k];
+        }
+        for (auto& pr : inner) emit(pr.second, {n2[pr.first].a, n2[pr.first].a + 1}, pushed, depth + 1);
+    }
+};
+
+}  // namespace
+
+void collapse_bvh4(const BvhResult& bvh2, int stack_budget, Bvh4Result& out) {
+    out.words.clear();
+    out.stack_need = 0;
+    out.depth = 0;
+    out.children = 0;
+    if (bvh2.nodes.empty()) return;
+    Collapser c{bvh2.nodes, out, stack_budget, std::vector<int>(bvh2.nodes.size(), 0)};
+    c.fill_height(0);
+    const uint32_t root = c.alloc();
+    if (c.is_leaf(0)) c.emit(root, {0u}, 0, 0);
+    else c.emit(root, {bvh2.nodes[0].a, bvh2.nodes[0].a + 1}, 0, 0);
+}
+
 }  // namespace pt

@@ -8,6 +8,7 @@
 // depth bounded by kMaxDepth so the traversal stack fits a fixed LDS budget.
 #pragma once
 #include <stdint.h>
+#include <cstddef>
 #include <vector>
 
 namespace pt {
@@ -34,5 +35,28 @@ struct BvhResult {
 
 // prim_min/prim_max: [n][3] AABBs.  Builds with up to `threads` host threads.
 void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out);
+
+// 4-wide BVH collapsed from the BVH2: one 128-byte node (one cache line) per
+// step of the traversal instead of a 64-byte child pair, so a ray makes about
+// half as many dependent loads.  Node = 32 words, children as SoA:
+//   [0..3] lo.x  [4..7] hi.x  [8..11] lo.y  [12..15] hi.y  [16..19] lo.z  [20..23] hi.z
+//   [24..27] child ref  [28..31] 0
+// ref: bit31 = 0 → inner node index; bit31 = 1 → leaf, bits 29..30 = count-1,
+// bits 0..28 = first primitive; kEmpty4 = unused slot.  Node 0 is the root.
+constexpr uint32_t kEmpty4 = 0x7FFFFFFFu;
+constexpr int kNode4Words = 32;
+
+struct Bvh4Result {
+    std::vector<uint32_t> words;   // kNode4Words per node
+    int stack_need = 0;            // worst-case traversal stack entries (<= budget)
+    int depth = 0;
+    int64_t children = 0;          // used child slots (fill = children / (4 * nodes))
+    size_t nodes() const { return words.size() / kNode4Words; }
+};
+
+// A traversal pushes up to (children - 1) entries per node, so collapsing is
+// limited on the tallest paths to keep every root-to-leaf path's pushes within
+// `stack_budget` (the LDS stack depth) — the guarantee the BVH2 had by depth.
+void collapse_bvh4(const BvhResult& bvh2, int stack_budget, Bvh4Result& out);
 
 }  // namespace pt

@@ -25,19 +25,6 @@ struct Counters {
 
 __device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
 
-// Conservative fp32 slab test: (b - o) * (1/d) carries <= 3 ulp of relative error,
-// so the far distance is widened by 2^-21 relative; NaN slabs (o on a plane with
-// d = 0) drop out of fminf/fmaxf, which only widens the interval.
-__device__ __forceinline__ bool slab(float4 lo, float4 hi, v3 o, v3 invd, float tmax, float& tentry) {
-    float tx1 = (lo.x - o.x) * invd.x, tx2 = (hi.x - o.x) * invd.x;
-    float ty1 = (lo.y - o.y) * invd.y, ty2 = (hi.y - o.y) * invd.y;
-    float tz1 = (lo.z - o.z) * invd.z, tz2 = (hi.z - o.z) * invd.z;
-    float tn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fmaxf(fminf(tz1, tz2), 0.0f));
-    float tf = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fminf(fmaxf(tz1, tz2), tmax));
-    tentry = tn;
-    return tn <= tf * 1.0000005f;
-}
-
 // Round a hit distance up so the fp32 cull never drops an equal-t candidate.
 __device__ __forceinline__ float tmax_bound(double t) {
     float f = (float)t;
@@ -63,41 +50,71 @@ __device__ __forceinline__ double prim_t(const float4* __restrict__ recs, uint32
     return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
 }
 
-// Stack-based BVH2 traversal.  A child pair is fetched together (64 B, one
-// line); the nearer child is descended, the farther pushed on the per-lane LDS
-// stack (`stack` points at this lane's column, entries STRIDE words apart).
-// Node ref (host encoding, pt_api.hip): bit31 = 0 → inner, value = index of the
-// pair's left node; bit31 = 1 → leaf, bits 29..30 = count-1, bits 0..28 = first.
+// Conservative fp32 slab test of one child box: (b - o) * (1/d) carries <= 3 ulp
+// of relative error, so the far distance is widened by 2^-21 relative; NaN slabs
+// (o on a plane with d = 0) drop out of fminf/fmaxf, which only widens the interval.
+__device__ __forceinline__ float slab1(float lx, float hx, float ly, float hy, float lz, float hz, v3 o, v3 invd,
+                                       float tmax) {
+    float tx1 = (lx - o.x) * invd.x, tx2 = (hx - o.x) * invd.x;
+    float ty1 = (ly - o.y) * invd.y, ty2 = (hy - o.y) * invd.y;
+    float tz1 = (lz - o.z) * invd.z, tz2 = (hz - o.z) * invd.z;
+    float tn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fmaxf(fminf(tz1, tz2), 0.0f));
+    float tf = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fminf(fmaxf(tz1, tz2), tmax));
+    return tn <= tf * 1.0000005f ? tn : __int_as_float(0x7f800000);  // entry distance, +inf = miss
+}
+
+__device__ __forceinline__ void cswap(float& ka, uint32_t& va, float& kb, uint32_t& vb) {
+    const bool s = kb < ka;
+    const float k = s ? kb : ka;
+    kb = s ? ka : kb;
+    ka = k;
+    const uint32_t v = s ? vb : va;
+    vb = s ? va : vb;
+    va = v;
+}
+
+// Stack-based BVH4 traversal (node layout: pt_bvh.h, collapse_bvh4).  A node is
+// one 128-byte line fetched with seven independent 16-byte loads; the four
+// child slabs are tested, hits sorted nearest-first with a 5-comparator network,
+// the nearest descended and the others pushed far-to-near on the per-lane LDS
+// stack (`stack` = this lane's column, entries STRIDE words apart).  The builder
+// bounds every path's pushes by kMaxDepth, the stack depth.
 // ANY: stop at the first primitive with t < best.t (shadow visibility).
 template <bool TRI, bool COUNT, bool ANY, int STRIDE>
 __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32_t num_nodes,
                                          const float4* __restrict__ recs, v3 o, v3 d, v3 invd, HitRec& best,
                                          uint32_t* __restrict__ stack, Counters& ctr) {
     if (num_nodes <= 0) return false;
-    float4 r0 = nodes[0], r1 = nodes[1];
-    float te;
-    if (!slab(r0, r1, o, invd, tmax_bound(best.t), te)) return false;
-    uint32_t ref = f2u(r0.w);
+    uint32_t ref = 0;  // root: always an inner node
     int sp = 0;
     for (;;) {
         if (!(ref & 0x80000000u)) {
-            const float4* c = nodes + 2 * (size_t)ref;
-            float4 l0 = c[0], l1 = c[1], q0 = c[2], q1 = c[3];
+            const float4* c = nodes + 8 * (size_t)ref;
+            const float4 lx = c[0], hx = c[1], ly = c[2], hy = c[3], lz = c[4], hz = c[5];
+            const uint4 rf = *reinterpret_cast<const uint4*>(c + 6);
             if (COUNT) ctr.nodes++;
-            float tmax = tmax_bound(best.t);
-            float tl, tr;
-            bool hl = slab(l0, l1, o, invd, tmax, tl);
-            bool hr = slab(q0, q1, o, invd, tmax, tr);
-            if (hl && hr) {
-                uint32_t nearr = f2u(l0.w), farr = f2u(q0.w);
-                if (tr < tl) { uint32_t s = nearr; nearr = farr; farr = s; }
-                stack[sp * STRIDE] = farr;
-                sp++;
-                ref = nearr;
+            const float tmax = tmax_bound(best.t);
+            const float inf = __int_as_float(0x7f800000);
+            float k0 = slab1(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, o, invd, tmax);
+            float k1 = slab1(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, o, invd, tmax);
+            float k2 = slab1(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, o, invd, tmax);
+            float k3 = slab1(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, o, invd, tmax);
+            uint32_t v0 = rf.x, v1 = rf.y, v2 = rf.z, v3r = rf.w;
+            if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
+            if (v2 == kEmpty4) k2 = inf;
+            if (v3r == kEmpty4) k3 = inf;
+            cswap(k0, v0, k1, v1);
+            cswap(k2, v2, k3, v3r);
+            cswap(k0, v0, k2, v2);
+            cswap(k1, v1, k3, v3r);
+            cswap(k1, v1, k2, v2);
+            if (k0 != inf) {
+                if (k3 != inf) { stack[sp * STRIDE] = v3r; sp++; }
+                if (k2 != inf) { stack[sp * STRIDE] = v2; sp++; }
+                if (k1 != inf) { stack[sp * STRIDE] = v1; sp++; }
+                ref = v0;
                 continue;
             }
-            if (hl) { ref = f2u(l0.w); continue; }
-            if (hr) { ref = f2u(q0.w); continue; }
         } else {
             const uint32_t first = ref & 0x1FFFFFFFu, cnt = ((ref >> 29) & 3u) + 1u;
             for (uint32_t k = 0; k < cnt; k++) {
