@@ -157,6 +157,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
     if ((rc = wf_alloc(c, &Q.n_w, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.n_k, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.counts, 8))) return rc;
+    if ((rc = wf_alloc(c, &Q.ovf, (size_t)(pt::kMaxDepth - pt::kLdsStack) * pt::kWfMaxThreads))) return rc;
     size_t P = (size_t)c->width * (size_t)c->height;
     if ((rc = wf_alloc(c, &Q.acc, P * 3))) return rc;
     PT_HIP(hipMemsetAsync(Q.acc, 0, P * 3 * sizeof(double), c->stream));
@@ -540,7 +541,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     plan.root_children = (uint32_t)std::max(1, n_root * n_root * nm_root);
     plan.children = (uint32_t)nm;
     plan.lights_per_child = (uint32_t)(sampler->light_mode == PT_LIGHT_ALL ? std::max(1, c->S.num_lights) : 1);
-    plan.trace_blocks = 256 * 8;
+    plan.trace_blocks = pt::kWfMaxBlocks;   // the stack overflow columns are sized for this grid
     plan.shade_blocks = 256 * 8;
     const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp);
     double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)

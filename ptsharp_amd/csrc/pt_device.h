@@ -50,6 +50,32 @@ __device__ __forceinline__ double prim_t(const float4* __restrict__ recs, uint32
     return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
 }
 
+// Per-lane traversal stacks.  LdsStack: all kMaxDepth entries in LDS (column
+// `lds`, entries STRIDE words apart).  SpillStack: the first LDSN entries in LDS
+// and the rarely used deeper ones in a per-thread global column (entries
+// `ostride` words apart, coalesced across lanes), so a traversal kernel's LDS
+// footprint no longer caps its occupancy.
+template <int STRIDE>
+struct LdsStack {
+    uint32_t* lds;
+    __device__ __forceinline__ void put(int i, uint32_t v) const { lds[i * STRIDE] = v; }
+    __device__ __forceinline__ uint32_t get(int i) const { return lds[i * STRIDE]; }
+};
+
+template <int STRIDE, int LDSN>
+struct SpillStack {
+    uint32_t* lds;
+    uint32_t* ovf;
+    uint32_t ostride;
+    __device__ __forceinline__ void put(int i, uint32_t v) const {
+        if (i < LDSN) lds[i * STRIDE] = v;
+        else ovf[(size_t)(i - LDSN) * ostride] = v;
+    }
+    __device__ __forceinline__ uint32_t get(int i) const {
+        return i < LDSN ? lds[i * STRIDE] : ovf[(size_t)(i - LDSN) * ostride];
+    }
+};
+
 // Conservative fp32 slab test of one child box: (b - o) * (1/d) carries <= 3 ulp
 // of relative error, so the far distance is widened by 2^-21 relative; NaN slabs
 // (o on a plane with d = 0) drop out of fminf/fmaxf, which only widens the interval.
@@ -76,14 +102,13 @@ __device__ __forceinline__ void cswap(float& ka, uint32_t& va, float& kb, uint32
 // Stack-based BVH4 traversal (node layout: pt_bvh.h, collapse_bvh4).  A node is
 // one 128-byte line fetched with seven independent 16-byte loads; the four
 // child slabs are tested, hits sorted nearest-first with a 5-comparator network,
-// the nearest descended and the others pushed far-to-near on the per-lane LDS
-// stack (`stack` = this lane's column, entries STRIDE words apart).  The builder
-// bounds every path's pushes by kMaxDepth, the stack depth.
+// the nearest descended and the others pushed far-to-near on the per-lane stack
+// (LdsStack / SpillStack).  The builder bounds every path's pushes by kMaxDepth.
 // ANY: stop at the first primitive with t < best.t (shadow visibility).
-template <bool TRI, bool COUNT, bool ANY, int STRIDE>
+template <bool TRI, bool COUNT, bool ANY, class STK>
 __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32_t num_nodes,
                                          const float4* __restrict__ recs, v3 o, v3 d, v3 invd, HitRec& best,
-                                         uint32_t* __restrict__ stack, Counters& ctr) {
+                                         const STK& stack, Counters& ctr) {
     if (num_nodes <= 0) return false;
     uint32_t ref = 0;  // root: always an inner node
     int sp = 0;
@@ -109,9 +134,9 @@ __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32
             cswap(k1, v1, k3, v3r);
             cswap(k1, v1, k2, v2);
             if (k0 != inf) {
-                if (k3 != inf) { stack[sp * STRIDE] = v3r; sp++; }
-                if (k2 != inf) { stack[sp * STRIDE] = v2; sp++; }
-                if (k1 != inf) { stack[sp * STRIDE] = v1; sp++; }
+                if (k3 != inf) { stack.put(sp, v3r); sp++; }
+                if (k2 != inf) { stack.put(sp, v2); sp++; }
+                if (k1 != inf) { stack.put(sp, v1); sp++; }
                 ref = v0;
                 continue;
             }
@@ -129,14 +154,14 @@ __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32
         }
         if (sp == 0) break;
         sp--;
-        ref = stack[sp * STRIDE];
+        ref = stack.get(sp);
     }
     return false;
 }
 
 // Scene.Intersect (Scene.cs:75-79): closest hit over planes, analytic BVH, triangle BVH.
-template <bool COUNT, int STRIDE>
-__device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, uint32_t* stack, Counters& ctr) {
+template <bool COUNT, class STK>
+__device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK& stack, Counters& ctr) {
     ctr.rays++;
     HitRec best{kHitInf, -1, -1};
     for (int i = 0; i < S.num_planes; i++) {
@@ -145,8 +170,8 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, uint32_t*
         if (t < best.t) { best.t = t; best.kind = KIND_PLANE; best.idx = i; }
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    traverse<false, COUNT, false, STRIDE>(S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
-    traverse<true, COUNT, false, STRIDE>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr);
+    traverse<false, COUNT, false>(S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
+    traverse<true, COUNT, false>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr);
     return best;
 }
 
@@ -163,8 +188,8 @@ __device__ __forceinline__ double light_t(const DevScene& S, const DevLight& L, 
 // Shadow visibility (Sampler.cs:261-265): the reference takes the nearest hit and
 // compares it with the light by reference.  Equivalent query: the light's own t,
 // then "is any primitive strictly nearer" (any-hit, early exit).  Counts one ray.
-template <bool COUNT, int STRIDE>
-__device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight& L, v3 o, v3 d, uint32_t* stack,
+template <bool COUNT, class STK>
+__device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight& L, v3 o, v3 d, const STK& stack,
                                               Counters& ctr) {
     ctr.rays++;
     if (L.phantom) {
@@ -172,7 +197,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         // traces the ray, so trace it (the answer is "not visible" either way)
         HitRec h{kHitInf, -1, -1};
         v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-        traverse<true, COUNT, true, STRIDE>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, h, stack, ctr);
+        traverse<true, COUNT, true>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, h, stack, ctr);
         return false;
     }
     double tl = light_t(S, L, o, d);
@@ -183,9 +208,9 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    if (traverse<false, COUNT, true, STRIDE>(S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr))
+    if (traverse<false, COUNT, true>(S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr))
         return false;
-    if (traverse<true, COUNT, true, STRIDE>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr))
+    if (traverse<true, COUNT, true>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr))
         return false;
     return true;
 }

@@ -22,17 +22,18 @@
 namespace pt {
 
 constexpr int kBlock = 256;
+using MStack = LdsStack<kBlock>;
 constexpr int kMaxFrames = 34;   // MaxBounces <= 32 under SpecularModeAll (checked on the host)
 
 // Sampler.sampleLight (Sampler.cs:212-296): the megakernel keeps the reference's
 // nearest-hit + identity structure for the shadow query.
 template <bool COUNT>
 __device__ __noinline__ float3 sample_light(const DevScene& S, const DevSampler& smp, const DevLight& L, v3 o, v3 n,
-                                            uint64_t key, uint32_t* stack, Counters& ctr) {
+                                            uint64_t key, MStack stack, Counters& ctr) {
     v3 dir;
     float3 contrib;
     if (!light_setup(S, smp, L, o, n, key, dir, contrib)) return make_float3(0.f, 0.f, 0.f);
-    HitRec h = trace<COUNT, kBlock>(S, o, dir, stack, ctr);
+    HitRec h = trace<COUNT>(S, o, dir, stack, ctr);
     // hit.Shape != light is a reference compare; struct Triangle lights never match.
     if (!(h.t < kHitInf) || L.phantom || h.kind != L.kind || h.idx != L.index) return make_float3(0.f, 0.f, 0.f);
     return contrib;
@@ -41,7 +42,7 @@ __device__ __noinline__ float3 sample_light(const DevScene& S, const DevSampler&
 // Sampler.sampleLights (Sampler.cs:191-210)
 template <bool COUNT>
 __device__ __forceinline__ float3 sample_lights(const DevScene& S, const DevSampler& smp, v3 o, v3 n, uint64_t key,
-                                                uint32_t* stack, Counters& ctr) {
+                                                MStack stack, Counters& ctr) {
     int nl = S.num_lights;
     if (nl == 0) return make_float3(0.f, 0.f, 0.f);
     if (smp.light_mode == 1) {
@@ -74,7 +75,7 @@ template <bool COUNT>
 __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& smp, const Shade& sh, v3 indir,
                                            const float thr[3], uint64_t node, int n, int nm, int c, float3& acc,
                                            v3& no, v3& nd, bool& emission, float nthr[3], uint64_t& nkey,
-                                           uint32_t* stack, Counters& ctr) {
+                                           MStack stack, Counters& ctr) {
     const DevMaterial& m = S.mats[sh.mat];
     int ma = nm == 2 ? 1 : 0;
     int mode = ma + c % nm;
@@ -111,7 +112,7 @@ __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& 
 // DefaultSampler.Sample(scene, ray) for one camera ray; returns the sample colour.
 template <bool COUNT>
 __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3 d, uint64_t root_key,
-                              uint32_t* stack, Frame* frames, Counters& ctr) {
+                              MStack stack, Frame* frames, Counters& ctr) {
     float3 acc = make_float3(0.f, 0.f, 0.f);
     // current vertex to visit
     bool have = true;
@@ -125,7 +126,7 @@ __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3
         if (have) {
             have = false;
             if (depth <= smp.mb) {
-                HitRec h = trace<COUNT, kBlock>(S, o, d, stack, ctr);
+                HitRec h = trace<COUNT>(S, o, d, stack, ctr);
                 if (!(h.t < kHitInf)) {
                     acc.x += thr[0] * S.env[0];
                     acc.y += thr[1] * S.env[1];
@@ -203,7 +204,7 @@ template <bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera cam, DevSampler smp, DevPass P,
                                                         DevBuffer B) {
     __shared__ uint32_t s_stack[kMaxDepth * kBlock];
-    uint32_t* stack = s_stack + threadIdx.x;
+    const MStack stack{s_stack + threadIdx.x};
     const int tile_slot = blockIdx.x >> 2;
     const int quarter = blockIdx.x & 3;
     const int tile = P.tiles ? P.tiles[tile_slot] : tile_slot;

@@ -24,7 +24,12 @@ struct WfQueues {
     uint32_t cap;        // entries per ray queue
     uint32_t s_cap;      // NEE queue entries
     double* acc;         // [P][3] per-pixel sum of this pass' sample colours
+    uint32_t* ovf;       // traversal stack entries beyond kLdsStack: [kMaxDepth - kLdsStack][kWfMaxThreads]
 };
+
+constexpr int kLdsStack = 16;                    // LDS stack entries per lane (traversal kernels)
+constexpr uint32_t kWfMaxBlocks = 256 * 8;        // grid cap of the traversal kernels
+constexpr uint32_t kWfMaxThreads = kWfMaxBlocks * 256;
 
 struct WfPlan {
     uint64_t chunk;            // camera samples per chunk

@@ -29,6 +29,7 @@
 namespace pt {
 
 constexpr int kTB = 256;   // threads per block, traversal kernels (LDS stack column stride)
+using WStack = SpillStack<kTB, kLdsStack>;
 
 // Streaming (nt) accesses for queue traffic: read or written once per depth, they
 // should not displace the BVH from L2 / the Infinity Cache.
@@ -155,8 +156,8 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
 // ---------------------------------------------------------------- closest hit
 template <bool COUNT>
 __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
-    __shared__ uint32_t s_stack[kMaxDepth * kTB];
-    uint32_t* stack = s_stack + threadIdx.x;
+    __shared__ uint32_t s_stack[kLdsStack * kTB];
+    const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // the other pair (consumed) is free now: reset it for k_wf_shade's output
         Q.counts[2 * (1 - qi)] = 0;
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
         float4 b = nt_load(&Q.q_d[qi][i]);
         float4 a = nt_load(&Q.q_o[qi][i]);
         if (__float_as_uint(b.w) == kDead) continue;
-        HitRec h = trace<COUNT, kTB>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+        HitRec h = trace<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
         unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
         nt_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
     }
@@ -319,8 +320,8 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
 template <bool COUNT>
 __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, DevSampler smp, WfQueues Q, int qo,
                                                    unsigned long long* counters) {
-    __shared__ uint32_t s_stack[kMaxDepth * kTB];
-    uint32_t* stack = s_stack + threadIdx.x;
+    __shared__ uint32_t s_stack[kLdsStack * kTB];
+    const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const uint32_t n = Q.counts[2 * qo + 1] < Q.s_cap ? Q.counts[2 * qo + 1] : Q.s_cap;
     const int nl = S.num_lights;
     const bool all = smp.light_mode == 1;
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, DevSampler smp, W
             v3 ldir;
             float3 lc;
             if (!light_setup(S, smp, L, o, nrm, all ? light_key(E, (uint32_t)li) : E, ldir, lc)) continue;
-            if (light_visible<COUNT, kTB>(S, L, o, ldir, stack, ctr))
+            if (light_visible<COUNT>(S, L, o, ldir, stack, ctr))
                 acc_add(Q.acc, __float_as_uint(a.w), wt.x * (lc.x * scale), wt.y * (lc.y * scale),
                         wt.z * (lc.z * scale));
         }
