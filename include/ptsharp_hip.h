@@ -152,6 +152,8 @@ typedef struct pt_pass_params {
     const int32_t* tiles;    /* tile id = ty * ceil(W/32) + tx                   */
     int32_t engine;          /* pt_engine                                        */
     int32_t flags;           /* PT_PASS_KERNEL_TIMING: per-kernel hipEvent timing */
+    int32_t adaptive_samples;/* Renderer.AdaptiveSamples (Renderer.cs:340-410): per-sample AddSample x N */
+    int32_t firefly_samples; /* Renderer.FireflySamples (Renderer.cs:412-470, FireflyThreshold = 1) */
 } pt_pass_params;
 
 #define PT_PASS_KERNEL_TIMING 1

@@ -57,6 +57,7 @@ typedef struct or_pass_params {
     int32_t num_tiles;
     const int32_t* tiles;
     int32_t engine, flags;  /* product-only (GPU scheduling / timing); ignored by the oracle */
+    int32_t adaptive_samples, firefly_samples;  /* Renderer.AdaptiveSamples / FireflySamples */
 } or_pass_params;
 
 /* Build the scene (k-d trees as Scene.Compile/Tree.NewTree do).  Returns NULL on error. */

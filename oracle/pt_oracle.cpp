@@ -753,6 +753,53 @@ void render_pixel(Integrator& in, const or_camera& cam, int x, int y, int w, int
     welford(M + 3 * i, Vv + 3 * i, N + i, c);
 }
 
+// Sample-index domains of the per-pass extra phases: the main
+// loop uses 0..spp-1.
+constexpr uint32_t kAdaptiveBase = 0x40000000u, kFireflyBase = 0x80000000u;
+
+// One sample of the adaptive / firefly loops: CastRay(x, y, w, h, NextDouble(),
+// NextDouble()) — these loops pass the jitter directly (Renderer.cs:357-361, 432).
+C extra_sample(Integrator& in, const or_camera& cam, int x, int y, int w, int h, const or_pass_params& pp,
+               uint32_t sample) {
+    uint64_t pix = (uint64_t)y * (uint64_t)w + (uint64_t)x;
+    uint64_t K = camera_key(pp.seed, pp.pass_index, pix, sample);
+    double fu = draw(K, D_JX), fv = draw(K, D_JY);
+    Ray ray = cast_ray(cam, x, y, w, h, fu, fv, K);
+    return in.sample(ray, true, in.smp.fh, 0, K);
+}
+
+// buf.StandardDeviation(x, y).MaxComponent() > FireflyThreshold (= 1, Renderer.cs:48, 426):
+// Variance() is black below 2 samples, else V / (N-1) (Buffer.cs:48-55); Pow(0.5) is the
+// correctly rounded root, i.e. sqrt.
+bool firefly_candidate(const double* V, int32_t N) {
+    if (N < 2) return false;
+    double r = std::sqrt(V[0] / (double)(N - 1)), g = std::sqrt(V[1] / (double)(N - 1)),
+           b = std::sqrt(V[2] / (double)(N - 1));
+    return net_max(net_max(r, g), b) > 1.0;
+}
+
+// IsFirefly + CalculateLocalDeviation (Renderer.cs:473-537), 3x3 window clipped to the
+// image.  The reference reads the neighbours while other threads update them; here
+// they come from `snap` (M at the start of the firefly phase) and the pixel's own M
+// is live (`own`), which is what the pixel's own thread sees in the reference.
+bool is_firefly(C s, int x, int y, int w, int h, const double* snap, const double* own) {
+    double brightness = s.r * 0.2126 + s.g * 0.7152 + s.b * 0.0722;
+    if (!(brightness > 0.9)) return false;
+    int sx = std::max(0, x - 1), sy = std::max(0, y - 1);
+    int ex = std::min(w - 1, x + 1), ey = std::min(h - 1, y + 1);
+    double tr = 0, tg = 0, tb = 0;
+    int count = 0;
+    for (int j = sy; j <= ey; j++)
+        for (int i = sx; i <= ex; i++) {
+            const double* c = (i == x && j == y) ? own : snap + 3 * ((size_t)j * (size_t)w + (size_t)i);
+            tr += c[0]; tg += c[1]; tb += c[2];
+            count++;
+        }
+    double ar = tr / count, ag = tg / count, ab = tb / count;
+    double dr = std::fabs(s.r - ar), dg = std::fabs(s.g - ag), db = std::fabs(s.b - ab);
+    return std::sqrt(dr * dr + dg * dg + db * db) > 0.2;
+}
+
 template <class F>
 void parallel_tasks(int64_t ntasks, int nthreads, F&& fn) {
     if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
@@ -855,16 +902,43 @@ int64_t or_render_pass(void* scene, int32_t width, int32_t height, const or_came
     else { tiles.resize((size_t)tx * ty); for (int i = 0; i < tx * ty; i++) tiles[i] = i; }
     int nt = num_threads <= 0 ? (int)std::max(1u, std::thread::hardware_concurrency()) : num_threads;
     std::vector<uint64_t> rays((size_t)nt, 0);
-    parallel_tasks((int64_t)tiles.size(), nt, [&](int64_t t, int tid) {
-        int tile = tiles[(size_t)t];
-        int x0 = (tile % tx) * 32, y0 = (tile / tx) * 32;
-        Tracer tr(s, brute_force != 0);
-        Integrator in(s, sm, tr);
-        for (int y = y0; y < std::min(y0 + 32, (int)height); y++)
-            for (int x = x0; x < std::min(x0 + 32, (int)width); x++)
-                render_pixel(in, *cam, x, y, width, height, *pass, m, v, n);
-        rays[(size_t)tid] += tr.rays;
-    });
+    auto for_tiles = [&](auto&& per_pixel) {
+        parallel_tasks((int64_t)tiles.size(), nt, [&](int64_t t, int tid) {
+            int tile = tiles[(size_t)t];
+            int x0 = (tile % tx) * 32, y0 = (tile / tx) * 32;
+            Tracer tr(s, brute_force != 0);
+            Integrator in(s, sm, tr);
+            for (int y = y0; y < std::min(y0 + 32, (int)height); y++)
+                for (int x = x0; x < std::min(x0 + 32, (int)width); x++) per_pixel(in, x, y);
+            rays[(size_t)tid] += tr.rays;
+        });
+    };
+    for_tiles([&](Integrator& in, int x, int y) { render_pixel(in, *cam, x, y, width, height, *pass, m, v, n); });
+    if (pass->adaptive_samples > 0) {
+        // Adaptive phase (Renderer.cs:340-410): every pixel gets AdaptiveSamples
+        // individual AddSample calls.  The second loop only feeds pixelVariances,
+        // which nothing reads, so it is not traced.
+        for_tiles([&](Integrator& in, int x, int y) {
+            size_t i = (size_t)y * (size_t)width + (size_t)x;
+            for (int j = 0; j < pass->adaptive_samples; j++)
+                welford(m + 3 * i, v + 3 * i, n + i,
+                        extra_sample(in, *cam, x, y, width, height, *pass, kAdaptiveBase + (uint32_t)j));
+        });
+    }
+    if (pass->firefly_samples > 0) {
+        // Firefly phase (Renderer.cs:412-470).  skippedPixels is created empty per call
+        // and each pixel is visited once, so only its first branch is reachable.
+        std::vector<double> snap(m, m + 3 * (size_t)width * (size_t)height);
+        for_tiles([&](Integrator& in, int x, int y) {
+            size_t i = (size_t)y * (size_t)width + (size_t)x;
+            if (!firefly_candidate(v + 3 * i, n[i])) return;
+            for (int j = 0; j < pass->firefly_samples; j++) {
+                C smp = extra_sample(in, *cam, x, y, width, height, *pass, kFireflyBase + (uint32_t)j);
+                if (is_firefly(smp, x, y, width, height, snap.data(), m + 3 * i)) break;
+                welford(m + 3 * i, v + 3 * i, n + i, smp);
+            }
+        });
+    }
     uint64_t total = 0;
     for (uint64_t r : rays) total += r;
     return (int64_t)total;

@@ -64,7 +64,8 @@ class pt_sampler(C.Structure):
 
 class pt_pass_params(C.Structure):
     _fields_ = [("spp", C.c_int32), ("stratified", C.c_int32), ("seed", C.c_uint64), ("pass_index", C.c_uint32),
-                ("num_tiles", C.c_int32), ("tiles", _i), ("engine", C.c_int32), ("flags", C.c_int32)]
+                ("num_tiles", C.c_int32), ("tiles", _i), ("engine", C.c_int32), ("flags", C.c_int32),
+                ("adaptive_samples", C.c_int32), ("firefly_samples", C.c_int32)]
 
 
 class pt_device_opts(C.Structure):

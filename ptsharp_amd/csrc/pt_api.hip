@@ -114,6 +114,10 @@ struct Ctx {
     pt::WfQueues Q{};
     std::vector<DeviceArray> wf_arrays;
     uint32_t wf_cap = 0, wf_scap = 0;
+    // adaptive / firefly phases (allocated on first use, with the queues)
+    uint32_t* d_plist = nullptr;   // [P] firefly candidates
+    uint32_t* d_fcount = nullptr;
+    double* d_snap = nullptr;      // [P][3] M at the start of the firefly phase
     int last_engine = 0;
     EventTimer timer;
 };
@@ -125,6 +129,9 @@ void free_wavefront(Ctx* c) {
     c->wf_arrays.clear();
     c->Q = pt::WfQueues{};
     c->wf_cap = c->wf_scap = 0;
+    c->d_plist = nullptr;
+    c->d_fcount = nullptr;
+    c->d_snap = nullptr;
 }
 
 template <class T>
@@ -156,17 +163,33 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
     if ((rc = wf_alloc(c, &Q.n_n, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.n_w, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.n_k, scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.counts, 8))) return rc;
+    if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
     if ((rc = wf_alloc(c, &Q.ovf, (size_t)(pt::kMaxDepth - pt::kLdsStack) * pt::kWfMaxThreads))) return rc;
     size_t P = (size_t)c->width * (size_t)c->height;
     if ((rc = wf_alloc(c, &Q.acc, P * 3))) return rc;
     PT_HIP(hipMemsetAsync(Q.acc, 0, P * 3 * sizeof(double), c->stream));
-    PT_HIP(hipMemsetAsync(Q.counts, 0, 8 * sizeof(uint32_t), c->stream));
+    PT_HIP(hipMemsetAsync(Q.counts, 0, pt::kCountWords * sizeof(uint32_t), c->stream));
     Q.cap = cap;
     Q.s_cap = scap;
+    Q.pcap = cap / pt::kParts;
+    Q.spcap = scap / pt::kParts;
     c->Q = Q;
     c->wf_cap = cap;
     c->wf_scap = scap;
+    return PT_OK;
+}
+
+// Buffers of the adaptive / firefly phases: per-sample accumulators for one
+// queue's worth of camera samples, the candidate list and the M snapshot.
+int ensure_extra(Ctx* c) {
+    if (c->Q.acc_s) return PT_OK;
+    int rc;
+    const size_t P = (size_t)c->width * (size_t)c->height;
+    if ((rc = wf_alloc(c, &c->Q.acc_s, (size_t)c->wf_cap * 3))) return rc;
+    if ((rc = wf_alloc(c, &c->d_plist, P))) return rc;
+    if ((rc = wf_alloc(c, &c->d_fcount, 1))) return rc;
+    if ((rc = wf_alloc(c, &c->d_snap, P * 3))) return rc;
+    PT_HIP(hipMemsetAsync(c->Q.acc_s, 0, (size_t)c->wf_cap * 3 * sizeof(double), c->stream));
     return PT_OK;
 }
 
@@ -547,29 +570,64 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)
     if (nm == 2) growth = std::ldexp(1.0, std::min(std::max(sampler->max_bounces - 1, 0), 60));
     const double per_sample = (double)plan.root_children * growth;   // NEE requests: at most one per child
-    uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples, std::floor((double)kWfMaxCap / per_sample));
+    // Queues are kParts partitions.  Camera samples are dealt to the XCD groups in
+    // 256-sample blocks, so a group gets at most ceil(ceil(chunk/256)/kParts)·256 of
+    // them, and everything it appends stays in its own partition.
+    const double pmax = (double)(kWfMaxCap / pt::kParts);
+    auto group_max = [](uint64_t ch) { return (double)(((ch + 255) / 256 + pt::kParts - 1) / pt::kParts * 256); };
+    uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples,
+                                                std::floor(pmax / per_sample / 256.0) * 256.0 * pt::kParts);
+    const bool extra = pass->adaptive_samples > 0 || pass->firefly_samples > 0;
+    if (pass->adaptive_samples < 0 || pass->firefly_samples < 0) return fail(PT_ERR_INVALID_ARG, "negative extra samples");
     int engine = pass->engine;
-    if (engine == PT_ENGINE_AUTO) engine = chunk >= 4096 || chunk >= cam_samples ? PT_ENGINE_WAVEFRONT : PT_ENGINE_MEGAKERNEL;
+    if (engine == PT_ENGINE_AUTO)
+        engine = extra || chunk >= 4096 || chunk >= cam_samples ? PT_ENGINE_WAVEFRONT : PT_ENGINE_MEGAKERNEL;
+    if (engine == PT_ENGINE_MEGAKERNEL && extra)
+        return fail(PT_ERR_UNSUPPORTED, "adaptive / firefly phases run on the wavefront engine");
     if (engine == PT_ENGINE_WAVEFRONT && chunk < 1)
         return fail(PT_ERR_UNSUPPORTED, "wavefront queues cannot hold one camera sample of this sampler (use the megakernel)");
     if (engine != PT_ENGINE_WAVEFRONT && engine != PT_ENGINE_MEGAKERNEL) return fail(PT_ERR_INVALID_ARG, "bad engine");
     if (engine == PT_ENGINE_WAVEFRONT) {
         plan.chunk = chunk;
-        const double rays_needed = (double)chunk * (double)plan.root_children * growth;
-        uint32_t cap = (uint32_t)std::min<double>((double)kWfMaxCap, std::max(65536.0, std::max((double)chunk, rays_needed)));
-        uint32_t scap = (uint32_t)std::min<double>((double)kWfMaxCap, std::max(65536.0, rays_needed));
+        const double group_samples = group_max(chunk);
+        const double need = group_samples * per_sample;   // a partition's widest depth
+        const uint32_t pcap = (uint32_t)std::min(pmax, std::max(8192.0, std::max(group_samples, need)));
+        const uint32_t spcap = (uint32_t)std::min(pmax, std::max(8192.0, need));
+        uint32_t cap = pcap * pt::kParts, scap = spcap * pt::kParts;
         int rc = ensure_wavefront(c, cap, scap);
         if (rc) return rc;
+        if (extra && (uint64_t)std::max(pass->adaptive_samples, pass->firefly_samples) > chunk)
+            return fail(PT_ERR_UNSUPPORTED, "adaptive / firefly samples exceed one wavefront chunk");
+        if (extra && (rc = ensure_extra(c))) return rc;
     }
     c->last_engine = engine;
     const bool timing = (pass->flags & PT_PASS_KERNEL_TIMING) != 0;
     c->timer.reset(c->stream);
     PT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
-    if (engine == PT_ENGINE_WAVEFRONT) PT_HIP(hipMemsetAsync(c->Q.counts + 4, 0, sizeof(uint32_t), c->stream));
+    if (engine == PT_ENGINE_WAVEFRONT)
+        PT_HIP(hipMemsetAsync(c->Q.counts + pt::kFlagWord, 0, sizeof(uint32_t), c->stream));
     PT_HIP(hipEventRecord(c->ev0, c->stream));
     if (engine == PT_ENGINE_WAVEFRONT) {
-        PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream,
-                                  timing ? &c->timer : nullptr));
+        pt::LaunchTimer* tm = timing ? &c->timer : nullptr;
+        PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm));
+        if (pass->adaptive_samples > 0)  // Renderer.cs:340-410
+            PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm, 0,
+                                       pass->adaptive_samples, (uint64_t)num_tiles * 1024u, nullptr, nullptr));
+        if (pass->firefly_samples > 0) {  // Renderer.cs:412-470
+            PT_HIP(pt::firefly_select(P, B, c->d_plist, c->d_fcount, c->stream));
+            uint32_t nsel = 0;
+            PT_HIP(hipMemcpyAsync(&nsel, c->d_fcount, sizeof nsel, hipMemcpyDeviceToHost, c->stream));
+            const size_t npx = (size_t)c->width * (size_t)c->height;
+            PT_HIP(hipMemcpyAsync(c->d_snap, c->d_m, npx * 3 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+            if (c->comm) {
+                // neighbours on other ranks' tiles: the disjoint M buffers sum to the full frame
+                ncclResult_t r = ncclAllReduce(c->d_snap, c->d_snap, npx * 3, ncclFloat64, ncclSum, c->comm, c->stream);
+                if (r != ncclSuccess) return fail(PT_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+            }
+            PT_HIP(hipStreamSynchronize(c->stream));
+            PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm, 1,
+                                       pass->firefly_samples, nsel, c->d_plist, c->d_snap));
+        }
     } else {
         if (timing) c->timer.begin(PT_K_MEGAKERNEL);
         PT_HIP(pt::launch_render_pass(c->S, cam, smp, P, B, num_tiles, counted != nullptr, c->stream));
@@ -581,9 +639,9 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     PT_HIP(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
     if (engine == PT_ENGINE_WAVEFRONT) {
-        uint32_t flags[8];
-        PT_HIP(hipMemcpy(flags, c->Q.counts, sizeof flags, hipMemcpyDeviceToHost));
-        if (flags[4]) return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
+        uint32_t flag = 0;
+        PT_HIP(hipMemcpy(&flag, c->Q.counts + pt::kFlagWord, sizeof flag, hipMemcpyDeviceToHost));
+        if (flag) return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
     }
     float ms = 0.f;
     PT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));

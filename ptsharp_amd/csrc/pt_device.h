@@ -378,6 +378,37 @@ __device__ __forceinline__ void cast_ray(const DevCamera& cam, int x, int y, int
 }
 
 // Pixel.AddSample (Buffer.cs:33-44)
+// buf.StandardDeviation(x, y).MaxComponent() > FireflyThreshold (= 1; Renderer.cs:48, 426,
+// Buffer.cs:48-57): black below 2 samples, else sqrt(V / (N-1)) (Pow(0.5) correctly rounded).
+__device__ __forceinline__ bool firefly_candidate(const DevBuffer& B, size_t i) {
+    const int32_t n = B.n[i];
+    if (n < 2) return false;
+    const double* V = B.v + 3 * i;
+    double r = sqrt(V[0] / (double)(n - 1)), g = sqrt(V[1] / (double)(n - 1)), b = sqrt(V[2] / (double)(n - 1));
+    return net_max(net_max(r, g), b) > 1.0;
+}
+
+// IsFirefly + CalculateLocalDeviation (Renderer.cs:473-537): brightness > 0.9 and the
+// 3x3 (image-clipped) neighbourhood mean deviates by > 0.2.  Neighbours from `snap`
+// (M at the start of the firefly phase), the pixel's own M live.
+__device__ __forceinline__ bool is_firefly(double sr, double sg, double sb, int x, int y, int w, int h,
+                                           const double* __restrict__ snap, const double* own) {
+    double brightness = sr * 0.2126 + sg * 0.7152 + sb * 0.0722;
+    if (!(brightness > 0.9)) return false;
+    const int sx = max(0, x - 1), sy = max(0, y - 1), ex = min(w - 1, x + 1), ey = min(h - 1, y + 1);
+    double tr = 0, tg = 0, tb = 0;
+    int count = 0;
+    for (int j = sy; j <= ey; j++)
+        for (int i = sx; i <= ex; i++) {
+            const double* c = (i == x && j == y) ? own : snap + 3 * ((size_t)j * (size_t)w + (size_t)i);
+            tr += c[0]; tg += c[1]; tb += c[2];
+            count++;
+        }
+    double ar = tr / count, ag = tg / count, ab = tb / count;
+    double dr = fabs(sr - ar), dg = fabs(sg - ag), db = fabs(sb - ab);
+    return sqrt(dr * dr + dg * dg + db * db) > 0.2;
+}
+
 __device__ __forceinline__ void welford(const DevBuffer& B, size_t i, double r, double g, double b) {
     int32_t n = B.n[i] + 1;
     B.n[i] = n;

@@ -87,6 +87,10 @@ PT_HD uint64_t camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t
     k = mix64(k ^ (pixel + 0xA4093822299F31D0ull));
     return mix64(k ^ ((uint64_t)sample + 0x082EFA98EC4E6C89ull));
 }
+// Sample-index domains of camera_key: the main loop uses 0..spp-1, the adaptive
+// and firefly phases (Renderer.cs:340-470) their own ranges.
+constexpr uint32_t kAdaptiveSampleBase = 0x40000000u;
+constexpr uint32_t kFireflySampleBase = 0x80000000u;
 PT_HD uint64_t child_key(uint64_t k, uint32_t c) { return mix64(k ^ ((uint64_t)c + 0x452821E638D01377ull)); }
 PT_HD uint64_t light_key(uint64_t k, uint32_t i) { return mix64(k ^ ((uint64_t)i + 0xBE5466CF34E90C6Cull)); }
 PT_HD double draw(uint64_t k, uint32_t dim) {
@@ -167,16 +171,28 @@ PT_HD double isect_plane(v3 point, v3 normal, v3 o, v3 d) {
 // e1 = V2-V1, e2 = V3-V1 (bit-identical to the per-call Sub in the reference).
 PT_HD double isect_tri(v3 v1, v3 e1, v3 e2, v3 o, v3 d) {
     v3 h = cross(d, e2);
-    double det = dot(e1, h);
-    if (det > -kEps && det < kEps) return kHitInf;
-    double invDet = 1.0 / det;
+    const float det = dotf(e1, h);
+    if ((double)det > -kEps && (double)det < kEps) return kHitInf;
+    // det, u·det, v·det and t·det are fp32 dot products, so most rejections are
+    // decided here, before the fp64 division: a sign test is exact (the fp64
+    // product of nonzero finite values never rounds to 0), and "> 1" is only
+    // taken with a 1e-4 margin, far beyond the fp64 products' 2^-52 error.  Every
+    // triangle not rejected here takes the reference's own fp64 sequence below.
     v3 s = sub(o, v1);
-    double u = dot(s, h) * invDet;
-    if (u < 0 || u > 1) return kHitInf;
+    const float a = dotf(s, h), ad = fabsf(det), lim = ad * 1.0001f;
+    const bool neg = det < 0;
+    const float as = neg ? -a : a;
+    if (as < 0 || as > lim) return kHitInf;           // u < 0 or u > 1
     v3 q = cross(s, e1);
-    double v = dot(d, q) * invDet;
+    const float b = dotf(d, q), c = dotf(e2, q);
+    const float bs = neg ? -b : b, cs = neg ? -c : c;
+    if (bs < 0 || as + bs > lim || cs < 0) return kHitInf;  // v < 0, u + v > 1, t < 0
+    double invDet = 1.0 / det;
+    double u = (double)a * invDet;
+    if (u < 0 || u > 1) return kHitInf;
+    double v = (double)b * invDet;
     if (v < 0 || (u + v) > 1) return kHitInf;
-    double t = dot(e2, q) * invDet;
+    double t = (double)c * invDet;
     if (t < kEps) return kHitInf;
     return t;
 }

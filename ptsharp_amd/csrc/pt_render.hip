@@ -9,9 +9,9 @@
 // frame stack; chain vertices (one child) are processed inline.  The estimator
 // is linear, so the recursion becomes throughput-weighted accumulation
 // ("Recursion → iteration").
-// Every Scene.Intersect is a closest-hit query over planes (linear), a BVH2 over
-// spheres/cubes and a BVH2 over all triangles, with the per-lane traversal stack
-// in LDS.  The Welford update (Pixel.AddSample, Buffer.cs:33-44) is done by the
+// Every Scene.Intersect is a closest-hit query over planes (linear), a 4-wide
+// BVH over spheres/cubes and one over all triangles, with the per-lane traversal
+// stack in LDS.  The Welford update (Pixel.AddSample, Buffer.cs:33-44) is done by the
 // owning lane: no atomics on the Buffer.
 #include <hip/hip_runtime.h>
 

@@ -8,7 +8,13 @@
 namespace pt {
 
 // Ray queues are double-buffered by depth parity; every array is float4 /
-// uint64 SoA so each lane moves 16 B per access.
+// uint64 SoA so each lane moves 16 B per access.  Every queue is split into
+// kParts partitions, one per XCD group (blocks b, b + 8, ... share an XCD and
+// its L2): group g consumes partition g and appends the children and NEE
+// requests it makes to partition g of the next queues, so each XCD's L2 keeps
+// working on one region of the image at every depth, and the reservation
+// atomics spread over kParts counter words.
+constexpr int kParts = 8;
 struct WfQueues {
     float4* q_o[2];      // {origin.xyz, pixel}
     float4* q_d[2];      // {direction.xyz, depth | emission << 8}
@@ -19,13 +25,19 @@ struct WfQueues {
     float4* n_n;         // {normal.xyz, -}
     float4* n_w;         // {throughput·weight.rgb, -}
     uint64_t* n_k;       // RNG key of the child edge (light choice, soft-shadow point)
-    uint32_t* counts;    // pair q = {counts[2q], counts[2q+1]}: ray queue q and the NEE requests made
-                         // with it (one packed 64-bit word, reserved together); [4] overflow flag
-    uint32_t cap;        // entries per ray queue
-    uint32_t s_cap;      // NEE queue entries
+    uint32_t* counts;    // word (q, g) = {counts[2(q·kParts+g)], +1}: partition g of ray queue q and the
+                         // NEE requests made with it (one packed 64-bit word, reserved together);
+                         // counts[kFlagWord] = overflow flag
+    uint32_t cap;        // entries per ray queue (kParts partitions of pcap)
+    uint32_t s_cap;      // NEE queue entries (kParts partitions of spcap)
+    uint32_t pcap, spcap;
     double* acc;         // [P][3] per-pixel sum of this pass' sample colours
     uint32_t* ovf;       // traversal stack entries beyond kLdsStack: [kMaxDepth - kLdsStack][kWfMaxThreads]
+    double* acc_s;       // [cap][3] per-sample accumulators of the adaptive / firefly phases
 };
+
+constexpr int kFlagWord = 4 * kParts;
+constexpr int kCountWords = 4 * kParts + 2;
 
 constexpr int kLdsStack = 16;                    // LDS stack entries per lane (traversal kernels)
 constexpr uint32_t kWfMaxBlocks = 256 * 8;        // grid cap of the traversal kernels
@@ -50,5 +62,15 @@ struct LaunchTimer {
 hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                           const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
                           LaunchTimer* timer);
+
+// Adaptive (firefly = 0) or firefly (firefly = 1) phase of a pass: `entries` pixels
+// (tile order, or `plist`), K samples each.  `snap`: M at the start of the firefly phase.
+hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
+                           const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
+                           LaunchTimer* timer, int firefly, int32_t K, uint64_t entries, const uint32_t* plist,
+                           const double* snap);
+
+// Firefly candidates of the pass' pixels into plist; *count = how many (device word).
+hipError_t firefly_select(const DevPass& P, const DevBuffer& B, uint32_t* plist, uint32_t* count, hipStream_t stream);
 
 }  // namespace pt

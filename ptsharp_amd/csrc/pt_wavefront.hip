@@ -54,6 +54,23 @@ __device__ __forceinline__ uint4 nt_load(const uint4* p) {
 }
 __device__ __forceinline__ uint64_t nt_load(const uint64_t* p) { return __builtin_nontemporal_load(p); }
 
+__device__ __forceinline__ uint32_t* ray_count(const WfQueues& Q, int q, int g) { return Q.counts + 2 * (q * kParts + g); }
+__device__ __forceinline__ uint32_t* nee_count(const WfQueues& Q, int q, int g) {
+    return Q.counts + 2 * (q * kParts + g) + 1;
+}
+__device__ __forceinline__ unsigned long long* pair_word(const WfQueues& Q, int q, int g) {
+    return reinterpret_cast<unsigned long long*>(Q.counts) + q * kParts + g;
+}
+
+// XCD group of this block (grids are multiples of kParts): group g = b % kParts,
+// local block index lb, nb blocks per group.
+struct Group {
+    uint32_t g, lb, nb;
+};
+__device__ __forceinline__ Group xcd_group() {
+    return Group{blockIdx.x % (uint32_t)kParts, blockIdx.x / (uint32_t)kParts, gridDim.x / (uint32_t)kParts};
+}
+
 __device__ __forceinline__ uint32_t append(uint32_t* counter) {
     return atomicAdd(counter, 1u);  // hipcc aggregates a uniform +1 into one atomic per wave
 }
@@ -122,7 +139,10 @@ __device__ __forceinline__ void acc_add(double* acc, uint32_t pixel, float r, fl
 // ---------------------------------------------------------------- camera
 __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQueues Q, uint64_t begin,
                                                    uint32_t count, int32_t spp_launch, int32_t sample_base) {
-    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < count; g += gridDim.x * blockDim.x) {
+    // Camera samples are dealt to the XCD groups in interleaved 256-slot blocks
+    // (16 pixels' samples): every group gets an even share of sky, floor and mesh.
+    const Group G = xcd_group();
+    for (uint32_t g = (G.g + kParts * G.lb) * 256u + threadIdx.x; g < count; g += kParts * G.nb * 256u) {
         const uint64_t slot = begin + g;
         const uint64_t pslot = slot / (uint64_t)spp_launch;
         const int s = (int)(slot % (uint64_t)spp_launch);
@@ -147,9 +167,9 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
             double fv = (y + draw(K, D_JY)) / h;
             cast_ray(cam, x, y, w, h, fu, fv, K, o, d);
         }
-        const uint32_t i = append(&Q.counts[0]);
-        if (i >= Q.cap) { Q.counts[4] = 1; continue; }
-        ray_store(Q, 0, i, o, d, make_float3(1.f, 1.f, 1.f), (uint32_t)pix, 0u | (1u << 8), K);
+        const uint32_t i = append(ray_count(Q, 0, G.g));
+        if (i >= Q.pcap) { Q.counts[kFlagWord] = 1; continue; }
+        ray_store(Q, 0, G.g * Q.pcap + i, o, d, make_float3(1.f, 1.f, 1.f), (uint32_t)pix, 0u | (1u << 8), K);
     }
 }
 
@@ -158,14 +178,13 @@ template <bool COUNT>
 __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        // the other pair (consumed) is free now: reset it for k_wf_shade's output
-        Q.counts[2 * (1 - qi)] = 0;
-        Q.counts[2 * (1 - qi) + 1] = 0;
-    }
-    const uint32_t n = Q.counts[2 * qi] < Q.cap ? Q.counts[2 * qi] : Q.cap;
+    if (blockIdx.x == 0 && threadIdx.x < kParts)  // the other words (consumed) are free: reset them for k_wf_shade
+        *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;
+    const Group G = xcd_group();
+    const uint32_t cnt = *ray_count(Q, qi, G.g);
+    const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
     Counters ctr{0, 0, 0, 0};
-    for (uint32_t i = blockIdx.x * kTB + threadIdx.x; i < n; i += gridDim.x * kTB) {
+    for (uint32_t i = base + G.lb * kTB + threadIdx.x; i < base + n; i += G.nb * kTB) {
         float4 b = nt_load(&Q.q_d[qi][i]);
         float4 a = nt_load(&Q.q_o[qi][i]);
         if (__float_as_uint(b.w) == kDead) continue;
@@ -199,13 +218,15 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
 template <bool COUNT>
 __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
-    const uint32_t n = Q.counts[2 * qi] < Q.cap ? Q.counts[2 * qi] : Q.cap;
+    const Group G = xcd_group();
+    const uint32_t cnt = *ray_count(Q, qi, G.g);
+    const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
     const int qo = 1 - qi;
     const bool nee_on = smp.dl && S.num_lights > 0;
     Counters ctr{0, 0, 0, 0};
-    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {  // block-uniform
-        const uint32_t i = i0 + threadIdx.x;
-        bool alive = i < n;
+    for (uint32_t k0 = G.lb * blockDim.x; k0 < n; k0 += G.nb * blockDim.x) {  // block-uniform
+        const uint32_t i = base + k0 + threadIdx.x;
+        bool alive = k0 + threadIdx.x < n;
         float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, rt = ro;
         uint4 hr = make_uint4(0, 0, 0, 0);
         uint32_t meta = kDead;
@@ -269,8 +290,8 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
             n_nee += (live && !refl && !m.transparent && nee_on) ? 1u : 0u;
         }
         uint32_t ebase, nbase;
-        block_reserve2(reinterpret_cast<unsigned long long*>(&Q.counts[2 * qo]), n_ext, n_nee, ebase, nbase);
-        if (ebase + n_ext > Q.cap || nbase + n_nee > Q.s_cap) Q.counts[4] = 1;
+        block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase);
+        if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) Q.counts[kFlagWord] = 1;
         uint32_t ej = ebase, nj = nbase;
         for (int c = 0; c < nch; c++) {
             const int mode = ma + c % nm;
@@ -286,11 +307,12 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
             } else {
                 for (int k = 0; k < 3; k++) w[k] = fp * m.color[k];
                 if (nee_on) {  // diffuse child: sampleLights from the normal ray, in k_wf_shadow
-                    if (nj < Q.s_cap) {
-                        nt_store(&Q.n_o[nj], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
-                        nt_store(&Q.n_n[nj], make_float4(sh.nrm.x, sh.nrm.y, sh.nrm.z, 0.f));
-                        nt_store(&Q.n_w[nj], make_float4(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2], 0.f));
-                        nt_store(&Q.n_k[nj], E);
+                    if (nj < Q.spcap) {
+                        const uint32_t at = G.g * Q.spcap + nj;
+                        nt_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
+                        nt_store(&Q.n_n[at], make_float4(sh.nrm.x, sh.nrm.y, sh.nrm.z, 0.f));
+                        nt_store(&Q.n_w[at], make_float4(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2], 0.f));
+                        nt_store(&Q.n_k[at], E);
                     }
                     nj++;
                 }
@@ -302,8 +324,8 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
             const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
             v3 no, nd;
             bounce_dir(m, sh, d, fu, fv, refl, n1, n2, E, no, nd);
-            if (ej < Q.cap)
-                ray_store(Q, qo, ej, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
+            if (ej < Q.pcap)
+                ray_store(Q, qo, G.g * Q.pcap + ej, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
                           (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
             ej++;
         }
@@ -322,11 +344,13 @@ __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, DevSampler smp, W
                                                    unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
-    const uint32_t n = Q.counts[2 * qo + 1] < Q.s_cap ? Q.counts[2 * qo + 1] : Q.s_cap;
+    const Group G = xcd_group();
+    const uint32_t cnt = *nee_count(Q, qo, G.g);
+    const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
     const int nl = S.num_lights;
     const bool all = smp.light_mode == 1;
     Counters ctr{0, 0, 0, 0};
-    for (uint32_t i = blockIdx.x * kTB + threadIdx.x; i < n; i += gridDim.x * kTB) {
+    for (uint32_t i = base + G.lb * kTB + threadIdx.x; i < base + n; i += G.nb * kTB) {
         const float4 a = nt_load(&Q.n_o[i]);
         const float4 b = nt_load(&Q.n_n[i]);
         const float4 wt = nt_load(&Q.n_w[i]);
@@ -373,12 +397,115 @@ __global__ __launch_bounds__(256) void k_wf_finalize(DevPass P, DevBuffer B, WfQ
     }
 }
 
+// ---------------------------------------------------------------- adaptive / firefly phases
+// Entry e of a phase is one pixel with K individually accumulated samples
+// (Renderer.cs:340-470): the adaptive phase walks the pass' pixels in tile order,
+// the firefly phase the candidate list of k_wf_firefly_select.  A camera ray's
+// accumulator index is its chunk-relative slot e·K + j, not its pixel.
+__device__ __forceinline__ bool entry_pixel(const DevPass& P, const uint32_t* plist, uint64_t e, int& x, int& y) {
+    if (plist) {
+        const uint32_t pix = plist[e];
+        x = (int)(pix % (uint32_t)P.width);
+        y = (int)(pix / (uint32_t)P.width);
+        return true;
+    }
+    const int tile = P.tiles ? P.tiles[e >> 10] : (int)(e >> 10);
+    tile_pixel(tile, (int)(e & 1023), P.tiles_x, x, y);
+    return x < P.width && y < P.height;
+}
+
+__global__ __launch_bounds__(256) void k_wf_camera_extra(DevCamera cam, DevPass P, WfQueues Q, uint64_t begin,
+                                                         uint32_t count, int32_t K, uint32_t sample_base,
+                                                         const uint32_t* plist) {
+    // Camera samples are dealt to the XCD groups in interleaved 256-slot blocks
+    // (16 pixels' samples): every group gets an even share of sky, floor and mesh.
+    const Group G = xcd_group();
+    for (uint32_t g = (G.g + kParts * G.lb) * 256u + threadIdx.x; g < count; g += kParts * G.nb * 256u) {
+        const uint64_t slot = begin + g;
+        const uint64_t e = slot / (uint64_t)K;
+        const uint32_t j = (uint32_t)(slot % (uint64_t)K);
+        int x, y;
+        if (!entry_pixel(P, plist, e, x, y)) continue;
+        const uint64_t pix = (uint64_t)y * (uint64_t)P.width + (uint64_t)x;
+        const uint64_t Kc = camera_key(P.seed, P.pass_index, pix, sample_base + j);
+        v3 o, d;
+        // CastRay(x, y, w, h, NextDouble(), NextDouble()): no jitter bug in these loops
+        cast_ray(cam, x, y, P.width, P.height, draw(Kc, D_JX), draw(Kc, D_JY), Kc, o, d);
+        const uint32_t i = append(ray_count(Q, 0, G.g));
+        if (i >= Q.pcap) { Q.counts[kFlagWord] = 1; continue; }
+        ray_store(Q, 0, G.g * Q.pcap + i, o, d, make_float3(1.f, 1.f, 1.f), g, 0u | (1u << 8), Kc);
+    }
+}
+
+// One thread per entry: the K samples in order — AddSample each (adaptive), or stop
+// at the first IsFirefly sample (firefly).  Clears the entry's accumulators.
+__global__ __launch_bounds__(256) void k_wf_finalize_extra(DevPass P, DevBuffer B, double* __restrict__ acc,
+                                                           uint64_t begin_entry, uint32_t entries, int32_t K,
+                                                           const uint32_t* plist, int firefly,
+                                                           const double* __restrict__ snap) {
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < entries; e += gridDim.x * blockDim.x) {
+        int x, y;
+        const bool in = entry_pixel(P, plist, begin_entry + e, x, y);
+        const size_t pix = (size_t)y * (size_t)P.width + (size_t)x;
+        double* a = acc + 3 * (size_t)e * (size_t)K;
+        bool stop = !in;
+        for (int j = 0; j < K; j++, a += 3) {
+            const double r = a[0], g = a[1], b = a[2];
+            a[0] = 0.0; a[1] = 0.0; a[2] = 0.0;
+            if (stop) continue;
+            if (firefly && is_firefly(r, g, b, x, y, P.width, P.height, snap, B.m + 3 * pix)) { stop = true; continue; }
+            welford(B, pix, r, g, b);
+        }
+    }
+}
+
+// Pixels of the pass whose standard deviation exceeds FireflyThreshold (Renderer.cs:426).
+__global__ __launch_bounds__(256) void k_wf_firefly_select(DevPass P, DevBuffer B, uint32_t* plist, uint32_t* count) {
+    const uint32_t total = (uint32_t)P.num_tiles * 1024u;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < total; s += gridDim.x * blockDim.x) {
+        int x, y;
+        if (!entry_pixel(P, nullptr, s, x, y)) continue;
+        const uint32_t pix = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+        if (firefly_candidate(B, pix)) plist[atomicAdd(count, 1u)] = pix;
+    }
+}
+
 // ---------------------------------------------------------------- host driver
+// Grid for `items` work items; a multiple of kParts (XCD groups), at most cap_blocks.
 static unsigned grid_for(uint64_t items, unsigned block, unsigned cap_blocks) {
     uint64_t g = (items + block - 1) / block;
-    if (g < 1) g = 1;
-    if (g > cap_blocks) g = cap_blocks;
+    g = (g + kParts - 1) / kParts * kParts;
+    if (g < (uint64_t)kParts) g = kParts;
+    if (g > cap_blocks) g = cap_blocks / kParts * kParts;
     return (unsigned)g;
+}
+
+// Trace / shade / shadow for every depth of one chunk whose camera rays are queued.
+static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer& B, const WfQueues& Q,
+                       const WfPlan& plan, bool count, hipStream_t stream, LaunchTimer* timer, uint64_t bound) {
+    auto begin_k = [&](int cls) { if (timer) timer->begin(cls); };
+    auto end_k = [&](int cls) { if (timer) timer->end(cls); };
+    int qi = 0;
+    for (int depth = 0; depth <= smp.mb; depth++) {
+        const unsigned tg = grid_for(bound, kTB, plan.trace_blocks);
+        begin_k(1);
+        if (count) hipLaunchKernelGGL(k_wf_trace<true>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else hipLaunchKernelGGL(k_wf_trace<false>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        end_k(1);
+        const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
+        begin_k(2);
+        if (count) hipLaunchKernelGGL(k_wf_shade<true>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        else hipLaunchKernelGGL(k_wf_shade<false>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        end_k(2);
+        const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
+        const unsigned hg = grid_for(children, kTB, plan.trace_blocks);
+        begin_k(3);
+        if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
+        else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
+        end_k(3);
+        bound = children < Q.cap ? children : Q.cap;
+        qi = 1 - qi;
+    }
 }
 
 hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
@@ -394,39 +521,57 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     for (int r = 0; r < rounds; r++) {
         for (uint64_t begin = 0; begin < total; begin += plan.chunk) {
             const uint32_t cnt = (uint32_t)((total - begin) < plan.chunk ? (total - begin) : plan.chunk);
-            hipError_t e = hipMemsetAsync(Q.counts, 0, 4 * sizeof(uint32_t), stream);
+            hipError_t e = hipMemsetAsync(Q.counts, 0, 4 * kParts * sizeof(uint32_t), stream);
             if (e != hipSuccess) return e;
             begin_k(0);
             hipLaunchKernelGGL(k_wf_camera, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Q, begin,
                                cnt, spp_launch, r);
             end_k(0);
-            int qi = 0;
-            uint64_t bound = cnt;
-            for (int depth = 0; depth <= smp.mb; depth++) {
-                const unsigned tg = grid_for(bound, kTB, plan.trace_blocks);
-                begin_k(1);
-                if (count) hipLaunchKernelGGL(k_wf_trace<true>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-                else hipLaunchKernelGGL(k_wf_trace<false>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-                end_k(1);
-                const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
-                begin_k(2);
-                if (count) hipLaunchKernelGGL(k_wf_shade<true>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
-                else hipLaunchKernelGGL(k_wf_shade<false>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
-                end_k(2);
-                const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
-                const unsigned hg = grid_for(children, kTB, plan.trace_blocks);
-                begin_k(3);
-                if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
-                else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
-                end_k(3);
-                bound = children < Q.cap ? children : Q.cap;
-                qi = 1 - qi;
-            }
+            depth_loop(S, smp, B, Q, plan, count, stream, timer, cnt);
         }
         begin_k(4);
         hipLaunchKernelGGL(k_wf_finalize, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, Q, inv_spp);
         end_k(4);
     }
+    return hipGetLastError();
+}
+
+hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
+                           const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
+                           LaunchTimer* timer, int firefly, int32_t K, uint64_t entries, const uint32_t* plist,
+                           const double* snap) {
+    if (K <= 0 || entries == 0) return hipSuccess;
+    auto begin_k = [&](int cls) { if (timer) timer->begin(cls); };
+    auto end_k = [&](int cls) { if (timer) timer->end(cls); };
+    WfQueues Qx = Q;
+    Qx.acc = Q.acc_s;  // per-sample accumulators
+    uint64_t per_chunk = plan.chunk / (uint64_t)K;  // entries per chunk (whole pixels)
+    if (per_chunk < 1) per_chunk = 1;
+    const uint32_t base = firefly ? kFireflySampleBase : kAdaptiveSampleBase;
+    for (uint64_t e0 = 0; e0 < entries; e0 += per_chunk) {
+        const uint64_t ne = (entries - e0) < per_chunk ? (entries - e0) : per_chunk;
+        const uint32_t cnt = (uint32_t)(ne * (uint64_t)K);
+        hipError_t e = hipMemsetAsync(Q.counts, 0, 4 * kParts * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        begin_k(0);
+        hipLaunchKernelGGL(k_wf_camera_extra, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Qx,
+                           e0 * (uint64_t)K, cnt, K, base, plist);
+        end_k(0);
+        depth_loop(S, smp, B, Qx, plan, count, stream, timer, cnt);
+        begin_k(4);
+        hipLaunchKernelGGL(k_wf_finalize_extra, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, stream, P, B, Q.acc_s,
+                           e0, (uint32_t)ne, K, plist, firefly, snap);
+        end_k(4);
+    }
+    return hipGetLastError();
+}
+
+hipError_t firefly_select(const DevPass& P, const DevBuffer& B, uint32_t* plist, uint32_t* count, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const uint64_t pix_slots = (uint64_t)P.num_tiles * 1024u;
+    hipLaunchKernelGGL(k_wf_firefly_select, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, plist,
+                       count);
     return hipGetLastError();
 }
 

@@ -171,7 +171,8 @@ class Renderer:
                                  int(self._pass if pass_index is None else pass_index),
                                  0 if tiles is None else len(tiles),
                                  C.POINTER(C.c_int32)() if tiles is None else tiles.ctypes.data_as(C.POINTER(C.c_int32)),
-                                 int(self.Engine), int(self.Flags))
+                                 int(self.Engine), int(self.Flags), int(self.AdaptiveSamples),
+                                 int(self.FireflySamples))
         return pp
 
     def RenderParallel(self) -> None:
@@ -222,10 +223,8 @@ class Renderer:
         return s
 
     def IterativeRender(self, pathTemplate: str | None, iterations: int) -> np.ndarray:
-        """Renderer.IterativeRender (Renderer.cs:702-765)."""
-        if self.AdaptiveSamples or self.FireflySamples:
-            raise _abi.PTError(_abi.PT_ERR_UNSUPPORTED, "IterativeRender",
-                               "adaptive/firefly passes are not on the GPU path yet (SURVEY.md §8f rank 1)")
+        """Renderer.IterativeRender (Renderer.cs:702-765).  Each iteration is one
+        RenderParallel pass, including its adaptive / firefly phases."""
         self.iterations = iterations
         img = None
         for i in range(1, iterations + 1):

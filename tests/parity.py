@@ -33,9 +33,12 @@ def compare(gpu_m: np.ndarray, ref_m: np.ndarray):
     return float(ok.mean()), float(err.max()), psnr8(gpu_m, ref_m)
 
 
-def render_gpu(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None, device=0, engine=0):
+def render_gpu(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None, device=0, engine=0,
+               adaptive=0, firefly=0):
     r = Renderer.NewRenderer(scene, camera, sampler, w, h, True, device=device)
     r.SamplesPerPixel = spp
+    r.AdaptiveSamples = adaptive
+    r.FireflySamples = firefly
     r.StratifiedSampling = stratified
     r.Seed = seed
     r.Tiles = tiles
@@ -51,8 +54,10 @@ def render_gpu(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=F
     return out, rays
 
 
-def render_both(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None, engine=0):
-    g, grays = render_gpu(scene, camera, sampler, w, h, spp, passes, seed, stratified, tiles, engine=engine)
+def render_both(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None, engine=0,
+                adaptive=0, firefly=0):
+    g, grays = render_gpu(scene, camera, sampler, w, h, spp, passes, seed, stratified, tiles, engine=engine,
+                          adaptive=adaptive, firefly=firefly)
     o, orays = O.render(O.OracleScene(scene), camera, sampler, w, h, spp, passes=passes, seed=seed,
-                        stratified=stratified, tiles=tiles)
+                        stratified=stratified, tiles=tiles, adaptive=adaptive, firefly=firefly)
     return g, grays, o, orays

@@ -121,3 +121,34 @@ def test_wavefront_many_chunks(gpu):
     b, rb = render_gpu(s, c, smp, 640, 360, spp=8, seed=31, engine=_abi.ENGINE_WAVEFRONT)
     assert ra == rb
     assert np.allclose(a.M, b.M, rtol=2e-5, atol=1e-6)
+
+
+# ---- adaptive / firefly phases of RenderParallel (Renderer.cs:340-537), wavefront engine
+def test_adaptive_phase(gpu):
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 4
+    g, gr, o, orr = render_both(s, c, smp, 64, 48, spp=2, passes=2, seed=21, engine=_abi.ENGINE_WAVEFRONT,
+                                adaptive=3)
+    assert (g.N == 2 * (1 + 3)).all()   # one averaged sample + 3 individual samples per pass
+    check(g, gr, o, orr)
+
+
+def test_firefly_phase(gpu):
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 4
+    g, gr, o, orr = render_both(s, c, smp, 64, 48, spp=1, passes=3, seed=23, engine=_abi.ENGINE_WAVEFRONT,
+                                firefly=4)
+    assert (g.N >= 3).all() and (g.N > 3).any(), "no firefly candidates: the test scene exercises nothing"
+    # Candidate choice and the IsFirefly stop are threshold tests on colours; a last-bit
+    # colour difference may flip one, so N must match on all but a handful of pixels.
+    same_n = float((g.N == o.N).mean())
+    assert same_n >= 0.998, f"N differs on {(1 - same_n) * g.N.size:.0f} pixels"
+    frac, maxerr, psnr = compare(g.M, o.M)
+    assert frac >= 0.995 and psnr >= 40.0, (frac, maxerr, psnr)
+    assert abs(gr - orr) <= 5e-3 * orr, (gr, orr)
+
+
+def test_extra_phases_unsupported_on_megakernel(gpu):
+    s, c, smp = scenes.gopher3()
+    with pytest.raises(_abi.PTError):
+        render_gpu(s, c, smp, 32, 32, spp=1, engine=_abi.ENGINE_MEGAKERNEL, adaptive=1)

@@ -259,3 +259,40 @@ def test_light_identity_struct_triangle_never_lights():
     s2.Add(Sphere.NewSphere(Vector(0, 2, 0), 0.5, Material.LightMaterial(Colour.White, 10)))
     buf2, _ = O.render(O.OracleScene(s2), c, smp, 32, 24, spp=1, seed=1)
     assert (buf2.M > 0).any(axis=2).mean() > 0.5  # a sphere light does light the floor
+
+
+# ---- adaptive / firefly phases (Renderer.cs:340-537)
+def test_adaptive_phase_furnace_exact():
+    """Every furnace sample is exactly 0.5 (floor) or 1 (sky), and N grows by
+    1 + AdaptiveSamples per pass.  The adaptive loop jitters over the whole pixel
+    (no (x+ξ)/w bug, Renderer.cs:357-361), so only horizon pixels mix both values:
+    every other pixel keeps an exact M and zero variance."""
+    s, c, smp = scenes.furnace(0.5)
+    buf, _ = O.render(O.OracleScene(s), c, smp, 32, 24, spp=2, passes=2, seed=4, adaptive=3)
+    assert (buf.N == 2 * 4).all()
+    assert ((buf.M >= 0.5) & (buf.M <= 1.0)).all()
+    pure = ((buf.M == 0.5) | (buf.M == 1.0)).all(axis=2)
+    assert pure.mean() > 0.9
+    assert (buf.V[pure] == 0).all()
+    assert (buf.V[~pure] > 0).any(axis=1).all()
+
+
+def test_firefly_candidates_and_stop():
+    """gopher3 (an 80-emittance light): high-variance pixels get extra samples, the
+    others none; every pixel's extra count stays within FireflySamples."""
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 4
+    osc = O.OracleScene(s)
+    ref, _ = O.render(osc, c, smp, 48, 32, spp=1, passes=2, seed=9)
+    ff, _ = O.render(osc, c, smp, 48, 32, spp=1, passes=2, seed=9, firefly=5)
+    extra = ff.N - ref.N
+    assert (extra >= 0).all() and (extra <= 2 * 5).all()
+    assert (extra > 0).any()
+    # a pixel whose first pass left variance <= 1 in every channel gets nothing in pass 1
+    assert (extra[ref.N == 0] == 0).all()
+
+
+def test_extra_phases_rng_domains_disjoint():
+    """Adaptive and firefly samples use their own camera_key sample domains."""
+    k = {O.lib().or_camera_key(7, 1, 100, s) for s in (0, 1, 0x40000000, 0x40000001, 0x80000000, 0x80000001)}
+    assert len(k) == 6
