@@ -119,10 +119,11 @@ struct Ctx {
     uint32_t* d_fcount = nullptr;
     double* d_snap = nullptr;      // [P][3] M at the start of the firefly phase
     int last_engine = 0;
+    pt::WfPlan grids{};            // persistent grid sizes (pt::wavefront_grids), once per context
     EventTimer timer;
 };
 
-constexpr uint32_t kWfMaxCap = 1u << 23;   // 8M rays per queue: ~1.5 GB of queues at most
+constexpr uint32_t kWfMaxCap = 1u << 25;   // 32M rays per queue: ~6 GB of queues at most (of 288 GB HBM)
 
 void free_wavefront(Ctx* c) {
     for (auto& a : c->wf_arrays) a.release();
@@ -564,8 +565,10 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     plan.root_children = (uint32_t)std::max(1, n_root * n_root * nm_root);
     plan.children = (uint32_t)nm;
     plan.lights_per_child = (uint32_t)(sampler->light_mode == PT_LIGHT_ALL ? std::max(1, c->S.num_lights) : 1);
-    plan.trace_blocks = pt::kWfMaxBlocks;   // the stack overflow columns are sized for this grid
-    plan.shade_blocks = 256 * 8;
+    if (!c->grids.trace_blocks) PT_HIP(pt::wavefront_grids(c->grids));
+    plan.trace_blocks = c->grids.trace_blocks;
+    plan.shade_blocks = c->grids.shade_blocks;
+    plan.shadow_blocks = c->grids.shadow_blocks;
     const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp);
     double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)
     if (nm == 2) growth = std::ldexp(1.0, std::min(std::max(sampler->max_bounces - 1, 0), 60));

@@ -27,7 +27,8 @@ struct WfQueues {
     uint64_t* n_k;       // RNG key of the child edge (light choice, soft-shadow point)
     uint32_t* counts;    // word (q, g) = {counts[2(q·kParts+g)], +1}: partition g of ray queue q and the
                          // NEE requests made with it (one packed 64-bit word, reserved together);
-                         // counts[kFlagWord] = overflow flag
+                         // counts[kFetchWord + k·kParts + g] = work-fetch cursor of kernel k
+                         // (0 trace, 1 shade, 2 shadow) in partition g; counts[kFlagWord] = overflow
     uint32_t cap;        // entries per ray queue (kParts partitions of pcap)
     uint32_t s_cap;      // NEE queue entries (kParts partitions of spcap)
     uint32_t pcap, spcap;
@@ -36,8 +37,10 @@ struct WfQueues {
     double* acc_s;       // [cap][3] per-sample accumulators of the adaptive / firefly phases
 };
 
-constexpr int kFlagWord = 4 * kParts;
-constexpr int kCountWords = 4 * kParts + 2;
+constexpr int kFetchWord = 4 * kParts;
+constexpr int kFlagWord = 7 * kParts;
+constexpr int kCountWords = 7 * kParts + 2;
+constexpr int kChunkResetWords = 7 * kParts;   // pair words + fetch cursors, zeroed per chunk
 
 constexpr int kLdsStack = 16;                    // LDS stack entries per lane (traversal kernels)
 constexpr uint32_t kWfMaxBlocks = 256 * 8;        // grid cap of the traversal kernels
@@ -48,8 +51,9 @@ struct WfPlan {
     uint32_t root_children;    // ⌊√FH⌋² · modes at depth 0
     uint32_t children;         // modes at depth >= 1 (1, or 2 under SpecularModeAll)
     uint32_t lights_per_child; // shadow rays per NEE request: 1, or #lights under LightModeAll
-    uint32_t trace_blocks;     // grid caps (grid-stride loops)
+    uint32_t trace_blocks;     // persistent grids: resident capacity of each kernel
     uint32_t shade_blocks;
+    uint32_t shadow_blocks;
 };
 
 // Optional per-launch timing hook (hipEvent pairs recorded around each kernel; pt_api.hip).
@@ -69,6 +73,9 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
                            const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
                            LaunchTimer* timer, int firefly, int32_t K, uint64_t entries, const uint32_t* plist,
                            const double* snap);
+
+// Persistent grid sizes (resident capacity on this device) of the traversal / shade kernels.
+hipError_t wavefront_grids(WfPlan& plan);
 
 // Firefly candidates of the pass' pixels into plist; *count = how many (device word).
 hipError_t firefly_select(const DevPass& P, const DevBuffer& B, uint32_t* plist, uint32_t* count, hipStream_t stream);

@@ -178,21 +178,32 @@ template <bool COUNT>
 __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
-    if (blockIdx.x == 0 && threadIdx.x < kParts)  // the other words (consumed) are free: reset them for k_wf_shade
-        *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;
+    if (blockIdx.x == 0 && threadIdx.x < kParts) {
+        *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
+        Q.counts[kFetchWord + kParts + threadIdx.x] = 0u;        // k_wf_shade's fetch cursors
+    }
     const Group G = xcd_group();
     const uint32_t cnt = *ray_count(Q, qi, G.g);
     const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
+    uint32_t* cursor = Q.counts + kFetchWord + G.g;
+    const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
-    for (uint32_t i = base + G.lb * kTB + threadIdx.x; i < base + n; i += G.nb * kTB) {
+    // Persistent grid (resident capacity); each wave takes 64 rays of its partition
+    // at a time, so no wave waits for a second dispatch round and the tail is one
+    // traversal long.
+    for (;;) {
+        uint32_t k0 = 0;
+        if (lane == 0) k0 = atomicAdd(cursor, 64u);
+        k0 = __shfl(k0, 0, 64);
+        if (k0 >= n) break;
+        if (k0 + lane >= n) continue;
+        const uint32_t i = base + k0 + lane;
         float4 b = nt_load(&Q.q_d[qi][i]);
         float4 a = nt_load(&Q.q_o[qi][i]);
-        if (__float_as_uint(b.w) == kDead) continue;
         HitRec h = trace<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
         unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
         nt_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
     }
-    const uint32_t lane = threadIdx.x & 63;
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
     if (COUNT) {
@@ -218,13 +229,19 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
 template <bool COUNT>
 __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
+    if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + 2 * kParts + threadIdx.x] = 0u;  // k_wf_shadow's
     const Group G = xcd_group();
     const uint32_t cnt = *ray_count(Q, qi, G.g);
     const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
     const int qo = 1 - qi;
     const bool nee_on = smp.dl && S.num_lights > 0;
     Counters ctr{0, 0, 0, 0};
-    for (uint32_t k0 = G.lb * blockDim.x; k0 < n; k0 += G.nb * blockDim.x) {  // block-uniform
+    __shared__ uint32_t s_k0;
+    for (;;) {  // block-uniform: the block takes 256 vertices of its partition at a time
+        if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + kFetchWord + kParts + G.g, 256u);
+        __syncthreads();
+        const uint32_t k0 = s_k0;  // thread 0 rewrites it only after block_reserve2's barriers below
+        if (k0 >= n) break;
         const uint32_t i = base + k0 + threadIdx.x;
         bool alive = k0 + threadIdx.x < n;
         float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, rt = ro;
@@ -344,13 +361,22 @@ __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, DevSampler smp, W
                                                    unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
+    if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + threadIdx.x] = 0u;  // next k_wf_trace's
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
     const int nl = S.num_lights;
     const bool all = smp.light_mode == 1;
+    uint32_t* cursor = Q.counts + kFetchWord + 2 * kParts + G.g;
+    const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
-    for (uint32_t i = base + G.lb * kTB + threadIdx.x; i < base + n; i += G.nb * kTB) {
+    for (;;) {  // 64 requests per wave at a time (see k_wf_trace)
+        uint32_t k0 = 0;
+        if (lane == 0) k0 = atomicAdd(cursor, 64u);
+        k0 = __shfl(k0, 0, 64);
+        if (k0 >= n) break;
+        if (k0 + lane >= n) continue;
+        const uint32_t i = base + k0 + lane;
         const float4 a = nt_load(&Q.n_o[i]);
         const float4 b = nt_load(&Q.n_n[i]);
         const float4 wt = nt_load(&Q.n_w[i]);
@@ -369,7 +395,6 @@ __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, DevSampler smp, W
                         wt.z * (lc.z * scale));
         }
     }
-    const uint32_t lane = threadIdx.x & 63;
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
     if (COUNT) {
@@ -498,7 +523,7 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         else hipLaunchKernelGGL(k_wf_shade<false>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         end_k(2);
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
-        const unsigned hg = grid_for(children, kTB, plan.trace_blocks);
+        const unsigned hg = grid_for(children, kTB, plan.shadow_blocks);
         begin_k(3);
         if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
@@ -521,7 +546,7 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     for (int r = 0; r < rounds; r++) {
         for (uint64_t begin = 0; begin < total; begin += plan.chunk) {
             const uint32_t cnt = (uint32_t)((total - begin) < plan.chunk ? (total - begin) : plan.chunk);
-            hipError_t e = hipMemsetAsync(Q.counts, 0, 4 * kParts * sizeof(uint32_t), stream);
+            hipError_t e = hipMemsetAsync(Q.counts, 0, kChunkResetWords * sizeof(uint32_t), stream);
             if (e != hipSuccess) return e;
             begin_k(0);
             hipLaunchKernelGGL(k_wf_camera, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Q, begin,
@@ -551,7 +576,7 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
     for (uint64_t e0 = 0; e0 < entries; e0 += per_chunk) {
         const uint64_t ne = (entries - e0) < per_chunk ? (entries - e0) : per_chunk;
         const uint32_t cnt = (uint32_t)(ne * (uint64_t)K);
-        hipError_t e = hipMemsetAsync(Q.counts, 0, 4 * kParts * sizeof(uint32_t), stream);
+        hipError_t e = hipMemsetAsync(Q.counts, 0, kChunkResetWords * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
         begin_k(0);
         hipLaunchKernelGGL(k_wf_camera_extra, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Qx,
@@ -564,6 +589,24 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
         end_k(4);
     }
     return hipGetLastError();
+}
+
+hipError_t wavefront_grids(WfPlan& plan) {
+    int dev = 0, cus = 0, nb = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    auto resident = [&](int per_cu, uint32_t cap) {
+        uint64_t g = (uint64_t)per_cu * (uint64_t)cus / kParts * kParts;
+        if (g < (uint64_t)kParts) g = kParts;
+        return (uint32_t)(g < cap ? g : cap / kParts * kParts);
+    };
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace<false>, kTB, 0);
+    if (e == hipSuccess) plan.trace_blocks = resident(nb, kWfMaxBlocks);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shade<false>, 256, 0);
+    if (e == hipSuccess) plan.shade_blocks = resident(nb, 1u << 20);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false>, kTB, 0);
+    if (e == hipSuccess) plan.shadow_blocks = resident(nb, kWfMaxBlocks);
+    return e;
 }
 
 hipError_t firefly_select(const DevPass& P, const DevBuffer& B, uint32_t* plist, uint32_t* count, hipStream_t stream) {
