@@ -67,17 +67,28 @@ namespace PTSharpCore
             public uint pass_index;
             public int num_tiles;
             public IntPtr tiles;
-            public int engine, _pad;
+            public int engine, flags;
+            public int adaptive_samples, firefly_samples;   // Renderer.AdaptiveSamples / FireflySamples
         }
 
         [StructLayout(LayoutKind.Sequential)]
         public struct pt_device_opts { public int device, width, height; }
 
         [StructLayout(LayoutKind.Sequential)]
-        public struct pt_stats
+        public unsafe struct pt_stats
         {
             public ulong rays, rays_total; public double last_pass_ms, total_ms;
             public ulong bvh_nodes, bvh_bytes; public double build_ms; public ulong passes;
+            public ulong shadow_rays;
+            public fixed double kernel_ms[6];
+            public fixed uint kernel_launches[6];
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_mesh_data
+        {
+            public int num_triangles;
+            public IntPtr v1, v2, v3, n1, n2, n3, t1, t2, t3;   // [n][3] float, owned by the library
         }
 
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_get_version();
@@ -89,6 +100,10 @@ namespace PTSharpCore
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_stats_get(IntPtr ctx, out pt_stats stats);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern IntPtr pt_last_error();
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern void pt_destroy(IntPtr ctx);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl, CharSet = CharSet.Ansi)] public static extern int pt_obj_load(string path, out pt_mesh_data mesh);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern void pt_mesh_free(ref pt_mesh_data mesh);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern IntPtr pt_obj_last_error();
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_mesh_smooth_normals(int n, float[] v1, float[] v2, float[] v3, float[] n1, float[] n2, float[] n3);
 
         public static void Check(int rc, string where)
         {
@@ -103,6 +118,8 @@ namespace PTSharpCore
         Scene Scene; Camera Camera; DefaultSampler Sampler;
         public int SamplesPerPixel = 2;           // Renderer.cs:42
         public bool StratifiedSampling = false;   // Renderer.cs:44
+        public int AdaptiveSamples = 0;           // Renderer.cs:23, phase at :340-410
+        public int FireflySamples = 0;            // Renderer.cs:26, phase at :412-470
         public ulong Seed = 0;                     // Random.Shared is unseedable; this keys the GPU stream
         IntPtr ctx;
         int W, H, pass;
@@ -207,7 +224,8 @@ namespace PTSharpCore
                 direct_lighting = directLighting ? 1 : 0, soft_shadows = softShadows ? 1 : 0,
                 light_mode = (int)Sampler.LightMode, specular_mode = (int)Sampler.SpecularMode };
             var pass = new PtHip.pt_pass_params { spp = SamplesPerPixel, stratified = StratifiedSampling ? 1 : 0,
-                seed = Seed, pass_index = (uint)(++this.pass) };
+                seed = Seed, pass_index = (uint)(++this.pass), adaptive_samples = AdaptiveSamples,
+                firefly_samples = FireflySamples };
             PtHip.Check(PtHip.pt_render_pass(ctx, ref cam, ref smp, ref pass), "pt_render_pass");
         }
 
@@ -243,5 +261,35 @@ namespace PTSharpCore
         }
 
         public void Dispose() { if (ctx != IntPtr.Zero) { PtHip.pt_destroy(ctx); ctx = IntPtr.Zero; } }
+    }
+
+    /// <summary>OBJ.Load (OBJ.cs:11-165) parsed natively, same quirks; the Triangle[] is then
+    /// built as Mesh.NewMesh does.  Replaces `OBJ.Load(path, material)` in Example.*.</summary>
+    static class HipObj
+    {
+        static Vector V(float[] a, int i) => new Vector(a[3 * i], a[3 * i + 1], a[3 * i + 2]);
+
+        internal static Mesh Load(string path, Material parent)
+        {
+            var rc = PtHip.pt_obj_load(path, out var md);
+            if (rc != PtHip.PT_OK)
+                throw new InvalidOperationException($"pt_obj_load failed ({rc}): {Marshal.PtrToStringAnsi(PtHip.pt_obj_last_error())}");
+            try
+            {
+                int n = md.num_triangles;
+                float[] Copy(IntPtr p) { var a = new float[3 * n]; if (n > 0) Marshal.Copy(p, a, 0, 3 * n); return a; }
+                float[] v1 = Copy(md.v1), v2 = Copy(md.v2), v3 = Copy(md.v3), n1 = Copy(md.n1), n2 = Copy(md.n2),
+                        n3 = Copy(md.n3), t1 = Copy(md.t1), t2 = Copy(md.t2), t3 = Copy(md.t3);
+                var tris = new Triangle[n];
+                for (int i = 0; i < n; i++)
+                {
+                    var t = new Triangle { V1 = V(v1, i), V2 = V(v2, i), V3 = V(v3, i), N1 = V(n1, i), N2 = V(n2, i),
+                                           N3 = V(n3, i), T1 = V(t1, i), T2 = V(t2, i), T3 = V(t3, i), Material = parent };
+                    tris[i] = t;   // FixNormals already applied by the loader
+                }
+                return Mesh.NewMesh(tris);
+            }
+            finally { PtHip.pt_mesh_free(ref md); }
+        }
     }
 }

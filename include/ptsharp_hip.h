@@ -205,6 +205,23 @@ int pt_stats_get(void* ctx, pt_stats* out_stats);
 const char* pt_last_error(void);
 void pt_destroy(void* ctx);
 
+/* ---- Mesh ingest (host only; no device needed).  OBJ.Load (OBJ.cs:11-165) with its
+ * quirks: lower-cased lines split on ' ', the dummy normal 0, "v//n"
+ * read as a texture index, fan triangulation, Triangle.FixNormals.  Arrays are [n][3]
+ * float, allocated by the library; release them with pt_mesh_free. */
+typedef struct pt_mesh_data {
+    int32_t num_triangles;
+    float *v1, *v2, *v3;   /* Triangle.V1..V3 */
+    float *n1, *n2, *n3;   /* Triangle.N1..N3 (after FixNormals) */
+    float *t1, *t2, *t3;   /* Triangle.T1..T3 (u, v, 0) */
+} pt_mesh_data;
+int pt_obj_load(const char* path, pt_mesh_data* out);
+void pt_mesh_free(pt_mesh_data* mesh);
+const char* pt_obj_last_error(void);
+/* Mesh.SmoothNormals (Mesh.cs:191-229), in place on n1..n3. */
+int pt_mesh_smooth_normals(int32_t n, const float* v1, const float* v2, const float* v3, float* n1, float* n2,
+                           float* n3);
+
 /* Multi-GPU: one context per GPU (one process per GPU, or one thread per GPU).
  * Rank 0 creates the id, every rank joins, pt_comm_gather sums the disjoint
  * per-rank tile buffers into rank `root` (grouped RCCL send/recv over xGMI). */

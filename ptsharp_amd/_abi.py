@@ -86,6 +86,14 @@ class pt_trace_counters(C.Structure):
 
 
 # name -> (restype, argtypes); every symbol declared in include/ptsharp_hip.h
+_f = C.POINTER(C.c_float)
+
+
+class pt_mesh_data(C.Structure):
+    _fields_ = [("num_triangles", C.c_int32)] + [(n, _f) for n in ("v1", "v2", "v3", "n1", "n2", "n3",
+                                                                    "t1", "t2", "t3")]
+
+
 SIGNATURES = {
     "pt_get_version": (C.c_int, []),
     "pt_device_count": (C.c_int, [_i]),
@@ -104,6 +112,10 @@ SIGNATURES = {
     "pt_comm_destroy": (C.c_int, [C.c_void_p]),
     "pt_render_pass_counted": (C.c_int, [C.c_void_p, C.POINTER(pt_camera), C.POINTER(pt_sampler),
                                          C.POINTER(pt_pass_params), C.POINTER(pt_trace_counters)]),
+    "pt_obj_load": (C.c_int, [C.c_char_p, C.POINTER(pt_mesh_data)]),
+    "pt_mesh_free": (None, [C.POINTER(pt_mesh_data)]),
+    "pt_obj_last_error": (C.c_char_p, []),
+    "pt_mesh_smooth_normals": (C.c_int, [C.c_int32, _f, _f, _f, _f, _f, _f]),
 }
 
 

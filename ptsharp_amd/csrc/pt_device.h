@@ -55,8 +55,13 @@ __device__ __forceinline__ double prim_t(const float4* __restrict__ recs, uint32
 // and the rarely used deeper ones in a per-thread global column (entries
 // `ostride` words apart, coalesced across lanes), so a traversal kernel's LDS
 // footprint no longer caps its occupancy.
+// push_hits() pushes the hit children after the nearest, far-to-near.  While
+// the three slots above sp are in LDS (nearly always) it stores all three
+// unconditionally and advances sp by predicate: no per-push branch.
 template <int STRIDE>
 struct LdsStack {
+    static constexpr int kLds = kMaxDepth;
+    static constexpr int kStride = STRIDE;
     uint32_t* lds;
     __device__ __forceinline__ void put(int i, uint32_t v) const { lds[i * STRIDE] = v; }
     __device__ __forceinline__ uint32_t get(int i) const { return lds[i * STRIDE]; }
@@ -64,6 +69,8 @@ struct LdsStack {
 
 template <int STRIDE, int LDSN>
 struct SpillStack {
+    static constexpr int kLds = LDSN;
+    static constexpr int kStride = STRIDE;
     uint32_t* lds;
     uint32_t* ovf;
     uint32_t ostride;
@@ -72,9 +79,26 @@ struct SpillStack {
         else ovf[(size_t)(i - LDSN) * ostride] = v;
     }
     __device__ __forceinline__ uint32_t get(int i) const {
-        return i < LDSN ? lds[i * STRIDE] : ovf[(size_t)(i - LDSN) * ostride];
+        if (__builtin_expect(i >= LDSN, 0)) return ovf[(size_t)(i - LDSN) * ostride];
+        return lds[i * STRIDE];
     }
 };
+
+template <class STK>
+__device__ __forceinline__ void push_hits(const STK& st, int& sp, int n, uint32_t v1, uint32_t v2, uint32_t v3) {
+    if (__builtin_expect(sp <= STK::kLds - 3, 1)) {
+        st.lds[sp * STK::kStride] = v3;
+        sp += n > 3;
+        st.lds[sp * STK::kStride] = v2;
+        sp += n > 2;
+        st.lds[sp * STK::kStride] = v1;
+        sp += n > 1;
+    } else {
+        if (n > 3) { st.put(sp, v3); sp++; }
+        if (n > 2) { st.put(sp, v2); sp++; }
+        if (n > 1) { st.put(sp, v1); sp++; }
+    }
+}
 
 // Conservative fp32 slab test of one child box: (b - o) * (1/d) carries <= 3 ulp
 // of relative error, so the far distance is widened by 2^-21 relative; NaN slabs
@@ -112,13 +136,13 @@ __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32
     if (num_nodes <= 0) return false;
     uint32_t ref = 0;  // root: always an inner node
     int sp = 0;
+    float tmax = tmax_bound(best.t);  // fp32 cull bound, refreshed when best.t changes
     for (;;) {
         if (!(ref & 0x80000000u)) {
             const float4* c = nodes + 8 * (size_t)ref;
             const float4 lx = c[0], hx = c[1], ly = c[2], hy = c[3], lz = c[4], hz = c[5];
             const uint4 rf = *reinterpret_cast<const uint4*>(c + 6);
             if (COUNT) ctr.nodes++;
-            const float tmax = tmax_bound(best.t);
             const float inf = __int_as_float(0x7f800000);
             float k0 = slab1(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, o, invd, tmax);
             float k1 = slab1(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, o, invd, tmax);
@@ -134,9 +158,7 @@ __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32
             cswap(k1, v1, k3, v3r);
             cswap(k1, v1, k2, v2);
             if (k0 != inf) {
-                if (k3 != inf) { stack.put(sp, v3r); sp++; }
-                if (k2 != inf) { stack.put(sp, v2); sp++; }
-                if (k1 != inf) { stack.put(sp, v1); sp++; }
+                push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
                 ref = v0;
                 continue;
             }
@@ -149,6 +171,7 @@ __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32
                 if (t < best.t) {
                     if (ANY) return true;
                     best.t = t; best.kind = kind; best.idx = (int32_t)(first + k);
+                    tmax = tmax_bound(t);
                 }
             }
         }

@@ -253,21 +253,40 @@ class Mesh:
         self.Transform(m)
 
     def SmoothNormals(self) -> None:
-        """Mesh.SmoothNormals (Mesh.cs:191-229): per distinct vertex, the fp32 sum of the
-        corner normals in triangle order (V1,V2,V3 of each triangle), normalised."""
+        """Mesh.SmoothNormals (Mesh.cs:191-229), natively (pt_mesh_smooth_normals): per
+        distinct vertex, the fp32 sum of the corner normals in triangle order, normalised."""
         n = len(self)
         if n == 0:
             return
-        verts = np.stack([self.v1, self.v2, self.v3], axis=1).reshape(-1, 3) + np.float32(0.0)  # -0 → +0
-        norms = np.stack([self.n1, self.n2, self.n3], axis=1).reshape(-1, 3)
-        _, inv = np.unique(verts, axis=0, return_inverse=True)
-        inv = inv.reshape(-1)
-        acc = np.zeros((inv.max() + 1, 3), np.float32)
-        for k in range(3):  # sequential fp32 accumulation in reference order
-            np.add.at(acc[:, k], inv, norms[:, k])
-        unit = normalize_rows(acc)
-        sm = unit[inv].reshape(n, 3, 3)
-        self.n1, self.n2, self.n3 = (np.ascontiguousarray(sm[:, k]) for k in range(3))
+        lib = _abi.load_library()
+        self.n1, self.n2, self.n3 = (np.ascontiguousarray(a, np.float32).copy() for a in (self.n1, self.n2, self.n3))
+        f = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data_as(C.POINTER(C.c_float))
+        rc = lib.pt_mesh_smooth_normals(n, f(self.v1), f(self.v2), f(self.v3), f(self.n1), f(self.n2), f(self.n3))
+        if rc != 0:
+            raise _abi.PTError(rc, "pt_mesh_smooth_normals", lib.pt_obj_last_error().decode())
+
+
+class OBJ:
+    """PTSharpCore.OBJ (OBJ.cs), parsed natively by libptsharp_hip.so (pt_obj_load)
+    with the reference's quirks; see include/ptsharp_hip.h and DESIGN.md §9a."""
+
+    @staticmethod
+    def Load(path: str, parent: "Material" = None) -> Mesh:
+        lib = _abi.load_library()
+        md = _abi.pt_mesh_data()
+        rc = lib.pt_obj_load(str(path).encode(), C.byref(md))
+        if rc != 0:
+            raise _abi.PTError(rc, "pt_obj_load", lib.pt_obj_last_error().decode())
+        try:
+            n = md.num_triangles
+            arr = lambda p: np.ctypeslib.as_array(p, shape=(n, 3)).copy() if n else np.zeros((0, 3), np.float32)
+            m = Mesh(arr(md.v1), arr(md.v2), arr(md.v3), arr(md.n1), arr(md.n2), arr(md.n3))
+            m.t1, m.t2, m.t3 = arr(md.t1), arr(md.t2), arr(md.t3)
+        finally:
+            lib.pt_mesh_free(C.byref(md))
+        if parent is not None:
+            m.SetMaterial(parent)
+        return m
 
 
 class Scene:

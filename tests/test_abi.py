@@ -42,6 +42,7 @@ def test_version():
 
 def test_struct_layouts_match_header():
     # sizes computed by hand from the C declarations (x86-64 SysV alignment)
+    assert C.sizeof(_abi.pt_mesh_data) == 8 + 9 * 8
     assert C.sizeof(_abi.pt_material) == 8 * 8 + 8
     assert C.sizeof(_abi.pt_camera) == 12 * 4 + 3 * 8
     assert C.sizeof(_abi.pt_sampler) == 24
@@ -88,3 +89,46 @@ def test_no_device_reports_error_not_fallback():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(ImportError):
         _abi.load_library(str(tmp_path / "missing.so"))
+
+
+def _fields_c(src, name):
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), src, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    out = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        names = decl.split(None, 1)[1] if " " in decl else ""
+        for n in names.replace("*", " ").split(","):
+            n = n.strip().split()[-1] if n.strip() else ""
+            m = re.match(r"(\w+)(?:\[(\d+)\])?", n)
+            if m:
+                out.append((m.group(1), int(m.group(2) or 1)))
+    return out
+
+
+def _fields_cs(src, name):
+    body = re.search(r"struct %s\s*\{(.*?)\}" % name, src, re.S).group(1)
+    body = re.sub(r"//[^\n]*", "", body)
+    out = []
+    for decl in body.split(";"):
+        decl = decl.replace("public", "").replace("fixed", "").strip()
+        if not decl:
+            continue
+        names = decl.split(None, 1)[1]
+        for n in names.split(","):
+            m = re.match(r"\s*(\w+)(?:\[(\d+)\])?", n)
+            out.append((m.group(1), int(m.group(2) or 1)))
+    return out
+
+
+@pytest.mark.parametrize("name", ["pt_pass_params", "pt_stats", "pt_mesh_data", "pt_sampler", "pt_device_opts",
+                                  "pt_camera"])
+def test_csharp_binding_matches_header(name):
+    """csharp/HipRenderer.cs mirrors include/ptsharp_hip.h field for field (the library
+    writes pt_stats into the caller's struct, so a stale C# layout would be overrun)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    c = _fields_c(open(HEADER).read(), name)
+    cs = _fields_cs(open(os.path.join(root, "csharp", "HipRenderer.cs")).read(), name)
+    assert cs == c
