@@ -163,7 +163,6 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
     if ((rc = wf_alloc(c, &Q.n_o, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.n_n, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.n_w, scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.n_k, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
     if ((rc = wf_alloc(c, &Q.ovf, (size_t)(pt::kMaxDepth - pt::kLdsStack) * pt::kWfMaxThreads))) return rc;
     size_t P = (size_t)c->width * (size_t)c->height;
@@ -572,14 +571,15 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp);
     double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)
     if (nm == 2) growth = std::ldexp(1.0, std::min(std::max(sampler->max_bounces - 1, 0), 60));
-    const double per_sample = (double)plan.root_children * growth;   // NEE requests: at most one per child
+    const double per_sample = (double)plan.root_children * growth;   // extension rays per camera sample (widest depth)
+    const double per_sample_nee = per_sample * (double)plan.lights_per_child;  // shadow-ray slots per camera sample
     // Queues are kParts partitions.  Camera samples are dealt to the XCD groups in
     // 256-sample blocks, so a group gets at most ceil(ceil(chunk/256)/kParts)·256 of
     // them, and everything it appends stays in its own partition.
     const double pmax = (double)(kWfMaxCap / pt::kParts);
     auto group_max = [](uint64_t ch) { return (double)(((ch + 255) / 256 + pt::kParts - 1) / pt::kParts * 256); };
     uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples,
-                                                std::floor(pmax / per_sample / 256.0) * 256.0 * pt::kParts);
+                                                std::floor(pmax / per_sample_nee / 256.0) * 256.0 * pt::kParts);
     const bool extra = pass->adaptive_samples > 0 || pass->firefly_samples > 0;
     if (pass->adaptive_samples < 0 || pass->firefly_samples < 0) return fail(PT_ERR_INVALID_ARG, "negative extra samples");
     int engine = pass->engine;
@@ -595,7 +595,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         const double group_samples = group_max(chunk);
         const double need = group_samples * per_sample;   // a partition's widest depth
         const uint32_t pcap = (uint32_t)std::min(pmax, std::max(8192.0, std::max(group_samples, need)));
-        const uint32_t spcap = (uint32_t)std::min(pmax, std::max(8192.0, need));
+        const uint32_t spcap = (uint32_t)std::min(pmax, std::max(8192.0, group_samples * per_sample_nee));
         uint32_t cap = pcap * pt::kParts, scap = spcap * pt::kParts;
         int rc = ensure_wavefront(c, cap, scap);
         if (rc) return rc;

@@ -21,10 +21,9 @@ struct WfQueues {
     float4* q_t[2];      // {throughput.rgb, -}
     uint64_t* q_k[2];    // RNG node key of the vertex the ray leads to
     uint4* hits;         // {t (fp64 bits), kind, record}
-    float4* n_o;         // NEE requests (a diffuse child's sampleLights): {position.xyz, pixel}
-    float4* n_n;         // {normal.xyz, -}
-    float4* n_w;         // {throughput·weight.rgb, -}
-    uint64_t* n_k;       // RNG key of the child edge (light choice, soft-shadow point)
+    float4* n_o;         // shadow rays (a diffuse child's sampleLights, set up by k_wf_shade): {origin.xyz, pixel}
+    float4* n_n;         // {direction.xyz, light index | kDead: no ray cast (diffuse <= 0)}
+    float4* n_w;         // {throughput·weight·light colour·coverage.rgb, -}: added if the light is visible
     uint32_t* counts;    // word (q, g) = {counts[2(q·kParts+g)], +1}: partition g of ray queue q and the
                          // NEE requests made with it (one packed 64-bit word, reserved together);
                          // counts[kFetchWord + k·kParts + g] = work-fetch cursor of kernel k
@@ -50,7 +49,7 @@ struct WfPlan {
     uint64_t chunk;            // camera samples per chunk
     uint32_t root_children;    // ⌊√FH⌋² · modes at depth 0
     uint32_t children;         // modes at depth >= 1 (1, or 2 under SpecularModeAll)
-    uint32_t lights_per_child; // shadow rays per NEE request: 1, or #lights under LightModeAll
+    uint32_t lights_per_child; // shadow-ray slots per diffuse child: 1, or #lights under LightModeAll
     uint32_t trace_blocks;     // persistent grids: resident capacity of each kernel
     uint32_t shade_blocks;
     uint32_t shadow_blocks;

@@ -8,10 +8,11 @@
 //   k_wf_camera   camera samples → extension rays, depth 0      (Renderer.cs:294-305, Camera.cs:98-119)
 //   k_wf_trace    closest hit for every queued ray               (Scene.Intersect, Scene.cs:75-79)
 //   k_wf_shade    Hit.Info, emission, and every child of the vertex: Ray.Bounce →
-//                 next-depth extension ray, sampleLights → shadow ray
-//                                                                (Sampler.cs:62-131, Ray.cs:44-85)
+//                 next-depth extension ray; sampleLights up to the shadow query
+//                 (light choice, soft-shadow point, coverage) → shadow ray
+//                                                                (Sampler.cs:62-131,191-296, Ray.cs:44-85)
 //   k_wf_shadow   shadow visibility (nearest-hit == light ⇔ no primitive nearer
-//                 than the light's own t: any-hit, early exit)   (Sampler.cs:255-296)
+//                 than the light's own t: any-hit, early exit)   (Sampler.cs:261-265)
 //   k_wf_finalize per-pixel mean of the pass → Welford           (Renderer.cs:308-309, Buffer.cs:33-44)
 //
 // The traversal kernels keep only ray + stack state, so they run at the
@@ -217,15 +218,16 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
 
 // ---------------------------------------------------------------- shade / bounce
 #ifndef PT_SHADE_WAVES
-#define PT_SHADE_WAVES 2
+#define PT_SHADE_WAVES 3
 #endif
 // One thread per queued ray: Hit.Info, emission, then every child of the vertex
 // (the u/v/mode loop of Sampler.cs:96-131).  Which children are reflected / live
 // depends only on the vertex' Fresnel p and one draw per Any-mode child, so each
 // lane counts its extension rays and NEE requests before computing any bounce, and
-// the wave reserves both queues with ONE atomic each (a returning atomic on one
+// the block reserves both queues with ONE atomic (a returning atomic on one
 // word saturates near 88 per µs on MI355X, MI355X_MICROARCH.md "dequeue").  Light
-// sampling itself runs in k_wf_shadow.
+// sampling up to the shadow query runs here too, so k_wf_shadow is a lean
+// traversal kernel (ray + stack state only).
 template <bool COUNT>
 __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
@@ -235,6 +237,9 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
     const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
     const int qo = 1 - qi;
     const bool nee_on = smp.dl && S.num_lights > 0;
+    const int nl = S.num_lights;
+    const bool all_lights = smp.light_mode == 1;
+    const uint32_t rays_per_nee = all_lights ? (uint32_t)nl : 1u;   // shadow rays of one sampleLights call
     Counters ctr{0, 0, 0, 0};
     __shared__ uint32_t s_k0;
     for (;;) {  // block-uniform: the block takes 256 vertices of its partition at a time
@@ -304,7 +309,7 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
             const bool refl = mode == 2 || (mode == 0 && draw(child_key(node, (uint32_t)c), D_REFLECT) < pv);
             const bool live = mode == 0 || (refl ? pv > 0 : (1 - pv) > 0);
             n_ext += (live && ext_on) ? 1u : 0u;
-            n_nee += (live && !refl && !m.transparent && nee_on) ? 1u : 0u;
+            n_nee += (live && !refl && !m.transparent && nee_on) ? rays_per_nee : 0u;
         }
         uint32_t ebase, nbase;
         block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase);
@@ -323,15 +328,28 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
                 for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * m.color[k]);
             } else {
                 for (int k = 0; k < 3; k++) w[k] = fp * m.color[k];
-                if (nee_on) {  // diffuse child: sampleLights from the normal ray, in k_wf_shadow
-                    if (nj < Q.spcap) {
-                        const uint32_t at = G.g * Q.spcap + nj;
-                        nt_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
-                        nt_store(&Q.n_n[at], make_float4(sh.nrm.x, sh.nrm.y, sh.nrm.z, 0.f));
-                        nt_store(&Q.n_w[at], make_float4(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2], 0.f));
-                        nt_store(&Q.n_k[at], E);
+                if (nee_on) {
+                    // diffuse child: sampleLights from the normal ray (Sampler.cs:191-296) up to the
+                    // shadow query — light choice, soft-shadow point, coverage — here, so the
+                    // visibility kernel carries only ray + stack state.  One shadow-ray slot per
+                    // light considered; a light with diffuse <= 0 casts no ray (dead slot).
+                    const int first = all_lights ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
+                    const float scale = all_lights ? 1.0f / (float)nl : (float)nl;
+                    for (uint32_t j = 0; j < rays_per_nee; j++) {
+                        const int li = first + (int)j;
+                        v3 ldir;
+                        float3 lc;
+                        const bool cast = light_setup(S, smp, S.lights[li], sh.pos, sh.nrm,
+                                                      all_lights ? light_key(E, (uint32_t)li) : E, ldir, lc);
+                        if (nj < Q.spcap) {
+                            const uint32_t at = G.g * Q.spcap + nj;
+                            nt_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
+                            nt_store(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
+                            nt_store(&Q.n_w[at], make_float4((t2[0] * w[0]) * (lc.x * scale), (t2[1] * w[1]) * (lc.y * scale),
+                                                             (t2[2] * w[2]) * (lc.z * scale), 0.f));
+                        }
+                        nj++;
                     }
-                    nj++;
                 }
             }
             if (!ext_on) continue;
@@ -354,45 +372,34 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
 }
 
 // ---------------------------------------------------------------- shadow rays
-// One thread per NEE request: sampleLights / sampleLight (Sampler.cs:191-296) —
-// light choice, soft-shadow point, coverage — then the visibility query.
+// One thread per shadow ray that k_wf_shade set up (light, direction, the colour the
+// light adds if it is the nearest hit): the visibility query of Sampler.cs:261-265.
 template <bool COUNT>
-__global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, DevSampler smp, WfQueues Q, int qo,
-                                                   unsigned long long* counters) {
+__global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + threadIdx.x] = 0u;  // next k_wf_trace's
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
-    const int nl = S.num_lights;
-    const bool all = smp.light_mode == 1;
     uint32_t* cursor = Q.counts + kFetchWord + 2 * kParts + G.g;
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
-    for (;;) {  // 64 requests per wave at a time (see k_wf_trace)
+    for (;;) {  // 64 rays per wave at a time (see k_wf_trace)
         uint32_t k0 = 0;
         if (lane == 0) k0 = atomicAdd(cursor, 64u);
         k0 = __shfl(k0, 0, 64);
         if (k0 >= n) break;
         if (k0 + lane >= n) continue;
         const uint32_t i = base + k0 + lane;
-        const float4 a = nt_load(&Q.n_o[i]);
         const float4 b = nt_load(&Q.n_n[i]);
-        const float4 wt = nt_load(&Q.n_w[i]);
-        const uint64_t E = nt_load(&Q.n_k[i]);
-        const v3 o{a.x, a.y, a.z}, nrm{b.x, b.y, b.z};
-        const int first = all ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
-        const int last = all ? nl : first + 1;
-        const float scale = all ? 1.0f / (float)nl : (float)nl;
-        for (int li = first; li < last; li++) {
-            const DevLight L = S.lights[li];
-            v3 ldir;
-            float3 lc;
-            if (!light_setup(S, smp, L, o, nrm, all ? light_key(E, (uint32_t)li) : E, ldir, lc)) continue;
-            if (light_visible<COUNT>(S, L, o, ldir, stack, ctr))
-                acc_add(Q.acc, __float_as_uint(a.w), wt.x * (lc.x * scale), wt.y * (lc.y * scale),
-                        wt.z * (lc.z * scale));
+        const uint32_t li = __float_as_uint(b.w);
+        if (li == kDead) continue;
+        const float4 a = nt_load(&Q.n_o[i]);
+        const DevLight L = S.lights[li];
+        if (light_visible<COUNT>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) {
+            const float4 wt = nt_load(&Q.n_w[i]);
+            acc_add(Q.acc, __float_as_uint(a.w), wt.x, wt.y, wt.z);
         }
     }
     uint32_t rays = wave_sum(ctr.rays);
@@ -523,10 +530,10 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         else hipLaunchKernelGGL(k_wf_shade<false>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         end_k(2);
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
-        const unsigned hg = grid_for(children, kTB, plan.shadow_blocks);
+        const unsigned hg = grid_for(children * plan.lights_per_child, kTB, plan.shadow_blocks);
         begin_k(3);
-        if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
-        else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, smp, Q, 1 - qi, B.counters);
+        if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
+        else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
         end_k(3);
         bound = children < Q.cap ? children : Q.cap;
         qi = 1 - qi;
