@@ -27,14 +27,24 @@ namespace PTSharpCore
         public const int SHAPE_SPHERE = 0, SHAPE_CUBE = 1, SHAPE_PLANE = 2, SHAPE_TRIANGLE = 3, SHAPE_MESH = 4;
 
         [StructLayout(LayoutKind.Sequential)]
-        public struct pt_material
+        public struct pt_texture
         {
-            public double r, g, b, emittance, index, gloss, tint, reflectivity;
-            public int transparent, _pad;
+            public int width; public int height; public IntPtr data;   // ColorTexture.Data as [h][w][3] double
         }
 
         [StructLayout(LayoutKind.Sequential)]
-        public struct pt_scene_desc
+        public unsafe struct pt_material
+        {
+            public fixed double color[3];
+            public double emittance, index, gloss, tint, reflectivity;
+            public int transparent;
+            public int texture, normal_texture, bump_texture, gloss_texture;   // 1-based into textures, 0 = null
+            public int _pad;
+            public double bump_multiplier;
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public unsafe struct pt_scene_desc
         {
             public int num_materials; public IntPtr materials;
             public int num_shapes; public IntPtr shape_kind; public IntPtr shape_index;
@@ -43,7 +53,10 @@ namespace PTSharpCore
             public int num_planes; public IntPtr plane_point; public IntPtr plane_normal; public IntPtr plane_material;
             public int num_triangles; public IntPtr tri_v1, tri_v2, tri_v3, tri_n1, tri_n2, tri_n3; public IntPtr tri_material;
             public int num_meshes; public IntPtr mesh_first; public IntPtr mesh_count;
-            public double env_r, env_g, env_b;
+            public fixed double env_color[3];
+            public int num_textures; public IntPtr textures;
+            public IntPtr tri_t1, tri_t2, tri_t3;
+            public int env_texture; public int _pad; public double env_texture_angle;
         }
 
         [StructLayout(LayoutKind.Sequential)]
@@ -145,19 +158,35 @@ namespace PTSharpCore
 
         // Flatten Scene.Shapes (Scene.cs:19) with a type switch; returns PT_ERR_UNSUPPORTED kinds as exceptions
         // so the caller can fall back to the CPU Renderer.
-        void Upload()
+        unsafe void Upload()
         {
+            // ColorTexture instances (Texture.cs:96-252) by reference; 1-based ids, 0 = null.
+            var texs = new List<PtHip.pt_texture>(); var texIds = new Dictionary<ITexture, int>(ReferenceEqualityComparer.Instance);
+            int Tid(ITexture t)
+            {
+                if (t == null) return 0;
+                if (t is not ColorTexture ct) throw new NotSupportedException($"{t.GetType().Name} is not on the GPU path");
+                if (!texIds.TryGetValue(t, out int id))
+                {
+                    var data = new double[3 * ct.Data.Length];
+                    for (int i = 0; i < ct.Data.Length; i++) { data[3 * i] = ct.Data[i].r; data[3 * i + 1] = ct.Data[i].g; data[3 * i + 2] = ct.Data[i].b; }
+                    texs.Add(new PtHip.pt_texture { width = ct.Width, height = ct.Height, data = Pin(data) });
+                    id = texs.Count; texIds[t] = id;
+                }
+                return id;
+            }
             var mats = new List<PtHip.pt_material>(); var matIds = new Dictionary<Material, int>();
             int Mid(Material m)
             {
-                if (m.Texture != null || m.NormalTexture != null || m.BumpTexture != null || m.GlossTexture != null)
-                    throw new NotSupportedException("textured materials are not on the GPU path");
                 if (!matIds.TryGetValue(m, out int id))
                 {
                     id = mats.Count; matIds[m] = id;
-                    mats.Add(new PtHip.pt_material { r = m.Color.r, g = m.Color.g, b = m.Color.b, emittance = m.Emittance,
-                        index = m.Index, gloss = m.Gloss, tint = m.Tint, reflectivity = m.Reflectivity,
-                        transparent = m.Transparent ? 1 : 0 });
+                    var pm = new PtHip.pt_material { emittance = m.Emittance, index = m.Index, gloss = m.Gloss, tint = m.Tint,
+                        reflectivity = m.Reflectivity, transparent = m.Transparent ? 1 : 0,
+                        texture = Tid(m.Texture), normal_texture = Tid(m.NormalTexture), bump_texture = Tid(m.BumpTexture),
+                        gloss_texture = Tid(m.GlossTexture), bump_multiplier = m.BumpMultiplier };
+                    pm.color[0] = m.Color.r; pm.color[1] = m.Color.g; pm.color[2] = m.Color.b;
+                    mats.Add(pm);
                 }
                 return id;
             }
@@ -167,11 +196,13 @@ namespace PTSharpCore
             var pp = new List<float>(); var pn = new List<float>(); var pm = new List<int>();
             var v1 = new List<float>(); var v2 = new List<float>(); var v3 = new List<float>();
             var n1 = new List<float>(); var n2 = new List<float>(); var n3 = new List<float>(); var tm = new List<int>();
+            var t1 = new List<float>(); var t2 = new List<float>(); var t3 = new List<float>();
             var mf = new List<int>(); var mc = new List<int>();
             void Add3(List<float> l, Vector v) { l.Add((float)v.X); l.Add((float)v.Y); l.Add((float)v.Z); }
             void AddTri(Triangle t)
             {
                 Add3(v1, t.V1); Add3(v2, t.V2); Add3(v3, t.V3); Add3(n1, t.N1); Add3(n2, t.N2); Add3(n3, t.N3);
+                Add3(t1, t.T1); Add3(t2, t.T2); Add3(t3, t.T3);
                 tm.Add(Mid(t.Material));
             }
             foreach (var s in Scene.Shapes)
@@ -198,8 +229,11 @@ namespace PTSharpCore
                 num_triangles = tm.Count, tri_v1 = Pin(v1.ToArray()), tri_v2 = Pin(v2.ToArray()), tri_v3 = Pin(v3.ToArray()),
                 tri_n1 = Pin(n1.ToArray()), tri_n2 = Pin(n2.ToArray()), tri_n3 = Pin(n3.ToArray()), tri_material = Pin(tm.ToArray()),
                 num_meshes = mf.Count, mesh_first = Pin(mf.ToArray()), mesh_count = Pin(mc.ToArray()),
-                env_r = Scene.Color.r, env_g = Scene.Color.g, env_b = Scene.Color.b,
+                tri_t1 = Pin(t1.ToArray()), tri_t2 = Pin(t2.ToArray()), tri_t3 = Pin(t3.ToArray()),
+                env_texture = Tid(Scene.Texture), env_texture_angle = Scene.TextureAngle,
             };
+            d.env_color[0] = Scene.Color.r; d.env_color[1] = Scene.Color.g; d.env_color[2] = Scene.Color.b;
+            d.num_textures = texs.Count; d.textures = Pin(texs.ToArray());
             try { PtHip.Check(PtHip.pt_upload_scene(ctx, ref d), "pt_upload_scene"); }
             finally { foreach (var g in pins) g.Free(); pins.Clear(); }   // arrays are copied during the call
             uploaded = true;

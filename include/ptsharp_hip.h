@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+#define PT_ABI_VERSION 2
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -65,7 +65,19 @@ typedef enum pt_shape_kind {
     PT_SHAPE_MESH = 4       /* Mesh.cs, a range of triangles with its own tree */
 } pt_shape_kind;
 
-/* Material (Material.cs:8-62); textures are not part of the GPU path (PT_ERR_UNSUPPORTED). */
+/* ColorTexture (Texture.cs:96-252): Width x Height Colour texels, row-major, as the
+ * C# object holds them (Data[y * Width + x], already through Pow(2.2) and any
+ * ITexture.Pow / MulScalar the scene applied).  Width and Height must be >= 2
+ * (BilinearSample reads texel x0 + 1 and y0 + 1, Texture.cs:198-206). */
+typedef struct pt_texture {
+    int32_t width;
+    int32_t height;
+    const double* data;   /* [height][width][3] */
+} pt_texture;
+
+/* Material (Material.cs:8-62).  Texture slots are 1-based references into
+ * pt_scene_desc.textures: 0 = null (no map), k = textures[k - 1], so a zeroed
+ * pt_material is a valid untextured material. */
 typedef struct pt_material {
     double color[3];      /* Colour Color            */
     double emittance;     /* Emittance               */
@@ -74,7 +86,12 @@ typedef struct pt_material {
     double tint;          /* Tint                    */
     double reflectivity;  /* Reflectivity (<0: Fresnel) */
     int32_t transparent;  /* Transparent             */
+    int32_t texture;          /* Texture       → Color (Material.MaterialAt, Material.cs:124-138)  */
+    int32_t normal_texture;   /* NormalTexture → Triangle.NormalAt normal map (Triangle.cs:147-168) */
+    int32_t bump_texture;     /* BumpTexture   → Triangle.NormalAt bump (Triangle.cs:170-184)       */
+    int32_t gloss_texture;    /* GlossTexture  → Gloss = mean of the sampled colour               */
     int32_t _pad;
+    double bump_multiplier;   /* BumpMultiplier */
 } pt_material;
 
 /* Flattened Scene.  Triangle arrays hold every triangle: directly-added ones
@@ -117,6 +134,16 @@ typedef struct pt_scene_desc {
     const int32_t* mesh_count;
 
     double env_color[3];          /* Scene.Color (Scene.cs:25), returned on a miss */
+
+    /* textures (§8f row 3); all optional */
+    int32_t num_textures;
+    const pt_texture* textures;
+    const float* tri_t1;          /* [n][3] Triangle.T1..T3 texture coordinates; NULL = all zero */
+    const float* tri_t2;
+    const float* tri_t3;
+    int32_t env_texture;          /* Scene.Texture (1-based, 0 = null): sampleEnvironment, Sampler.cs:177-189 */
+    int32_t _pad;
+    double env_texture_angle;     /* Scene.TextureAngle */
 } pt_scene_desc;
 
 /* Camera struct fields (Camera.cs:11-14) as produced by Camera.LookAt/SetFocus. */

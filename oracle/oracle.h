@@ -22,10 +22,18 @@
 extern "C" {
 #endif
 
+typedef struct or_texture {
+    int32_t width, height;
+    const double* data;   /* [h][w][3] ColorTexture.Data */
+} or_texture;
+
 typedef struct or_material {
     double color[3];
     double emittance, index, gloss, tint, reflectivity;
-    int32_t transparent, _pad;
+    int32_t transparent;
+    int32_t texture, normal_texture, bump_texture, gloss_texture;  /* 1-based, 0 = null */
+    int32_t _pad;
+    double bump_multiplier;
 } or_material;
 
 typedef struct or_scene_desc {
@@ -39,6 +47,10 @@ typedef struct or_scene_desc {
     const int32_t* tri_material;
     int32_t num_meshes; const int32_t* mesh_first; const int32_t* mesh_count;
     double env_color[3];
+    int32_t num_textures; const or_texture* textures;
+    const float *tri_t1, *tri_t2, *tri_t3;
+    int32_t env_texture, _pad;
+    double env_texture_angle;
 } or_scene_desc;
 
 typedef struct or_camera {
@@ -94,6 +106,16 @@ double or_prim_intersect(int32_t kind, const float* a, const float* b, const flo
 void or_prim_normal(int32_t kind, const float* a, const float* b, const float* c,
                     const float* n1, const float* n2, const float* n3,
                     const float pos[3], float out_normal[3]);
+
+/* Texture KATs (Texture.cs:188-251): kind 0 Sample -> colour, 1 NormalSample, 2 BumpSample
+ * -> vector; texture is 1-based as in or_material. */
+void or_texture_sample(void* scene, int32_t texture, int32_t kind, double u, double v, double out[3]);
+/* IShape.UVector of scene primitive (kind K_*, index into the per-kind arrays) at p. */
+void or_shape_uv(void* scene, int32_t kind, int32_t index, const float p[3], float out_uv[3]);
+/* sampleEnvironment (Sampler.cs:177-189) for a ray direction. */
+void or_environment(void* scene, const float dir[3], double out[3]);
+/* Hit.Info's material after Material.MaterialAt (Material.cs:124-138): colour and gloss. */
+int32_t or_hit_surface(void* scene, const float origin[3], const float dir[3], double out_color[3], double* out_gloss);
 
 /* Counter-based RNG that replaces Random.Shared (spec in DESIGN.md §RNG). */
 uint64_t or_camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample);

@@ -170,11 +170,19 @@ enum Kind { K_SPHERE = 0, K_CUBE = 1, K_PLANE = 2, K_TRI = 3, K_MESH = 4 };
 
 struct Material {
     C color; double emittance, index, gloss, tint, reflectivity; bool transparent;
+    int tex, ntex, btex, gtex;  // texture slots, 0-based (-1 = null)
+    double bump_multiplier;
+};
+// ColorTexture (Texture.cs:96-252): Width x Height fp64 Colour texels, row-major.
+struct Tex {
+    int w, h;
+    std::vector<double> d;
+    C at(size_t i) const { return C{d[3 * i], d[3 * i + 1], d[3 * i + 2]}; }
 };
 struct Sphere { V center; double radius; int mat; Box box; };
 struct Cube { V min, max; int mat; };
 struct Plane { V point, normal; int mat; };
-struct Tri { V v1, v2, v3, n1, n2, n3; int mat; };
+struct Tri { V v1, v2, v3, n1, n2, n3; int mat; V t1, t2, t3; };
 struct ShapeRef { int kind; int idx; };
 
 struct Hit { double t; int kind; int idx; };  // kind: K_* of the primitive hit (mesh hits report K_TRI)
@@ -203,6 +211,9 @@ struct Scene {
     std::vector<ShapeRef> lights;  // Scene.Lights (Scene.cs:33-37)
     KdTree tree;
     C env;
+    std::vector<Tex> texs;
+    int env_tex = -1;        // Scene.Texture (-1 = null)
+    double env_angle = 0;    // Scene.TextureAngle
 };
 
 // ---------------------------------------------------------------- primitives
@@ -268,8 +279,8 @@ inline V cube_normal(V mn, V mx, V p) {
     if (std::fabs((double)p.z - (double)mx.z) < EPS) return vmk(0, 0, 1);
     return vmk(0, 1, 0);
 }
-// Triangle.NormalAt via Barycentric (Triangle.cs:142-189, 208-223), no normal/bump maps.
-inline V tri_normal(const Tri& t, V p) {
+// Triangle.Barycentric (Triangle.cs:208-223)
+inline void barycentric(const Tri& t, V p, double& bu, double& bv, double& bw) {
     V v0 = vsub(t.v2, t.v1);
     V v1 = vsub(t.v3, t.v1);
     V v2 = vsub(p, t.v1);
@@ -279,14 +290,155 @@ inline V tri_normal(const Tri& t, V p) {
     double d20 = vdot(v2, v0);
     double d21 = vdot(v2, v1);
     double d = d00 * d11 - d01 * d01;
-    double bv = (d11 * d20 - d01 * d21) / d;
-    double bw = (d00 * d21 - d01 * d20) / d;
-    double bu = 1 - bv - bw;
+    bv = (d11 * d20 - d01 * d21) / d;
+    bw = (d00 * d21 - d01 * d20) / d;
+    bu = 1 - bv - bw;
+}
+// Triangle.NormalAt without maps (Triangle.cs:142-145, 186-188).
+inline V tri_normal(const Tri& t, V p) {
+    double bu, bv, bw;
+    barycentric(t, p, bu, bv, bw);
     V n = vadd(vadd(vmuls(t.n1, bu), vmuls(t.n2, bv)), vmuls(t.n3, bw));
     return vnorm(n);
 }
 
+// ---------------------------------------------------------------- textures (Texture.cs:96-252)
+// Util.Modf / ColorTexture.Fract (Util.cs:108-113, Texture.cs:218-222): the fractional part, sign kept.
+inline double fract(double x) { return x - std::trunc(x); }
+// Texel coordinates are Convert.ToInt32(Math.Truncate(.)) / (int) casts, which throw
+// OverflowException in the reference for non-finite inputs (CheckForOverflowUnderflow);
+// such a lookup returns black here (and on the GPU).
+// ColorTexture.BilinearSample (Texture.cs:188-216)
+C bilinear(const Tex& t, double u, double v) {
+    if (u == 1) u -= EPS;
+    if (v == 1) v -= EPS;
+    double w = (double)t.w - 1;
+    double h = (double)t.h - 1;
+    double uw = u * w, vh = v * h;
+    if (!std::isfinite(uw) || !std::isfinite(vh)) return BLACK;
+    double X = std::trunc(uw), x = uw - X;
+    double Y = std::trunc(vh), y = vh - Y;
+    int x0 = (int)X, y0 = (int)Y, x1 = x0 + 1, y1 = y0 + 1;
+    C c00 = t.at((size_t)y0 * t.w + x0);
+    C c01 = t.at((size_t)y1 * t.w + x0);
+    C c10 = t.at((size_t)y0 * t.w + x1);
+    C c11 = t.at((size_t)y1 * t.w + x1);
+    C c = BLACK;
+    c = cadd(c, cmuls(c00, (1 - x) * (1 - y)));
+    c = cadd(c, cmuls(c10, x * (1 - y)));
+    c = cadd(c, cmuls(c01, (1 - x) * y));
+    c = cadd(c, cmuls(c11, x * y));
+    return c;
+}
+// ITexture.Sample (Texture.cs:224-229)
+C tex_sample(const Tex& t, double u, double v) {
+    u = fract(fract(u) + 1);
+    v = fract(fract(v) + 1);
+    return bilinear(t, u, 1 - v);
+}
+// ITexture.NormalSample (Texture.cs:231-237)
+V tex_normal_sample(const Tex& t, double u, double v) {
+    u = fract(fract(u) + 1);
+    v = fract(fract(v) + 1);
+    C c = bilinear(t, u, 1 - v);
+    return vnorm(vmk(c.r * 2 - 1, c.g * 2 - 1, c.b * 2 - 1));
+}
+// ITexture.BumpSample (Texture.cs:239-251).  At v == 0 the reference reads row Height
+// (y = (int)(1 * Height)) and throws IndexOutOfRangeException; the row is clamped here.
+V tex_bump_sample(const Tex& t, double u, double v) {
+    u = fract(fract(u) + 1);
+    v = fract(fract(v) + 1);
+    v = 1 - v;
+    double fx = u * t.w, fy = v * t.h;
+    if (!std::isfinite(fx) || !std::isfinite(fy)) return vzero();
+    int x = std::min((int)fx, t.w - 1), y = std::min((int)fy, t.h - 1);
+    auto clampi = [](int a, int lo, int hi) { return a < lo ? lo : (a > hi ? hi : a); };  // Util.ClampInt
+    int x1 = clampi(x - 1, 0, t.w - 1), x2 = clampi(x + 1, 0, t.w - 1);
+    int y1 = clampi(y - 1, 0, t.h - 1), y2 = clampi(y + 1, 0, t.h - 1);
+    C cx = csub(t.at((size_t)y * t.w + x1), t.at((size_t)y * t.w + x2));
+    C cy = csub(t.at((size_t)y1 * t.w + x), t.at((size_t)y2 * t.w + x));
+    return vmk(cx.r, cy.r, 0);
+}
+inline bool vnonzero(V a) { return !(a.x == 0 && a.y == 0 && a.z == 0); }  // Vector != Vector.Zero (Vector.cs:446-454)
+
+// Triangle.NormalAt with NormalTexture / BumpTexture (Triangle.cs:142-189).
+V tri_normal_mapped(const Tri& t, V p, const Tex* ntex, const Tex* btex, double bump_multiplier) {
+    double u, v, w;
+    barycentric(t, p, u, v, w);
+    V n = vadd(vadd(vmuls(t.n1, u), vmuls(t.n2, v)), vmuls(t.n3, w));
+    if (ntex) {
+        V b = vadd(vadd(vmuls(t.t1, u), vmuls(t.t2, v)), vmuls(t.t3, w));
+        V ns = tex_normal_sample(*ntex, b.x, b.y);
+        if (vnonzero(ns)) {
+            V dv1 = vsub(t.v2, t.v1), dv2 = vsub(t.v3, t.v1);
+            V dt1 = vsub(t.t2, t.t1), dt2 = vsub(t.t3, t.t1);
+            V T = vnorm(vsub(vmuls(dv1, dt2.y), vmuls(dv2, dt1.y)));
+            V B = vnorm(vsub(vmuls(dv2, dt1.x), vmuls(dv1, dt2.x)));
+            V N = vcross(T, B);
+            // Matrix(T.X, B.X, N.X, 0, ...).MulDirection(ns) (Matrix.cs:144-150): fp64 rows, then Normalize
+            double x = (double)T.x * ns.x + (double)B.x * ns.y + (double)N.x * ns.z;
+            double y = (double)T.y * ns.x + (double)B.y * ns.y + (double)N.y * ns.z;
+            double z = (double)T.z * ns.x + (double)B.z * ns.y + (double)N.z * ns.z;
+            n = vnorm(vmk(x, y, z));
+        }
+    }
+    if (btex) {
+        V b = vadd(vadd(vmuls(t.t1, u), vmuls(t.t2, v)), vmuls(t.t3, w));
+        V bump = tex_bump_sample(*btex, b.x, b.y);
+        if (vnonzero(bump)) {
+            V dv1 = vsub(t.v2, t.v1), dv2 = vsub(t.v3, t.v1);
+            V dt1 = vsub(t.t2, t.t1), dt2 = vsub(t.t3, t.t1);
+            V tangent = vnorm(vsub(vmuls(dv1, dt2.y), vmuls(dv2, dt1.y)));
+            V bitangent = vnorm(vsub(vmuls(dv2, dt1.x), vmuls(dv1, dt2.x)));
+            n = vadd(n, vmuls(tangent, (double)bump.x * bump_multiplier));
+            n = vadd(n, vmuls(bitangent, (double)bump.y * bump_multiplier));
+        }
+    }
+    return vnorm(n);
+}
+
 inline Box tri_box(const Tri& t) { return Box{vmin(vmin(t.v1, t.v2), t.v3), vmax(vmax(t.v1, t.v2), t.v3)}; }
+
+// IShape.UVector (Sphere.cs:62-69 with its p.Y-for-p.Z slip, Cube.cs:49-53, Plane.cs:52-55,
+// Triangle.cs:127-136).  Returns (u, v, 0) as the Vector the reference builds.
+V shape_uv(const Scene& s, int kind, int idx, V p) {
+    switch (kind) {
+        case K_SPHERE: {
+            V q = vsub(p, s.spheres[idx].center);
+            double u = std::atan2((double)q.z, (double)q.x);
+            double v = std::atan2((double)q.y, vlen(V{q.x, 0.f, q.y}));
+            u = 1 - (u + PI) / (2 * PI);
+            v = (v + PI / 2) / PI;
+            return vmk(u, v, 0);
+        }
+        case K_CUBE: {
+            V q = vdiv(vsub(p, s.cubes[idx].min), vsub(s.cubes[idx].max, s.cubes[idx].min));
+            return V{q.x, q.z, 0.f};
+        }
+        case K_TRI: {
+            const Tri& t = s.tris[idx];
+            double u, v, w;
+            barycentric(t, p, u, v, w);
+            V n = vadd(vadd(vadd(vzero(), vmuls(t.t1, u)), vmuls(t.t2, v)), vmuls(t.t3, w));
+            return V{n.x, n.y, 0.f};
+        }
+        default: return vzero();  // Plane.UVector, Mesh.UVector
+    }
+}
+// Material.MaterialAt (Material.cs:124-138): the colour / gloss a shading point sees.
+struct Surf { C color; double gloss; };
+Surf material_at(const Scene& s, int kind, int idx, int mat, V p) {
+    const Material& m = s.mats[mat];
+    Surf r{m.color, m.gloss};
+    if (m.tex < 0 && m.gtex < 0) return r;
+    V uv = shape_uv(s, kind, idx, p);
+    if (m.tex >= 0) r.color = tex_sample(s.texs[m.tex], uv.x, uv.y);
+    if (m.gtex >= 0) {
+        C c = tex_sample(s.texs[m.gtex], uv.x, uv.y);
+        r.gloss = (c.r + c.g + c.b) / 3;
+    }
+    return r;
+}
 
 Box shape_box(const Scene& s, ShapeRef r) {
     switch (r.kind) {
@@ -481,14 +633,20 @@ struct Tracer {
     }
 };
 
-struct HitInfo { V position, normal; Ray ray; int mat; bool inside; };
+struct HitInfo { V position, normal; Ray ray; int mat; bool inside; C color; double gloss; };
 
 V shape_normal(const Scene& s, const Hit& h, V p) {
     switch (h.kind) {
         case K_SPHERE: return vnorm(vsub(p, s.spheres[h.idx].center));  // Sphere.NormalAt :78-81
         case K_CUBE: return cube_normal(s.cubes[h.idx].min, s.cubes[h.idx].max, p);
         case K_PLANE: return s.planes[h.idx].normal;                      // Plane.NormalAt :61-64
-        default: return tri_normal(s.tris[h.idx], p);
+        default: {
+            const Tri& t = s.tris[h.idx];
+            const Material& m = s.mats[t.mat];
+            if (m.ntex < 0 && m.btex < 0) return tri_normal(t, p);
+            return tri_normal_mapped(t, p, m.ntex >= 0 ? &s.texs[m.ntex] : nullptr,
+                                     m.btex >= 0 ? &s.texs[m.btex] : nullptr, m.bump_multiplier);
+        }
     }
 }
 int shape_mat(const Scene& s, const Hit& h) {
@@ -505,6 +663,9 @@ HitInfo hit_info(const Scene& s, const Hit& h, const Ray& r) {
     info.position = ray_position(r, h.t);
     V normal = shape_normal(s, h, info.position);
     info.mat = shape_mat(s, h);
+    Surf sf = material_at(s, h.kind, h.idx, info.mat, info.position);
+    info.color = sf.color;
+    info.gloss = sf.gloss;
     info.inside = false;
     if (vdot(normal, r.d) > 0) { normal = vneg(normal); info.inside = true; }
     info.normal = normal;
@@ -563,13 +724,13 @@ struct Integrator {
         if (reflect) {
             Ray r{n.o, vreflect(n.d, in.d)};
             reflected = true;
-            return Ray{r.o, cone(r.d, m.gloss, u, v, key)};
+            return Ray{r.o, cone(r.d, info.gloss, u, v, key)};
         } else if (m.transparent) {
             Ray r{n.o, vrefract(n.d, in.d, n1, n2)};
             r.o = vadd(r.o, vmuls(r.d, 1e-4));
             reflected = true;
             p = 1 - p;
-            return Ray{r.o, cone(r.d, m.gloss, u, v, key)};
+            return Ray{r.o, cone(r.d, info.gloss, u, v, key)};
         }
         reflected = false;
         p = 1 - p;
@@ -623,9 +784,10 @@ struct Integrator {
         int mi = light.kind == K_SPHERE ? s.spheres[light.idx].mat
                : light.kind == K_CUBE ? s.cubes[light.idx].mat
                : light.kind == K_PLANE ? s.planes[light.idx].mat : s.tris[light.idx].mat;
-        const Material& m = s.mats[mi];
-        double mm = m.emittance * diffuse * coverage;
-        return cmuls(m.color, mm);
+        // Material.MaterialAt(light, point) (Sampler.cs:292): the colour at the sampled point
+        Surf sf = material_at(s, light.kind, light.idx, mi, point);
+        double mm = s.mats[mi].emittance * diffuse * coverage;
+        return cmuls(sf.color, mm);
     }
     // Sampler.sampleLights (Sampler.cs:191-210)
     C sample_lights(const Ray& n, uint64_t key) {
@@ -641,16 +803,26 @@ struct Integrator {
         return cmuls(sample_light(n, s.lights[idx], key), (double)nLights);
     }
     // DefaultSampler.sample (Sampler.cs:55-145); Russian roulette is never enabled.
+    // sampleEnvironment (Sampler.cs:177-189)
+    C sample_environment(const Ray& r) const {
+        if (s.env_tex < 0) return s.env;
+        V d = r.d;
+        double u = std::atan2((double)d.z, (double)d.x) + s.env_angle;
+        double v = std::atan2((double)d.y, vlen(V{d.x, 0.f, d.z}));
+        u = (u + PI) / (2 * PI);
+        v = (v + PI / 2) / PI;
+        return tex_sample(s.texs[s.env_tex], u, v);
+    }
     C sample(const Ray& ray, bool emission, int samples, int depth, uint64_t node) {
         if (depth > smp.mb) return BLACK;
         Hit hit = tr.intersect(ray);
-        if (!(hit.t < HIT_INF)) return s.env;  // sampleEnvironment (Sampler.cs:177-189), no texture
+        if (!(hit.t < HIT_INF)) return sample_environment(ray);
         HitInfo info = hit_info(s, hit, ray);
         const Material& material = s.mats[info.mat];
         C result{0, 0, 0};
         if (material.emittance > 0) {
             if (smp.dl && !emission) return BLACK;
-            result = cadd(result, cmuls(material.color, material.emittance * samples));
+            result = cadd(result, cmuls(info.color, material.emittance * samples));
         }
         int n = (int)std::sqrt((double)samples);
         int ma, mb;
@@ -669,14 +841,14 @@ struct Integrator {
                     if (mode == 0) p = 1;
                     if (p > 0 && reflected) {
                         C indirect = sample(newRay, reflected, 1, depth + 1, E);
-                        C tinted = cmix(indirect, cmul(material.color, indirect), material.tint);
+                        C tinted = cmix(indirect, cmul(info.color, indirect), material.tint);
                         result = cadd(result, cmuls(tinted, p));
                     }
                     if (p > 0 && !reflected) {
                         C indirect = sample(newRay, reflected, 1, depth + 1, E);
                         C direct = BLACK;
                         if (smp.dl) direct = sample_lights(info.ray, E);
-                        result = cadd(result, cmuls(cmul(material.color, cadd(direct, indirect)), p));
+                        result = cadd(result, cmuls(cmul(info.color, cadd(direct, indirect)), p));
                     }
                 }
             }
@@ -822,8 +994,15 @@ Scene* build_scene(const or_scene_desc* d) {
     for (int i = 0; i < d->num_materials; i++) {
         const or_material& m = d->materials[i];
         s->mats.push_back(Material{C{m.color[0], m.color[1], m.color[2]}, m.emittance, m.index, m.gloss, m.tint,
-                                   m.reflectivity, m.transparent != 0});
+                                   m.reflectivity, m.transparent != 0, m.texture - 1, m.normal_texture - 1,
+                                   m.bump_texture - 1, m.gloss_texture - 1, m.bump_multiplier});
     }
+    for (int i = 0; i < d->num_textures; i++) {
+        const or_texture& t = d->textures[i];
+        s->texs.push_back(Tex{t.width, t.height, std::vector<double>(t.data, t.data + 3 * (size_t)t.width * t.height)});
+    }
+    s->env_tex = d->env_texture - 1;
+    s->env_angle = d->env_texture_angle;
     for (int i = 0; i < d->num_spheres; i++) {
         V c = vload(d->sphere_center + 3 * i);
         double r = d->sphere_radius[i];
@@ -835,10 +1014,14 @@ Scene* build_scene(const or_scene_desc* d) {
         s->cubes.push_back(Cube{vload(d->cube_min + 3 * i), vload(d->cube_max + 3 * i), d->cube_material[i]});
     for (int i = 0; i < d->num_planes; i++)
         s->planes.push_back(Plane{vload(d->plane_point + 3 * i), vload(d->plane_normal + 3 * i), d->plane_material[i]});
-    for (int i = 0; i < d->num_triangles; i++)
+    for (int i = 0; i < d->num_triangles; i++) {
+        V t1 = d->tri_t1 ? vload(d->tri_t1 + 3 * i) : vzero();
+        V t2 = d->tri_t2 ? vload(d->tri_t2 + 3 * i) : vzero();
+        V t3 = d->tri_t3 ? vload(d->tri_t3 + 3 * i) : vzero();
         s->tris.push_back(Tri{vload(d->tri_v1 + 3 * i), vload(d->tri_v2 + 3 * i), vload(d->tri_v3 + 3 * i),
                               vload(d->tri_n1 + 3 * i), vload(d->tri_n2 + 3 * i), vload(d->tri_n3 + 3 * i),
-                              d->tri_material[i]});
+                              d->tri_material[i], t1, t2, t3});
+    }
     for (int i = 0; i < d->num_meshes; i++) {
         s->mesh_first.push_back(d->mesh_first[i]);
         s->mesh_count.push_back(d->mesh_count[i]);
@@ -1019,11 +1202,49 @@ void or_prim_normal(int32_t kind, const float* a, const float* b, const float* c
         case K_CUBE: n = cube_normal(vload(a), vload(b), p); break;
         case K_PLANE: n = vload(b); break;
         default: {
-            Tri t{vload(a), vload(b), vload(c), vload(n1), vload(n2), vload(n3), 0};
+            Tri t{vload(a), vload(b), vload(c), vload(n1), vload(n2), vload(n3), 0, vzero(), vzero(), vzero()};
             n = tri_normal(t, p);
         }
     }
     out_normal[0] = n.x; out_normal[1] = n.y; out_normal[2] = n.z;
+}
+
+void or_texture_sample(void* scene, int32_t texture, int32_t kind, double u, double v, double out[3]) {
+    const Scene& s = *(Scene*)scene;
+    const Tex& t = s.texs[(size_t)(texture - 1)];
+    if (kind == 0) {
+        C c = tex_sample(t, u, v);
+        out[0] = c.r; out[1] = c.g; out[2] = c.b;
+        return;
+    }
+    V r = kind == 1 ? tex_normal_sample(t, u, v) : tex_bump_sample(t, u, v);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+
+void or_shape_uv(void* scene, int32_t kind, int32_t index, const float p[3], float out_uv[3]) {
+    V r = shape_uv(*(Scene*)scene, kind, index, vload(p));
+    out_uv[0] = r.x; out_uv[1] = r.y; out_uv[2] = r.z;
+}
+
+void or_environment(void* scene, const float dir[3], double out[3]) {
+    const Scene& s = *(Scene*)scene;
+    Tracer tr(s, false);
+    Sampler sm{1, 0, false, false, 0, 0};
+    Integrator in(s, sm, tr);
+    C c = in.sample_environment(Ray{vzero(), vload(dir)});
+    out[0] = c.r; out[1] = c.g; out[2] = c.b;
+}
+
+int32_t or_hit_surface(void* scene, const float origin[3], const float dir[3], double out_color[3], double* out_gloss) {
+    const Scene& s = *(Scene*)scene;
+    Tracer tr(s, false);
+    Ray r{vload(origin), vload(dir)};
+    Hit h = tr.intersect(r);
+    if (!(h.t < HIT_INF)) return 0;
+    HitInfo info = hit_info(s, h, r);
+    out_color[0] = info.color.r; out_color[1] = info.color.g; out_color[2] = info.color.b;
+    *out_gloss = info.gloss;
+    return 1;
 }
 
 uint64_t or_camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {

@@ -7,10 +7,10 @@ per-pixel work.  There is no CPU fallback: the product path fails loudly when
 the HIP library is missing.
 """
 from .geometry import Box, Colour, Matrix, Util, Vector
-from .scene import (OBJ, Camera, Cube, DefaultSampler, LightMode, Material, Mesh, Plane, Scene, SpecularMode,
+from .scene import (OBJ, Camera, ColorTexture, Cube, DefaultSampler, LightMode, Material, Mesh, Plane, Scene, SpecularMode,
                     Sphere, Triangle)
 from .renderer import Buffer, Channel, Renderer, tiles_for_rank, write_png
 
-__all__ = ["Box", "Colour", "Matrix", "Util", "Vector", "Camera", "Cube", "DefaultSampler", "LightMode", "Material",
+__all__ = ["Box", "Colour", "Matrix", "Util", "Vector", "Camera", "ColorTexture", "Cube", "DefaultSampler", "LightMode", "Material",
            "Mesh", "OBJ", "Plane", "Scene", "SpecularMode", "Sphere", "Triangle", "Buffer", "Channel", "Renderer",
            "tiles_for_rank", "write_png"]

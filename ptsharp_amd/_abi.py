@@ -12,6 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptsharp_hip.so")
 
+ABI_VERSION = 2   # PT_ABI_VERSION
 PT_OK = 0
 PT_ERR_INVALID_ARG = -1
 PT_ERR_HIP = -2
@@ -32,10 +33,16 @@ _d = C.POINTER(C.c_double)
 _i = C.POINTER(C.c_int32)
 
 
+class pt_texture(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("data", _d)]
+
+
 class pt_material(C.Structure):
     _fields_ = [("color", C.c_double * 3), ("emittance", C.c_double), ("index", C.c_double),
                 ("gloss", C.c_double), ("tint", C.c_double), ("reflectivity", C.c_double),
-                ("transparent", C.c_int32), ("_pad", C.c_int32)]
+                ("transparent", C.c_int32), ("texture", C.c_int32), ("normal_texture", C.c_int32),
+                ("bump_texture", C.c_int32), ("gloss_texture", C.c_int32), ("_pad", C.c_int32),
+                ("bump_multiplier", C.c_double)]
 
 
 class pt_scene_desc(C.Structure):
@@ -49,6 +56,9 @@ class pt_scene_desc(C.Structure):
         ("tri_n1", _f), ("tri_n2", _f), ("tri_n3", _f), ("tri_material", _i),
         ("num_meshes", C.c_int32), ("mesh_first", _i), ("mesh_count", _i),
         ("env_color", C.c_double * 3),
+        ("num_textures", C.c_int32), ("textures", C.POINTER(pt_texture)),
+        ("tri_t1", _f), ("tri_t2", _f), ("tri_t3", _f),
+        ("env_texture", C.c_int32), ("_pad", C.c_int32), ("env_texture_angle", C.c_double),
     ]
 
 

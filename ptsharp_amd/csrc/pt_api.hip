@@ -268,6 +268,21 @@ int validate_scene(const pt_scene_desc* d) {
                                  !d->tri_material || !chk_mat(d->tri_material, d->num_triangles)))
         return fail(PT_ERR_INVALID_ARG, "bad triangle arrays");
     if (d->num_meshes > 0 && (!d->mesh_first || !d->mesh_count)) return fail(PT_ERR_INVALID_ARG, "bad mesh arrays");
+    if (d->num_textures < 0 || (d->num_textures > 0 && !d->textures)) return fail(PT_ERR_INVALID_ARG, "bad texture arrays");
+    for (int i = 0; i < d->num_textures; i++) {
+        const pt_texture& t = d->textures[i];
+        if (t.width < 2 || t.height < 2 || !t.data)   // BilinearSample reads x0 + 1 / y0 + 1 (Texture.cs:198-206)
+            return fail(PT_ERR_INVALID_ARG, "texture " + std::to_string(i) + ": needs data and width, height >= 2");
+    }
+    auto chk_tex = [&](int32_t t) { return t >= 0 && t <= d->num_textures; };
+    for (int i = 0; i < d->num_materials; i++) {
+        const pt_material& m = d->materials[i];
+        if (!chk_tex(m.texture) || !chk_tex(m.normal_texture) || !chk_tex(m.bump_texture) || !chk_tex(m.gloss_texture))
+            return fail(PT_ERR_INVALID_ARG, "material " + std::to_string(i) + ": texture reference out of range");
+    }
+    if (!chk_tex(d->env_texture)) return fail(PT_ERR_INVALID_ARG, "env_texture out of range");
+    if (d->num_triangles > 0 && ((d->tri_t1 != nullptr) != (d->tri_t2 != nullptr) || (d->tri_t1 != nullptr) != (d->tri_t3 != nullptr)))
+        return fail(PT_ERR_INVALID_ARG, "tri_t1/t2/t3 must be all set or all NULL");
     for (int i = 0; i < d->num_shapes; i++) {
         int k = d->shape_kind[i], j = d->shape_index[i];
         int lim = k == PT_SHAPE_SPHERE ? d->num_spheres : k == PT_SHAPE_CUBE ? d->num_cubes
@@ -363,7 +378,20 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         o.index = m.index;
         o.gloss = m.gloss;
         o.reflectivity = m.reflectivity;
+        o.tex = m.texture - 1; o.ntex = m.normal_texture - 1; o.btex = m.bump_texture - 1; o.gtex = m.gloss_texture - 1;
+        o.bump_multiplier = m.bump_multiplier;
     }
+    // textures: one fp64 texel array in HBM, DevTexture views into it
+    std::vector<size_t> tex_off((size_t)std::max(d->num_textures, 0));
+    size_t texels = 0;
+    for (int i = 0; i < d->num_textures; i++) {
+        tex_off[(size_t)i] = texels;
+        texels += 3 * (size_t)d->textures[i].width * (size_t)d->textures[i].height;
+    }
+    std::vector<double> tex_data(texels);
+    for (int i = 0; i < d->num_textures; i++)
+        std::memcpy(tex_data.data() + tex_off[(size_t)i], d->textures[i].data,
+                    3 * (size_t)d->textures[i].width * (size_t)d->textures[i].height * sizeof(double));
 
     // --- gather primitives in Scene.Shapes order
     std::vector<int32_t> ana_kind, ana_scene;     // analytic prims (sphere, cube)
@@ -394,6 +422,8 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     pt::BvhResult tb;
     pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb);
     std::vector<float4> tri_recs(nt * 3), tri_shade(nt * 3);
+    const bool want_uv = d->num_textures > 0 && nt > 0;   // texture coordinates only matter with textures
+    std::vector<float4> tri_uv(want_uv ? nt * 2 : 0);
     for (size_t i = 0; i < nt; i++) {
         int s = tri_src[tb.order[i]];
         pt::v3 v1 = ld3(d->tri_v1 + 3 * s), v2 = ld3(d->tri_v2 + 3 * s), v3_ = ld3(d->tri_v3 + 3 * s);
@@ -405,6 +435,14 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         tri_shade[3 * i + 0] = f4(n1[0], n1[1], n1[2], n2[0]);
         tri_shade[3 * i + 1] = f4(n2[1], n2[2], n3[0], n3[1]);
         tri_shade[3 * i + 2] = f4(n3[2], u2f((uint32_t)d->tri_material[s]), 0.f, 0.f);
+        if (want_uv) {
+            const float zero[3] = {0.f, 0.f, 0.f};
+            const float* t1 = d->tri_t1 ? d->tri_t1 + 3 * s : zero;
+            const float* t2 = d->tri_t2 ? d->tri_t2 + 3 * s : zero;
+            const float* t3 = d->tri_t3 ? d->tri_t3 + 3 * s : zero;
+            tri_uv[2 * i + 0] = f4(t1[0], t1[1], t2[0], t2[1]);
+            tri_uv[2 * i + 1] = f4(t3[0], t3[1], 0.f, 0.f);
+        }
     }
     std::vector<float4> tri_nodes;
     int32_t tri_num_nodes = 0;
@@ -503,6 +541,15 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, planes, &S.planes); if (rc) return rc;
     rc = upload(c, mats, &S.mats); if (rc) return rc;
     rc = upload(c, lights, &S.lights); if (rc) return rc;
+    rc = upload(c, tri_uv, &S.tri_uv); if (rc) return rc;
+    const double* d_tex = nullptr;
+    rc = upload(c, tex_data, &d_tex); if (rc) return rc;
+    std::vector<pt::DevTexture> texs((size_t)std::max(d->num_textures, 0));
+    for (int i = 0; i < d->num_textures; i++)
+        texs[(size_t)i] = pt::DevTexture{d_tex + tex_off[(size_t)i], d->textures[i].width, d->textures[i].height};
+    rc = upload(c, texs, &S.texs); if (rc) return rc;
+    S.env_tex = d->env_texture - 1;
+    S.env_angle = d->env_texture_angle;
     S.tri_num_nodes = tri_num_nodes;
     S.ana_num_nodes = ana_num_nodes;
     S.num_planes = (int32_t)plane_scene.size();

@@ -238,14 +238,175 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
     return true;
 }
 
+// ---------------------------------------------------------------- textures (§8f row 3)
+// Util.Modf / ColorTexture.Fract (Util.cs:108-113, Texture.cs:218-222): fractional part, sign kept.
+__device__ __forceinline__ double fract_d(double x) { return x - trunc(x); }
+
+// ColorTexture.BilinearSample (Texture.cs:188-216), fp64 over the C# texels.  The
+// reference's int conversions throw OverflowException on non-finite coordinates; such a
+// lookup is black here and in the oracle.
+__device__ inline void tex_bilinear(const DevTexture& T, double u, double v, double c[3]) {
+    if (u == 1) u -= kEps;
+    if (v == 1) v -= kEps;
+    const double w = (double)T.w - 1, h = (double)T.h - 1;
+    const double uw = u * w, vh = v * h;
+    c[0] = 0.0; c[1] = 0.0; c[2] = 0.0;
+    if (!isfinite(uw) || !isfinite(vh)) return;
+    const double X = trunc(uw), x = uw - X, Y = trunc(vh), y = vh - Y;
+    const double* r0 = T.data + 3 * ((size_t)(int)Y * (size_t)T.w + (size_t)(int)X);
+    const double* r1 = r0 + 3 * (size_t)T.w;
+    const double w00 = (1 - x) * (1 - y), w10 = x * (1 - y), w01 = (1 - x) * y, w11 = x * y;
+    for (int k = 0; k < 3; k++) {   // Black.Add(c00·w00).Add(c10·w10).Add(c01·w01).Add(c11·w11)
+        double a = 0.0;
+        a = a + r0[k] * w00;
+        a = a + r0[3 + k] * w10;
+        a = a + r1[k] * w01;
+        a = a + r1[3 + k] * w11;
+        c[k] = a;
+    }
+}
+// ITexture.Sample (Texture.cs:224-229)
+__device__ inline void tex_sample(const DevTexture& T, double u, double v, double c[3]) {
+    u = fract_d(fract_d(u) + 1);
+    v = fract_d(fract_d(v) + 1);
+    tex_bilinear(T, u, 1 - v, c);
+}
+// ITexture.NormalSample (Texture.cs:231-237)
+__device__ inline v3 tex_normal_sample(const DevTexture& T, double u, double v) {
+    double c[3];
+    tex_sample(T, u, v, c);
+    return normalize(mk(c[0] * 2 - 1, c[1] * 2 - 1, c[2] * 2 - 1));
+}
+// ITexture.BumpSample (Texture.cs:239-251); row Height (v == 0, an IndexOutOfRange in the
+// reference) is clamped, as in the oracle.
+__device__ inline v3 tex_bump_sample(const DevTexture& T, double u, double v) {
+    u = fract_d(fract_d(u) + 1);
+    v = 1 - fract_d(fract_d(v) + 1);
+    const double fx = u * T.w, fy = v * T.h;
+    if (!isfinite(fx) || !isfinite(fy)) return zero3();
+    const int x = min((int)fx, T.w - 1), y = min((int)fy, T.h - 1);
+    const int x1 = max(x - 1, 0), x2 = min(x + 1, T.w - 1), y1 = max(y - 1, 0), y2 = min(y + 1, T.h - 1);
+    const double* d = T.data;
+    const size_t W = (size_t)T.w;
+    const double cx = d[3 * ((size_t)y * W + x1)] - d[3 * ((size_t)y * W + x2)];
+    const double cy = d[3 * ((size_t)y1 * W + x)] - d[3 * ((size_t)y2 * W + x)];
+    return mk(cx, cy, 0);
+}
+__device__ __forceinline__ bool nonzero3(v3 a) { return !(a.x == 0 && a.y == 0 && a.z == 0); }
+
+__device__ __forceinline__ void tri_uvs(const DevScene& S, int idx, v3& t1, v3& t2, v3& t3) {
+    const float4 A = S.tri_uv[2 * (size_t)idx], B = S.tri_uv[2 * (size_t)idx + 1];
+    t1 = v3{A.x, A.y, 0.f}; t2 = v3{A.z, A.w, 0.f}; t3 = v3{B.x, B.y, 0.f};
+}
+
+// IShape.UVector (Sphere.cs:62-69 with its p.Y-for-p.Z slip, Cube.cs:49-53, Plane.cs:52-55,
+// Triangle.cs:127-136) of the primitive at record `idx`.
+__device__ inline v3 shape_uv(const DevScene& S, int kind, int idx, v3 p) {
+    if (kind == KIND_TRI) {
+        const float4* r = S.tri_recs + 3 * (size_t)idx;
+        const float4 a = r[0], b = r[1], c = r[2];
+        double u, v, w;
+        barycentric(v3{a.x, a.y, a.z}, v3{a.w, b.x, b.y}, v3{b.z, b.w, c.x}, p, u, v, w);
+        v3 t1, t2, t3;
+        tri_uvs(S, idx, t1, t2, t3);
+        const v3 n = add(add(add(zero3(), muls(t1, u)), muls(t2, v)), muls(t3, w));
+        return v3{n.x, n.y, 0.f};
+    }
+    if (kind == KIND_PLANE) return zero3();
+    const float4* r = S.ana_recs + 3 * (size_t)idx;
+    const float4 a = r[0], b = r[1];
+    if (kind == KIND_SPHERE) {
+        const v3 q = sub(p, v3{a.x, a.y, a.z});
+        double u = atan2((double)q.z, (double)q.x);
+        double v = atan2((double)q.y, (double)lengthf(v3{q.x, 0.f, q.y}));
+        u = 1 - (u + kPi) / (2 * kPi);
+        v = (v + kPi / 2) / kPi;
+        return mk(u, v, 0);
+    }
+    const v3 q = divv(sub(p, v3{a.x, a.y, a.z}), sub(v3{b.x, b.y, b.z}, v3{a.x, a.y, a.z}));
+    return v3{q.x, q.z, 0.f};
+}
+
+// Material.MaterialAt (Material.cs:124-138): the colour and gloss seen at p.  TEX = the
+// scene has textures: kernels are instantiated both ways, so untextured scenes run the
+// shading code without any texture path (no extra registers in the hot kernels).
+template <bool TEX>
+__device__ __forceinline__ void surface_at(const DevScene& S, const DevMaterial& m, int kind, int idx, v3 p,
+                                           float col[3], double& gloss) {
+    col[0] = m.color[0]; col[1] = m.color[1]; col[2] = m.color[2];
+    gloss = m.gloss;
+    if (!TEX || (m.tex < 0 && m.gtex < 0)) return;
+    const v3 uv = shape_uv(S, kind, idx, p);
+    double c[3];
+    if (m.tex >= 0) {
+        tex_sample(S.texs[m.tex], uv.x, uv.y, c);
+        col[0] = (float)c[0]; col[1] = (float)c[1]; col[2] = (float)c[2];
+    }
+    if (m.gtex >= 0) {
+        tex_sample(S.texs[m.gtex], uv.x, uv.y, c);
+        gloss = (c[0] + c[1] + c[2]) / 3;
+    }
+}
+
+// Triangle.NormalAt with NormalTexture / BumpTexture (Triangle.cs:142-189).
+__device__ __noinline__ v3 tri_normal_mapped(const DevScene& S, const DevMaterial& m, int idx, v3 v1, v3 e1, v3 e2,
+                                             v3 n1, v3 n2, v3 n3, v3 p) {
+    double u, v, w;
+    barycentric(v1, e1, e2, p, u, v, w);
+    v3 n = add(add(muls(n1, u), muls(n2, v)), muls(n3, w));
+    v3 t1, t2, t3;
+    tri_uvs(S, idx, t1, t2, t3);
+    const v3 dt1 = sub(t2, t1), dt2 = sub(t3, t1);   // dv1 = V2 - V1 = e1, dv2 = V3 - V1 = e2
+    if (m.ntex >= 0) {
+        const v3 b = add(add(muls(t1, u), muls(t2, v)), muls(t3, w));
+        const v3 ns = tex_normal_sample(S.texs[m.ntex], b.x, b.y);
+        if (nonzero3(ns)) {
+            const v3 T = normalize(sub(muls(e1, dt2.y), muls(e2, dt1.y)));
+            const v3 B = normalize(sub(muls(e2, dt1.x), muls(e1, dt2.x)));
+            const v3 N = cross(T, B);
+            // Matrix(T.X, B.X, N.X, 0, ...).MulDirection(ns) (Matrix.cs:144-150)
+            const double x = (double)T.x * ns.x + (double)B.x * ns.y + (double)N.x * ns.z;
+            const double y = (double)T.y * ns.x + (double)B.y * ns.y + (double)N.y * ns.z;
+            const double z = (double)T.z * ns.x + (double)B.z * ns.y + (double)N.z * ns.z;
+            n = normalize(mk(x, y, z));
+        }
+    }
+    if (m.btex >= 0) {
+        const v3 b = add(add(muls(t1, u), muls(t2, v)), muls(t3, w));
+        const v3 bump = tex_bump_sample(S.texs[m.btex], b.x, b.y);
+        if (nonzero3(bump)) {
+            const v3 tangent = normalize(sub(muls(e1, dt2.y), muls(e2, dt1.y)));
+            const v3 bitangent = normalize(sub(muls(e2, dt1.x), muls(e1, dt2.x)));
+            n = add(n, muls(tangent, (double)bump.x * m.bump_multiplier));
+            n = add(n, muls(bitangent, (double)bump.y * m.bump_multiplier));
+        }
+    }
+    return normalize(n);
+}
+
+// sampleEnvironment (Sampler.cs:177-189)
+template <bool TEX>
+__device__ __forceinline__ float3 environment(const DevScene& S, v3 d) {
+    if (!TEX || S.env_tex < 0) return make_float3(S.env[0], S.env[1], S.env[2]);
+    double u = atan2((double)d.z, (double)d.x) + S.env_angle;
+    double v = atan2((double)d.y, (double)lengthf(v3{d.x, 0.f, d.z}));
+    u = (u + kPi) / (2 * kPi);
+    v = (v + kPi / 2) / kPi;
+    double c[3];
+    tex_sample(S.texs[S.env_tex], u, v, c);
+    return make_float3((float)c[0], (float)c[1], (float)c[2]);
+}
+
 struct Shade {
     v3 pos, nrm;
     int32_t mat;
     int32_t inside;
+    float col[3];    // Material.MaterialAt colour (texture applied)
+    double gloss;    // and gloss (gloss texture applied)
 };
 
 // Hit.Info (Hit.cs:26-55): position (fp32 re-rounded), NormalAt, MaterialAt, flip.
-template <bool COUNT>
+template <bool COUNT, bool TEX>
 __device__ __forceinline__ Shade hit_info(const DevScene& S, const HitRec& h, v3 o, v3 d, Counters& ctr) {
     Shade s;
     s.pos = add(o, muls(d, h.t));
@@ -256,9 +417,12 @@ __device__ __forceinline__ Shade hit_info(const DevScene& S, const HitRec& h, v3
         const float4* q = S.tri_shade + 3 * (size_t)h.idx;
         float4 a = r[0], b = r[1], c = r[2];
         float4 x = q[0], y = q[1], z = q[2];
-        n = tri_normal(v3{a.x, a.y, a.z}, v3{a.w, b.x, b.y}, v3{b.z, b.w, c.x}, v3{x.x, x.y, x.z},
-                       v3{x.w, y.x, y.y}, v3{y.z, y.w, z.x}, s.pos);
         s.mat = (int32_t)f2u(z.y);
+        const DevMaterial& m = S.mats[s.mat];
+        const v3 v1{a.x, a.y, a.z}, e1{a.w, b.x, b.y}, e2{b.z, b.w, c.x};
+        const v3 n1{x.x, x.y, x.z}, n2{x.w, y.x, y.y}, n3{y.z, y.w, z.x};
+        if (!TEX || (m.ntex < 0 && m.btex < 0)) n = tri_normal(v1, e1, e2, n1, n2, n3, s.pos);
+        else n = tri_normal_mapped(S, m, h.idx, v1, e1, e2, n1, n2, n3, s.pos);
     } else if (h.kind == KIND_PLANE) {
         float4 a = S.planes[2 * h.idx], b = S.planes[2 * h.idx + 1];
         n = v3{b.x, b.y, b.z};
@@ -270,6 +434,7 @@ __device__ __forceinline__ Shade hit_info(const DevScene& S, const HitRec& h, v3
         else n = cube_normal(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, s.pos);           // Cube.NormalAt
         s.mat = (int32_t)f2u(c.x);
     }
+    surface_at<TEX>(S, S.mats[s.mat], h.kind, h.idx, s.pos, s.col, s.gloss);
     s.inside = 0;
     if (dot(n, d) > 0) { n = neg(n); s.inside = 1; }
     s.nrm = n;
@@ -320,11 +485,11 @@ __device__ __forceinline__ void bounce_dir(const DevMaterial& m, const Shade& sh
                                            double n1, double n2, uint64_t key, v3& no, v3& nd) {
     if (refl) {
         no = sh.pos;
-        nd = cone(reflect(sh.nrm, indir), m.gloss, u, v, key);
+        nd = cone(reflect(sh.nrm, indir), sh.gloss, u, v, key);
     } else if (m.transparent) {
         v3 rd = refract(sh.nrm, indir, n1, n2);
         no = add(sh.pos, muls(rd, 1e-4));
-        nd = cone(rd, m.gloss, u, v, key);
+        nd = cone(rd, sh.gloss, u, v, key);
     } else {
         // Ray.WeightedBounce (Ray.cs:28-35) around the normal
         double radius = sqrt(u);
@@ -342,6 +507,7 @@ __device__ __forceinline__ void bounce_dir(const DevMaterial& m, const Shade& sh
 // direction and the colour the light contributes if it is the nearest hit
 // (coverage depends only on the light centre/radius, so it is computed here).
 // Returns false when diffuse <= 0 (no shadow ray is cast).
+template <bool TEX>
 __device__ __forceinline__ bool light_setup(const DevScene& S, const DevSampler& smp, const DevLight& L, v3 o, v3 n,
                                             uint64_t key, v3& dir, float3& contrib) {
     v3 center{L.center[0], L.center[1], L.center[2]};
@@ -372,9 +538,13 @@ __device__ __forceinline__ bool light_setup(const DevScene& S, const DevSampler&
     double coverage = (s * s) / (1 - s * s);
     if (hyp < radius) coverage = 1;
     coverage = net_min(coverage, 1);
+    // Material.MaterialAt(light, point) (Sampler.cs:292): a textured light's colour at the sampled point
     const DevMaterial& m = S.mats[L.mat];
+    float col[3] = {m.color[0], m.color[1], m.color[2]};
+    double gl;
+    if (!L.phantom) surface_at<TEX>(S, m, L.kind, L.index, point, col, gl);
     float mm = (float)((double)m.emittance * diffuse * coverage);
-    contrib = make_float3(m.color[0] * mm, m.color[1] * mm, m.color[2] * mm);
+    contrib = make_float3(col[0] * mm, col[1] * mm, col[2] * mm);
     return true;
 }
 

@@ -206,8 +206,8 @@ PT_HD v3 cube_normal(v3 mn, v3 mx, v3 p) {
     if (fabs((double)p.z - (double)mx.z) < kEps) return mk(0, 0, 1);
     return mk(0, 1, 0);
 }
-// Triangle.NormalAt via Barycentric (Triangle.cs:142-189, 208-223).
-PT_HD v3 tri_normal(v3 v1, v3 e1, v3 e2, v3 n1, v3 n2, v3 n3, v3 p) {
+// Triangle.Barycentric (Triangle.cs:208-223) with e1 = V2-V1, e2 = V3-V1.
+PT_HD void barycentric(v3 v1, v3 e1, v3 e2, v3 p, double& bu, double& bv, double& bw) {
     v3 w2 = sub(p, v1);
     double d00 = dot(e1, e1);
     double d01 = dot(e1, e2);
@@ -215,9 +215,14 @@ PT_HD v3 tri_normal(v3 v1, v3 e1, v3 e2, v3 n1, v3 n2, v3 n3, v3 p) {
     double d20 = dot(w2, e1);
     double d21 = dot(w2, e2);
     double den = d00 * d11 - d01 * d01;
-    double bv = (d11 * d20 - d01 * d21) / den;
-    double bw = (d00 * d21 - d01 * d20) / den;
-    double bu = 1 - bv - bw;
+    bv = (d11 * d20 - d01 * d21) / den;
+    bw = (d00 * d21 - d01 * d20) / den;
+    bu = 1 - bv - bw;
+}
+// Triangle.NormalAt without maps (Triangle.cs:142-145, 186-188).
+PT_HD v3 tri_normal(v3 v1, v3 e1, v3 e2, v3 n1, v3 n2, v3 n3, v3 p) {
+    double bu, bv, bw;
+    barycentric(v1, e1, e2, p, bu, bv, bw);
     v3 n = add(add(muls(n1, bu), muls(n2, bv)), muls(n3, bw));
     return normalize(n);
 }

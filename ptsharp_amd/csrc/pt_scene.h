@@ -23,6 +23,15 @@ struct DevMaterial {
     double index;
     double gloss;
     double reflectivity;
+    int32_t tex, ntex, btex, gtex;   // Texture / NormalTexture / BumpTexture / GlossTexture (-1 = null)
+    double bump_multiplier;
+};
+
+// ColorTexture (Texture.cs:96-252): fp64 Colour texels [h][w][3], exactly the C# Data,
+// so bilinear weights, gloss and normal-map decisions reproduce the reference's fp64 sums.
+struct DevTexture {
+    const double* data;
+    int32_t w, h;
 };
 
 // Scene.Lights entry (Scene.cs:33-37) with the centre/radius sampleLight derives
@@ -54,6 +63,11 @@ struct DevScene {
     const DevLight* lights;
     int32_t num_lights;
     float env[3];
+    // textures (§8f row 3)
+    const DevTexture* texs;
+    const float4* tri_uv;      // 2 float4 per triangle: {t1.xy, t2.xy} {t3.xy, -, -}; null without textured triangles
+    int32_t env_tex;           // Scene.Texture (-1 = null)
+    double env_angle;          // Scene.TextureAngle
 };
 
 struct DevCamera {

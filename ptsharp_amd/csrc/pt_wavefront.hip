@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
 // word saturates near 88 per µs on MI355X, MI355X_MICROARCH.md "dequeue").  Light
 // sampling up to the shadow query runs here too, so k_wf_shadow is a lean
 // traversal kernel (ray + stack state only).
-template <bool COUNT>
+template <bool COUNT, bool TEX>
 __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
     if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + 2 * kParts + threadIdx.x] = 0u;  // k_wf_shadow's
@@ -275,12 +275,13 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
         int mat = 0, nn = 1, nm = 1, nch = 0;
         float t2[3] = {0.f, 0.f, 0.f};
         double pv = 0.0, n1 = 1.0, n2 = 1.0;
-        if (alive && !(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67)
-            acc_add(Q.acc, pixel, thr[0] * S.env[0], thr[1] * S.env[1], thr[2] * S.env[2]);
+        if (alive && !(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67, 177-189)
+            const float3 env = environment<TEX>(S, d);
+            acc_add(Q.acc, pixel, thr[0] * env.x, thr[1] * env.y, thr[2] * env.z);
             alive = false;
         }
         if (alive) {
-            sh = hit_info<COUNT>(S, h, o, d, ctr);
+            sh = hit_info<COUNT, TEX>(S, h, o, d, ctr);
             mat = sh.mat;
             const DevMaterial& m = S.mats[mat];
             const int samples = depth == 0 ? smp.fh : 1;
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
                     alive = false;  // Sampler.cs:75-78
                 } else {
                     float e = (float)((double)m.emittance * samples) * inv_n2;
-                    acc_add(Q.acc, pixel, thr[0] * m.color[0] * e, thr[1] * m.color[1] * e, thr[2] * m.color[2] * e);
+                    acc_add(Q.acc, pixel, thr[0] * sh.col[0] * e, thr[1] * sh.col[1] * e, thr[2] * sh.col[2] * e);
                 }
             }
             nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
@@ -325,9 +326,9 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
             const float fp = mode == 0 ? 1.0f : (float)(refl ? pv : 1 - pv);
             float w[3];
             if (reflected) {
-                for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * m.color[k]);
+                for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * sh.col[k]);
             } else {
-                for (int k = 0; k < 3; k++) w[k] = fp * m.color[k];
+                for (int k = 0; k < 3; k++) w[k] = fp * sh.col[k];
                 if (nee_on) {
                     // diffuse child: sampleLights from the normal ray (Sampler.cs:191-296) up to the
                     // shadow query — light choice, soft-shadow point, coverage — here, so the
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
                         const int li = first + (int)j;
                         v3 ldir;
                         float3 lc;
-                        const bool cast = light_setup(S, smp, S.lights[li], sh.pos, sh.nrm,
+                        const bool cast = light_setup<TEX>(S, smp, S.lights[li], sh.pos, sh.nrm,
                                                       all_lights ? light_key(E, (uint32_t)li) : E, ldir, lc);
                         if (nj < Q.spcap) {
                             const uint32_t at = G.g * Q.spcap + nj;
@@ -526,8 +527,11 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         end_k(1);
         const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
         begin_k(2);
-        if (count) hipLaunchKernelGGL(k_wf_shade<true>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
-        else hipLaunchKernelGGL(k_wf_shade<false>, dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        const bool tex = S.texs != nullptr;
+        if (count && tex) hipLaunchKernelGGL((k_wf_shade<true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        else if (count) hipLaunchKernelGGL((k_wf_shade<true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        else if (tex) hipLaunchKernelGGL((k_wf_shade<false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        else hipLaunchKernelGGL((k_wf_shade<false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         end_k(2);
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
         const unsigned hg = grid_for(children * plan.lights_per_child, kTB, plan.shadow_blocks);
@@ -609,7 +613,7 @@ hipError_t wavefront_grids(WfPlan& plan) {
     };
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace<false>, kTB, 0);
     if (e == hipSuccess) plan.trace_blocks = resident(nb, kWfMaxBlocks);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shade<false>, 256, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shade<false, false>, 256, 0);
     if (e == hipSuccess) plan.shade_blocks = resident(nb, 1u << 20);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false>, kTB, 0);
     if (e == hipSuccess) plan.shadow_blocks = resident(nb, kWfMaxBlocks);

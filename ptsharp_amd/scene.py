@@ -1,7 +1,8 @@
 """Host-side mirror of PTSharp's plugin surface for the render path: Material,
-the IShape kinds the GPU path covers (Sphere, Cube, Plane, Triangle, Mesh),
-Scene, Camera and DefaultSampler (PTSharpCore/Material.cs, Sphere.cs, Cube.cs,
-Plane.cs, Triangle.cs, Mesh.cs, Scene.cs, Camera.cs, Sampler.cs).
+ColorTexture, the IShape kinds the GPU path covers (Sphere, Cube, Plane,
+Triangle, Mesh), Scene, Camera and DefaultSampler (PTSharpCore/Material.cs,
+Texture.cs, Sphere.cs, Cube.cs, Plane.cs, Triangle.cs, Mesh.cs, Scene.cs,
+Camera.cs, Sampler.cs).
 
 `Scene.flatten()` produces the caller-owned arrays of pt_scene_desc
 (include/ptsharp_hip.h) — the same flattening the C# HipRenderer performs with
@@ -11,6 +12,8 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import struct
+import zlib
 from dataclasses import dataclass, field, replace
 from enum import IntEnum
 
@@ -31,9 +34,104 @@ class SpecularMode(IntEnum):       # SpecularMode.cs
     SpecularModeAll = 2
 
 
+def _read_png_rgb8(path: str) -> np.ndarray:
+    """Minimal PNG decoder (8-bit grey / grey+alpha / RGB / RGBA / palette, not
+    interlaced) standing in for SkiaSharp's decode in Util.LoadImage (Util.cs:57-70).
+    Returns [h][w][3] uint8; alpha is dropped (NewTexture reads Red/Green/Blue only)."""
+    data = open(path, "rb").read()
+    if data[:8] != b"\x89PNG\r\n\x1a\n":
+        raise ValueError(f"{path}: not a PNG file")
+    pos, idat, plte = 8, [], None
+    w = h = depth = ctype = interlace = None
+    while pos < len(data):
+        (n,), tag = struct.unpack(">I", data[pos:pos + 4]), data[pos + 4:pos + 8]
+        body = data[pos + 8:pos + 8 + n]
+        pos += 12 + n
+        if tag == b"IHDR":
+            w, h, depth, ctype, _, _, interlace = struct.unpack(">IIBBBBB", body)
+        elif tag == b"PLTE":
+            plte = np.frombuffer(body, np.uint8).reshape(-1, 3)
+        elif tag == b"IDAT":
+            idat.append(body)
+        elif tag == b"IEND":
+            break
+    if depth != 8 or interlace != 0 or ctype not in (0, 2, 3, 4, 6):
+        raise ValueError(f"{path}: only 8-bit non-interlaced PNG is supported")
+    bpp = {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}[ctype]
+    raw = np.frombuffer(zlib.decompress(b"".join(idat)), np.uint8).reshape(h, 1 + w * bpp)
+    out = np.zeros((h, w * bpp), np.int32)
+    prev = np.zeros(w * bpp, np.int32)
+    for y in range(h):
+        f, line = raw[y, 0], raw[y, 1:].astype(np.int32)
+        if f == 0:
+            cur = line
+        elif f == 2:
+            cur = (line + prev) & 255
+        else:
+            cur = line.copy()
+            for i in range(w * bpp):
+                a = cur[i - bpp] if i >= bpp else 0
+                b = prev[i]
+                if f == 1:
+                    cur[i] = (cur[i] + a) & 255
+                elif f == 3:
+                    cur[i] = (cur[i] + ((a + b) >> 1)) & 255
+                else:
+                    c = prev[i - bpp] if i >= bpp else 0
+                    pa, pb, pc = abs(b - c), abs(a - c), abs(a + b - 2 * c)
+                    cur[i] = (cur[i] + (a if pa <= pb and pa <= pc else b if pb <= pc else c)) & 255
+        out[y], prev = cur, cur
+    px = out.astype(np.uint8).reshape(h, w, bpp)
+    if ctype == 3:
+        return plte[px[:, :, 0]]
+    if ctype in (0, 4):
+        return np.repeat(px[:, :, :1], 3, axis=2)
+    return px[:, :, :3].copy()
+
+
+class ColorTexture:
+    """PTSharpCore.ColorTexture (Texture.cs:96-252): Width x Height fp64 Colour texels,
+    row-major (Data[y*Width + x]).  Sampling runs on the GPU (pt_device.h); this host
+    object holds the data the C-ABI uploads (pt_texture)."""
+
+    _cache: dict = {}   # ColorTexture.textures (Texture.cs:102)
+
+    def __init__(self, width: int, height: int, data):
+        self.Width, self.Height = int(width), int(height)
+        self.Data = np.ascontiguousarray(np.asarray(data, np.float64).reshape(self.Height * self.Width, 3))
+
+    @staticmethod
+    def NewTexture(rgb8) -> "ColorTexture":
+        """ColorTexture.NewTexture (Texture.cs:150-166): Colour(c / 255).Pow(2.2F)."""
+        a = np.asarray(rgb8)
+        h, w = a.shape[:2]
+        gamma = float(np.float32(2.2))   # Pow(2.2F): the float literal widened to double
+        return ColorTexture(w, h, (a[:, :, :3].astype(np.float64) / 255) ** gamma)
+
+    @staticmethod
+    def LoadTexture(path: str) -> "ColorTexture":
+        """ColorTexture.LoadTexture (Texture.cs:134-148) for 8-bit PNG files."""
+        return ColorTexture.NewTexture(_read_png_rgb8(path))
+
+    @staticmethod
+    def GetTexture(path: str) -> "ColorTexture":
+        """ColorTexture.GetTexture (Texture.cs:118-132): cached by path."""
+        if path not in ColorTexture._cache:
+            ColorTexture._cache[path] = ColorTexture.LoadTexture(path)
+        return ColorTexture._cache[path]
+
+    def Pow(self, a: float) -> "ColorTexture":   # ITexture.Pow (Texture.cs:170-177), in place
+        self.Data = self.Data ** float(a)
+        return self
+
+    def MulScalar(self, a: float) -> "ColorTexture":   # ITexture.MulScalar (Texture.cs:179-186), in place
+        self.Data = self.Data * float(a)
+        return self
+
+
 @dataclass(frozen=True)
 class Material:
-    """PTSharpCore.Material (Material.cs:8-62); texture maps are not on the GPU path."""
+    """PTSharpCore.Material (Material.cs:8-62), texture maps included (§8f row 3)."""
     Color: Colour = field(default_factory=lambda: Colour(0, 0, 0))
     BumpMultiplier: float = 0.0
     Emittance: float = 0.0
@@ -43,10 +141,14 @@ class Material:
     Reflectivity: float = 0.0
     Transparent: bool = False
     Texture: object = None
+    NormalTexture: object = None
+    BumpTexture: object = None
+    GlossTexture: object = None
 
     def key(self):
         return (self.Color.r, self.Color.g, self.Color.b, self.Emittance, self.Index, self.Gloss, self.Tint,
-                self.Reflectivity, bool(self.Transparent))
+                self.Reflectivity, bool(self.Transparent), self.BumpMultiplier, id(self.Texture),
+                id(self.NormalTexture), id(self.BumpTexture), id(self.GlossTexture))
 
     # factories (Material.cs:64-97)
     @staticmethod
@@ -141,16 +243,20 @@ class Triangle:
     is boxed, so as a light it never passes Sampler's identity test."""
 
     def __init__(self, v1: Vector, v2: Vector, v3: Vector, n1: Vector = None, n2: Vector = None, n3: Vector = None,
-                 material: Material = DEFAULT_MATERIAL):
+                 material: Material = DEFAULT_MATERIAL, t1: Vector = None, t2: Vector = None, t3: Vector = None):
         self.V1, self.V2, self.V3 = v1, v2, v3
         self.N1 = n1 if n1 is not None else Vector()
         self.N2 = n2 if n2 is not None else Vector()
         self.N3 = n3 if n3 is not None else Vector()
+        self.T1 = t1 if t1 is not None else Vector()
+        self.T2 = t2 if t2 is not None else Vector()
+        self.T3 = t3 if t3 is not None else Vector()
         self.Material = material
 
     @staticmethod
     def NewTriangle(v1, v2, v3, t1=None, t2=None, t3=None, material: Material = DEFAULT_MATERIAL) -> "Triangle":
-        t = Triangle(v1, v2, v3, material=material)
+        """Triangle.NewTriangle (Triangle.cs:43-55): vertices, texture coordinates, FixNormals."""
+        t = Triangle(v1, v2, v3, material=material, t1=t1, t2=t2, t3=t3)
         t.FixNormals()
         return t
 
@@ -192,10 +298,12 @@ class Mesh:
     """PTSharpCore.Mesh (Mesh.cs): a triangle container held as [n,3] float32 arrays
     plus a per-triangle material index into `materials`."""
 
-    def __init__(self, v1, v2, v3, n1, n2, n3, mat_index=None, materials=None):
+    def __init__(self, v1, v2, v3, n1, n2, n3, mat_index=None, materials=None, t1=None, t2=None, t3=None):
         self.v1, self.v2, self.v3 = (np.ascontiguousarray(a, dtype=np.float32) for a in (v1, v2, v3))
         self.n1, self.n2, self.n3 = (np.ascontiguousarray(a, dtype=np.float32) for a in (n1, n2, n3))
         n = len(self.v1)
+        z = lambda t: np.zeros((n, 3), np.float32) if t is None else np.ascontiguousarray(t, dtype=np.float32)
+        self.t1, self.t2, self.t3 = z(t1), z(t2), z(t3)   # Triangle.T1..T3
         self.mat_index = np.zeros(n, np.int32) if mat_index is None else np.asarray(mat_index, np.int32)
         self.materials = list(materials) if materials else [DEFAULT_MATERIAL]
 
@@ -207,14 +315,15 @@ class Mesh:
                 mats.append(t.Material)
             idx.append(mats.index(t.Material))
         arr = lambda name: np.array([getattr(t, name).f32() for t in triangles], dtype=np.float32).reshape(-1, 3)
-        return Mesh(arr("V1"), arr("V2"), arr("V3"), arr("N1"), arr("N2"), arr("N3"), idx, mats)
+        return Mesh(arr("V1"), arr("V2"), arr("V3"), arr("N1"), arr("N2"), arr("N3"), idx, mats, arr("T1"), arr("T2"),
+                    arr("T3"))
 
     def __len__(self):
         return len(self.v1)
 
     def copy(self) -> "Mesh":
         return Mesh(self.v1.copy(), self.v2.copy(), self.v3.copy(), self.n1.copy(), self.n2.copy(), self.n3.copy(),
-                    self.mat_index.copy(), list(self.materials))
+                    self.mat_index.copy(), list(self.materials), self.t1.copy(), self.t2.copy(), self.t3.copy())
 
     def MaterialAt(self, p=None) -> Material:
         return DEFAULT_MATERIAL
@@ -280,8 +389,8 @@ class OBJ:
         try:
             n = md.num_triangles
             arr = lambda p: np.ctypeslib.as_array(p, shape=(n, 3)).copy() if n else np.zeros((0, 3), np.float32)
-            m = Mesh(arr(md.v1), arr(md.v2), arr(md.v3), arr(md.n1), arr(md.n2), arr(md.n3))
-            m.t1, m.t2, m.t3 = arr(md.t1), arr(md.t2), arr(md.t3)
+            m = Mesh(arr(md.v1), arr(md.v2), arr(md.v3), arr(md.n1), arr(md.n2), arr(md.n3),
+                     t1=arr(md.t1), t2=arr(md.t2), t3=arr(md.t3))
         finally:
             lib.pt_mesh_free(C.byref(md))
         if parent is not None:
@@ -297,6 +406,8 @@ class Scene:
         self.Shapes: list = []
         self.Lights: list = []
         self.Color = Colour()
+        self.Texture = None        # Scene.Texture: environment map (Scene.cs:12, Sampler.cs:177-189)
+        self.TextureAngle = 0.0    # Scene.TextureAngle
         self._flat = None
 
     def Add(self, shape) -> None:
@@ -322,6 +433,17 @@ class FlatScene:
 
     def __init__(self, scene: Scene):
         mats, mat_ids = [], {}
+        texs, tex_ids = [], {}
+
+        def tid(t) -> int:   # 1-based texture slot, 0 = null
+            if t is None:
+                return 0
+            if not isinstance(t, ColorTexture):
+                raise _abi.PTError(_abi.PT_ERR_UNSUPPORTED, "Scene.flatten", f"{type(t).__name__} is not on the GPU path")
+            if id(t) not in tex_ids:
+                texs.append(t)
+                tex_ids[id(t)] = len(texs)
+            return tex_ids[id(t)]
 
         def mid(m: Material) -> int:
             k = m.key()
@@ -334,7 +456,7 @@ class FlatScene:
         sph_c, sph_r, sph_m = [], [], []
         cub_a, cub_b, cub_m = [], [], []
         pl_p, pl_n, pl_m = [], [], []
-        tri_parts = []  # list of (v1,v2,v3,n1,n2,n3,mat)
+        tri_parts = []  # list of (v1,v2,v3,n1,n2,n3,mat,t1,t2,t3)
         ntri = 0
         mesh_first, mesh_count = [], []
         for s in scene.Shapes:
@@ -351,12 +473,13 @@ class FlatScene:
                 kinds.append(_abi.SHAPE_TRIANGLE); idxs.append(ntri)
                 tri_parts.append(tuple(np.array([getattr(s, a).f32()], np.float32)
                                        for a in ("V1", "V2", "V3", "N1", "N2", "N3"))
-                                 + (np.array([mid(s.Material)], np.int32),))
+                                 + (np.array([mid(s.Material)], np.int32),)
+                                 + tuple(np.array([getattr(s, a).f32()], np.float32) for a in ("T1", "T2", "T3")))
                 ntri += 1
             elif isinstance(s, Mesh):
                 kinds.append(_abi.SHAPE_MESH); idxs.append(len(mesh_first))
                 remap = np.array([mid(m) for m in s.materials], np.int32)
-                tri_parts.append((s.v1, s.v2, s.v3, s.n1, s.n2, s.n3, remap[s.mat_index]))
+                tri_parts.append((s.v1, s.v2, s.v3, s.n1, s.n2, s.n3, remap[s.mat_index], s.t1, s.t2, s.t3))
                 mesh_first.append(ntri); mesh_count.append(len(s))
                 ntri += len(s)
             else:
@@ -367,8 +490,18 @@ class FlatScene:
         self.materials = (_abi.pt_material * len(mats))()
         for i, m in enumerate(mats):
             self.materials[i] = _abi.pt_material((C.c_double * 3)(m.Color.r, m.Color.g, m.Color.b), m.Emittance,
-                                                 m.Index, m.Gloss, m.Tint, m.Reflectivity, int(bool(m.Transparent)), 0)
+                                                 m.Index, m.Gloss, m.Tint, m.Reflectivity, int(bool(m.Transparent)),
+                                                 tid(m.Texture), tid(m.NormalTexture), tid(m.BumpTexture),
+                                                 tid(m.GlossTexture), 0, m.BumpMultiplier)
         self.material_list = mats
+        self.env_texture = tid(scene.Texture)
+        self.env_texture_angle = float(scene.TextureAngle)
+        self.texture_list = texs
+        self.textures = (_abi.pt_texture * max(1, len(texs)))()
+        for i, t in enumerate(texs):
+            if t.Width < 2 or t.Height < 2:
+                raise _abi.PTError(_abi.PT_ERR_INVALID_ARG, "Scene.flatten", "textures must be at least 2x2")
+            self.textures[i] = _abi.pt_texture(t.Width, t.Height, t.Data.ctypes.data_as(C.POINTER(C.c_double)))
         f3 = lambda L: np.ascontiguousarray(np.array(L, np.float32).reshape(-1, 3))
         i32 = lambda L: np.ascontiguousarray(np.array(L, np.int32).reshape(-1))
         self.shape_kind, self.shape_index = i32(kinds), i32(idxs)
@@ -376,11 +509,12 @@ class FlatScene:
         self.cube_min, self.cube_max, self.cube_material = f3(cub_a), f3(cub_b), i32(cub_m)
         self.plane_point, self.plane_normal, self.plane_material = f3(pl_p), f3(pl_n), i32(pl_m)
         if tri_parts:
-            cat = [np.ascontiguousarray(np.concatenate([p[k] for p in tri_parts])) for k in range(7)]
+            cat = [np.ascontiguousarray(np.concatenate([p[k] for p in tri_parts])) for k in range(10)]
         else:
-            cat = [np.zeros((0, 3), np.float32)] * 6 + [np.zeros(0, np.int32)]
+            cat = [np.zeros((0, 3), np.float32)] * 6 + [np.zeros(0, np.int32)] + [np.zeros((0, 3), np.float32)] * 3
         (self.tri_v1, self.tri_v2, self.tri_v3, self.tri_n1, self.tri_n2, self.tri_n3) = cat[:6]
         self.tri_material = cat[6].astype(np.int32)
+        self.tri_t1, self.tri_t2, self.tri_t3 = (np.ascontiguousarray(a, np.float32) for a in cat[7:10])
         self.mesh_first, self.mesh_count = i32(mesh_first), i32(mesh_count)
         self.env = scene.Color.tuple()
         self.desc = self._make_desc(_abi.pt_scene_desc)
@@ -398,7 +532,10 @@ class FlatScene:
                    len(self.tri_material), P(self.tri_v1, fl), P(self.tri_v2, fl), P(self.tri_v3, fl),
                    P(self.tri_n1, fl), P(self.tri_n2, fl), P(self.tri_n3, fl), P(self.tri_material, it),
                    len(self.mesh_first), P(self.mesh_first, it), P(self.mesh_count, it),
-                   (C.c_double * 3)(*self.env))
+                   (C.c_double * 3)(*self.env),
+                   len(self.texture_list), C.cast(self.textures, C.POINTER(_abi.pt_texture)),
+                   P(self.tri_t1, fl), P(self.tri_t2, fl), P(self.tri_t3, fl),
+                   self.env_texture, 0, self.env_texture_angle)
 
     @property
     def num_triangles(self) -> int:

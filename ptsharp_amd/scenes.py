@@ -9,6 +9,9 @@ as PTSharpCore/Example.cs builds them.  No model assets ship with the reference
   materialspheres  Example.materialspheres (Example.cs:1204-1227)
   simplesphere     Example.simplesphere (Example.cs:1670-1697)
   example1         Example.example1 (Example.cs:341-359), no adaptive/firefly passes
+  textured         §8f row 3: colour / gloss / normal / bump maps, a textured light and an
+                   environment map with TextureAngle, on seeded synthetic textures (no
+                   texture assets ship with the reference either)
 """
 from __future__ import annotations
 
@@ -17,7 +20,8 @@ import math
 import numpy as np
 
 from .geometry import Box, Colour, Util, Vector
-from .scene import Camera, Cube, DefaultSampler, Material, Mesh, Plane, Scene, SpecularMode, Sphere
+from .scene import (Camera, ColorTexture, Cube, DefaultSampler, Material, Mesh, Plane, Scene, SpecularMode, Sphere,
+                    Triangle)
 
 F = lambda x: float(np.float32(x))  # C# float literal (e.g. 0.75F)
 
@@ -118,7 +122,10 @@ def blob_mesh(n_target: int, seed: int = 1234, amplitude: float = 0.05) -> Mesh:
     tris.append(np.stack([np.full(ns, south), ring(nr - 2, j), ring(nr - 2, j + 1)], axis=1))
     t = np.concatenate(tris)
     z = np.zeros((len(t), 3), np.float32)
-    m = Mesh(verts[t[:, 0]], verts[t[:, 1]], verts[t[:, 2]], z, z, z)
+    # texture coordinates: the sphere parametrisation (u = φ/2π, v = θ/π), poles at the ring's u
+    uv = np.stack([ph.reshape(-1) / (2 * np.pi), th.reshape(-1) / np.pi, np.zeros(th.size)], axis=-1)
+    uv = np.concatenate([uv, [[0.5, 0, 0], [0.5, 1, 0]]]).astype(np.float32)
+    m = Mesh(verts[t[:, 0]], verts[t[:, 1]], verts[t[:, 2]], z, z, z, t1=uv[t[:, 0]], t2=uv[t[:, 1]], t3=uv[t[:, 2]])
     from .scene import fix_normals_arrays
     m.n1, m.n2, m.n3 = fix_normals_arrays(m.v1, m.v2, m.v3, m.n1, m.n2, m.n3)
     return m
@@ -165,6 +172,53 @@ def emitter(fh: int = 16):
     return scene, camera, sampler
 
 
+def seeded_texture(w: int, h: int, seed: int, kind: str = "color") -> ColorTexture:
+    """ColorTexture.NewTexture over seeded 8-bit pixels: 'color' uniform noise, 'normal' a
+    tangent-space normal map around (128, 128, 255), 'bump' smooth grey noise."""
+    rng = np.random.default_rng(seed)
+    if kind == "normal":
+        px = np.stack([rng.integers(88, 168, (h, w)), rng.integers(88, 168, (h, w)), rng.integers(200, 256, (h, w))], -1)
+    elif kind == "bump":
+        g = rng.integers(0, 256, (h, w))
+        g = (g + np.roll(g, 1, 0) + np.roll(g, 1, 1) + np.roll(g, (1, 1), (0, 1))) // 4
+        px = np.repeat(g[:, :, None], 3, axis=2)
+    else:
+        px = rng.integers(0, 256, (h, w, 3))
+    return ColorTexture.NewTexture(px.astype(np.uint8))
+
+
+def textured(mesh_tris: int = 2000):
+    """§8f row 3 on one scene: Material.Texture on a cube, spheres, a light sphere and a mesh;
+    GlossTexture on a glossy sphere; NormalTexture + BumpTexture on the mesh (Triangle.NormalAt);
+    Scene.Texture (environment map) with a TextureAngle; a directly added textured Triangle."""
+    scene = Scene()
+    scene.Texture = seeded_texture(64, 32, 11)
+    scene.TextureAngle = Util.Radians(30)
+    floor = Material.GlossyMaterial(Colour.White, F(1.2), Util.Radians(20)).with_(Texture=seeded_texture(32, 32, 12))
+    scene.Add(Cube.NewCube(Vector(-12, -1, -12), Vector(12, 0, 12), floor))
+    scene.Add(Sphere.NewSphere(Vector(-1.6, 0.7, 0.4), 0.7,
+                               Material.DiffuseMaterial(Colour.White).with_(Texture=seeded_texture(24, 12, 13))))
+    glossy = Material.GlossyMaterial(Colour.HexColor(0x334D5C), 1.5, Util.Radians(10))
+    scene.Add(Sphere.NewSphere(Vector(1.6, 0.6, 0.6), 0.6, glossy.with_(GlossTexture=seeded_texture(16, 8, 14))))
+    light = Material.LightMaterial(Colour.White, 12).with_(Texture=seeded_texture(8, 8, 15))
+    scene.Add(Sphere.NewSphere(Vector(0, 4.5, 1), 0.8, light))
+    mesh = blob_mesh(mesh_tris, seed=16, amplitude=0.1)
+    mat = Material.GlossyMaterial(Colour.White, 1.4, Util.Radians(15)).with_(
+        Texture=seeded_texture(32, 16, 17), NormalTexture=seeded_texture(32, 16, 18, "normal"),
+        BumpTexture=seeded_texture(32, 16, 19, "bump"), BumpMultiplier=0.5)
+    mesh.SetMaterial(mat)
+    mesh.SmoothNormals()
+    mesh.FitInside(Box(Vector(-0.8, 0, -0.8), Vector(0.8, 1.6, 0.8)), Vector(F(0.5), 0, F(0.5)))
+    scene.Add(mesh)
+    scene.Add(Triangle.NewTriangle(Vector(-3, 0.01, -2), Vector(3, 0.01, -2), Vector(0, 2.5, -2.5),
+                                   Vector(0, 0, 0), Vector(1, 0, 0), Vector(0.5, 1, 0),
+                                   Material.DiffuseMaterial(Colour.White).with_(Texture=seeded_texture(16, 16, 20))))
+    camera = Camera.LookAt(Vector(0, 2.2, 5), Vector(0, 0.8, 0), Vector(0, 1, 0), 45)
+    sampler = DefaultSampler.NewSampler(4, 4)
+    sampler.SetSpecularMode(SpecularMode.SpecularModeFirst)
+    return scene, camera, sampler
+
+
 SCENES = {
     "gopher3": gopher3,
     "materialspheres": materialspheres,
@@ -174,4 +228,5 @@ SCENES = {
     "mesh1m": lambda: bunny_frame(1_000_000),
     "furnace": furnace,
     "emitter": emitter,
+    "textured": textured,
 }

@@ -54,6 +54,11 @@ def lib() -> C.CDLL:
         L.or_prim_intersect.restype = C.c_double
         L.or_prim_intersect.argtypes = [C.c_int32, f3, f3, f3, C.c_double, f3, f3]
         L.or_prim_normal.argtypes = [C.c_int32, f3, f3, f3, f3, f3, f3, f3, f3]
+        L.or_texture_sample.argtypes = [vp, C.c_int32, C.c_int32, C.c_double, C.c_double, dp]
+        L.or_shape_uv.argtypes = [vp, C.c_int32, C.c_int32, f3, f3]
+        L.or_environment.argtypes = [vp, f3, dp]
+        L.or_hit_surface.restype = C.c_int32
+        L.or_hit_surface.argtypes = [vp, f3, f3, dp, dp]
         L.or_camera_key.restype = C.c_uint64
         L.or_camera_key.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]
         L.or_child_key.restype = C.c_uint64
@@ -89,6 +94,27 @@ class OracleScene:
 
     def tree_nodes(self) -> int:
         return lib().or_scene_tree_nodes(self.h)
+
+    def texture_sample(self, texture: int, kind: int, u: float, v: float):
+        out = (C.c_double * 3)()
+        lib().or_texture_sample(self.h, texture, kind, u, v, out)
+        return tuple(out)
+
+    def shape_uv(self, kind: int, index: int, p):
+        out = (C.c_float * 3)()
+        lib().or_shape_uv(self.h, kind, index, f3(p), out)
+        return tuple(out)
+
+    def environment(self, direction):
+        out = (C.c_double * 3)()
+        lib().or_environment(self.h, f3(direction), out)
+        return tuple(out)
+
+    def hit_surface(self, origin, direction):
+        col, gloss = (C.c_double * 3)(), C.c_double()
+        if not lib().or_hit_surface(self.h, f3(origin), f3(direction), col, C.byref(gloss)):
+            return None
+        return tuple(col), gloss.value
 
 
 def pass_params(spp, seed=0, pass_index=1, stratified=False, tiles=None, adaptive=0, firefly=0):

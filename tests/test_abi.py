@@ -37,13 +37,14 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version():
-    assert _abi.load_library().pt_get_version() == 1
+    assert _abi.load_library().pt_get_version() == _abi.ABI_VERSION
 
 
 def test_struct_layouts_match_header():
     # sizes computed by hand from the C declarations (x86-64 SysV alignment)
     assert C.sizeof(_abi.pt_mesh_data) == 8 + 9 * 8
-    assert C.sizeof(_abi.pt_material) == 8 * 8 + 8
+    assert C.sizeof(_abi.pt_material) == 8 * 8 + 6 * 4 + 8
+    assert C.sizeof(_abi.pt_texture) == 16
     assert C.sizeof(_abi.pt_camera) == 12 * 4 + 3 * 8
     assert C.sizeof(_abi.pt_sampler) == 24
     assert C.sizeof(_abi.pt_pass_params) == 4 + 4 + 8 + 4 + 4 + 8 + 8 + 8
@@ -124,7 +125,7 @@ def _fields_cs(src, name):
 
 
 @pytest.mark.parametrize("name", ["pt_pass_params", "pt_stats", "pt_mesh_data", "pt_sampler", "pt_device_opts",
-                                  "pt_camera"])
+                                  "pt_camera", "pt_material", "pt_texture", "pt_scene_desc"])
 def test_csharp_binding_matches_header(name):
     """csharp/HipRenderer.cs mirrors include/ptsharp_hip.h field for field (the library
     writes pt_stats into the caller's struct, so a stale C# layout would be overrun)."""
