@@ -25,6 +25,7 @@ namespace PTSharpCore
         public const int PT_OK = 0;
         public const int PT_ERR_UNSUPPORTED = -4;
         public const int SHAPE_SPHERE = 0, SHAPE_CUBE = 1, SHAPE_PLANE = 2, SHAPE_TRIANGLE = 3, SHAPE_MESH = 4;
+        public const int SHAPE_SDF = 5, SHAPE_VOLUME = 6, SHAPE_TRANSFORMED = 7;
 
         [StructLayout(LayoutKind.Sequential)]
         public struct pt_texture
@@ -44,6 +45,41 @@ namespace PTSharpCore
         }
 
         [StructLayout(LayoutKind.Sequential)]
+        public unsafe struct pt_sdf_node
+        {
+            public int op, num_children, first_child, _pad;
+            public fixed double @params[8];
+            public fixed double matrix[16];
+            public fixed double inverse[16];
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_sdf_shape { public int root, material; }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_volume_window { public double lo, hi; public int material, _pad; }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public unsafe struct pt_volume
+        {
+            public int w, h, d;
+            public int num_windows;
+            public double zscale;
+            public IntPtr data;
+            public IntPtr windows;
+            public fixed float box_min[3];
+            public fixed float box_max[3];
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public unsafe struct pt_transformed_shape
+        {
+            public int shape_kind, shape_index;
+            public fixed double matrix[16];
+            public fixed double inverse[16];
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
         public unsafe struct pt_scene_desc
         {
             public int num_materials; public IntPtr materials;
@@ -57,6 +93,10 @@ namespace PTSharpCore
             public int num_textures; public IntPtr textures;
             public IntPtr tri_t1, tri_t2, tri_t3;
             public int env_texture; public int _pad; public double env_texture_angle;
+            public int num_sdf_nodes; public IntPtr sdf_nodes; public IntPtr sdf_children;
+            public int num_sdf_shapes; public IntPtr sdf_shapes;
+            public int num_volumes; public IntPtr volumes;
+            public int num_transformed; public IntPtr transformed;
         }
 
         [StructLayout(LayoutKind.Sequential)]
@@ -199,6 +239,70 @@ namespace PTSharpCore
             var t1 = new List<float>(); var t2 = new List<float>(); var t3 = new List<float>();
             var mf = new List<int>(); var mc = new List<int>();
             void Add3(List<float> l, Vector v) { l.Add((float)v.X); l.Add((float)v.Y); l.Add((float)v.Z); }
+            // SDF trees, volumes and transformed shapes (§8f row 4).  SDF / Volume / TransformedShape keep
+            // their fields private in the reference (SDF.cs, Volume.cs:21-27, TransformedShape.cs:11-13):
+            // the integration marks them `internal` (INTEGRATION.md), as for Plane.
+            var sdfNodes = new List<PtHip.pt_sdf_node>(); var sdfKids = new List<int>(); var sdfIds = new Dictionary<SDF, int>(ReferenceEqualityComparer.Instance);
+            var sdfShapes = new List<PtHip.pt_sdf_shape>(); var vols = new List<PtHip.pt_volume>(); var xfs = new List<PtHip.pt_transformed_shape>();
+            void Mat16(double* dst, Matrix m)
+            {
+                double[] a = { m.M11, m.M12, m.M13, m.M14, m.M21, m.M22, m.M23, m.M24, m.M31, m.M32, m.M33, m.M34, m.M41, m.M42, m.M43, m.M44 };
+                for (int k = 0; k < 16; k++) dst[k] = a[k];
+            }
+            int Sdf(SDF n)
+            {
+                if (sdfIds.TryGetValue(n, out int id)) return id;
+                var node = new PtHip.pt_sdf_node();
+                SDF[] kids = n switch
+                {
+                    TransformSDF t => new[] { t.SDF }, ScaleSDF sc => new[] { sc.SDF }, RepeatSDF r => new[] { r.SDF },
+                    UnionSDF u => u.Items, DifferenceSDF df => df.Items, IntersectionSDF i => i.Items, _ => Array.Empty<SDF>(),
+                };
+                var kidIds = new List<int>(); foreach (var k in kids) kidIds.Add(Sdf(k));
+                node.num_children = kidIds.Count; node.first_child = sdfKids.Count; sdfKids.AddRange(kidIds);
+                switch (n)
+                {
+                    case SphereSDF sp: node.op = 0; node.@params[0] = sp.Radius; node.@params[1] = sp.Exponent; break;
+                    case CubeSDF cu: node.op = 1; node.@params[0] = cu.Size.X; node.@params[1] = cu.Size.Y; node.@params[2] = cu.Size.Z; break;
+                    case CylinderSDF cy: node.op = 2; node.@params[0] = cy.Radius; node.@params[1] = cy.Height; break;
+                    case CapsuleSDF ca: node.op = 3; node.@params[0] = ca.A.X; node.@params[1] = ca.A.Y; node.@params[2] = ca.A.Z;
+                        node.@params[3] = ca.B.X; node.@params[4] = ca.B.Y; node.@params[5] = ca.B.Z; node.@params[6] = ca.Radius; node.@params[7] = ca.Exponent; break;
+                    case TorusSDF to: node.op = 4; node.@params[0] = to.MajorRadius; node.@params[1] = to.MinRadius;
+                        node.@params[2] = to.MajorExponent; node.@params[3] = to.MinorExponent; break;
+                    case TransformSDF tr: node.op = 5; Mat16(node.matrix, tr.Matrix); Mat16(node.inverse, tr.Inverse); break;
+                    case ScaleSDF sc: node.op = 6; node.@params[0] = sc.Factor; break;
+                    case UnionSDF: node.op = 7; break;
+                    case DifferenceSDF: node.op = 8; break;
+                    case IntersectionSDF: node.op = 9; break;
+                    case RepeatSDF re: node.op = 10; node.@params[0] = re.Step.X; node.@params[1] = re.Step.Y; node.@params[2] = re.Step.Z; break;
+                    default: throw new NotSupportedException($"{n.GetType().Name} is not on the GPU path");
+                }
+                id = sdfNodes.Count; sdfIds[n] = id; sdfNodes.Add(node);
+                return id;
+            }
+            (int, int) Inner(IShape s)
+            {
+                switch (s)
+                {
+                    case Sphere sp: Add3(sc, sp.Center); sr.Add(sp.Radius); sm.Add(Mid(sp.Material)); return (PtHip.SHAPE_SPHERE, sr.Count - 1);
+                    case Cube cu: Add3(cmin, cu.Min); Add3(cmax, cu.Max); cm.Add(Mid(cu.Material)); return (PtHip.SHAPE_CUBE, cm.Count - 1);
+                    case Plane pl: Add3(pp, pl.Point); Add3(pn, pl.Normal); pm.Add(Mid(pl.Material)); return (PtHip.SHAPE_PLANE, pm.Count - 1);
+                    case SDFShape sd: sdfShapes.Add(new PtHip.pt_sdf_shape { root = Sdf(sd.SDF), material = Mid(sd.Material) }); return (PtHip.SHAPE_SDF, sdfShapes.Count - 1);
+                    case Volume vo:
+                    {
+                        var wins = new PtHip.pt_volume_window[vo.Windows.Length];
+                        for (int k = 0; k < wins.Length; k++)
+                            wins[k] = new PtHip.pt_volume_window { lo = vo.Windows[k].Lo, hi = vo.Windows[k].Hi, material = Mid(vo.Windows[k].VolumeWindowMaterial) };
+                        var v = new PtHip.pt_volume { w = vo.W, h = vo.H, d = vo.D, num_windows = wins.Length, zscale = vo.ZScale,
+                                                      data = Pin(vo.Data), windows = Pin(wins) };
+                        v.box_min[0] = (float)vo.Box.Min.X; v.box_min[1] = (float)vo.Box.Min.Y; v.box_min[2] = (float)vo.Box.Min.Z;
+                        v.box_max[0] = (float)vo.Box.Max.X; v.box_max[1] = (float)vo.Box.Max.Y; v.box_max[2] = (float)vo.Box.Max.Z;
+                        vols.Add(v);
+                        return (PtHip.SHAPE_VOLUME, vols.Count - 1);
+                    }
+                    default: throw new NotSupportedException($"{s.GetType().Name} inside a TransformedShape is not on the GPU path");
+                }
+            }
             void AddTri(Triangle t)
             {
                 Add3(v1, t.V1); Add3(v2, t.V2); Add3(v3, t.V3); Add3(n1, t.N1); Add3(n2, t.N2); Add3(n3, t.N3);
@@ -215,6 +319,15 @@ namespace PTSharpCore
                     // marks them `internal`, the same visibility Sphere and Cube already use (INTEGRATION.md).
                     case Plane pl: kind.Add(PtHip.SHAPE_PLANE); index.Add(pm.Count); Add3(pp, pl.Point); Add3(pn, pl.Normal); pm.Add(Mid(pl.Material)); break;
                     case Triangle tr: kind.Add(PtHip.SHAPE_TRIANGLE); index.Add(tm.Count); AddTri(tr); break;
+                    case SDFShape or Volume: { var (k, i) = Inner(s); kind.Add(k); index.Add(i); break; }
+                    case TransformedShape ts:
+                    {
+                        var (k, i) = Inner(ts.Shape);
+                        var x = new PtHip.pt_transformed_shape { shape_kind = k, shape_index = i };
+                        Mat16(x.matrix, ts.Matrix); Mat16(x.inverse, ts.Inverse);
+                        kind.Add(PtHip.SHAPE_TRANSFORMED); index.Add(xfs.Count); xfs.Add(x);
+                        break;
+                    }
                     case Mesh me: kind.Add(PtHip.SHAPE_MESH); index.Add(mf.Count); mf.Add(tm.Count); mc.Add(me.Triangles.Length); foreach (var t in me.Triangles) AddTri(t); break;
                     default: throw new NotSupportedException($"{s.GetType().Name} is not on the GPU path");
                 }
@@ -234,6 +347,10 @@ namespace PTSharpCore
             };
             d.env_color[0] = Scene.Color.r; d.env_color[1] = Scene.Color.g; d.env_color[2] = Scene.Color.b;
             d.num_textures = texs.Count; d.textures = Pin(texs.ToArray());
+            d.num_sdf_nodes = sdfNodes.Count; d.sdf_nodes = Pin(sdfNodes.ToArray()); d.sdf_children = Pin(sdfKids.ToArray());
+            d.num_sdf_shapes = sdfShapes.Count; d.sdf_shapes = Pin(sdfShapes.ToArray());
+            d.num_volumes = vols.Count; d.volumes = Pin(vols.ToArray());
+            d.num_transformed = xfs.Count; d.transformed = Pin(xfs.ToArray());
             try { PtHip.Check(PtHip.pt_upload_scene(ctx, ref d), "pt_upload_scene"); }
             finally { foreach (var g in pins) g.Free(); pins.Clear(); }   // arrays are copied during the call
             uploaded = true;

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 2
+#define PT_ABI_VERSION 3
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -62,8 +62,66 @@ typedef enum pt_shape_kind {
     PT_SHAPE_CUBE = 1,      /* Cube.cs     */
     PT_SHAPE_PLANE = 2,     /* Plane.cs    */
     PT_SHAPE_TRIANGLE = 3,  /* Triangle.cs, added directly to the scene (a boxed struct) */
-    PT_SHAPE_MESH = 4       /* Mesh.cs, a range of triangles with its own tree */
+    PT_SHAPE_MESH = 4,      /* Mesh.cs, a range of triangles with its own tree */
+    PT_SHAPE_SDF = 5,       /* SDF.cs SDFShape (sphere-traced signed distance tree) */
+    PT_SHAPE_VOLUME = 6,    /* Volume.cs (voxel grid, iso-window marching) */
+    PT_SHAPE_TRANSFORMED = 7 /* TransformedShape.cs (instancing of one inner shape) */
 } pt_shape_kind;
+
+/* ---- §8f row 4: SDF.cs, Volume.cs, TransformedShape.cs ----------------------
+ * SDF nodes form a tree (children listed in pt_scene_desc.sdf_children).  Vector-
+ * valued parameters are the reference's fp32 Vector fields widened to double. */
+typedef enum pt_sdf_op {
+    PT_SDF_SPHERE = 0,        /* SphereSDF       params: Radius, Exponent                 SDF.cs:115-140 */
+    PT_SDF_CUBE = 1,          /* CubeSDF         params: Size.xyz                          SDF.cs:142-195 */
+    PT_SDF_CYLINDER = 2,      /* CylinderSDF     params: Radius, Height                    SDF.cs:197-252 */
+    PT_SDF_CAPSULE = 3,       /* CapsuleSDF      params: A.xyz, B.xyz, Radius, Exponent    SDF.cs:254-285 */
+    PT_SDF_TORUS = 4,         /* TorusSDF        params: MajorRadius, MinRadius, MajorExponent, MinorExponent  SDF.cs:287-319 */
+    PT_SDF_TRANSFORM = 5,     /* TransformSDF    matrix, inverse; 1 child                  SDF.cs:321-353 */
+    PT_SDF_SCALE = 6,         /* ScaleSDF        params: Factor; 1 child                   SDF.cs:355-382 */
+    PT_SDF_UNION = 7,         /* UnionSDF        n children                                SDF.cs:384-435 */
+    PT_SDF_DIFFERENCE = 8,    /* DifferenceSDF   n >= 1 children                           SDF.cs:437-477 */
+    PT_SDF_INTERSECTION = 9,  /* IntersectionSDF n children                                SDF.cs:479-531 */
+    PT_SDF_REPEAT = 10        /* RepeatSDF       params: Step.xyz; 1 child                 SDF.cs:533-559 */
+} pt_sdf_op;
+
+typedef struct pt_sdf_node {
+    int32_t op;               /* pt_sdf_op */
+    int32_t num_children;
+    int32_t first_child;      /* children: sdf_children[first_child .. first_child + num_children) */
+    int32_t _pad;
+    double params[8];
+    double matrix[16];        /* PT_SDF_TRANSFORM: Matrix M11..M44, row-major */
+    double inverse[16];       /* and the Inverse TransformSDF stores */
+} pt_sdf_node;
+
+typedef struct pt_sdf_shape {  /* SDFShape.NewSDFShape(sdf, material), SDF.cs:12-113 */
+    int32_t root;             /* node index */
+    int32_t material;
+} pt_sdf_shape;
+
+typedef struct pt_volume_window {  /* Volume.VolumeWindow, Volume.cs:8-19 */
+    double lo, hi;
+    int32_t material;
+    int32_t _pad;
+} pt_volume_window;
+
+typedef struct pt_volume {    /* Volume fields W, H, D, ZScale, Data, Windows, Box (Volume.cs:21-38) */
+    int32_t w, h, d;
+    int32_t num_windows;
+    double zscale;
+    const double* data;       /* [d][h][w] */
+    const pt_volume_window* windows;
+    float box_min[3];
+    float box_max[3];
+} pt_volume;
+
+typedef struct pt_transformed_shape {  /* TransformedShape(Shape, Matrix, Inverse), TransformedShape.cs:9-24 */
+    int32_t shape_kind;       /* inner IShape: SPHERE, CUBE, PLANE, SDF or VOLUME */
+    int32_t shape_index;      /* index into that kind's arrays */
+    double matrix[16];
+    double inverse[16];
+} pt_transformed_shape;
 
 /* ColorTexture (Texture.cs:96-252): Width x Height Colour texels, row-major, as the
  * C# object holds them (Data[y * Width + x], already through Pow(2.2) and any
@@ -144,6 +202,17 @@ typedef struct pt_scene_desc {
     int32_t env_texture;          /* Scene.Texture (1-based, 0 = null): sampleEnvironment, Sampler.cs:177-189 */
     int32_t _pad;
     double env_texture_angle;     /* Scene.TextureAngle */
+
+    /* SDF shapes, volumes, transformed shapes (§8f row 4); all optional */
+    int32_t num_sdf_nodes;
+    const pt_sdf_node* sdf_nodes;
+    const int32_t* sdf_children;
+    int32_t num_sdf_shapes;
+    const pt_sdf_shape* sdf_shapes;
+    int32_t num_volumes;
+    const pt_volume* volumes;
+    int32_t num_transformed;
+    const pt_transformed_shape* transformed;
 } pt_scene_desc;
 
 /* Camera struct fields (Camera.cs:11-14) as produced by Camera.LookAt/SetFocus. */

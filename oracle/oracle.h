@@ -36,6 +36,25 @@ typedef struct or_material {
     double bump_multiplier;
 } or_material;
 
+typedef struct or_sdf_node {
+    int32_t op, num_children, first_child, _pad;
+    double params[8];
+    double matrix[16], inverse[16];
+} or_sdf_node;
+typedef struct or_sdf_shape { int32_t root, material; } or_sdf_shape;
+typedef struct or_volume_window { double lo, hi; int32_t material, _pad; } or_volume_window;
+typedef struct or_volume {
+    int32_t w, h, d, num_windows;
+    double zscale;
+    const double* data;
+    const or_volume_window* windows;
+    float box_min[3], box_max[3];
+} or_volume;
+typedef struct or_transformed_shape {
+    int32_t shape_kind, shape_index;
+    double matrix[16], inverse[16];
+} or_transformed_shape;
+
 typedef struct or_scene_desc {
     int32_t num_materials; const or_material* materials;
     int32_t num_shapes; const int32_t* shape_kind; const int32_t* shape_index;
@@ -51,6 +70,10 @@ typedef struct or_scene_desc {
     const float *tri_t1, *tri_t2, *tri_t3;
     int32_t env_texture, _pad;
     double env_texture_angle;
+    int32_t num_sdf_nodes; const or_sdf_node* sdf_nodes; const int32_t* sdf_children;
+    int32_t num_sdf_shapes; const or_sdf_shape* sdf_shapes;
+    int32_t num_volumes; const or_volume* volumes;
+    int32_t num_transformed; const or_transformed_shape* transformed;
 } or_scene_desc;
 
 typedef struct or_camera {
@@ -116,6 +139,12 @@ void or_shape_uv(void* scene, int32_t kind, int32_t index, const float p[3], flo
 void or_environment(void* scene, const float dir[3], double out[3]);
 /* Hit.Info's material after Material.MaterialAt (Material.cs:124-138): colour and gloss. */
 int32_t or_hit_surface(void* scene, const float origin[3], const float dir[3], double out_color[3], double* out_gloss);
+
+/* SDF.Evaluate of node `node` at p (SDF.cs), Volume.Sample (Volume.cs:73-105). */
+double or_sdf_evaluate(void* scene, int32_t node, const float p[3]);
+double or_volume_sample(void* scene, int32_t volume, double x, double y, double z);
+/* Bounding box of scene primitive (kind, index): IShape.BoundingBox. */
+void or_shape_box(void* scene, int32_t kind, int32_t index, float out_min[3], float out_max[3]);
 
 /* Counter-based RNG that replaces Random.Shared (spec in DESIGN.md §RNG). */
 uint64_t or_camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample);

@@ -166,7 +166,9 @@ inline V box_center(const Box& b) { return vadd(b.min, vmul(vsub(b.max, b.min), 
 inline double box_outer_radius(const Box& b) { return vlen(vsub(b.min, box_center(b))); }              // :320
 
 // ---------------------------------------------------------------- scene
-enum Kind { K_SPHERE = 0, K_CUBE = 1, K_PLANE = 2, K_TRI = 3, K_MESH = 4 };
+enum Kind { K_SPHERE = 0, K_CUBE = 1, K_PLANE = 2, K_TRI = 3, K_MESH = 4, K_SDF = 5, K_VOLUME = 6, K_XFORM = 7 };
+enum SdfOp { S_SPHERE = 0, S_CUBE, S_CYLINDER, S_CAPSULE, S_TORUS, S_TRANSFORM, S_SCALE, S_UNION, S_DIFFERENCE,
+             S_INTERSECTION, S_REPEAT };
 
 struct Material {
     C color; double emittance, index, gloss, tint, reflectivity; bool transparent;
@@ -184,6 +186,11 @@ struct Cube { V min, max; int mat; };
 struct Plane { V point, normal; int mat; };
 struct Tri { V v1, v2, v3, n1, n2, n3; int mat; V t1, t2, t3; };
 struct ShapeRef { int kind; int idx; };
+struct SdfNode { int op; std::vector<int> kids; double p[8]; double M[16], Inv[16]; };
+struct SdfShape { int root; int mat; Box box; };
+struct VolWindow { double lo, hi; int mat; };
+struct Volume { int w, h, d; double zscale; std::vector<double> data; std::vector<VolWindow> windows; Box box; };
+struct Xform { int kind, idx; double M[16], Inv[16]; Box box; };
 
 struct Hit { double t; int kind; int idx; };  // kind: K_* of the primitive hit (mesh hits report K_TRI)
 const Hit NOHIT{HIT_INF, -1, -1};
@@ -214,6 +221,11 @@ struct Scene {
     std::vector<Tex> texs;
     int env_tex = -1;        // Scene.Texture (-1 = null)
     double env_angle = 0;    // Scene.TextureAngle
+    std::vector<SdfNode> sdf;
+    std::vector<SdfShape> sdf_shapes;
+    std::vector<Volume> volumes;
+    std::vector<Xform> xforms;
+    int default_mat = 0;     // `new Material()` (all zero): Volume.MaterialAt when no window is near
 };
 
 // ---------------------------------------------------------------- primitives
@@ -399,6 +411,278 @@ V tri_normal_mapped(const Tri& t, V p, const Tex* ntex, const Tex* btex, double 
 
 inline Box tri_box(const Tri& t) { return Box{vmin(vmin(t.v1, t.v2), t.v3), vmax(vmax(t.v1, t.v2), t.v3)}; }
 
+// ---------------------------------------------------------------- Matrix (Matrix.cs), row-major M11..M44
+// MulPosition (Matrix.cs:134-141): fp64 rows, then a Vector (fp32).
+inline V mat_position(const double* m, V b) {
+    double x = m[0] * b.x + m[1] * b.y + m[2] * b.z + m[3];
+    double y = m[4] * b.x + m[5] * b.y + m[6] * b.z + m[7];
+    double z = m[8] * b.x + m[9] * b.y + m[10] * b.z + m[11];
+    return vmk(x, y, z);
+}
+// MulDirection (Matrix.cs:144-150), normalised
+inline V mat_direction(const double* m, V b) {
+    double x = m[0] * b.x + m[1] * b.y + m[2] * b.z;
+    double y = m[4] * b.x + m[5] * b.y + m[6] * b.z;
+    double z = m[8] * b.x + m[9] * b.y + m[10] * b.z;
+    return vnorm(vmk(x, y, z));
+}
+// Transpose().MulDirection (Matrix.cs:176, 144-150)
+inline V mat_direction_transposed(const double* m, V b) {
+    double x = m[0] * b.x + m[4] * b.y + m[8] * b.z;
+    double y = m[1] * b.x + m[5] * b.y + m[9] * b.z;
+    double z = m[2] * b.x + m[6] * b.y + m[10] * b.z;
+    return vnorm(vmk(x, y, z));
+}
+// MulBox (Matrix.cs:156-173)
+inline Box mat_box(const double* m, const Box& box) {
+    V r = vmk(m[0], m[4], m[8]), u = vmk(m[1], m[5], m[9]), b = vmk(m[2], m[6], m[10]), t = vmk(m[3], m[7], m[11]);
+    V xa = vmuls(r, box.min.x), xb = vmuls(r, box.max.x);
+    V ya = vmuls(u, box.min.y), yb = vmuls(u, box.max.y);
+    V za = vmuls(b, box.min.z), zb = vmuls(b, box.max.z);
+    V xlo = vmin(xa, xb), xhi = vmax(xa, xb), ylo = vmin(ya, yb), yhi = vmax(ya, yb), zlo = vmin(za, zb), zhi = vmax(za, zb);
+    return Box{vadd(vadd(vadd(xlo, ylo), zlo), t), vadd(vadd(vadd(xhi, yhi), zhi), t)};
+}
+
+// ---------------------------------------------------------------- SDF (SDF.cs)
+// Vector.LengthN (Vector.cs:359-367)
+inline double length_n(V a, double n) {
+    if (n == 2) return vlen(a);
+    V b = V{std::fabs(a.x), std::fabs(a.y), std::fabs(a.z)};  // Abs (Vector.cs:402-405)
+    return std::pow(std::pow((double)b.x, n) + std::pow((double)b.y, n) + std::pow((double)b.z, n), 1 / n);
+}
+// SDF.Evaluate per node kind (SDF.cs:131-548)
+double sdf_eval(const Scene& s, int ni, V p) {
+    const SdfNode& n = s.sdf[(size_t)ni];
+    switch (n.op) {
+        case S_SPHERE: return length_n(p, n.p[1]) - n.p[0];
+        case S_CUBE: {
+            double x = p.x, y = p.y, z = p.z;
+            if (x < 0) x = -x;
+            if (y < 0) y = -y;
+            if (z < 0) z = -z;
+            x -= (double)(float)n.p[0] / 2;
+            y -= (double)(float)n.p[1] / 2;
+            z -= (double)(float)n.p[2] / 2;
+            double a = x;
+            if (y > a) a = y;
+            if (z > a) a = z;
+            if (a > 0) a = 0;
+            if (x < 0) x = 0;
+            if (y < 0) y = 0;
+            if (z < 0) z = 0;
+            double b = std::sqrt(x * x + y * y + z * z);
+            return a + b;
+        }
+        case S_CYLINDER: {
+            double x = std::sqrt((double)p.x * p.x + (double)p.z * p.z);
+            double y = p.y;
+            if (x < 0) x = -x;
+            if (y < 0) y = -y;
+            x -= n.p[0];
+            y -= n.p[1] / 2;
+            double a = x;
+            if (y > a) a = y;
+            if (a > 0) a = 0;
+            if (x < 0) x = 0;
+            if (y < 0) y = 0;
+            double b = std::sqrt(x * x + y * y);
+            return a + b;
+        }
+        case S_CAPSULE: {
+            V A = vmk(n.p[0], n.p[1], n.p[2]), B = vmk(n.p[3], n.p[4], n.p[5]);
+            V pa = vsub(p, A), ba = vsub(B, A);
+            double h = net_max(0, net_min(1, vdot(pa, ba) / vdot(ba, ba)));
+            return length_n(vsub(pa, vmuls(ba, h)), n.p[7]) - n.p[6];
+        }
+        case S_TORUS: {
+            V q = vmk(length_n(V{p.x, p.y, 0.f}, n.p[2]) - n.p[0], p.z, 0);
+            return length_n(q, n.p[3]) - n.p[1];
+        }
+        case S_TRANSFORM: return sdf_eval(s, n.kids[0], mat_position(n.Inv, p));
+        case S_SCALE: return sdf_eval(s, n.kids[0], vmk((double)p.x / n.p[0], (double)p.y / n.p[0], (double)p.z / n.p[0])) * n.p[0];
+        case S_UNION: {
+            double result = 0;
+            for (size_t i = 0; i < n.kids.size(); i++) {
+                double d = sdf_eval(s, n.kids[i], p);
+                if (i == 0 || d < result) result = d;
+            }
+            return result;
+        }
+        case S_DIFFERENCE: {
+            double result = 0;
+            for (size_t i = 0; i < n.kids.size(); i++) {
+                double d = sdf_eval(s, n.kids[i], p);
+                if (i == 0) result = d;
+                else if (-d > result) result = -d;
+            }
+            return result;
+        }
+        case S_INTERSECTION: {
+            double result = 0;
+            for (size_t i = 0; i < n.kids.size(); i++) {
+                double d = sdf_eval(s, n.kids[i], p);
+                if (i == 0 || d > result) result = d;
+            }
+            return result;
+        }
+        default: {  // S_REPEAT: p.Mod(Step).Sub(Step.DivScalar(2)) (Vector.cs:420-426)
+            V st = vmk(n.p[0], n.p[1], n.p[2]);
+            V m = vmk((double)p.x - (double)st.x * std::floor((double)p.x / st.x),
+                      (double)p.y - (double)st.y * std::floor((double)p.y / st.y),
+                      (double)p.z - (double)st.z * std::floor((double)p.z / st.z));
+            V half = vmk((double)st.x / 2, (double)st.y / 2, (double)st.z / 2);
+            return sdf_eval(s, n.kids[0], vsub(m, half));
+        }
+    }
+}
+// SDF.BoundingBox per node kind
+Box sdf_box(const Scene& s, int ni) {
+    const SdfNode& n = s.sdf[(size_t)ni];
+    switch (n.op) {
+        case S_SPHERE: { double r = n.p[0]; return Box{vmk(-r, -r, -r), vmk(r, r, r)}; }
+        case S_CUBE: {
+            double x = (double)(float)n.p[0] / 2, y = (double)(float)n.p[1] / 2, z = (double)(float)n.p[2] / 2;
+            return Box{vmk(-x, -y, -z), vmk(x, y, z)};
+        }
+        case S_CYLINDER: { double r = n.p[0], h = n.p[1] / 2; return Box{vmk(-r, -h, -r), vmk(r, h, r)}; }
+        case S_CAPSULE: {
+            V A = vmk(n.p[0], n.p[1], n.p[2]), B = vmk(n.p[3], n.p[4], n.p[5]);
+            V a = vmin(A, B), b = vmax(A, B);
+            double r = n.p[6];
+            return Box{vmk(a.x - r, a.y - r, a.z - r), vmk(b.x + r, b.y + r, b.z + r)};  // SubScalar / AddScalar
+        }
+        case S_TORUS: { double a = n.p[1], b = n.p[1] + n.p[0]; return Box{vmk(-b, -b, a), vmk(b, b, a)}; }
+        case S_TRANSFORM: return mat_box(n.M, sdf_box(s, n.kids[0]));
+        case S_SCALE: {
+            double f = (double)(float)n.p[0];   // new Matrix().Scale(new Vector(f, f, f))
+            double m[16] = {f, 0, 0, 0, 0, f, 0, 0, 0, 0, f, 0, 0, 0, 0, 1};
+            return mat_box(m, sdf_box(s, n.kids[0]));
+        }
+        case S_UNION:
+        case S_INTERSECTION: {
+            Box r{vzero(), vzero()};
+            for (size_t i = 0; i < n.kids.size(); i++) r = i == 0 ? sdf_box(s, n.kids[i]) : box_extend(r, sdf_box(s, n.kids[i]));
+            return r;
+        }
+        case S_DIFFERENCE: return sdf_box(s, n.kids[0]);
+        default: return Box{vzero(), vzero()};   // RepeatSDF: new Box()
+    }
+}
+// SDFShape.Intersect (SDF.cs:32-76): sphere tracing inside the box.
+double sdf_t(const Scene& s, const SdfShape& sh, const Ray& ray) {
+    const double epsilon = (double)0.00001f, start = (double)0.0001f, jump_size = (double)0.001f;
+    double t1, t2;
+    box_intersect(sh.box, ray, t1, t2);
+    if (t2 < t1 || t2 < 0) return HIT_INF;
+    double t = net_max(start, t1);
+    bool jump = true;
+    for (int i = 0; i < 1000; i++) {
+        double d = sdf_eval(s, sh.root, ray_position(ray, t));
+        if (jump && d < 0) {
+            t -= jump_size;
+            jump = false;
+            continue;
+        }
+        if (d < epsilon) return t;
+        if (jump && d < jump_size) d = jump_size;
+        t += d;
+        if (t > t2) return HIT_INF;
+    }
+    return HIT_INF;
+}
+// SDFShape.NormalAt (SDF.cs:83-92)
+V sdf_normal(const Scene& s, const SdfShape& sh, V p) {
+    const double e = 0.0001;
+    double x = p.x, y = p.y, z = p.z;
+    auto ev = [&](double a, double b, double c) { return sdf_eval(s, sh.root, vmk(a, b, c)); };
+    return vnorm(vmk(ev(x - e, y, z) - ev(x + e, y, z), ev(x, y - e, z) - ev(x, y + e, z), ev(x, y, z - e) - ev(x, y, z + e)));
+}
+
+// ---------------------------------------------------------------- Volume (Volume.cs)
+inline double vol_get(const Volume& v, int x, int y, int z) {  // Volume.Get (Volume.cs:40-46)
+    if (x < 0 || y < 0 || z < 0 || x >= v.w || y >= v.h || z >= v.d) return 0;
+    return v.data[(size_t)x + (size_t)y * v.w + (size_t)z * v.w * v.h];
+}
+// Volume.Sample (Volume.cs:73-105), including its y-from-z slip (:77).  Non-finite or
+// out-of-int-range coordinates (an OverflowException in the reference) sample 0.
+double vol_sample(const Volume& v, double x, double y, double z) {
+    (void)y;
+    z /= v.zscale;
+    x = ((x + 1) / 2) * (double)v.w;
+    y = ((z + 1) / 2) * (double)v.h;
+    z = ((z + 2) / 2) * (double)v.d;
+    const double lim = 2147483647.0;
+    if (!(std::fabs(x) < lim && std::fabs(y) < lim && std::fabs(z) < lim)) return 0;
+    int x0 = (int)std::floor(x), y0 = (int)std::floor(y), z0 = (int)std::floor(z);
+    int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
+    double v000 = vol_get(v, x0, y0, z0), v001 = vol_get(v, x0, y0, z1), v010 = vol_get(v, x0, y1, z0);
+    double v011 = vol_get(v, x0, y1, z1), v100 = vol_get(v, x1, y0, z0), v101 = vol_get(v, x1, y0, z1);
+    double v110 = vol_get(v, x1, y1, z0), v111 = vol_get(v, x1, y1, z1);
+    x -= (double)x0;
+    y -= (double)y0;
+    z -= (double)z0;
+    double c00 = v000 * (1 - x) + v100 * x;
+    double c01 = v001 * (1 - x) + v101 * x;
+    double c10 = v010 * (1 - x) + v110 * x;
+    double c11 = v011 * (1 - x) + v111 * x;
+    double c0 = c00 * (1 - y) + c10 * y;
+    double c1 = c01 * (1 - y) + c11 * y;
+    return c0 * (1 - z) + c1 * z;
+}
+// Volume.Sign (Volume.cs:114-131): `i` is never incremented, so below a window is 1.
+int vol_sign(const Volume& v, V a) {
+    double s = vol_sample(v, a.x, a.y, a.z);
+    for (const VolWindow& w : v.windows) {
+        if (s < w.lo) return 1;
+        if (s > w.hi) continue;
+        return 0;
+    }
+    return (int)v.windows.size() + 1;
+}
+// Volume.NormalAt (Volume.cs:138-145)
+V vol_normal(const Volume& v, V p) {
+    const double eps = (double)0.001f;
+    return vnorm(vmk(vol_sample(v, p.x - eps, p.y, p.z) - vol_sample(v, p.x + eps, p.y, p.z),
+                     vol_sample(v, p.x, p.y - eps, p.z) - vol_sample(v, p.x, p.y + eps, p.z),
+                     vol_sample(v, p.x, p.y, p.z - eps) - vol_sample(v, p.x, p.y, p.z + eps)));
+}
+// Volume.MaterialAt (Volume.cs:148-166): the window holding the sample, else the nearest.
+int vol_material(const Scene& s, const Volume& v, V p) {
+    double be = (double)1e9f;
+    int bm = s.default_mat;
+    double smp = vol_sample(v, p.x, p.y, p.z);
+    for (const VolWindow& w : v.windows) {
+        if (smp >= w.lo && smp <= w.hi) return w.mat;
+        double e = net_min(std::fabs(smp - w.lo), std::fabs(smp - w.hi));
+        if (e < be) { be = e; bm = w.mat; }
+    }
+    return bm;
+}
+// Volume.Intersect (Volume.cs:168-197).  The reference has no iteration bound; 2^24
+// steps stand in for it (a ray that needs more never ends in the reference).
+double vol_t(const Volume& v, const Ray& ray) {
+    double tmin, tmax;
+    box_intersect(v.box, ray, tmin, tmax);
+    double step = (double)(1.0f / 512.0f);
+    double start = net_max(step, tmin);
+    int sign = -1;
+    int64_t iters = 0;
+    for (double t = start; t <= tmax && iters < (1 << 24); t += step, iters++) {
+        int sg = vol_sign(v, ray_position(ray, t));
+        if (sg == 0 || (sign >= 0 && sg != sign)) {
+            t -= step;
+            step /= 64;
+            t += step;
+            for (int i = 0; i < 64; i++) {
+                if (vol_sign(v, ray_position(ray, t)) == 0) return t - step;
+                t += step;
+            }
+        }
+        sign = sg;
+    }
+    return HIT_INF;
+}
+
 // IShape.UVector (Sphere.cs:62-69 with its p.Y-for-p.Z slip, Cube.cs:49-53, Plane.cs:52-55,
 // Triangle.cs:127-136).  Returns (u, v, 0) as the Vector the reference builds.
 V shape_uv(const Scene& s, int kind, int idx, V p) {
@@ -422,7 +706,8 @@ V shape_uv(const Scene& s, int kind, int idx, V p) {
             V n = vadd(vadd(vadd(vzero(), vmuls(t.t1, u)), vmuls(t.t2, v)), vmuls(t.t3, w));
             return V{n.x, n.y, 0.f};
         }
-        default: return vzero();  // Plane.UVector, Mesh.UVector
+        case K_XFORM: return shape_uv(s, s.xforms[(size_t)idx].kind, s.xforms[(size_t)idx].idx, p);  // Shape.UVector(uv)
+        default: return vzero();  // Plane, Mesh, SDFShape, Volume .UVector
     }
 }
 // Material.MaterialAt (Material.cs:124-138): the colour / gloss a shading point sees.
@@ -442,6 +727,9 @@ Surf material_at(const Scene& s, int kind, int idx, int mat, V p) {
 
 Box shape_box(const Scene& s, ShapeRef r) {
     switch (r.kind) {
+        case K_SDF: return s.sdf_shapes[(size_t)r.idx].box;
+        case K_VOLUME: return s.volumes[(size_t)r.idx].box;
+        case K_XFORM: return s.xforms[(size_t)r.idx].box;
         case K_SPHERE: return s.spheres[r.idx].box;
         case K_CUBE: return Box{s.cubes[r.idx].min, s.cubes[r.idx].max};
         case K_PLANE: return Box{vmk(-1e9, -1e9, -1e9), vmk(1e9, 1e9, 1e9)};  // Plane.cs:31-34 (Util.INF)
@@ -556,6 +844,30 @@ struct TreeBuilder {
     }
 };
 
+// Intersect of a shape that can sit inside a TransformedShape (Sphere, Cube, Plane, SDFShape, Volume).
+double inner_t(const Scene& s, int kind, int idx, const Ray& ray) {
+    switch (kind) {
+        case K_SPHERE: return sphere_t(s.spheres[(size_t)idx].center, s.spheres[(size_t)idx].radius, ray);
+        case K_CUBE: return cube_t(s.cubes[(size_t)idx].min, s.cubes[(size_t)idx].max, ray);
+        case K_PLANE: return plane_t(s.planes[(size_t)idx].point, s.planes[(size_t)idx].normal, ray);
+        case K_SDF: return sdf_t(s, s.sdf_shapes[(size_t)idx], ray);
+        case K_VOLUME: return vol_t(s.volumes[(size_t)idx], ray);
+    }
+    return HIT_INF;
+}
+// TransformedShape.Intersect (TransformedShape.cs:43-73) up to hit.T: the inner shape's hit
+// mapped back to world space, T = |position - origin| (fp32 Length).
+inline Ray xform_shape_ray(const Xform& x, const Ray& r) {  // Matrix.Inverse().MulRay(r)
+    return Ray{mat_position(x.Inv, r.o), mat_direction(x.Inv, r.d)};
+}
+double xform_t(const Scene& s, const Xform& x, const Ray& r) {
+    Ray sr = xform_shape_ray(x, r);
+    double t = inner_t(s, x.kind, x.idx, sr);
+    if (!(t < HIT_INF)) return HIT_INF;
+    V position = mat_position(x.M, ray_position(sr, t));
+    return vlen(vsub(position, r.o));
+}
+
 // ---------------------------------------------------------------- tracing
 struct Tracer {
     const Scene& s;
@@ -570,6 +882,9 @@ struct Tracer {
             case K_CUBE: t = cube_t(s.cubes[r.idx].min, s.cubes[r.idx].max, ray); break;
             case K_PLANE: t = plane_t(s.planes[r.idx].point, s.planes[r.idx].normal, ray); break;
             case K_TRI: { const Tri& tr = s.tris[r.idx]; t = tri_t(tr.v1, tr.v2, tr.v3, ray); break; }
+            case K_SDF: t = sdf_t(s, s.sdf_shapes[(size_t)r.idx], ray); break;
+            case K_VOLUME: t = vol_t(s.volumes[(size_t)r.idx], ray); break;
+            case K_XFORM: t = xform_t(s, s.xforms[(size_t)r.idx], ray); break;
             case K_MESH:
                 if (brute) {
                     Hit h = NOHIT;
@@ -640,6 +955,8 @@ V shape_normal(const Scene& s, const Hit& h, V p) {
         case K_SPHERE: return vnorm(vsub(p, s.spheres[h.idx].center));  // Sphere.NormalAt :78-81
         case K_CUBE: return cube_normal(s.cubes[h.idx].min, s.cubes[h.idx].max, p);
         case K_PLANE: return s.planes[h.idx].normal;                      // Plane.NormalAt :61-64
+        case K_SDF: return sdf_normal(s, s.sdf_shapes[(size_t)h.idx], p);
+        case K_VOLUME: return vol_normal(s.volumes[(size_t)h.idx], p);
         default: {
             const Tri& t = s.tris[h.idx];
             const Material& m = s.mats[t.mat];
@@ -649,25 +966,51 @@ V shape_normal(const Scene& s, const Hit& h, V p) {
         }
     }
 }
-int shape_mat(const Scene& s, const Hit& h) {
-    switch (h.kind) {
-        case K_SPHERE: return s.spheres[h.idx].mat;
-        case K_CUBE: return s.cubes[h.idx].mat;
-        case K_PLANE: return s.planes[h.idx].mat;
-        default: return s.tris[h.idx].mat;
+// IShape.MaterialAt(p): the material index a shape reports at p.
+int material_index_at(const Scene& s, int kind, int idx, V p) {
+    switch (kind) {
+        case K_SPHERE: return s.spheres[(size_t)idx].mat;
+        case K_CUBE: return s.cubes[(size_t)idx].mat;
+        case K_PLANE: return s.planes[(size_t)idx].mat;
+        case K_TRI: return s.tris[(size_t)idx].mat;
+        case K_SDF: return s.sdf_shapes[(size_t)idx].mat;
+        case K_VOLUME: return vol_material(s, s.volumes[(size_t)idx], p);
+        case K_XFORM: return material_index_at(s, s.xforms[(size_t)idx].kind, s.xforms[(size_t)idx].idx, p);
+        default: return s.default_mat;   // Mesh.MaterialAt: `new Material()`
     }
 }
-// Hit.Info (Hit.cs:26-55)
+// Hit.Info (Hit.cs:26-55); SDFShape / Volume keep inside = false (Hit.cs:42-49).
 HitInfo hit_info(const Scene& s, const Hit& h, const Ray& r) {
     HitInfo info;
+    if (h.kind == K_XFORM) {  // the HitInfo TransformedShape.Intersect builds (TransformedShape.cs:52-70)
+        const Xform& x = s.xforms[(size_t)h.idx];
+        Ray sr = xform_shape_ray(x, r);
+        double t = inner_t(s, x.kind, x.idx, sr);
+        V sp = ray_position(sr, t);
+        V sn = shape_normal(s, Hit{t, x.kind, x.idx}, sp);
+        info.position = mat_position(x.M, sp);
+        V normal = mat_direction_transposed(x.Inv, sn);   // Matrix.Inverse().Transpose().MulDirection
+        info.mat = material_index_at(s, x.kind, x.idx, sp);
+        Surf sf = material_at(s, x.kind, x.idx, info.mat, sp);
+        info.color = sf.color;
+        info.gloss = sf.gloss;
+        info.inside = false;
+        if (vdot(sn, sr.d) > 0) { normal = vneg(normal); info.inside = true; }
+        info.normal = normal;
+        info.ray = Ray{info.position, normal};
+        return info;
+    }
     info.position = ray_position(r, h.t);
     V normal = shape_normal(s, h, info.position);
-    info.mat = shape_mat(s, h);
+    info.mat = material_index_at(s, h.kind, h.idx, info.position);
     Surf sf = material_at(s, h.kind, h.idx, info.mat, info.position);
     info.color = sf.color;
     info.gloss = sf.gloss;
     info.inside = false;
-    if (vdot(normal, r.d) > 0) { normal = vneg(normal); info.inside = true; }
+    if (vdot(normal, r.d) > 0) {
+        normal = vneg(normal);
+        info.inside = h.kind != K_SDF && h.kind != K_VOLUME;
+    }
     info.normal = normal;
     info.ray = Ray{info.position, normal};
     return info;
@@ -739,7 +1082,7 @@ struct Integrator {
     bool light_identity(ShapeRef light, const Hit& h) const {
         // hit.Shape != light is a reference compare (Sampler.cs:264): class shapes
         // compare equal to themselves; a struct Triangle is re-boxed per Hit, never equal.
-        if (light.kind == K_TRI || light.kind == K_MESH) return false;
+        if (light.kind == K_TRI || light.kind == K_MESH || light.kind == K_XFORM) return false;
         return h.kind == light.kind && h.idx == light.idx;
     }
     // Sampler.sampleLight (Sampler.cs:212-296)
@@ -781,9 +1124,7 @@ struct Integrator {
         double coverage = (r * r) / (d * d);
         if (hyp < radius) coverage = 1;
         coverage = net_min(coverage, 1);
-        int mi = light.kind == K_SPHERE ? s.spheres[light.idx].mat
-               : light.kind == K_CUBE ? s.cubes[light.idx].mat
-               : light.kind == K_PLANE ? s.planes[light.idx].mat : s.tris[light.idx].mat;
+        int mi = material_index_at(s, light.kind, light.idx, point);
         // Material.MaterialAt(light, point) (Sampler.cs:292): the colour at the sampled point
         Surf sf = material_at(s, light.kind, light.idx, mi, point);
         double mm = s.mats[mi].emittance * diffuse * coverage;
@@ -997,6 +1338,31 @@ Scene* build_scene(const or_scene_desc* d) {
                                    m.reflectivity, m.transparent != 0, m.texture - 1, m.normal_texture - 1,
                                    m.bump_texture - 1, m.gloss_texture - 1, m.bump_multiplier});
     }
+    s->default_mat = (int)s->mats.size();   // `new Material()`: all zero
+    s->mats.push_back(Material{C{0, 0, 0}, 0, 0, 0, 0, 0, false, -1, -1, -1, -1, 0});
+    for (int i = 0; i < d->num_sdf_nodes; i++) {
+        const or_sdf_node& n = d->sdf_nodes[i];
+        SdfNode o;
+        o.op = n.op;
+        for (int k = 0; k < n.num_children; k++) o.kids.push_back(d->sdf_children[n.first_child + k]);
+        std::memcpy(o.p, n.params, sizeof o.p);
+        std::memcpy(o.M, n.matrix, sizeof o.M);
+        std::memcpy(o.Inv, n.inverse, sizeof o.Inv);
+        s->sdf.push_back(std::move(o));
+    }
+    for (int i = 0; i < d->num_sdf_shapes; i++)
+        s->sdf_shapes.push_back(SdfShape{d->sdf_shapes[i].root, d->sdf_shapes[i].material, Box{vzero(), vzero()}});
+    for (auto& sh : s->sdf_shapes) sh.box = sdf_box(*s, sh.root);   // SDFShape.BoundingBox = SDF.BoundingBox()
+    for (int i = 0; i < d->num_volumes; i++) {
+        const or_volume& v = d->volumes[i];
+        Volume o;
+        o.w = v.w; o.h = v.h; o.d = v.d; o.zscale = v.zscale;
+        o.data.assign(v.data, v.data + (size_t)v.w * v.h * v.d);
+        for (int k = 0; k < v.num_windows; k++)
+            o.windows.push_back(VolWindow{v.windows[k].lo, v.windows[k].hi, v.windows[k].material});
+        o.box = Box{vload(v.box_min), vload(v.box_max)};
+        s->volumes.push_back(std::move(o));
+    }
     for (int i = 0; i < d->num_textures; i++) {
         const or_texture& t = d->textures[i];
         s->texs.push_back(Tex{t.width, t.height, std::vector<double>(t.data, t.data + 3 * (size_t)t.width * t.height)});
@@ -1026,18 +1392,20 @@ Scene* build_scene(const or_scene_desc* d) {
         s->mesh_first.push_back(d->mesh_first[i]);
         s->mesh_count.push_back(d->mesh_count[i]);
     }
+    for (int i = 0; i < d->num_transformed; i++) {
+        const or_transformed_shape& x = d->transformed[i];
+        Xform o;
+        o.kind = x.shape_kind; o.idx = x.shape_index;
+        std::memcpy(o.M, x.matrix, sizeof o.M);
+        std::memcpy(o.Inv, x.inverse, sizeof o.Inv);
+        s->xforms.push_back(o);
+    }
+    for (auto& x : s->xforms) x.box = mat_box(x.M, shape_box(*s, ShapeRef{x.kind, x.idx}));  // TransformedShape.BoundingBox
     for (int i = 0; i < d->num_shapes; i++) {
         ShapeRef r{d->shape_kind[i], d->shape_index[i]};
         s->shapes.push_back(r);
         // Scene.Add (Scene.cs:29-38): MaterialAt(new Vector()).Emittance > 0; Mesh.MaterialAt is `default`.
-        double em = 0;
-        switch (r.kind) {
-            case K_SPHERE: em = s->mats[s->spheres[r.idx].mat].emittance; break;
-            case K_CUBE: em = s->mats[s->cubes[r.idx].mat].emittance; break;
-            case K_PLANE: em = s->mats[s->planes[r.idx].mat].emittance; break;
-            case K_TRI: em = s->mats[s->tris[r.idx].mat].emittance; break;
-            default: em = 0; break;
-        }
+        double em = s->mats[(size_t)material_index_at(*s, r.kind, r.idx, vzero())].emittance;
         if (em > 0) s->lights.push_back(r);
     }
     s->env = C{d->env_color[0], d->env_color[1], d->env_color[2]};
@@ -1245,6 +1613,18 @@ int32_t or_hit_surface(void* scene, const float origin[3], const float dir[3], d
     out_color[0] = info.color.r; out_color[1] = info.color.g; out_color[2] = info.color.b;
     *out_gloss = info.gloss;
     return 1;
+}
+
+double or_sdf_evaluate(void* scene, int32_t node, const float p[3]) { return sdf_eval(*(Scene*)scene, node, vload(p)); }
+
+double or_volume_sample(void* scene, int32_t volume, double x, double y, double z) {
+    return vol_sample(((Scene*)scene)->volumes[(size_t)volume], x, y, z);
+}
+
+void or_shape_box(void* scene, int32_t kind, int32_t index, float out_min[3], float out_max[3]) {
+    Box b = shape_box(*(Scene*)scene, ShapeRef{kind, index});
+    out_min[0] = b.min.x; out_min[1] = b.min.y; out_min[2] = b.min.z;
+    out_max[0] = b.max.x; out_max[1] = b.max.y; out_max[2] = b.max.z;
 }
 
 uint64_t or_camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample) {

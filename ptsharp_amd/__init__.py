@@ -7,10 +7,13 @@ per-pixel work.  There is no CPU fallback: the product path fails loudly when
 the HIP library is missing.
 """
 from .geometry import Box, Colour, Matrix, Util, Vector
-from .scene import (OBJ, Camera, ColorTexture, Cube, DefaultSampler, LightMode, Material, Mesh, Plane, Scene, SpecularMode,
-                    Sphere, Triangle)
+from .scene import (OBJ, Camera, CapsuleSDF, ColorTexture, Cube, CubeSDF, CylinderSDF, DefaultSampler, DifferenceSDF,
+                    IntersectionSDF, LightMode, Material, Mesh, Plane, RepeatSDF, ScaleSDF, Scene, SDFShape, SpecularMode,
+                    Sphere, SphereSDF, TorusSDF, TransformedShape, TransformSDF, Triangle, UnionSDF, Volume, VolumeWindow)
 from .renderer import Buffer, Channel, Renderer, tiles_for_rank, write_png
 
 __all__ = ["Box", "Colour", "Matrix", "Util", "Vector", "Camera", "ColorTexture", "Cube", "DefaultSampler", "LightMode", "Material",
-           "Mesh", "OBJ", "Plane", "Scene", "SpecularMode", "Sphere", "Triangle", "Buffer", "Channel", "Renderer",
+           "Mesh", "OBJ", "Plane", "Scene", "SpecularMode", "Sphere", "Triangle", "SDFShape", "SphereSDF", "CubeSDF",
+           "CylinderSDF", "CapsuleSDF", "TorusSDF", "TransformSDF", "ScaleSDF", "UnionSDF", "DifferenceSDF",
+           "IntersectionSDF", "RepeatSDF", "Volume", "VolumeWindow", "TransformedShape", "Buffer", "Channel", "Renderer",
            "tiles_for_rank", "write_png"]

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptsharp_hip.so")
 
-ABI_VERSION = 2   # PT_ABI_VERSION
+ABI_VERSION = 3   # PT_ABI_VERSION
 PT_OK = 0
 PT_ERR_INVALID_ARG = -1
 PT_ERR_HIP = -2
@@ -27,6 +27,7 @@ PASS_KERNEL_TIMING = 1
 K_CAMERA, K_TRACE, K_SHADE, K_SHADOW, K_FINALIZE, K_MEGAKERNEL = range(6)
 
 SHAPE_SPHERE, SHAPE_CUBE, SHAPE_PLANE, SHAPE_TRIANGLE, SHAPE_MESH = 0, 1, 2, 3, 4
+SHAPE_SDF, SHAPE_VOLUME, SHAPE_TRANSFORMED = 5, 6, 7
 
 _f = C.POINTER(C.c_float)
 _d = C.POINTER(C.c_double)
@@ -45,6 +46,30 @@ class pt_material(C.Structure):
                 ("bump_multiplier", C.c_double)]
 
 
+class pt_sdf_node(C.Structure):
+    _fields_ = [("op", C.c_int32), ("num_children", C.c_int32), ("first_child", C.c_int32), ("_pad", C.c_int32),
+                ("params", C.c_double * 8), ("matrix", C.c_double * 16), ("inverse", C.c_double * 16)]
+
+
+class pt_sdf_shape(C.Structure):
+    _fields_ = [("root", C.c_int32), ("material", C.c_int32)]
+
+
+class pt_volume_window(C.Structure):
+    _fields_ = [("lo", C.c_double), ("hi", C.c_double), ("material", C.c_int32), ("_pad", C.c_int32)]
+
+
+class pt_volume(C.Structure):
+    _fields_ = [("w", C.c_int32), ("h", C.c_int32), ("d", C.c_int32), ("num_windows", C.c_int32),
+                ("zscale", C.c_double), ("data", _d), ("windows", C.POINTER(pt_volume_window)),
+                ("box_min", C.c_float * 3), ("box_max", C.c_float * 3)]
+
+
+class pt_transformed_shape(C.Structure):
+    _fields_ = [("shape_kind", C.c_int32), ("shape_index", C.c_int32), ("matrix", C.c_double * 16),
+                ("inverse", C.c_double * 16)]
+
+
 class pt_scene_desc(C.Structure):
     _fields_ = [
         ("num_materials", C.c_int32), ("materials", C.POINTER(pt_material)),
@@ -59,6 +84,10 @@ class pt_scene_desc(C.Structure):
         ("num_textures", C.c_int32), ("textures", C.POINTER(pt_texture)),
         ("tri_t1", _f), ("tri_t2", _f), ("tri_t3", _f),
         ("env_texture", C.c_int32), ("_pad", C.c_int32), ("env_texture_angle", C.c_double),
+        ("num_sdf_nodes", C.c_int32), ("sdf_nodes", C.POINTER(pt_sdf_node)), ("sdf_children", _i),
+        ("num_sdf_shapes", C.c_int32), ("sdf_shapes", C.POINTER(pt_sdf_shape)),
+        ("num_volumes", C.c_int32), ("volumes", C.POINTER(pt_volume)),
+        ("num_transformed", C.c_int32), ("transformed", C.POINTER(pt_transformed_shape)),
     ]
 
 

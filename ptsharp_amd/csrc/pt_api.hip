@@ -247,6 +247,122 @@ void light_sphere_of_box(pt::v3 mn, pt::v3 mx, pt::DevLight& L) {
     L.radius = (double)pt::lengthf(pt::sub(mn, center));
 }
 
+// ---- §8f row 4 host side: SDF tree → postfix program, boxes (IShape.BoundingBox)
+struct HostBox { pt::v3 mn, mx; };
+inline HostBox box_extend(const HostBox& a, const HostBox& b) { return HostBox{pt::vmin(a.mn, b.mn), pt::vmax(a.mx, b.mx)}; }
+inline HostBox box_mul(const double* m, const HostBox& b) { HostBox r; pt::mat_box(m, b.mn, b.mx, r.mn, r.mx); return r; }
+inline void rows12(const double* m16, double* out) { for (int k = 0; k < 12; k++) out[k] = m16[k]; }
+
+// SDF.BoundingBox per node (SDF.cs:136-139, 191-195, 214-219, 280-284, 313-318, 344-353, 374-382, 413-434, 470-476, 509-530, 555-558)
+HostBox sdf_box(const pt_scene_desc* d, int ni) {
+    const pt_sdf_node& n = d->sdf_nodes[ni];
+    const double* P = n.params;
+    switch (n.op) {
+        case PT_SDF_SPHERE: { double r = P[0]; return HostBox{pt::mk(-r, -r, -r), pt::mk(r, r, r)}; }
+        case PT_SDF_CUBE: {
+            double x = (double)(float)P[0] / 2, y = (double)(float)P[1] / 2, z = (double)(float)P[2] / 2;
+            return HostBox{pt::mk(-x, -y, -z), pt::mk(x, y, z)};
+        }
+        case PT_SDF_CYLINDER: { double r = P[0], h = P[1] / 2; return HostBox{pt::mk(-r, -h, -r), pt::mk(r, h, r)}; }
+        case PT_SDF_CAPSULE: {
+            pt::v3 A = pt::mk(P[0], P[1], P[2]), B = pt::mk(P[3], P[4], P[5]);
+            pt::v3 a = pt::vmin(A, B), b = pt::vmax(A, B);
+            double r = P[6];   // SubScalar / AddScalar
+            return HostBox{pt::mk((double)a.x - r, (double)a.y - r, (double)a.z - r),
+                           pt::mk((double)b.x + r, (double)b.y + r, (double)b.z + r)};
+        }
+        case PT_SDF_TORUS: { double a = P[1], b = P[1] + P[0]; return HostBox{pt::mk(-b, -b, a), pt::mk(b, b, a)}; }
+        case PT_SDF_TRANSFORM: return box_mul(n.matrix, sdf_box(d, d->sdf_children[n.first_child]));
+        case PT_SDF_SCALE: {
+            double f = (double)(float)P[0];   // new Matrix().Scale(new Vector(f, f, f))
+            const double m[16] = {f, 0, 0, 0, 0, f, 0, 0, 0, 0, f, 0, 0, 0, 0, 1};
+            return box_mul(m, sdf_box(d, d->sdf_children[n.first_child]));
+        }
+        case PT_SDF_UNION:
+        case PT_SDF_INTERSECTION: {
+            HostBox r{pt::zero3(), pt::zero3()};
+            for (int i = 0; i < n.num_children; i++) {
+                HostBox b = sdf_box(d, d->sdf_children[n.first_child + i]);
+                r = i == 0 ? b : box_extend(r, b);
+            }
+            return r;
+        }
+        case PT_SDF_DIFFERENCE:
+            return n.num_children > 0 ? sdf_box(d, d->sdf_children[n.first_child]) : HostBox{pt::zero3(), pt::zero3()};
+        default: return HostBox{pt::zero3(), pt::zero3()};   // RepeatSDF: new Box()
+    }
+}
+
+// Postfix program of an SDF tree (pt_ext.h SdfOp): SDF.Evaluate's recursion unrolled.
+struct SdfCompiler {
+    const pt_scene_desc* d;
+    std::vector<pt::DevSdfIns> prog;
+    std::vector<double> params;
+    int ps = 0, vs = 0, max_ps = 0, max_vs = 0;
+    void emit(int op, const double* P, int np) {
+        prog.push_back(pt::DevSdfIns{op, (int32_t)params.size()});
+        for (int k = 0; k < np; k++) params.push_back(P[k]);
+        if (np == 0) params.push_back(0.0);
+    }
+    void value() { vs++; max_vs = std::max(max_vs, vs); }
+    void node(int ni) {
+        const pt_sdf_node& n = d->sdf_nodes[ni];
+        const double* P = n.params;
+        auto child = [&](int k) { return d->sdf_children[n.first_child + k]; };
+        switch (n.op) {
+            case PT_SDF_SPHERE: emit(pt::SDF_LEAF_SPHERE, P, 2); value(); return;
+            case PT_SDF_CUBE: {   // Size is a Vector: its halves are taken from the fp32 values
+                const double q[3] = {(double)(float)P[0], (double)(float)P[1], (double)(float)P[2]};
+                emit(pt::SDF_LEAF_CUBE, q, 3); value(); return;
+            }
+            case PT_SDF_CYLINDER: emit(pt::SDF_LEAF_CYLINDER, P, 2); value(); return;
+            case PT_SDF_CAPSULE: emit(pt::SDF_LEAF_CAPSULE, P, 8); value(); return;
+            case PT_SDF_TORUS: emit(pt::SDF_LEAF_TORUS, P, 4); value(); return;
+            case PT_SDF_TRANSFORM:
+            case PT_SDF_SCALE:
+            case PT_SDF_REPEAT: {
+                if (n.op == PT_SDF_TRANSFORM) {
+                    double inv[12];
+                    rows12(n.inverse, inv);
+                    emit(pt::SDF_PUSH_TRANSFORM, inv, 12);
+                } else if (n.op == PT_SDF_SCALE) {
+                    emit(pt::SDF_PUSH_SCALE, P, 1);
+                } else {
+                    const double st[3] = {(double)(float)P[0], (double)(float)P[1], (double)(float)P[2]};
+                    emit(pt::SDF_PUSH_REPEAT, st, 3);
+                }
+                ps++;
+                max_ps = std::max(max_ps, ps);
+                node(child(0));
+                emit(pt::SDF_POP_POINT, nullptr, 0);
+                ps--;
+                if (n.op == PT_SDF_SCALE) emit(pt::SDF_MUL, P, 1);
+                return;
+            }
+            default: {   // Union / Difference / Intersection: fold over the children in order
+                const int fold = n.op == PT_SDF_UNION ? pt::SDF_UNION : n.op == PT_SDF_DIFFERENCE ? pt::SDF_DIFFERENCE
+                                                                                               : pt::SDF_INTERSECTION;
+                if (n.num_children == 0) { emit(pt::SDF_CONST0, nullptr, 0); value(); return; }
+                node(child(0));
+                for (int k = 1; k < n.num_children; k++) {
+                    node(child(k));
+                    emit(fold, nullptr, 0);
+                    vs--;
+                }
+            }
+        }
+    }
+};
+
+// A volume view over host (validation / light registration) or device data.
+pt::DevVolume dev_volume(const pt_volume& v, const double* data, const pt::DevWindow* windows) {
+    pt::DevVolume o{};
+    o.data = data; o.windows = windows;
+    o.w = v.w; o.h = v.h; o.d = v.d; o.nwin = v.num_windows; o.zscale = v.zscale;
+    for (int k = 0; k < 3; k++) { o.bmin[k] = v.box_min[k]; o.bmax[k] = v.box_max[k]; }
+    return o;
+}
+
 int validate_scene(const pt_scene_desc* d) {
     if (!d) return fail(PT_ERR_INVALID_ARG, "scene is NULL");
     if (d->num_materials <= 0 || !d->materials) return fail(PT_ERR_INVALID_ARG, "scene has no materials");
@@ -281,13 +397,52 @@ int validate_scene(const pt_scene_desc* d) {
             return fail(PT_ERR_INVALID_ARG, "material " + std::to_string(i) + ": texture reference out of range");
     }
     if (!chk_tex(d->env_texture)) return fail(PT_ERR_INVALID_ARG, "env_texture out of range");
+    // §8f row 4
+    if (d->num_sdf_nodes < 0 || (d->num_sdf_nodes > 0 && (!d->sdf_nodes || !d->sdf_children)))
+        return fail(PT_ERR_INVALID_ARG, "bad SDF node arrays");
+    for (int i = 0; i < d->num_sdf_nodes; i++) {
+        const pt_sdf_node& n = d->sdf_nodes[i];
+        if (n.op < PT_SDF_SPHERE || n.op > PT_SDF_REPEAT) return fail(PT_ERR_INVALID_ARG, "SDF node " + std::to_string(i) + ": bad op");
+        const bool one = n.op == PT_SDF_TRANSFORM || n.op == PT_SDF_SCALE || n.op == PT_SDF_REPEAT;
+        const bool many = n.op >= PT_SDF_UNION && n.op <= PT_SDF_INTERSECTION;
+        if ((one && n.num_children != 1) || (!one && !many && n.num_children != 0) || n.num_children < 0)
+            return fail(PT_ERR_INVALID_ARG, "SDF node " + std::to_string(i) + ": wrong number of children");
+        for (int k = 0; k < n.num_children; k++) {
+            int c = d->sdf_children[n.first_child + k];
+            if (c < 0 || c >= i) return fail(PT_ERR_INVALID_ARG, "SDF node " + std::to_string(i) + ": children must precede their parent");
+        }
+    }
+    if (d->num_sdf_shapes < 0 || (d->num_sdf_shapes > 0 && !d->sdf_shapes)) return fail(PT_ERR_INVALID_ARG, "bad SDF shapes");
+    for (int i = 0; i < d->num_sdf_shapes; i++)
+        if (d->sdf_shapes[i].root < 0 || d->sdf_shapes[i].root >= d->num_sdf_nodes ||
+            d->sdf_shapes[i].material < 0 || d->sdf_shapes[i].material >= d->num_materials)
+            return fail(PT_ERR_INVALID_ARG, "SDF shape " + std::to_string(i) + ": bad root or material");
+    if (d->num_volumes < 0 || (d->num_volumes > 0 && !d->volumes)) return fail(PT_ERR_INVALID_ARG, "bad volumes");
+    for (int i = 0; i < d->num_volumes; i++) {
+        const pt_volume& v = d->volumes[i];
+        if (v.w < 1 || v.h < 1 || v.d < 1 || !v.data || v.num_windows < 0 || (v.num_windows > 0 && !v.windows))
+            return fail(PT_ERR_INVALID_ARG, "volume " + std::to_string(i) + ": bad grid or windows");
+        for (int k = 0; k < v.num_windows; k++)
+            if (v.windows[k].material < 0 || v.windows[k].material >= d->num_materials)
+                return fail(PT_ERR_INVALID_ARG, "volume " + std::to_string(i) + ": window material out of range");
+    }
+    if (d->num_transformed < 0 || (d->num_transformed > 0 && !d->transformed)) return fail(PT_ERR_INVALID_ARG, "bad transformed shapes");
+    for (int i = 0; i < d->num_transformed; i++) {
+        const pt_transformed_shape& x = d->transformed[i];
+        int lim = x.shape_kind == PT_SHAPE_SPHERE ? d->num_spheres : x.shape_kind == PT_SHAPE_CUBE ? d->num_cubes
+                : x.shape_kind == PT_SHAPE_PLANE ? d->num_planes : x.shape_kind == PT_SHAPE_SDF ? d->num_sdf_shapes
+                : x.shape_kind == PT_SHAPE_VOLUME ? d->num_volumes : -1;
+        if (lim < 0) return fail(PT_ERR_UNSUPPORTED, "transformed shape " + std::to_string(i) + ": inner kind not on the GPU path");
+        if (x.shape_index < 0 || x.shape_index >= lim) return fail(PT_ERR_INVALID_ARG, "transformed shape " + std::to_string(i) + ": inner index out of range");
+    }
     if (d->num_triangles > 0 && ((d->tri_t1 != nullptr) != (d->tri_t2 != nullptr) || (d->tri_t1 != nullptr) != (d->tri_t3 != nullptr)))
         return fail(PT_ERR_INVALID_ARG, "tri_t1/t2/t3 must be all set or all NULL");
     for (int i = 0; i < d->num_shapes; i++) {
         int k = d->shape_kind[i], j = d->shape_index[i];
         int lim = k == PT_SHAPE_SPHERE ? d->num_spheres : k == PT_SHAPE_CUBE ? d->num_cubes
                 : k == PT_SHAPE_PLANE ? d->num_planes : k == PT_SHAPE_TRIANGLE ? d->num_triangles
-                : k == PT_SHAPE_MESH ? d->num_meshes : -1;
+                : k == PT_SHAPE_MESH ? d->num_meshes : k == PT_SHAPE_SDF ? d->num_sdf_shapes
+                : k == PT_SHAPE_VOLUME ? d->num_volumes : k == PT_SHAPE_TRANSFORMED ? d->num_transformed : -1;
         if (lim < 0) return fail(PT_ERR_UNSUPPORTED, "unsupported shape kind " + std::to_string(k));
         if (j < 0 || j >= lim) return fail(PT_ERR_INVALID_ARG, "shape index out of range at shape " + std::to_string(i));
         if (k == PT_SHAPE_MESH) {
@@ -394,18 +549,135 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
                     3 * (size_t)d->textures[i].width * (size_t)d->textures[i].height * sizeof(double));
 
     // --- gather primitives in Scene.Shapes order
-    std::vector<int32_t> ana_kind, ana_scene;     // analytic prims (sphere, cube)
+    std::vector<int32_t> ana_kind, ana_scene;     // analytic prims (sphere, cube, SDF, volume, transformed)
     std::vector<int32_t> tri_src;                  // source triangle index per BVH triangle
     std::vector<int32_t> plane_scene;
     for (int i = 0; i < d->num_shapes; i++) {
         int k = d->shape_kind[i], j = d->shape_index[i];
-        if (k == PT_SHAPE_SPHERE || k == PT_SHAPE_CUBE) { ana_kind.push_back(k); ana_scene.push_back(j); }
-        else if (k == PT_SHAPE_PLANE) plane_scene.push_back(j);
+        if (k == PT_SHAPE_PLANE) plane_scene.push_back(j);
         else if (k == PT_SHAPE_TRIANGLE) tri_src.push_back(j);
-        else for (int t = 0; t < d->mesh_count[j]; t++) tri_src.push_back(d->mesh_first[j] + t);
+        else if (k == PT_SHAPE_MESH) for (int t = 0; t < d->mesh_count[j]; t++) tri_src.push_back(d->mesh_first[j] + t);
+        else { ana_kind.push_back(k); ana_scene.push_back(j); }
     }
     if ((int64_t)tri_src.size() >= (int64_t)(1u << 29) || ana_kind.size() >= (1u << 29))
         return fail(PT_ERR_UNSUPPORTED, "more than 2^29 primitives");
+
+    // --- §8f row 4 tables: SDF programs, volumes, transformed shapes
+    mats.push_back(pt::DevMaterial{});   // `new Material()` (Volume.MaterialAt's fallback)
+    for (auto& m : mats.back().color) m = 0.f;
+    mats.back().tex = mats.back().ntex = mats.back().btex = mats.back().gtex = -1;
+    const int32_t default_mat = d->num_materials;
+    SdfCompiler sdfc{d};
+    std::vector<pt::DevSdfShape> sdf_shapes((size_t)std::max(d->num_sdf_shapes, 0));
+    std::vector<HostBox> sdf_boxes(sdf_shapes.size());
+    for (size_t i = 0; i < sdf_shapes.size(); i++) {
+        pt::DevSdfShape& o = sdf_shapes[i];
+        o.begin = (int32_t)sdfc.prog.size();
+        sdfc.ps = sdfc.vs = 0;
+        sdfc.node(d->sdf_shapes[i].root);
+        o.len = (int32_t)sdfc.prog.size() - o.begin;
+        o.mat = d->sdf_shapes[i].material;
+        sdf_boxes[i] = sdf_box(d, d->sdf_shapes[i].root);   // SDFShape.BoundingBox (SDF.cs:100-103)
+        o.bmin[0] = sdf_boxes[i].mn.x; o.bmin[1] = sdf_boxes[i].mn.y; o.bmin[2] = sdf_boxes[i].mn.z;
+        o.bmax[0] = sdf_boxes[i].mx.x; o.bmax[1] = sdf_boxes[i].mx.y; o.bmax[2] = sdf_boxes[i].mx.z;
+    }
+    if (sdfc.max_ps + 1 > pt::kSdfStack || sdfc.max_vs > pt::kSdfStack)
+        return fail(PT_ERR_UNSUPPORTED, "SDF tree nested deeper than the device evaluator's stacks");
+    std::vector<pt::DevWindow> windows;
+    std::vector<size_t> vol_off, win_off;
+    size_t voxels = 0;
+    for (int i = 0; i < d->num_volumes; i++) {
+        const pt_volume& v = d->volumes[i];
+        vol_off.push_back(voxels);
+        win_off.push_back(windows.size());
+        voxels += (size_t)v.w * v.h * v.d;
+        for (int k = 0; k < v.num_windows; k++)
+            windows.push_back(pt::DevWindow{v.windows[k].lo, v.windows[k].hi, v.windows[k].material, 0});
+    }
+    std::vector<double> vox(voxels);
+    for (int i = 0; i < d->num_volumes; i++)
+        std::memcpy(vox.data() + vol_off[(size_t)i], d->volumes[i].data,
+                    (size_t)d->volumes[i].w * d->volumes[i].h * d->volumes[i].d * sizeof(double));
+    // host views (Scene.Add's MaterialAt(new Vector()) for light registration)
+    auto host_volume = [&](int i) { return dev_volume(d->volumes[i], vox.data() + vol_off[(size_t)i], windows.data() + win_off[(size_t)i]); };
+    const pt::v3 origin = pt::zero3();
+    // IShape.BoundingBox of a shape that can be analytic or inner (exact, as the reference computes it)
+    auto shape_box = [&](int k, int j) -> HostBox {
+        switch (k) {
+            case PT_SHAPE_SPHERE: {
+                const float* cc = d->sphere_center + 3 * j;
+                double r = d->sphere_radius[j];
+                return HostBox{pt::mk((double)cc[0] - r, (double)cc[1] - r, (double)cc[2] - r),
+                               pt::mk((double)cc[0] + r, (double)cc[1] + r, (double)cc[2] + r)};
+            }
+            case PT_SHAPE_CUBE: return HostBox{ld3(d->cube_min + 3 * j), ld3(d->cube_max + 3 * j)};
+            case PT_SHAPE_PLANE: return HostBox{pt::mk(-1e9, -1e9, -1e9), pt::mk(1e9, 1e9, 1e9)};
+            case PT_SHAPE_SDF: return sdf_boxes[(size_t)j];
+            case PT_SHAPE_VOLUME: return HostBox{ld3(d->volumes[j].box_min), ld3(d->volumes[j].box_max)};
+        }
+        return HostBox{pt::zero3(), pt::zero3()};
+    };
+    // IShape.MaterialAt(p) of an analytic / inner shape
+    auto shape_mat = [&](int k, int j, pt::v3 p) -> int32_t {
+        switch (k) {
+            case PT_SHAPE_SPHERE: return d->sphere_material[j];
+            case PT_SHAPE_CUBE: return d->cube_material[j];
+            case PT_SHAPE_PLANE: return d->plane_material[j];
+            case PT_SHAPE_SDF: return d->sdf_shapes[j].material;
+            case PT_SHAPE_VOLUME: { pt::DevVolume v = host_volume(j); return pt::vol_material(v, p, default_mat); }
+        }
+        return default_mat;
+    };
+    // analytic-format record of a shape (top level: ana_recs; inner of a transformed shape: ext_recs)
+    auto make_rec = [&](int k, int j, int32_t ext_mat, float4* r) {
+        if (k == PT_SHAPE_SPHERE) {
+            const float* cc = d->sphere_center + 3 * j;
+            uint64_t rb; double rad = d->sphere_radius[j]; std::memcpy(&rb, &rad, 8);
+            r[0] = f4(cc[0], cc[1], cc[2], u2f(pt::KIND_SPHERE));
+            r[1] = f4(0.f, 0.f, 0.f, u2f((uint32_t)j));
+            r[2] = f4(u2f((uint32_t)d->sphere_material[j]), u2f((uint32_t)(rb & 0xFFFFFFFFu)), u2f((uint32_t)(rb >> 32)), 0.f);
+        } else if (k == PT_SHAPE_CUBE) {
+            const float* mn = d->cube_min + 3 * j; const float* mx = d->cube_max + 3 * j;
+            r[0] = f4(mn[0], mn[1], mn[2], u2f(pt::KIND_CUBE));
+            r[1] = f4(mx[0], mx[1], mx[2], u2f((uint32_t)j));
+            r[2] = f4(u2f((uint32_t)d->cube_material[j]), 0.f, 0.f, 0.f);
+        } else if (k == PT_SHAPE_PLANE) {
+            const float* pp = d->plane_point + 3 * j; const float* nn = d->plane_normal + 3 * j;
+            r[0] = f4(pp[0], pp[1], pp[2], u2f(pt::KIND_PLANE));
+            r[1] = f4(nn[0], nn[1], nn[2], u2f((uint32_t)j));
+            r[2] = f4(u2f((uint32_t)d->plane_material[j]), 0.f, 0.f, 0.f);
+        } else {   // SDF / volume / transformed: the shape lives in its table, `ext_mat` = MaterialAt(origin)
+            const int32_t kind = k == PT_SHAPE_SDF ? pt::KIND_SDF : k == PT_SHAPE_VOLUME ? pt::KIND_VOLUME : pt::KIND_XFORM;
+            r[0] = f4(0.f, 0.f, 0.f, u2f((uint32_t)kind));
+            r[1] = f4(0.f, 0.f, 0.f, u2f((uint32_t)j));
+            r[2] = f4(u2f((uint32_t)ext_mat), u2f((uint32_t)j), 0.f, 0.f);
+        }
+    };
+    std::vector<pt::DevXform> xforms((size_t)std::max(d->num_transformed, 0));
+    std::vector<float4> ext_recs(xforms.size() * 3);
+    std::vector<HostBox> xform_boxes(xforms.size()), xform_bvh_boxes(xforms.size());
+    // Hits of marched shapes can sit just outside their box (SDF: start 1e-4 and a 1e-3 jump back;
+    // Volume: one step of 1/512 before the box): the BVH boxes are widened by that much.
+    auto march_pad = [](int k) { return k == PT_SHAPE_SDF ? 2e-3 : k == PT_SHAPE_VOLUME ? 4.0 / 512 : 0.0; };
+    for (size_t i = 0; i < xforms.size(); i++) {
+        const pt_transformed_shape& x = d->transformed[i];
+        pt::DevXform& o = xforms[i];
+        rows12(x.matrix, o.m);
+        rows12(x.inverse, o.inv);
+        o.kind = x.shape_kind == PT_SHAPE_SDF ? pt::KIND_SDF : x.shape_kind == PT_SHAPE_VOLUME ? pt::KIND_VOLUME : x.shape_kind;
+        o.rec = (int32_t)i;
+        make_rec(x.shape_kind, x.shape_index, shape_mat(x.shape_kind, x.shape_index, origin), &ext_recs[3 * i]);
+        HostBox ib = shape_box(x.shape_kind, x.shape_index);
+        xform_boxes[i] = box_mul(x.matrix, ib);   // TransformedShape.BoundingBox (TransformedShape.cs:36-39)
+        const double mp = march_pad(x.shape_kind);
+        HostBox pb{pt::mk((double)ib.mn.x - mp, (double)ib.mn.y - mp, (double)ib.mn.z - mp),
+                   pt::mk((double)ib.mx.x + mp, (double)ib.mx.y + mp, (double)ib.mx.z + mp)};
+        xform_bvh_boxes[i] = box_mul(x.matrix, pb);
+    }
+    auto shape_mat_any = [&](int k, int j, pt::v3 p) -> int32_t {   // including TransformedShape.MaterialAt
+        if (k == PT_SHAPE_TRANSFORMED) return shape_mat(d->transformed[j].shape_kind, d->transformed[j].shape_index, p);
+        return shape_mat(k, j, p);
+    };
 
     // --- triangle BVH
     const size_t nt = tri_src.size();
@@ -448,46 +720,41 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     int32_t tri_num_nodes = 0;
     if ((rc = pack_nodes(tb, tri_nodes, tri_num_nodes))) return rc;
 
-    // --- analytic BVH (spheres, cubes)
+    // --- analytic BVH (spheres, cubes, SDF shapes, volumes, transformed shapes)
     const size_t na = ana_kind.size();
     std::vector<float> amin(na * 3), amax(na * 3);
     for (size_t i = 0; i < na; i++) {
-        int j = ana_scene[i];
-        if (ana_kind[i] == PT_SHAPE_SPHERE) {
+        int k = ana_kind[i], j = ana_scene[i];
+        if (k == PT_SHAPE_SPHERE) {
             double r = d->sphere_radius[j];
-            for (int k = 0; k < 3; k++) {
-                double cc = d->sphere_center[3 * j + k];
-                amin[3 * i + k] = std::nextafter((float)(cc - r), -INFINITY);
-                amax[3 * i + k] = std::nextafter((float)(cc + r), INFINITY);
+            for (int q = 0; q < 3; q++) {
+                double cc = d->sphere_center[3 * j + q];
+                amin[3 * i + q] = std::nextafter((float)(cc - r), -INFINITY);
+                amax[3 * i + q] = std::nextafter((float)(cc + r), INFINITY);
             }
         } else {
-            for (int k = 0; k < 3; k++) { amin[3 * i + k] = d->cube_min[3 * j + k]; amax[3 * i + k] = d->cube_max[3 * j + k]; }
+            HostBox b = k == PT_SHAPE_TRANSFORMED ? xform_bvh_boxes[(size_t)j] : shape_box(k, j);
+            const double mp = k == PT_SHAPE_TRANSFORMED ? 0.0 : march_pad(k);
+            const float lo[3] = {b.mn.x, b.mn.y, b.mn.z}, hi[3] = {b.mx.x, b.mx.y, b.mx.z};
+            for (int q = 0; q < 3; q++) {
+                amin[3 * i + q] = (float)((double)lo[q] - mp);
+                amax[3 * i + q] = (float)((double)hi[q] + mp);
+            }
         }
         pad_box(&amin[3 * i], &amax[3 * i]);
     }
     pt::BvhResult ab;
     pt::build_bvh(amin.data(), amax.data(), (int64_t)na, 0, ab);
     std::vector<float4> ana_recs(na * 3);
-    std::vector<int32_t> ana_pos_of_scene_sphere(d->num_spheres > 0 ? d->num_spheres : 0, -1);
-    std::vector<int32_t> ana_pos_of_scene_cube(d->num_cubes > 0 ? d->num_cubes : 0, -1);
+    // position in ana_recs of each shape (first occurrence), per kind: Sampler's identity test
+    std::vector<std::vector<int32_t>> ana_pos(8);
+    const int32_t counts[8] = {d->num_spheres, d->num_cubes, 0, 0, 0, d->num_sdf_shapes, d->num_volumes, d->num_transformed};
+    for (int k = 0; k < 8; k++) ana_pos[(size_t)k].assign((size_t)std::max(counts[k], 0), -1);
     for (size_t i = 0; i < na; i++) {
         size_t src = ab.order[i];
-        int j = ana_scene[src];
-        if (ana_kind[src] == PT_SHAPE_SPHERE) {
-            const float* cc = d->sphere_center + 3 * j;
-            uint64_t rb; double r = d->sphere_radius[j]; std::memcpy(&rb, &r, 8);
-            ana_recs[3 * i + 0] = f4(cc[0], cc[1], cc[2], u2f(pt::KIND_SPHERE));
-            ana_recs[3 * i + 1] = f4(0.f, 0.f, 0.f, u2f((uint32_t)j));
-            ana_recs[3 * i + 2] = f4(u2f((uint32_t)d->sphere_material[j]), u2f((uint32_t)(rb & 0xFFFFFFFFu)),
-                                     u2f((uint32_t)(rb >> 32)), 0.f);
-            if (ana_pos_of_scene_sphere[(size_t)j] < 0) ana_pos_of_scene_sphere[(size_t)j] = (int32_t)i;
-        } else {
-            const float* mn = d->cube_min + 3 * j; const float* mx = d->cube_max + 3 * j;
-            ana_recs[3 * i + 0] = f4(mn[0], mn[1], mn[2], u2f(pt::KIND_CUBE));
-            ana_recs[3 * i + 1] = f4(mx[0], mx[1], mx[2], u2f((uint32_t)j));
-            ana_recs[3 * i + 2] = f4(u2f((uint32_t)d->cube_material[j]), 0.f, 0.f, 0.f);
-            if (ana_pos_of_scene_cube[(size_t)j] < 0) ana_pos_of_scene_cube[(size_t)j] = (int32_t)i;
-        }
+        int k = ana_kind[src], j = ana_scene[src];
+        make_rec(k, j, shape_mat_any(k, j, origin), &ana_recs[3 * i]);
+        if (ana_pos[(size_t)k][(size_t)j] < 0) ana_pos[(size_t)k][(size_t)j] = (int32_t)i;
     }
     std::vector<float4> ana_nodes;
     int32_t ana_num_nodes = 0;
@@ -504,30 +771,34 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         if (plane_pos_of_scene[(size_t)j] < 0) plane_pos_of_scene[(size_t)j] = (int32_t)i;
     }
 
-    // --- lights, Scene.Add order (Scene.cs:29-38)
+    // --- lights, Scene.Add order (Scene.cs:29-38): MaterialAt(new Vector()).Emittance > 0
     std::vector<pt::DevLight> lights;
     for (int i = 0; i < d->num_shapes; i++) {
         int k = d->shape_kind[i], j = d->shape_index[i];
-        int mat = k == PT_SHAPE_SPHERE ? d->sphere_material[j] : k == PT_SHAPE_CUBE ? d->cube_material[j]
-                : k == PT_SHAPE_PLANE ? d->plane_material[j] : k == PT_SHAPE_TRIANGLE ? d->tri_material[j] : -1;
-        if (mat < 0 || !(d->materials[mat].emittance > 0)) continue;  // Mesh.MaterialAt is `default` → never a light
+        int mat = k == PT_SHAPE_TRIANGLE ? d->tri_material[j] : k == PT_SHAPE_MESH ? -1 : shape_mat_any(k, j, origin);
+        if (mat < 0 || mat >= d->num_materials || !(d->materials[mat].emittance > 0)) continue;  // Mesh: `default`
         pt::DevLight L{};
         L.kind = k; L.mat = mat; L.phantom = 0;
-        if (k == PT_SHAPE_SPHERE) {
-            L.index = ana_pos_of_scene_sphere[(size_t)j];
+        if (k == PT_SHAPE_SPHERE) {   // Sampler.cs:218-223
+            L.index = ana_pos[PT_SHAPE_SPHERE][(size_t)j];
             const float* cc = d->sphere_center + 3 * j;
             L.center[0] = cc[0]; L.center[1] = cc[1]; L.center[2] = cc[2];
             L.radius = d->sphere_radius[j];
-        } else if (k == PT_SHAPE_CUBE) {
-            L.index = ana_pos_of_scene_cube[(size_t)j];
-            light_sphere_of_box(ld3(d->cube_min + 3 * j), ld3(d->cube_max + 3 * j), L);
         } else if (k == PT_SHAPE_PLANE) {
             L.index = plane_pos_of_scene[(size_t)j];
             light_sphere_of_box(pt::mk(-1e9, -1e9, -1e9), pt::mk(1e9, 1e9, 1e9), L);  // Plane.BoundingBox
-        } else {  // a directly-added struct Triangle: counted as a light, never passes the identity test
+        } else if (k == PT_SHAPE_TRIANGLE) {  // a directly-added struct Triangle: never passes the identity test
             L.index = -1; L.phantom = 1;
             pt::v3 a = ld3(d->tri_v1 + 3 * j), b = ld3(d->tri_v2 + 3 * j), cc = ld3(d->tri_v3 + 3 * j);
             light_sphere_of_box(pt::vmin(pt::vmin(a, b), cc), pt::vmax(pt::vmax(a, b), cc), L);
+        } else {   // Cube, SDFShape, Volume: class shapes; TransformedShape: a struct, never identical
+            const int32_t kind = k == PT_SHAPE_CUBE ? pt::KIND_CUBE : k == PT_SHAPE_SDF ? pt::KIND_SDF
+                               : k == PT_SHAPE_VOLUME ? pt::KIND_VOLUME : pt::KIND_XFORM;
+            L.kind = kind;
+            L.index = ana_pos[(size_t)k][(size_t)j];
+            L.phantom = k == PT_SHAPE_TRANSFORMED;
+            HostBox b = k == PT_SHAPE_TRANSFORMED ? xform_boxes[(size_t)j] : shape_box(k, j);   // light.BoundingBox()
+            light_sphere_of_box(b.mn, b.mx, L);
         }
         lights.push_back(L);
     }
@@ -550,6 +821,21 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, texs, &S.texs); if (rc) return rc;
     S.env_tex = d->env_texture - 1;
     S.env_angle = d->env_texture_angle;
+    rc = upload(c, sdfc.prog, &S.sdf_prog); if (rc) return rc;
+    rc = upload(c, sdfc.params, &S.sdf_params); if (rc) return rc;
+    rc = upload(c, sdf_shapes, &S.sdf_shapes); if (rc) return rc;
+    const double* d_vox = nullptr;
+    const pt::DevWindow* d_win = nullptr;
+    rc = upload(c, vox, &d_vox); if (rc) return rc;
+    rc = upload(c, windows, &d_win); if (rc) return rc;
+    std::vector<pt::DevVolume> vols;
+    for (int i = 0; i < d->num_volumes; i++)
+        vols.push_back(dev_volume(d->volumes[i], d_vox + vol_off[(size_t)i], d_win ? d_win + win_off[(size_t)i] : nullptr));
+    rc = upload(c, vols, &S.volumes); if (rc) return rc;
+    rc = upload(c, xforms, &S.xforms); if (rc) return rc;
+    rc = upload(c, ext_recs, &S.ext_recs); if (rc) return rc;
+    S.default_mat = default_mat;
+    S.full = (d->num_textures > 0 || d->num_sdf_shapes > 0 || d->num_volumes > 0 || d->num_transformed > 0) ? 1 : 0;
     S.tri_num_nodes = tri_num_nodes;
     S.ana_num_nodes = ana_num_nodes;
     S.num_planes = (int32_t)plane_scene.size();

@@ -31,9 +31,41 @@ __device__ __forceinline__ float tmax_bound(double t) {
     return (double)f < t ? __uint_as_float(f2u(f) + 1u) : f;
 }
 
-// Intersect one record; returns t (kHitInf = miss) and the primitive kind.
-template <bool TRI>
-__device__ __forceinline__ double prim_t(const float4* __restrict__ recs, uint32_t pos, v3 o, v3 d, int32_t& kind) {
+__device__ __forceinline__ double rec_radius(const float4* r) {
+    const float4 c = r[2];
+    return __hiloint2double((int)f2u(c.z), (int)f2u(c.y));
+}
+__device__ __forceinline__ int32_t rec_ext(const float4* r) { return (int32_t)f2u(r[2].y); }   // SDF / volume / xform index
+
+// Intersect of a shape that can sit inside a TransformedShape: Sphere, Cube, Plane,
+// SDFShape, Volume (analytic-record format).
+__device__ __noinline__ double inner_t(const DevScene& S, const float4* r, int32_t kind, v3 o, v3 d) {
+    const float4 a = r[0], b = r[1];
+    switch (kind) {
+        case KIND_SPHERE: return isect_sphere(v3{a.x, a.y, a.z}, rec_radius(r), o, d);
+        case KIND_CUBE: return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+        case KIND_PLANE: return isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+        case KIND_SDF: return sdf_t(S.sdf_prog, S.sdf_params, S.sdf_shapes[rec_ext(r)], o, d);
+        case KIND_VOLUME: return vol_t(S.volumes[rec_ext(r)], o, d);
+    }
+    return kHitInf;
+}
+// TransformedShape.Intersect (TransformedShape.cs:43-73) up to hit.T: the inner hit mapped
+// back to world space, T = |position - origin| (fp32 Length).
+__device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 o, v3 d) {
+    const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);   // Matrix.Inverse().MulRay
+    const float4* ir = S.ext_recs + 3 * (size_t)X.rec;
+    const double t = inner_t(S, ir, X.kind, so, sd);
+    if (!(t < kHitInf)) return kHitInf;
+    const v3 position = mat_position(X.m, add(so, muls(sd, t)));
+    return (double)lengthf(sub(position, o));
+}
+
+// Intersect one record; returns t (kHitInf = miss) and the primitive kind.  FULL adds
+// the §8f row 4 kinds of the analytic BVH (SDF, volume, transformed shape).
+template <bool TRI, bool FULL = false>
+__device__ __forceinline__ double prim_t(const DevScene& S, const float4* __restrict__ recs, uint32_t pos, v3 o, v3 d,
+                                         int32_t& kind) {
     const float4* r = recs + 3 * (size_t)pos;
     if (TRI) {
         float4 a = r[0], b = r[1], c = r[2];
@@ -42,12 +74,10 @@ __device__ __forceinline__ double prim_t(const float4* __restrict__ recs, uint32
     }
     float4 a = r[0], b = r[1];
     kind = (int32_t)f2u(a.w);
-    if (kind == KIND_SPHERE) {
-        float4 c = r[2];
-        double radius = __hiloint2double((int)f2u(c.z), (int)f2u(c.y));
-        return isect_sphere(v3{a.x, a.y, a.z}, radius, o, d);
-    }
-    return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+    if (kind == KIND_SPHERE) return isect_sphere(v3{a.x, a.y, a.z}, rec_radius(r), o, d);
+    if (!FULL || kind == KIND_CUBE) return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+    if (kind == KIND_XFORM) return xform_t(S, S.xforms[rec_ext(r)], o, d);
+    return inner_t(S, r, kind, o, d);
 }
 
 // Per-lane traversal stacks.  LdsStack: all kMaxDepth entries in LDS (column
@@ -129,8 +159,8 @@ __device__ __forceinline__ void cswap(float& ka, uint32_t& va, float& kb, uint32
 // the nearest descended and the others pushed far-to-near on the per-lane stack
 // (LdsStack / SpillStack).  The builder bounds every path's pushes by kMaxDepth.
 // ANY: stop at the first primitive with t < best.t (shadow visibility).
-template <bool TRI, bool COUNT, bool ANY, class STK>
-__device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32_t num_nodes,
+template <bool TRI, bool COUNT, bool ANY, bool FULL, class STK>
+__device__ __forceinline__ bool traverse(const DevScene& S, const float4* __restrict__ nodes, int32_t num_nodes,
                                          const float4* __restrict__ recs, v3 o, v3 d, v3 invd, HitRec& best,
                                          const STK& stack, Counters& ctr) {
     if (num_nodes <= 0) return false;
@@ -167,7 +197,7 @@ __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32
             for (uint32_t k = 0; k < cnt; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
-                double t = prim_t<TRI>(recs, first + k, o, d, kind);
+                double t = prim_t<TRI, FULL>(S, recs, first + k, o, d, kind);
                 if (t < best.t) {
                     if (ANY) return true;
                     best.t = t; best.kind = kind; best.idx = (int32_t)(first + k);
@@ -183,7 +213,7 @@ __device__ __forceinline__ bool traverse(const float4* __restrict__ nodes, int32
 }
 
 // Scene.Intersect (Scene.cs:75-79): closest hit over planes, analytic BVH, triangle BVH.
-template <bool COUNT, class STK>
+template <bool COUNT, bool FULL, class STK>
 __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK& stack, Counters& ctr) {
     ctr.rays++;
     HitRec best{kHitInf, -1, -1};
@@ -193,25 +223,26 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         if (t < best.t) { best.t = t; best.kind = KIND_PLANE; best.idx = i; }
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    traverse<false, COUNT, false>(S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
-    traverse<true, COUNT, false>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr);
+    traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
+    traverse<true, COUNT, false, FULL>(S, S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr);
     return best;
 }
 
 // t of the light's own primitive along (o, d), exactly as the closest-hit query computes it.
+template <bool FULL>
 __device__ __forceinline__ double light_t(const DevScene& S, const DevLight& L, v3 o, v3 d) {
     if (L.kind == KIND_PLANE) {
         float4 a = S.planes[2 * L.index], b = S.planes[2 * L.index + 1];
         return isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
     }
     int32_t kind;
-    return prim_t<false>(S.ana_recs, (uint32_t)L.index, o, d, kind);
+    return prim_t<false, FULL>(S, S.ana_recs, (uint32_t)L.index, o, d, kind);
 }
 
 // Shadow visibility (Sampler.cs:261-265): the reference takes the nearest hit and
 // compares it with the light by reference.  Equivalent query: the light's own t,
 // then "is any primitive strictly nearer" (any-hit, early exit).  Counts one ray.
-template <bool COUNT, class STK>
+template <bool COUNT, bool FULL, class STK>
 __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight& L, v3 o, v3 d, const STK& stack,
                                               Counters& ctr) {
     ctr.rays++;
@@ -220,10 +251,10 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         // traces the ray, so trace it (the answer is "not visible" either way)
         HitRec h{kHitInf, -1, -1};
         v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-        traverse<true, COUNT, true>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, h, stack, ctr);
+        traverse<true, COUNT, true, FULL>(S, S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, h, stack, ctr);
         return false;
     }
-    double tl = light_t(S, L, o, d);
+    double tl = light_t<FULL>(S, L, o, d);
     if (!(tl < kHitInf)) return false;
     HitRec best{tl, -1, -1};
     for (int i = 0; i < S.num_planes; i++) {
@@ -231,9 +262,9 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    if (traverse<false, COUNT, true>(S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr))
+    if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr))
         return false;
-    if (traverse<true, COUNT, true>(S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr))
+    if (traverse<true, COUNT, true, FULL>(S, S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr))
         return false;
     return true;
 }
@@ -300,8 +331,9 @@ __device__ __forceinline__ void tri_uvs(const DevScene& S, int idx, v3& t1, v3& 
 }
 
 // IShape.UVector (Sphere.cs:62-69 with its p.Y-for-p.Z slip, Cube.cs:49-53, Plane.cs:52-55,
-// Triangle.cs:127-136) of the primitive at record `idx`.
-__device__ inline v3 shape_uv(const DevScene& S, int kind, int idx, v3 p) {
+// Triangle.cs:127-136; SDFShape / Volume give 0) of the primitive at record `idx` of `recs`
+// (default: the analytic records).
+__device__ inline v3 shape_uv(const DevScene& S, int kind, int idx, v3 p, const float4* recs = nullptr) {
     if (kind == KIND_TRI) {
         const float4* r = S.tri_recs + 3 * (size_t)idx;
         const float4 a = r[0], b = r[1], c = r[2];
@@ -312,8 +344,8 @@ __device__ inline v3 shape_uv(const DevScene& S, int kind, int idx, v3 p) {
         const v3 n = add(add(add(zero3(), muls(t1, u)), muls(t2, v)), muls(t3, w));
         return v3{n.x, n.y, 0.f};
     }
-    if (kind == KIND_PLANE) return zero3();
-    const float4* r = S.ana_recs + 3 * (size_t)idx;
+    if (kind != KIND_SPHERE && kind != KIND_CUBE) return zero3();
+    const float4* r = (recs ? recs : S.ana_recs) + 3 * (size_t)idx;
     const float4 a = r[0], b = r[1];
     if (kind == KIND_SPHERE) {
         const v3 q = sub(p, v3{a.x, a.y, a.z});
@@ -327,16 +359,16 @@ __device__ inline v3 shape_uv(const DevScene& S, int kind, int idx, v3 p) {
     return v3{q.x, q.z, 0.f};
 }
 
-// Material.MaterialAt (Material.cs:124-138): the colour and gloss seen at p.  TEX = the
+// Material.MaterialAt (Material.cs:124-138): the colour and gloss seen at p.  FULL = the
 // scene has textures: kernels are instantiated both ways, so untextured scenes run the
 // shading code without any texture path (no extra registers in the hot kernels).
-template <bool TEX>
+template <bool FULL>
 __device__ __forceinline__ void surface_at(const DevScene& S, const DevMaterial& m, int kind, int idx, v3 p,
-                                           float col[3], double& gloss) {
+                                           float col[3], double& gloss, const float4* recs = nullptr) {
     col[0] = m.color[0]; col[1] = m.color[1]; col[2] = m.color[2];
     gloss = m.gloss;
-    if (!TEX || (m.tex < 0 && m.gtex < 0)) return;
-    const v3 uv = shape_uv(S, kind, idx, p);
+    if (!FULL || (m.tex < 0 && m.gtex < 0)) return;
+    const v3 uv = shape_uv(S, kind, idx, p, recs);
     double c[3];
     if (m.tex >= 0) {
         tex_sample(S.texs[m.tex], uv.x, uv.y, c);
@@ -385,9 +417,9 @@ __device__ __noinline__ v3 tri_normal_mapped(const DevScene& S, const DevMateria
 }
 
 // sampleEnvironment (Sampler.cs:177-189)
-template <bool TEX>
+template <bool FULL>
 __device__ __forceinline__ float3 environment(const DevScene& S, v3 d) {
-    if (!TEX || S.env_tex < 0) return make_float3(S.env[0], S.env[1], S.env[2]);
+    if (!FULL || S.env_tex < 0) return make_float3(S.env[0], S.env[1], S.env[2]);
     double u = atan2((double)d.z, (double)d.x) + S.env_angle;
     double v = atan2((double)d.y, (double)lengthf(v3{d.x, 0.f, d.z}));
     u = (u + kPi) / (2 * kPi);
@@ -405,8 +437,55 @@ struct Shade {
     double gloss;    // and gloss (gloss texture applied)
 };
 
+// NormalAt / MaterialAt of an analytic-format record (kinds that can be a TransformedShape's inner shape).
+__device__ inline v3 inner_normal(const DevScene& S, const float4* r, int32_t kind, v3 p) {
+    const float4 a = r[0], b = r[1];
+    switch (kind) {
+        case KIND_SPHERE: return normalize(sub(p, v3{a.x, a.y, a.z}));                 // Sphere.NormalAt
+        case KIND_CUBE: return cube_normal(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, p);    // Cube.NormalAt
+        case KIND_PLANE: return v3{b.x, b.y, b.z};                                      // Plane.NormalAt
+        case KIND_SDF: return sdf_normal(S.sdf_prog, S.sdf_params, S.sdf_shapes[rec_ext(r)], p);
+        default: return vol_normal(S.volumes[rec_ext(r)], p);
+    }
+}
+__device__ inline int32_t inner_material(const DevScene& S, const float4* r, int32_t kind, v3 p) {
+    if (kind == KIND_VOLUME) return vol_material(S.volumes[rec_ext(r)], p, S.default_mat);
+    return (int32_t)f2u(r[2].x);
+}
+
+// Hit.Info for the §8f row 4 kinds.  SDFShape / Volume: the normal flips but `inside`
+// stays false (Hit.cs:42-49).  TransformedShape: the HitInfo its Intersect builds
+// (TransformedShape.cs:52-70), recomputed from the same inner intersect.
+__device__ __noinline__ void ext_hit_info(const DevScene& S, const HitRec& h, v3 o, v3 d, Shade& s) {
+    const float4* r = S.ana_recs + 3 * (size_t)h.idx;
+    v3 n;
+    if (h.kind == KIND_XFORM) {
+        const DevXform& X = S.xforms[rec_ext(r)];
+        const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
+        const float4* ir = S.ext_recs + 3 * (size_t)X.rec;
+        const double t = inner_t(S, ir, X.kind, so, sd);
+        const v3 sp = add(so, muls(sd, t));
+        const v3 sn = inner_normal(S, ir, X.kind, sp);
+        s.pos = mat_position(X.m, sp);
+        n = mat_direction_t(X.inv, sn);   // Matrix.Inverse().Transpose().MulDirection
+        s.mat = inner_material(S, ir, X.kind, sp);
+        surface_at<true>(S, S.mats[s.mat], X.kind, X.rec, sp, s.col, s.gloss, S.ext_recs);
+        s.inside = 0;
+        if (dot(sn, sd) > 0) { n = neg(n); s.inside = 1; }
+        s.nrm = n;
+        return;
+    }
+    s.pos = add(o, muls(d, h.t));
+    n = inner_normal(S, r, h.kind, s.pos);
+    s.mat = inner_material(S, r, h.kind, s.pos);
+    surface_at<true>(S, S.mats[s.mat], h.kind, h.idx, s.pos, s.col, s.gloss);
+    s.inside = 0;
+    if (dot(n, d) > 0) n = neg(n);
+    s.nrm = n;
+}
+
 // Hit.Info (Hit.cs:26-55): position (fp32 re-rounded), NormalAt, MaterialAt, flip.
-template <bool COUNT, bool TEX>
+template <bool COUNT, bool FULL>
 __device__ __forceinline__ Shade hit_info(const DevScene& S, const HitRec& h, v3 o, v3 d, Counters& ctr) {
     Shade s;
     s.pos = add(o, muls(d, h.t));
@@ -421,20 +500,23 @@ __device__ __forceinline__ Shade hit_info(const DevScene& S, const HitRec& h, v3
         const DevMaterial& m = S.mats[s.mat];
         const v3 v1{a.x, a.y, a.z}, e1{a.w, b.x, b.y}, e2{b.z, b.w, c.x};
         const v3 n1{x.x, x.y, x.z}, n2{x.w, y.x, y.y}, n3{y.z, y.w, z.x};
-        if (!TEX || (m.ntex < 0 && m.btex < 0)) n = tri_normal(v1, e1, e2, n1, n2, n3, s.pos);
+        if (!FULL || (m.ntex < 0 && m.btex < 0)) n = tri_normal(v1, e1, e2, n1, n2, n3, s.pos);
         else n = tri_normal_mapped(S, m, h.idx, v1, e1, e2, n1, n2, n3, s.pos);
     } else if (h.kind == KIND_PLANE) {
         float4 a = S.planes[2 * h.idx], b = S.planes[2 * h.idx + 1];
         n = v3{b.x, b.y, b.z};
         s.mat = (int32_t)f2u(a.w);
-    } else {
+    } else if (!FULL || h.kind == KIND_SPHERE || h.kind == KIND_CUBE) {
         const float4* r = S.ana_recs + 3 * (size_t)h.idx;
         float4 a = r[0], b = r[1], c = r[2];
         if (h.kind == KIND_SPHERE) n = normalize(sub(s.pos, v3{a.x, a.y, a.z}));   // Sphere.NormalAt
         else n = cube_normal(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, s.pos);           // Cube.NormalAt
         s.mat = (int32_t)f2u(c.x);
+    } else {
+        ext_hit_info(S, h, o, d, s);
+        return s;
     }
-    surface_at<TEX>(S, S.mats[s.mat], h.kind, h.idx, s.pos, s.col, s.gloss);
+    surface_at<FULL>(S, S.mats[s.mat], h.kind, h.idx, s.pos, s.col, s.gloss);
     s.inside = 0;
     if (dot(n, d) > 0) { n = neg(n); s.inside = 1; }
     s.nrm = n;
@@ -507,7 +589,7 @@ __device__ __forceinline__ void bounce_dir(const DevMaterial& m, const Shade& sh
 // direction and the colour the light contributes if it is the nearest hit
 // (coverage depends only on the light centre/radius, so it is computed here).
 // Returns false when diffuse <= 0 (no shadow ray is cast).
-template <bool TEX>
+template <bool FULL>
 __device__ __forceinline__ bool light_setup(const DevScene& S, const DevSampler& smp, const DevLight& L, v3 o, v3 n,
                                             uint64_t key, v3& dir, float3& contrib) {
     v3 center{L.center[0], L.center[1], L.center[2]};
@@ -538,11 +620,15 @@ __device__ __forceinline__ bool light_setup(const DevScene& S, const DevSampler&
     double coverage = (s * s) / (1 - s * s);
     if (hyp < radius) coverage = 1;
     coverage = net_min(coverage, 1);
-    // Material.MaterialAt(light, point) (Sampler.cs:292): a textured light's colour at the sampled point
-    const DevMaterial& m = S.mats[L.mat];
+    // Material.MaterialAt(light, point) (Sampler.cs:292): a textured light's colour, a volume
+    // light's window, at the sampled point
+    int32_t mat = L.mat;
+    if (FULL && L.kind == KIND_VOLUME)
+        mat = vol_material(S.volumes[rec_ext(S.ana_recs + 3 * (size_t)L.index)], point, S.default_mat);
+    const DevMaterial& m = S.mats[mat];
     float col[3] = {m.color[0], m.color[1], m.color[2]};
     double gl;
-    if (!L.phantom) surface_at<TEX>(S, m, L.kind, L.index, point, col, gl);
+    if (!L.phantom) surface_at<FULL>(S, m, L.kind, L.index, point, col, gl);
     float mm = (float)((double)m.emittance * diffuse * coverage);
     contrib = make_float3(col[0] * mm, col[1] * mm, col[2] * mm);
     return true;

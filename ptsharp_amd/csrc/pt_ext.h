@@ -1,0 +1,315 @@
+// pt_ext.h — §8f row 4 shapes on the render path: SDFShape (SDF.cs), Volume
+// (Volume.cs) and TransformedShape (TransformedShape.cs).
+//
+// Layout in HBM (pt_api.hip builds it):
+//   SDF trees are compiled on the host into one postfix program per SDFShape: point-
+//   stack pushes for TransformSDF / ScaleSDF / RepeatSDF, a leaf op per primitive SDF
+//   and a binary fold per Union / Difference / Intersection child, so the device
+//   evaluates SDF.Evaluate's recursion with two small stacks and no calls.
+//   Volumes keep the C# voxel grid (fp64 Data[x + y*W + z*W*H]) and windows.
+//   A TransformedShape holds Matrix (3 rows) and Inverse (3 rows) in fp64 and points
+//   at an object-space record of its inner shape (the analytic-record format).
+//
+// Every function restates its reference lines with the same fp32 Vector / fp64
+// scalar rounding sequence (pt_math.h); host and device share them (PT_HD).
+#pragma once
+#include <stdint.h>
+
+#include "pt_math.h"
+
+#pragma clang fp contract(off)
+
+namespace pt {
+
+enum SdfOp : int32_t {
+    SDF_LEAF_SPHERE = 0, SDF_LEAF_CUBE, SDF_LEAF_CYLINDER, SDF_LEAF_CAPSULE, SDF_LEAF_TORUS,
+    SDF_PUSH_TRANSFORM,   // point ← Inverse.MulPosition(point)          (TransformSDF, SDF.cs:338-342)
+    SDF_PUSH_SCALE,       // point ← point.DivScalar(Factor)             (ScaleSDF, SDF.cs:369-372)
+    SDF_PUSH_REPEAT,      // point ← point.Mod(Step).Sub(Step / 2)       (RepeatSDF, SDF.cs:549-553)
+    SDF_POP_POINT,
+    SDF_MUL,              // value ← value · Factor                      (ScaleSDF)
+    SDF_UNION,            // fold: d < result ? d : result               (SDF.cs:398-411)
+    SDF_DIFFERENCE,       // fold: -d > result ? -d : result             (SDF.cs:451-468)
+    SDF_INTERSECTION,     // fold: d > result ? d : result               (SDF.cs:493-507)
+    SDF_CONST0            // an empty Union / Difference / Intersection returns 0
+};
+constexpr int kSdfStack = 8;   // point / value stack depth of a compiled program (host-checked)
+
+struct DevSdfIns {
+    int32_t op;
+    int32_t param;   // offset into sdf_params (doubles)
+};
+struct DevSdfShape {
+    int32_t begin, len;   // program range
+    int32_t mat, _pad;
+    float bmin[3], bmax[3];   // SDFShape.BoundingBox (SDF.BoundingBox of the root)
+};
+struct DevWindow {
+    double lo, hi;
+    int32_t mat, _pad;
+};
+struct DevVolume {
+    const double* data;   // [d][h][w]
+    const DevWindow* windows;
+    int32_t w, h, d, nwin;
+    double zscale;
+    float bmin[3], bmax[3];
+};
+struct DevXform {
+    double m[12];     // Matrix rows 1-3 (row 4 is 0 0 0 1 for affine transforms; MulPosition ignores it)
+    double inv[12];   // Inverse rows 1-3
+    int32_t kind;     // inner shape kind (KIND_SPHERE, KIND_CUBE, KIND_PLANE, KIND_SDF, KIND_VOLUME)
+    int32_t rec;      // its record in ext_recs (analytic-record format)
+};
+
+// ---------------------------------------------------------------- Matrix (Matrix.cs)
+// MulPosition (Matrix.cs:134-141): fp64 rows, then a Vector (fp32).
+PT_HD v3 mat_position(const double* m, v3 b) {
+    double x = m[0] * b.x + m[1] * b.y + m[2] * b.z + m[3];
+    double y = m[4] * b.x + m[5] * b.y + m[6] * b.z + m[7];
+    double z = m[8] * b.x + m[9] * b.y + m[10] * b.z + m[11];
+    return mk(x, y, z);
+}
+// MulDirection (Matrix.cs:144-150), normalised
+PT_HD v3 mat_direction(const double* m, v3 b) {
+    double x = m[0] * b.x + m[1] * b.y + m[2] * b.z;
+    double y = m[4] * b.x + m[5] * b.y + m[6] * b.z;
+    double z = m[8] * b.x + m[9] * b.y + m[10] * b.z;
+    return normalize(mk(x, y, z));
+}
+// Transpose().MulDirection (Matrix.cs:176, 144-150) on the 3x3 part
+PT_HD v3 mat_direction_t(const double* m, v3 b) {
+    double x = m[0] * b.x + m[4] * b.y + m[8] * b.z;
+    double y = m[1] * b.x + m[5] * b.y + m[9] * b.z;
+    double z = m[2] * b.x + m[6] * b.y + m[10] * b.z;
+    return normalize(mk(x, y, z));
+}
+// MulBox (Matrix.cs:156-173)
+PT_HD void mat_box(const double* m, v3 mn, v3 mx, v3& omn, v3& omx) {
+    v3 r = mk(m[0], m[4], m[8]), u = mk(m[1], m[5], m[9]), b = mk(m[2], m[6], m[10]), t = mk(m[3], m[7], m[11]);
+    v3 xa = muls(r, mn.x), xb = muls(r, mx.x), ya = muls(u, mn.y), yb = muls(u, mx.y), za = muls(b, mn.z),
+       zb = muls(b, mx.z);
+    omn = add(add(add(vmin(xa, xb), vmin(ya, yb)), vmin(za, zb)), t);
+    omx = add(add(add(vmax(xa, xb), vmax(ya, yb)), vmax(za, zb)), t);
+}
+// Box.Intersect (Box.cs:72-94), fp64
+PT_HD void box_span(const float* mn, const float* mx, v3 o, v3 d, double& tmin, double& tmax) {
+    double x1 = ((double)mn[0] - (double)o.x) / (double)d.x, y1 = ((double)mn[1] - (double)o.y) / (double)d.y;
+    double z1 = ((double)mn[2] - (double)o.z) / (double)d.z;
+    double x2 = ((double)mx[0] - (double)o.x) / (double)d.x, y2 = ((double)mx[1] - (double)o.y) / (double)d.y;
+    double z2 = ((double)mx[2] - (double)o.z) / (double)d.z;
+    if (x1 > x2) { double t = x1; x1 = x2; x2 = t; }
+    if (y1 > y2) { double t = y1; y1 = y2; y2 = t; }
+    if (z1 > z2) { double t = z1; z1 = z2; z2 = t; }
+    tmin = net_max(net_max(x1, y1), z1);
+    tmax = net_min(net_min(x2, y2), z2);
+}
+
+// ---------------------------------------------------------------- SDF leaves (SDF.cs)
+// Vector.LengthN (Vector.cs:359-367)
+PT_HD double length_n(v3 a, double n) {
+    if (n == 2) return (double)lengthf(a);
+    const double x = fabs((double)a.x), y = fabs((double)a.y), z = fabs((double)a.z);   // Abs (Vector.cs:402-405)
+    return pow(pow(x, n) + pow(y, n) + pow(z, n), 1 / n);
+}
+PT_HD double sdf_leaf(int op, const double* P, v3 p) {
+    switch (op) {
+        case SDF_LEAF_SPHERE: return length_n(p, P[1]) - P[0];   // SDF.cs:131-134
+        case SDF_LEAF_CUBE: {                                     // SDF.cs:157-189
+            double x = p.x, y = p.y, z = p.z;
+            if (x < 0) x = -x;
+            if (y < 0) y = -y;
+            if (z < 0) z = -z;
+            x -= P[0] / 2;
+            y -= P[1] / 2;
+            z -= P[2] / 2;
+            double a = x;
+            if (y > a) a = y;
+            if (z > a) a = z;
+            if (a > 0) a = 0;
+            if (x < 0) x = 0;
+            if (y < 0) y = 0;
+            if (z < 0) z = 0;
+            return a + sqrt(x * x + y * y + z * z);
+        }
+        case SDF_LEAF_CYLINDER: {                                 // SDF.cs:226-251
+            double x = sqrt((double)p.x * p.x + (double)p.z * p.z);
+            double y = p.y;
+            if (x < 0) x = -x;
+            if (y < 0) y = -y;
+            x -= P[0];
+            y -= P[1] / 2;
+            double a = x;
+            if (y > a) a = y;
+            if (a > 0) a = 0;
+            if (x < 0) x = 0;
+            if (y < 0) y = 0;
+            return a + sqrt(x * x + y * y);
+        }
+        case SDF_LEAF_CAPSULE: {                                  // SDF.cs:273-279
+            v3 A = mk(P[0], P[1], P[2]), B = mk(P[3], P[4], P[5]);
+            v3 pa = sub(p, A), ba = sub(B, A);
+            double h = net_max(0, net_min(1, dot(pa, ba) / dot(ba, ba)));
+            return length_n(sub(pa, muls(ba, h)), P[7]) - P[6];
+        }
+        default: {                                                // SDF_LEAF_TORUS, SDF.cs:307-311
+            v3 q = mk(length_n(v3{p.x, p.y, 0.f}, P[2]) - P[0], p.z, 0);
+            return length_n(q, P[3]) - P[1];
+        }
+    }
+}
+
+// SDF.Evaluate of a compiled program (see the header comment).
+PT_HD double sdf_eval(const DevSdfIns* prog, const double* params, int begin, int len, v3 p) {
+    v3 pts[kSdfStack];
+    double vals[kSdfStack];
+    int ps = 0, vs = 0;
+    pts[0] = p;
+    for (int i = begin; i < begin + len; i++) {
+        const DevSdfIns I = prog[i];
+        const double* P = params + I.param;
+        const v3 q = pts[ps];
+        switch (I.op) {
+            case SDF_PUSH_TRANSFORM: pts[++ps] = mat_position(P, q); break;
+            case SDF_PUSH_SCALE: pts[++ps] = mk((double)q.x / P[0], (double)q.y / P[0], (double)q.z / P[0]); break;
+            case SDF_PUSH_REPEAT: {   // Vector.Mod (Vector.cs:420-426), then Sub(Step.DivScalar(2))
+                v3 st = mk(P[0], P[1], P[2]);
+                v3 m = mk((double)q.x - (double)st.x * floor((double)q.x / (double)st.x),
+                          (double)q.y - (double)st.y * floor((double)q.y / (double)st.y),
+                          (double)q.z - (double)st.z * floor((double)q.z / (double)st.z));
+                pts[++ps] = sub(m, mk((double)st.x / 2, (double)st.y / 2, (double)st.z / 2));
+                break;
+            }
+            case SDF_POP_POINT: ps--; break;
+            case SDF_MUL: vals[vs - 1] = vals[vs - 1] * P[0]; break;
+            case SDF_UNION: { double b = vals[--vs]; if (b < vals[vs - 1]) vals[vs - 1] = b; break; }
+            case SDF_DIFFERENCE: { double b = vals[--vs]; if (-b > vals[vs - 1]) vals[vs - 1] = -b; break; }
+            case SDF_INTERSECTION: { double b = vals[--vs]; if (b > vals[vs - 1]) vals[vs - 1] = b; break; }
+            case SDF_CONST0: vals[vs++] = 0.0; break;
+            default: vals[vs++] = sdf_leaf(I.op, P, q); break;
+        }
+    }
+    return vals[0];
+}
+
+// SDFShape.Intersect (SDF.cs:32-76): sphere tracing within the bounding box.
+PT_HD double sdf_t(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 o, v3 d) {
+    const double epsilon = (double)0.00001f, start = (double)0.0001f, jump_size = (double)0.001f;
+    double t1, t2;
+    box_span(sh.bmin, sh.bmax, o, d, t1, t2);
+    if (t2 < t1 || t2 < 0) return kHitInf;
+    double t = net_max(start, t1);
+    bool jump = true;
+    for (int i = 0; i < 1000; i++) {
+        double dist = sdf_eval(prog, params, sh.begin, sh.len, add(o, muls(d, t)));
+        if (jump && dist < 0) {
+            t -= jump_size;
+            jump = false;
+            continue;
+        }
+        if (dist < epsilon) return t;
+        if (jump && dist < jump_size) dist = jump_size;
+        t += dist;
+        if (t > t2) return kHitInf;
+    }
+    return kHitInf;
+}
+// SDFShape.NormalAt (SDF.cs:83-92)
+PT_HD v3 sdf_normal(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 p) {
+    const double e = 0.0001;
+    const double x = p.x, y = p.y, z = p.z;
+    const int b = sh.begin, n = sh.len;
+    double nx = sdf_eval(prog, params, b, n, mk(x - e, y, z)) - sdf_eval(prog, params, b, n, mk(x + e, y, z));
+    double ny = sdf_eval(prog, params, b, n, mk(x, y - e, z)) - sdf_eval(prog, params, b, n, mk(x, y + e, z));
+    double nz = sdf_eval(prog, params, b, n, mk(x, y, z - e)) - sdf_eval(prog, params, b, n, mk(x, y, z + e));
+    return normalize(mk(nx, ny, nz));
+}
+
+// ---------------------------------------------------------------- Volume (Volume.cs)
+PT_HD double vol_get(const DevVolume& v, int x, int y, int z) {   // Volume.Get (Volume.cs:40-46)
+    if (x < 0 || y < 0 || z < 0 || x >= v.w || y >= v.h || z >= v.d) return 0;
+    return v.data[(size_t)x + (size_t)y * (size_t)v.w + (size_t)z * (size_t)v.w * (size_t)v.h];
+}
+// Volume.Sample (Volume.cs:73-105), with its y-from-z slip (:77).  Coordinates outside
+// the int range (an OverflowException in the reference) sample 0, as in the oracle.
+PT_HD double vol_sample(const DevVolume& v, double x, double y, double z) {
+    (void)y;
+    z /= v.zscale;
+    x = ((x + 1) / 2) * (double)v.w;
+    y = ((z + 1) / 2) * (double)v.h;
+    z = ((z + 2) / 2) * (double)v.d;
+    const double lim = 2147483647.0;
+    if (!(fabs(x) < lim && fabs(y) < lim && fabs(z) < lim)) return 0;
+    const int x0 = (int)floor(x), y0 = (int)floor(y), z0 = (int)floor(z);
+    const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
+    const double v000 = vol_get(v, x0, y0, z0), v001 = vol_get(v, x0, y0, z1), v010 = vol_get(v, x0, y1, z0);
+    const double v011 = vol_get(v, x0, y1, z1), v100 = vol_get(v, x1, y0, z0), v101 = vol_get(v, x1, y0, z1);
+    const double v110 = vol_get(v, x1, y1, z0), v111 = vol_get(v, x1, y1, z1);
+    x -= (double)x0;
+    y -= (double)y0;
+    z -= (double)z0;
+    const double c00 = v000 * (1 - x) + v100 * x;
+    const double c01 = v001 * (1 - x) + v101 * x;
+    const double c10 = v010 * (1 - x) + v110 * x;
+    const double c11 = v011 * (1 - x) + v111 * x;
+    const double c0 = c00 * (1 - y) + c10 * y;
+    const double c1 = c01 * (1 - y) + c11 * y;
+    return c0 * (1 - z) + c1 * z;
+}
+// Volume.Sign (Volume.cs:114-131): its `i` is never incremented, so "below a window" is 1.
+PT_HD int vol_sign(const DevVolume& v, v3 a) {
+    const double s = vol_sample(v, a.x, a.y, a.z);
+    for (int i = 0; i < v.nwin; i++) {
+        if (s < v.windows[i].lo) return 1;
+        if (s > v.windows[i].hi) continue;
+        return 0;
+    }
+    return v.nwin + 1;
+}
+// Volume.NormalAt (Volume.cs:138-145)
+PT_HD v3 vol_normal(const DevVolume& v, v3 p) {
+    const double eps = (double)0.001f;
+    return normalize(mk(vol_sample(v, p.x - eps, p.y, p.z) - vol_sample(v, p.x + eps, p.y, p.z),
+                        vol_sample(v, p.x, p.y - eps, p.z) - vol_sample(v, p.x, p.y + eps, p.z),
+                        vol_sample(v, p.x, p.y, p.z - eps) - vol_sample(v, p.x, p.y, p.z + eps)));
+}
+// Volume.MaterialAt (Volume.cs:148-166): the window holding the sample, else the nearest
+// (`new Material()` = default_mat when none is nearer than 1e9F).
+PT_HD int vol_material(const DevVolume& v, v3 p, int default_mat) {
+    double be = (double)1e9f;
+    int bm = default_mat;
+    const double s = vol_sample(v, p.x, p.y, p.z);
+    for (int i = 0; i < v.nwin; i++) {
+        const DevWindow w = v.windows[i];
+        if (s >= w.lo && s <= w.hi) return w.mat;
+        const double e = net_min(fabs(s - w.lo), fabs(s - w.hi));
+        if (e < be) { be = e; bm = w.mat; }
+    }
+    return bm;
+}
+// Volume.Intersect (Volume.cs:168-197).  The reference loop has no bound; 2^24 steps
+// stand in for it (a ray that needs more never finishes in the reference either).
+PT_HD double vol_t(const DevVolume& v, v3 o, v3 d) {
+    double tmin, tmax;
+    box_span(v.bmin, v.bmax, o, d, tmin, tmax);
+    double step = (double)(1.0f / 512.0f);
+    const double start = net_max(step, tmin);
+    int sign = -1;
+    int iters = 0;
+    for (double t = start; t <= tmax && iters < (1 << 24); t += step, iters++) {
+        const int sg = vol_sign(v, add(o, muls(d, t)));
+        if (sg == 0 || (sign >= 0 && sg != sign)) {
+            t -= step;
+            step /= 64;
+            t += step;
+            for (int i = 0; i < 64; i++) {
+                if (vol_sign(v, add(o, muls(d, t))) == 0) return t - step;
+                t += step;
+            }
+        }
+        sign = sg;
+    }
+    return kHitInf;
+}
+
+}  // namespace pt

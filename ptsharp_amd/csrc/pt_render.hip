@@ -27,20 +27,20 @@ constexpr int kMaxFrames = 34;   // MaxBounces <= 32 under SpecularModeAll (chec
 
 // Sampler.sampleLight (Sampler.cs:212-296): the megakernel keeps the reference's
 // nearest-hit + identity structure for the shadow query.
-template <bool COUNT, bool TEX>
+template <bool COUNT, bool FULL>
 __device__ __noinline__ float3 sample_light(const DevScene& S, const DevSampler& smp, const DevLight& L, v3 o, v3 n,
                                             uint64_t key, MStack stack, Counters& ctr) {
     v3 dir;
     float3 contrib;
-    if (!light_setup<TEX>(S, smp, L, o, n, key, dir, contrib)) return make_float3(0.f, 0.f, 0.f);
-    HitRec h = trace<COUNT>(S, o, dir, stack, ctr);
+    if (!light_setup<FULL>(S, smp, L, o, n, key, dir, contrib)) return make_float3(0.f, 0.f, 0.f);
+    HitRec h = trace<COUNT, FULL>(S, o, dir, stack, ctr);
     // hit.Shape != light is a reference compare; struct Triangle lights never match.
     if (!(h.t < kHitInf) || L.phantom || h.kind != L.kind || h.idx != L.index) return make_float3(0.f, 0.f, 0.f);
     return contrib;
 }
 
 // Sampler.sampleLights (Sampler.cs:191-210)
-template <bool COUNT, bool TEX>
+template <bool COUNT, bool FULL>
 __device__ __forceinline__ float3 sample_lights(const DevScene& S, const DevSampler& smp, v3 o, v3 n, uint64_t key,
                                                 MStack stack, Counters& ctr) {
     int nl = S.num_lights;
@@ -48,7 +48,7 @@ __device__ __forceinline__ float3 sample_lights(const DevScene& S, const DevSamp
     if (smp.light_mode == 1) {
         float3 acc = make_float3(0.f, 0.f, 0.f);
         for (int i = 0; i < nl; i++) {
-            float3 c = sample_light<COUNT, TEX>(S, smp, S.lights[i], o, n, light_key(key, (uint32_t)i), stack, ctr);
+            float3 c = sample_light<COUNT, FULL>(S, smp, S.lights[i], o, n, light_key(key, (uint32_t)i), stack, ctr);
             acc.x += c.x; acc.y += c.y; acc.z += c.z;
         }
         float inv = 1.0f / (float)nl;
@@ -56,7 +56,7 @@ __device__ __forceinline__ float3 sample_lights(const DevScene& S, const DevSamp
     }
     int idx = (int)(draw(key, D_LIGHT) * nl);
     if (idx >= nl) idx = nl - 1;
-    float3 c = sample_light<COUNT, TEX>(S, smp, S.lights[idx], o, n, key, stack, ctr);
+    float3 c = sample_light<COUNT, FULL>(S, smp, S.lights[idx], o, n, key, stack, ctr);
     float fn = (float)nl;
     return make_float3(c.x * fn, c.y * fn, c.z * fn);
 }
@@ -73,7 +73,7 @@ struct Frame {
 
 // Child c of a vertex: one iteration of the u/v/mode loop of Sampler.cs:96-131.
 // Adds the vertex' direct-light term to acc and returns the child's ray/throughput.
-template <bool COUNT, bool TEX>
+template <bool COUNT, bool FULL>
 __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& smp, const Shade& sh, v3 indir,
                                            const float thr[3], uint64_t node, int n, int nm, int c, float3& acc,
                                            v3& no, v3& nd, bool& emission, float nthr[3], uint64_t& nkey,
@@ -99,7 +99,7 @@ __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& 
     } else {
         for (int k = 0; k < 3; k++) w[k] = fp * sh.col[k];
         if (smp.dl) {
-            float3 dl = sample_lights<COUNT, TEX>(S, smp, sh.pos, sh.nrm, E, stack, ctr);
+            float3 dl = sample_lights<COUNT, FULL>(S, smp, sh.pos, sh.nrm, E, stack, ctr);
             acc.x += thr[0] * w[0] * dl.x;
             acc.y += thr[1] * w[1] * dl.y;
             acc.z += thr[2] * w[2] * dl.z;
@@ -112,7 +112,7 @@ __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& 
 }
 
 // DefaultSampler.Sample(scene, ray) for one camera ray; returns the sample colour.
-template <bool COUNT, bool TEX>
+template <bool COUNT, bool FULL>
 __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3 d, uint64_t root_key,
                               MStack stack, Frame* frames, Counters& ctr) {
     float3 acc = make_float3(0.f, 0.f, 0.f);
@@ -128,14 +128,14 @@ __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3
         if (have) {
             have = false;
             if (depth <= smp.mb) {
-                HitRec h = trace<COUNT>(S, o, d, stack, ctr);
+                HitRec h = trace<COUNT, FULL>(S, o, d, stack, ctr);
                 if (!(h.t < kHitInf)) {
-                    const float3 env = environment<TEX>(S, d);   // sampleEnvironment (Sampler.cs:177-189)
+                    const float3 env = environment<FULL>(S, d);   // sampleEnvironment (Sampler.cs:177-189)
                     acc.x += thr[0] * env.x;
                     acc.y += thr[1] * env.y;
                     acc.z += thr[2] * env.z;
                 } else {
-                    Shade sh = hit_info<COUNT, TEX>(S, h, o, d, ctr);
+                    Shade sh = hit_info<COUNT, FULL>(S, h, o, d, ctr);
                     const DevMaterial& m = S.mats[sh.mat];
                     int n = (int)sqrt((double)samples);
                     float inv_n2 = 1.0f / (float)(n * n);
@@ -159,7 +159,7 @@ __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3
                             uint64_t nkey;
                             v3 no, nd;
                             bool em;
-                            if (child_step<COUNT, TEX>(S, smp, sh, d, t2, node, 1, 1, 0, acc, no, nd, em, nthr, nkey, stack,
+                            if (child_step<COUNT, FULL>(S, smp, sh, d, t2, node, 1, 1, 0, acc, no, nd, em, nthr, nkey, stack,
                                                   ctr)) {
                                 o = no; d = nd; emission = em; samples = 1; depth = depth + 1; node = nkey;
                                 thr[0] = nthr[0]; thr[1] = nthr[1]; thr[2] = nthr[2];
@@ -193,7 +193,7 @@ __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3
             uint64_t nkey;
             v3 no, nd;
             bool em;
-            if (child_step<COUNT, TEX>(S, smp, sh, indir, t2, fnode, fn, fnm, c, acc, no, nd, em, nthr, nkey, stack, ctr)) {
+            if (child_step<COUNT, FULL>(S, smp, sh, indir, t2, fnode, fn, fnm, c, acc, no, nd, em, nthr, nkey, stack, ctr)) {
                 o = no; d = nd; emission = em; samples = 1; depth = fdepth + 1; node = nkey;
                 thr[0] = nthr[0]; thr[1] = nthr[1]; thr[2] = nthr[2];
                 have = true;
@@ -204,7 +204,7 @@ __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3
     return acc;
 }
 
-template <bool COUNT, bool TEX>
+template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera cam, DevSampler smp, DevPass P,
                                                         DevBuffer B) {
     __shared__ uint32_t s_stack[kMaxDepth * kBlock];
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera ca
                     v3 o, d;
                     cast_ray(cam, x, y, w, h, ((double)u + 0.5) / (double)root, ((double)v + 0.5) / (double)root,
                              K, o, d);
-                    float3 c = sample_path<COUNT, TEX>(S, smp, o, d, K, stack, local_frames, ctr);
+                    float3 c = sample_path<COUNT, FULL>(S, smp, o, d, K, stack, local_frames, ctr);
                     welford(B, (size_t)pix, (double)c.x, (double)c.y, (double)c.z);
                 }
         } else {
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera ca
                 double fv = (y + draw(K, D_JY)) / h;
                 v3 o, d;
                 cast_ray(cam, x, y, w, h, fu, fv, K, o, d);
-                float3 c = sample_path<COUNT, TEX>(S, smp, o, d, K, stack, local_frames, ctr);
+                float3 c = sample_path<COUNT, FULL>(S, smp, o, d, K, stack, local_frames, ctr);
                 cr += c.x; cg += c.y; cb += c.z;
             }
             double inv = (double)P.spp;
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera ca
 hipError_t launch_render_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                               const DevBuffer& B, int num_tiles, bool count, hipStream_t stream) {
     dim3 grid((unsigned)num_tiles * 4u), block(kBlock);
-    const bool tex = S.texs != nullptr;
+    const bool tex = S.full != 0;
     if (count && tex) hipLaunchKernelGGL((k_render_pass<true, true>), grid, block, 0, stream, S, cam, smp, P, B);
     else if (count) hipLaunchKernelGGL((k_render_pass<true, false>), grid, block, 0, stream, S, cam, smp, P, B);
     else if (tex) hipLaunchKernelGGL((k_render_pass<false, true>), grid, block, 0, stream, S, cam, smp, P, B);

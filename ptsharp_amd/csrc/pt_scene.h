@@ -9,9 +9,12 @@
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 
+#include "pt_ext.h"
+
 namespace pt {
 
-enum PrimKind : int32_t { KIND_SPHERE = 0, KIND_CUBE = 1, KIND_PLANE = 2, KIND_TRI = 3, KIND_MESH = 4 };
+enum PrimKind : int32_t { KIND_SPHERE = 0, KIND_CUBE = 1, KIND_PLANE = 2, KIND_TRI = 3, KIND_MESH = 4,
+                          KIND_SDF = 5, KIND_VOLUME = 6, KIND_XFORM = 7 };
 
 // Material (Material.cs:8-62); colour terms in fp32 (they never feed a branch),
 // the terms that feed Fresnel / cone / branch decisions stay fp64.
@@ -55,7 +58,7 @@ struct DevScene {
     // analytic BVH (spheres, cubes)
     const float4* ana_nodes;
     int32_t ana_num_nodes;
-    const float4* ana_recs;    // 3 float4: {a.xyz,kind} {b.xyz,scene index} {mat, radius(double), -}
+    const float4* ana_recs;    // 3 float4: {a.xyz,kind} {b.xyz,scene index} {mat, radius(double) | ext index, -}
     // planes (unbounded: tested outside the BVHs)
     const float4* planes;      // 2 float4: {point.xyz, mat} {normal.xyz, scene index}
     int32_t num_planes;
@@ -68,6 +71,15 @@ struct DevScene {
     const float4* tri_uv;      // 2 float4 per triangle: {t1.xy, t2.xy} {t3.xy, -, -}; null without textured triangles
     int32_t env_tex;           // Scene.Texture (-1 = null)
     double env_angle;          // Scene.TextureAngle
+    // SDF shapes, volumes, transformed shapes (§8f row 4; pt_ext.h)
+    const DevSdfIns* sdf_prog;
+    const double* sdf_params;
+    const DevSdfShape* sdf_shapes;
+    const DevVolume* volumes;
+    const DevXform* xforms;
+    const float4* ext_recs;    // object-space records of transformed shapes' inner shapes (ana format)
+    int32_t default_mat;       // `new Material()` (Volume.MaterialAt with no window near)
+    int32_t full;              // textures or §8f row 4 shapes present: kernels run their FULL instantiation
 };
 
 struct DevCamera {

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
 }
 
 // ---------------------------------------------------------------- closest hit
-template <bool COUNT>
+template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
         const uint32_t i = base + k0 + lane;
         float4 b = nt_load(&Q.q_d[qi][i]);
         float4 a = nt_load(&Q.q_o[qi][i]);
-        HitRec h = trace<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+        HitRec h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
         unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
         nt_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
     }
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
 // word saturates near 88 per µs on MI355X, MI355X_MICROARCH.md "dequeue").  Light
 // sampling up to the shadow query runs here too, so k_wf_shadow is a lean
 // traversal kernel (ray + stack state only).
-template <bool COUNT, bool TEX>
+template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
     if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + 2 * kParts + threadIdx.x] = 0u;  // k_wf_shadow's
@@ -276,12 +276,12 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
         float t2[3] = {0.f, 0.f, 0.f};
         double pv = 0.0, n1 = 1.0, n2 = 1.0;
         if (alive && !(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67, 177-189)
-            const float3 env = environment<TEX>(S, d);
+            const float3 env = environment<FULL>(S, d);
             acc_add(Q.acc, pixel, thr[0] * env.x, thr[1] * env.y, thr[2] * env.z);
             alive = false;
         }
         if (alive) {
-            sh = hit_info<COUNT, TEX>(S, h, o, d, ctr);
+            sh = hit_info<COUNT, FULL>(S, h, o, d, ctr);
             mat = sh.mat;
             const DevMaterial& m = S.mats[mat];
             const int samples = depth == 0 ? smp.fh : 1;
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
                         const int li = first + (int)j;
                         v3 ldir;
                         float3 lc;
-                        const bool cast = light_setup<TEX>(S, smp, S.lights[li], sh.pos, sh.nrm,
+                        const bool cast = light_setup<FULL>(S, smp, S.lights[li], sh.pos, sh.nrm,
                                                       all_lights ? light_key(E, (uint32_t)li) : E, ldir, lc);
                         if (nj < Q.spcap) {
                             const uint32_t at = G.g * Q.spcap + nj;
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, De
 // ---------------------------------------------------------------- shadow rays
 // One thread per shadow ray that k_wf_shade set up (light, direction, the colour the
 // light adds if it is the nearest hit): the visibility query of Sampler.cs:261-265.
-template <bool COUNT>
+template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, int q
         if (li == kDead) continue;
         const float4 a = nt_load(&Q.n_o[i]);
         const DevLight L = S.lights[li];
-        if (light_visible<COUNT>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) {
+        if (light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) {
             const float4 wt = nt_load(&Q.n_w[i]);
             acc_add(Q.acc, __float_as_uint(a.w), wt.x, wt.y, wt.z);
         }
@@ -522,22 +522,26 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     for (int depth = 0; depth <= smp.mb; depth++) {
         const unsigned tg = grid_for(bound, kTB, plan.trace_blocks);
         begin_k(1);
-        if (count) hipLaunchKernelGGL(k_wf_trace<true>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-        else hipLaunchKernelGGL(k_wf_trace<false>, dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        const bool full = S.full != 0;
+        if (count && full) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (full) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         end_k(1);
         const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
         begin_k(2);
-        const bool tex = S.texs != nullptr;
-        if (count && tex) hipLaunchKernelGGL((k_wf_shade<true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        if (count && full) hipLaunchKernelGGL((k_wf_shade<true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_shade<true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
-        else if (tex) hipLaunchKernelGGL((k_wf_shade<false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        else if (full) hipLaunchKernelGGL((k_wf_shade<false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shade<false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         end_k(2);
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
         const unsigned hg = grid_for(children * plan.lights_per_child, kTB, plan.shadow_blocks);
         begin_k(3);
-        if (count) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
-        else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
+        if (count && full) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
+        else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
+        else if (full) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
+        else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
         end_k(3);
         bound = children < Q.cap ? children : Q.cap;
         qi = 1 - qi;
@@ -611,11 +615,11 @@ hipError_t wavefront_grids(WfPlan& plan) {
         if (g < (uint64_t)kParts) g = kParts;
         return (uint32_t)(g < cap ? g : cap / kParts * kParts);
     };
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace<false>, kTB, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace<false, false>, kTB, 0);
     if (e == hipSuccess) plan.trace_blocks = resident(nb, kWfMaxBlocks);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shade<false, false>, 256, 0);
     if (e == hipSuccess) plan.shade_blocks = resident(nb, 1u << 20);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false>, kTB, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false, false>, kTB, 0);
     if (e == hipSuccess) plan.shadow_blocks = resident(nb, kWfMaxBlocks);
     return e;
 }

@@ -252,6 +252,81 @@ class Matrix:
                 out[i, j] = a[i, 0] * bb[0, j] + a[i, 1] * bb[1, j] + a[i, 2] * bb[2, j] + a[i, 3] * bb[3, j]
         return Matrix(out)
 
+    def Determinant(self) -> float:
+        """Matrix.Determinant (Matrix.cs:179-193), the reference's term order."""
+        a = [[float(x) for x in row] for row in self.m]
+        return (a[0][0] * a[1][1] * a[2][2] * a[3][3] - a[0][0] * a[1][1] * a[2][3] * a[3][2]
+            + a[0][0] * a[1][2] * a[2][3] * a[3][1] - a[0][0] * a[1][2] * a[2][1] * a[3][3]
+            + a[0][0] * a[1][3] * a[2][1] * a[3][2] - a[0][0] * a[1][3] * a[2][2] * a[3][1]
+            - a[0][1] * a[1][2] * a[2][3] * a[3][0] + a[0][1] * a[1][2] * a[2][0] * a[3][3]
+            - a[0][1] * a[1][3] * a[2][0] * a[3][2] + a[0][1] * a[1][3] * a[2][2] * a[3][0]
+            - a[0][1] * a[1][0] * a[2][2] * a[3][3] + a[0][1] * a[1][0] * a[2][3] * a[3][2]
+            + a[0][2] * a[1][3] * a[2][0] * a[3][1] - a[0][2] * a[1][3] * a[2][1] * a[3][0]
+            + a[0][2] * a[1][0] * a[2][1] * a[3][3] - a[0][2] * a[1][0] * a[2][3] * a[3][1]
+            + a[0][2] * a[1][1] * a[2][3] * a[3][0] - a[0][2] * a[1][1] * a[2][0] * a[3][3]
+            - a[0][3] * a[1][0] * a[2][1] * a[3][2] + a[0][3] * a[1][0] * a[2][2] * a[3][1]
+            - a[0][3] * a[1][1] * a[2][2] * a[3][0] + a[0][3] * a[1][1] * a[2][0] * a[3][2]
+            - a[0][3] * a[1][2] * a[2][0] * a[3][1] + a[0][3] * a[1][2] * a[2][1] * a[3][0])
+
+    def Inverse(self) -> "Matrix":
+        """Matrix.Inverse (Matrix.cs:196-216), the reference's cofactor sums in order."""
+        a = [[float(x) for x in row] for row in self.m]
+        d = self.Determinant()
+        o = np.zeros((4, 4))
+        o[0, 0] = (a[1][2] * a[2][3] * a[3][1] - a[1][3] * a[2][2] * a[3][1] + a[1][3] * a[2][1] * a[3][2]
+            - a[1][1] * a[2][3] * a[3][2] - a[1][2] * a[2][1] * a[3][3] + a[1][1] * a[2][2] * a[3][3]) / d
+        o[0, 1] = (a[0][3] * a[2][2] * a[3][1] - a[0][2] * a[2][3] * a[3][1] - a[0][3] * a[2][1] * a[3][2]
+            + a[0][1] * a[2][3] * a[3][2] + a[0][2] * a[2][1] * a[3][3] - a[0][1] * a[2][2] * a[3][3]) / d
+        o[0, 2] = (a[0][2] * a[1][3] * a[3][1] - a[0][3] * a[1][2] * a[3][1] + a[0][3] * a[1][1] * a[3][2]
+            - a[0][1] * a[1][3] * a[3][2] - a[0][2] * a[1][1] * a[3][3] + a[0][1] * a[1][2] * a[3][3]) / d
+        o[0, 3] = (a[0][3] * a[1][2] * a[2][1] - a[0][2] * a[1][3] * a[2][1] - a[0][3] * a[1][1] * a[2][2]
+            + a[0][1] * a[1][3] * a[2][2] + a[0][2] * a[1][1] * a[2][3] - a[0][1] * a[1][2] * a[2][3]) / d
+        o[1, 0] = (a[1][3] * a[2][2] * a[3][0] - a[1][2] * a[2][3] * a[3][0] - a[1][3] * a[2][0] * a[3][2]
+            + a[1][0] * a[2][3] * a[3][2] + a[1][2] * a[2][0] * a[3][3] - a[1][0] * a[2][2] * a[3][3]) / d
+        o[1, 1] = (a[0][2] * a[2][3] * a[3][0] - a[0][3] * a[2][2] * a[3][0] + a[0][3] * a[2][0] * a[3][2]
+            - a[0][0] * a[2][3] * a[3][2] - a[0][2] * a[2][0] * a[3][3] + a[0][0] * a[2][2] * a[3][3]) / d
+        o[1, 2] = (a[0][3] * a[1][2] * a[3][0] - a[0][2] * a[1][3] * a[3][0] - a[0][3] * a[1][0] * a[3][2]
+            + a[0][0] * a[1][3] * a[3][2] + a[0][2] * a[1][0] * a[3][3] - a[0][0] * a[1][2] * a[3][3]) / d
+        o[1, 3] = (a[0][2] * a[1][3] * a[2][0] - a[0][3] * a[1][2] * a[2][0] + a[0][3] * a[1][0] * a[2][2]
+            - a[0][0] * a[1][3] * a[2][2] - a[0][2] * a[1][0] * a[2][3] + a[0][0] * a[1][2] * a[2][3]) / d
+        o[2, 0] = (a[1][1] * a[2][3] * a[3][0] - a[1][3] * a[2][1] * a[3][0] + a[1][3] * a[2][0] * a[3][1]
+            - a[1][0] * a[2][3] * a[3][1] - a[1][1] * a[2][0] * a[3][3] + a[1][0] * a[2][1] * a[3][3]) / d
+        o[2, 1] = (a[0][3] * a[2][1] * a[3][0] - a[0][1] * a[2][3] * a[3][0] - a[0][3] * a[2][0] * a[3][1]
+            + a[0][0] * a[2][3] * a[3][1] + a[0][1] * a[2][0] * a[3][3] - a[0][0] * a[2][1] * a[3][3]) / d
+        o[2, 2] = (a[0][1] * a[1][3] * a[3][0] - a[0][3] * a[1][1] * a[3][0] + a[0][3] * a[1][0] * a[3][1]
+            - a[0][0] * a[1][3] * a[3][1] - a[0][1] * a[1][0] * a[3][3] + a[0][0] * a[1][1] * a[3][3]) / d
+        o[2, 3] = (a[0][3] * a[1][1] * a[2][0] - a[0][1] * a[1][3] * a[2][0] - a[0][3] * a[1][0] * a[2][1]
+            + a[0][0] * a[1][3] * a[2][1] + a[0][1] * a[1][0] * a[2][3] - a[0][0] * a[1][1] * a[2][3]) / d
+        o[3, 0] = (a[1][2] * a[2][1] * a[3][0] - a[1][1] * a[2][2] * a[3][0] - a[1][2] * a[2][0] * a[3][1]
+            + a[1][0] * a[2][2] * a[3][1] + a[1][1] * a[2][0] * a[3][2] - a[1][0] * a[2][1] * a[3][2]) / d
+        o[3, 1] = (a[0][1] * a[2][2] * a[3][0] - a[0][2] * a[2][1] * a[3][0] + a[0][2] * a[2][0] * a[3][1]
+            - a[0][0] * a[2][2] * a[3][1] - a[0][1] * a[2][0] * a[3][2] + a[0][0] * a[2][1] * a[3][2]) / d
+        o[3, 2] = (a[0][2] * a[1][1] * a[3][0] - a[0][1] * a[1][2] * a[3][0] - a[0][2] * a[1][0] * a[3][1]
+            + a[0][0] * a[1][2] * a[3][1] + a[0][1] * a[1][0] * a[3][2] - a[0][0] * a[1][1] * a[3][2]) / d
+        o[3, 3] = (a[0][1] * a[1][2] * a[2][0] - a[0][2] * a[1][1] * a[2][0] + a[0][2] * a[1][0] * a[2][1]
+            - a[0][0] * a[1][2] * a[2][1] - a[0][1] * a[1][0] * a[2][2] + a[0][0] * a[1][1] * a[2][2]) / d
+        return Matrix(o)
+
+    def Transpose(self) -> "Matrix":   # Matrix.cs:176
+        return Matrix(self.m.T.copy())
+
+    def MulPosition(self, b: Vector) -> Vector:
+        """Matrix.MulPosition (Matrix.cs:134-141)."""
+        m = self.m
+        return Vector(*[((m[r, 0] * b.X + m[r, 1] * b.Y) + m[r, 2] * b.Z) + m[r, 3] for r in range(3)])
+
+    def MulBox(self, box: "Box") -> "Box":
+        """Matrix.MulBox (Matrix.cs:156-173)."""
+        m = self.m
+        r, u, b, t = (Vector(m[0, k], m[1, k], m[2, k]) for k in range(4))
+        xa, xb = r.MulScalar(box.Min.X), r.MulScalar(box.Max.X)
+        ya, yb = u.MulScalar(box.Min.Y), u.MulScalar(box.Max.Y)
+        za, zb = b.MulScalar(box.Min.Z), b.MulScalar(box.Max.Z)
+        xa, xb = xa.Min(xb), xa.Max(xb)
+        ya, yb = ya.Min(yb), ya.Max(yb)
+        za, zb = za.Min(zb), za.Max(zb)
+        return Box(xa.Add(ya).Add(za).Add(t), xb.Add(yb).Add(zb).Add(t))
+
     def MulPosition_arrays(self, p: np.ndarray) -> np.ndarray:
         """MulPosition on an [n,3] float32 array (Matrix.cs:134-141)."""
         m = self.m

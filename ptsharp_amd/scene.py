@@ -375,6 +375,195 @@ class Mesh:
             raise _abi.PTError(rc, "pt_mesh_smooth_normals", lib.pt_obj_last_error().decode())
 
 
+# ---------------------------------------------------------------- SDF.cs (§8f row 4)
+class _SDF:
+    """A node of an SDF tree (SDF.cs:6-10); evaluated on the GPU (pt_device.h sdf_eval)."""
+    op = -1
+
+    def __init__(self, params=(), children=(), matrix=None, inverse=None):
+        self.params = tuple(float(x) for x in params)
+        self.children = list(children)
+        self.matrix, self.inverse = matrix, inverse
+
+
+class SphereSDF(_SDF):      # SDF.cs:115-140
+    op = 0
+
+    @staticmethod
+    def NewSphereSDF(radius: float) -> "SphereSDF":
+        return SphereSDF((radius, 2))
+
+
+class CubeSDF(_SDF):        # SDF.cs:142-195
+    op = 1
+
+    @staticmethod
+    def NewCubeSDF(size: Vector) -> "CubeSDF":
+        return CubeSDF(size.f32())
+
+
+class CylinderSDF(_SDF):    # SDF.cs:197-252
+    op = 2
+
+    @staticmethod
+    def NewCylinderSDF(radius: float, height: float) -> "CylinderSDF":
+        return CylinderSDF((radius, height))
+
+
+class CapsuleSDF(_SDF):     # SDF.cs:254-285
+    op = 3
+
+    @staticmethod
+    def NewCapsuleSDF(a: Vector, b: Vector, radius: float) -> "CapsuleSDF":
+        return CapsuleSDF(a.f32() + b.f32() + (radius, 2))
+
+
+class TorusSDF(_SDF):       # SDF.cs:287-319
+    op = 4
+
+    @staticmethod
+    def NewTorusSDF(major: float, minor: float) -> "TorusSDF":
+        return TorusSDF((major, minor, 2, 2))
+
+
+class TransformSDF(_SDF):   # SDF.cs:321-353
+    op = 5
+
+    @staticmethod
+    def NewTransformSDF(sdf: _SDF, matrix: Matrix) -> "TransformSDF":
+        return TransformSDF((), [sdf], matrix, matrix.Inverse())
+
+
+class ScaleSDF(_SDF):       # SDF.cs:355-382
+    op = 6
+
+    @staticmethod
+    def NewScaleSDF(sdf: _SDF, factor: float) -> "ScaleSDF":
+        return ScaleSDF((factor,), [sdf])
+
+
+class UnionSDF(_SDF):       # SDF.cs:384-435
+    op = 7
+
+    @staticmethod
+    def NewUnionSDF(items) -> "UnionSDF":
+        return UnionSDF((), items)
+
+
+class DifferenceSDF(_SDF):  # SDF.cs:437-477
+    op = 8
+
+    @staticmethod
+    def NewDifferenceSDF(items) -> "DifferenceSDF":
+        return DifferenceSDF((), items)
+
+
+class IntersectionSDF(_SDF):  # SDF.cs:479-531
+    op = 9
+
+    @staticmethod
+    def NewIntersectionSDF(items) -> "IntersectionSDF":
+        return IntersectionSDF((), items)
+
+
+class RepeatSDF(_SDF):      # SDF.cs:533-559
+    op = 10
+
+    @staticmethod
+    def NewRepeaterSDF(sdf: _SDF, step: Vector) -> "RepeatSDF":
+        return RepeatSDF(step.f32(), [sdf])
+
+
+class SDFShape:
+    """PTSharpCore.SDFShape (SDF.cs:12-113): a sphere-traced SDF tree with one material."""
+
+    def __init__(self, sdf: _SDF, material: Material):
+        self.SDF, self.Material = sdf, material
+
+    @staticmethod
+    def NewSDFShape(sdf: _SDF, material: Material) -> "SDFShape":
+        return SDFShape(sdf, material)
+
+    def MaterialAt(self, p=None) -> Material:
+        return self.Material
+
+
+class VolumeWindow:
+    """Volume.VolumeWindow (Volume.cs:8-19)."""
+
+    def __init__(self, lo: float, hi: float, material: Material):
+        self.Lo, self.Hi, self.VolumeWindowMaterial = float(lo), float(hi), material
+
+
+class Volume:
+    """PTSharpCore.Volume (Volume.cs): a W x H x D voxel grid (Data[x + y*W + z*W*H] = red/255)
+    marched for iso-windows."""
+
+    def __init__(self, w, h, d, zscale, data, windows, box: Box):
+        self.W, self.H, self.D, self.ZScale = int(w), int(h), int(d), float(zscale)
+        self.Data = np.ascontiguousarray(np.asarray(data, np.float64).reshape(-1))
+        self.Windows = list(windows)
+        self.Box = box
+
+    @staticmethod
+    def NewVolume(box: Box, images, sliceSpacing: float, windows) -> "Volume":
+        """Volume.NewVolume (Volume.cs:48-71): images are [h][w] or [h][w][3+] 8-bit slices (red used)."""
+        sl = [np.asarray(im) for im in images]
+        sl = [im[:, :, 0] if im.ndim == 3 else im for im in sl]
+        h, w = sl[0].shape
+        d = len(sl)
+        zs = sliceSpacing * d / w
+        data = np.stack(sl).astype(np.float64) / 255
+        return Volume(w, h, d, zs, data, windows, box)
+
+    def MaterialAt(self, p=None) -> Material:
+        """Volume.MaterialAt at the origin, all Scene.Add asks (Volume.cs:148-166); the GPU
+        and the oracle evaluate it at every shading point."""
+        s = self._sample(0.0, 0.0, 0.0)
+        be, bm = float(np.float32(1e9)), DEFAULT_MATERIAL
+        for w in self.Windows:
+            if w.Lo <= s <= w.Hi:
+                return w.VolumeWindowMaterial
+            e = min(abs(s - w.Lo), abs(s - w.Hi))
+            if e < be:
+                be, bm = e, w.VolumeWindowMaterial
+        return bm
+
+    def _sample(self, x, y, z):  # Volume.Sample (Volume.cs:73-105), y-from-z slip kept
+        z /= self.ZScale
+        x = ((x + 1) / 2) * self.W
+        y = ((z + 1) / 2) * self.H
+        z = ((z + 2) / 2) * self.D
+        x0, y0, z0 = math.floor(x), math.floor(y), math.floor(z)
+        W, H, D = self.W, self.H, self.D
+        get = lambda a, b, c: 0.0 if (a < 0 or b < 0 or c < 0 or a >= W or b >= H or c >= D) else \
+            float(self.Data[a + b * W + c * W * H])
+        v = {(i, j, k): get(x0 + i, y0 + j, z0 + k) for i in (0, 1) for j in (0, 1) for k in (0, 1)}
+        x, y, z = x - x0, y - y0, z - z0
+        c00 = v[0, 0, 0] * (1 - x) + v[1, 0, 0] * x
+        c01 = v[0, 0, 1] * (1 - x) + v[1, 0, 1] * x
+        c10 = v[0, 1, 0] * (1 - x) + v[1, 1, 0] * x
+        c11 = v[0, 1, 1] * (1 - x) + v[1, 1, 1] * x
+        c0 = c00 * (1 - y) + c10 * y
+        c1 = c01 * (1 - y) + c11 * y
+        return c0 * (1 - z) + c1 * z
+
+
+class TransformedShape:
+    """PTSharpCore.TransformedShape (TransformedShape.cs), a struct: as a light it never passes
+    Sampler's identity test.  The inner shape may be a Sphere, Cube, Plane, SDFShape or Volume."""
+
+    def __init__(self, shape, matrix: Matrix, inverse: Matrix):
+        self.Shape, self.Matrix, self.Inverse = shape, matrix, inverse
+
+    @staticmethod
+    def NewTransformedShape(shape, matrix: Matrix) -> "TransformedShape":
+        return TransformedShape(shape, matrix, matrix.Inverse())
+
+    def MaterialAt(self, p=None) -> Material:
+        return self.Shape.MaterialAt(p)
+
+
 class OBJ:
     """PTSharpCore.OBJ (OBJ.cs), parsed natively by libptsharp_hip.so (pt_obj_load)
     with the reference's quirks; see include/ptsharp_hip.h and DESIGN.md §9a."""
@@ -459,6 +648,54 @@ class FlatScene:
         tri_parts = []  # list of (v1,v2,v3,n1,n2,n3,mat,t1,t2,t3)
         ntri = 0
         mesh_first, mesh_count = [], []
+        sdf_nodes, sdf_children, sdf_ids = [], [], {}
+        sdf_shapes, volumes, vol_keep, xforms = [], [], [], []
+
+        def sdf_node(n) -> int:   # post-order: children before their parent
+            if id(n) in sdf_ids:
+                return sdf_ids[id(n)]
+            kids = [sdf_node(c) for c in n.children]
+            nd = _abi.pt_sdf_node()
+            nd.op, nd.num_children, nd.first_child = n.op, len(kids), len(sdf_children)
+            sdf_children.extend(kids)
+            for k, v in enumerate(n.params):
+                nd.params[k] = v
+            if n.matrix is not None:
+                for k, v in enumerate(n.matrix.m.reshape(-1)):
+                    nd.matrix[k] = float(v)
+                for k, v in enumerate(n.inverse.m.reshape(-1)):
+                    nd.inverse[k] = float(v)
+            sdf_ids[id(n)] = len(sdf_nodes)
+            sdf_nodes.append(nd)
+            return sdf_ids[id(n)]
+
+        def ext(s):
+            """(kind, index) of a shape that lives in the per-kind arrays only (inner of a TransformedShape)."""
+            if isinstance(s, Sphere):
+                sph_c.append(s.Center.f32()); sph_r.append(s.Radius); sph_m.append(mid(s.Material))
+                return _abi.SHAPE_SPHERE, len(sph_r) - 1
+            if isinstance(s, Cube):
+                cub_a.append(s.Min.f32()); cub_b.append(s.Max.f32()); cub_m.append(mid(s.Material))
+                return _abi.SHAPE_CUBE, len(cub_m) - 1
+            if isinstance(s, Plane):
+                pl_p.append(s.Point.f32()); pl_n.append(s.Normal.f32()); pl_m.append(mid(s.Material))
+                return _abi.SHAPE_PLANE, len(pl_m) - 1
+            if isinstance(s, SDFShape):
+                sdf_shapes.append((sdf_node(s.SDF), mid(s.Material)))
+                return _abi.SHAPE_SDF, len(sdf_shapes) - 1
+            if isinstance(s, Volume):
+                wins = (_abi.pt_volume_window * max(1, len(s.Windows)))()
+                for k, w in enumerate(s.Windows):
+                    wins[k] = _abi.pt_volume_window(w.Lo, w.Hi, mid(w.VolumeWindowMaterial), 0)
+                vol_keep.append((s.Data, wins))
+                volumes.append(_abi.pt_volume(s.W, s.H, s.D, len(s.Windows), s.ZScale,
+                                              s.Data.ctypes.data_as(C.POINTER(C.c_double)),
+                                              C.cast(wins, C.POINTER(_abi.pt_volume_window)),
+                                              (C.c_float * 3)(*s.Box.Min.f32()), (C.c_float * 3)(*s.Box.Max.f32())))
+                return _abi.SHAPE_VOLUME, len(volumes) - 1
+            raise _abi.PTError(_abi.PT_ERR_UNSUPPORTED, "Scene.flatten",
+                               f"{type(s).__name__} inside a TransformedShape is not on the GPU path")
+
         for s in scene.Shapes:
             if isinstance(s, Sphere):
                 kinds.append(_abi.SHAPE_SPHERE); idxs.append(len(sph_r))
@@ -476,6 +713,19 @@ class FlatScene:
                                  + (np.array([mid(s.Material)], np.int32),)
                                  + tuple(np.array([getattr(s, a).f32()], np.float32) for a in ("T1", "T2", "T3")))
                 ntri += 1
+            elif isinstance(s, (SDFShape, Volume)):
+                k, i = ext(s)
+                kinds.append(k); idxs.append(i)
+            elif isinstance(s, TransformedShape):
+                k, i = ext(s.Shape)
+                x = _abi.pt_transformed_shape()
+                x.shape_kind, x.shape_index = k, i
+                for j, v in enumerate(s.Matrix.m.reshape(-1)):
+                    x.matrix[j] = float(v)
+                for j, v in enumerate(s.Inverse.m.reshape(-1)):
+                    x.inverse[j] = float(v)
+                kinds.append(_abi.SHAPE_TRANSFORMED); idxs.append(len(xforms))
+                xforms.append(x)
             elif isinstance(s, Mesh):
                 kinds.append(_abi.SHAPE_MESH); idxs.append(len(mesh_first))
                 remap = np.array([mid(m) for m in s.materials], np.int32)
@@ -494,6 +744,12 @@ class FlatScene:
                                                  tid(m.Texture), tid(m.NormalTexture), tid(m.BumpTexture),
                                                  tid(m.GlossTexture), 0, m.BumpMultiplier)
         self.material_list = mats
+        arr = lambda T, L: (T * max(1, len(L)))(*L)
+        self.sdf_nodes, self.sdf_children = arr(_abi.pt_sdf_node, sdf_nodes), np.array(sdf_children or [0], np.int32)
+        self.sdf_shapes = arr(_abi.pt_sdf_shape, [_abi.pt_sdf_shape(r, m) for r, m in sdf_shapes])
+        self.volumes, self._vol_keep = arr(_abi.pt_volume, volumes), vol_keep
+        self.transformed = arr(_abi.pt_transformed_shape, xforms)
+        self.counts_ext = (len(sdf_nodes), len(sdf_shapes), len(volumes), len(xforms))
         self.env_texture = tid(scene.Texture)
         self.env_texture_angle = float(scene.TextureAngle)
         self.texture_list = texs
@@ -535,7 +791,12 @@ class FlatScene:
                    (C.c_double * 3)(*self.env),
                    len(self.texture_list), C.cast(self.textures, C.POINTER(_abi.pt_texture)),
                    P(self.tri_t1, fl), P(self.tri_t2, fl), P(self.tri_t3, fl),
-                   self.env_texture, 0, self.env_texture_angle)
+                   self.env_texture, 0, self.env_texture_angle,
+                   self.counts_ext[0], C.cast(self.sdf_nodes, C.POINTER(_abi.pt_sdf_node)),
+                   self.sdf_children.ctypes.data_as(C.POINTER(C.c_int32)),
+                   self.counts_ext[1], C.cast(self.sdf_shapes, C.POINTER(_abi.pt_sdf_shape)),
+                   self.counts_ext[2], C.cast(self.volumes, C.POINTER(_abi.pt_volume)),
+                   self.counts_ext[3], C.cast(self.transformed, C.POINTER(_abi.pt_transformed_shape)))
 
     @property
     def num_triangles(self) -> int:

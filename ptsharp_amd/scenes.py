@@ -12,6 +12,11 @@ as PTSharpCore/Example.cs builds them.  No model assets ship with the reference
   textured         §8f row 3: colour / gloss / normal / bump maps, a textured light and an
                    environment map with TextureAngle, on seeded synthetic textures (no
                    texture assets ship with the reference either)
+  sdf              Example.sdf (Example.cs:1398-1424), §8f row 4
+  sdf_zoo          every other SDF node (capsule, torus, scale, union, repeat) and an SDF light
+  volume           Example.volume (Example.cs:1426-1471) on seeded synthetic slices
+  transformed      TransformedShape over spheres (Example.go's stones, Translate quirk kept),
+                   a cube, a plane, an SDF shape and a volume, and a transformed light
 """
 from __future__ import annotations
 
@@ -19,9 +24,11 @@ import math
 
 import numpy as np
 
-from .geometry import Box, Colour, Util, Vector
-from .scene import (Camera, ColorTexture, Cube, DefaultSampler, Material, Mesh, Plane, Scene, SpecularMode, Sphere,
-                    Triangle)
+from .geometry import Box, Colour, Matrix, Util, Vector
+from .scene import (Camera, CapsuleSDF, ColorTexture, Cube, CubeSDF, CylinderSDF, DefaultSampler, DifferenceSDF,
+                    IntersectionSDF, LightMode, Material, Mesh, Plane, RepeatSDF, ScaleSDF, Scene, SDFShape,
+                    SpecularMode, Sphere, SphereSDF, TorusSDF, TransformedShape, TransformSDF, Triangle, UnionSDF,
+                    Volume, VolumeWindow)
 
 F = lambda x: float(np.float32(x))  # C# float literal (e.g. 0.75F)
 
@@ -219,6 +226,121 @@ def textured(mesh_tris: int = 2000):
     return scene, camera, sampler
 
 
+def sdf():
+    """Example.sdf (Example.cs:1398-1424)."""
+    scene = Scene()
+    light = Material.LightMaterial(Colour.White, 180)
+    d = F(4.0)
+    for v in (Vector(-1, -1, F(0.5)), Vector(0, -1, F(0.25)), Vector(-1, 1, 0)):
+        scene.Add(Sphere.NewSphere(v.Normalize().MulScalar(d), F(0.25), light))
+    material = Material.GlossyMaterial(Colour.HexColor(0x468966), F(1.2), Util.Radians(20))
+    sphere = SphereSDF.NewSphereSDF(F(0.65))
+    cube = CubeSDF.NewCubeSDF(Vector(1, 1, 1))
+    rounded = IntersectionSDF.NewIntersectionSDF([sphere, cube])
+    a = CylinderSDF.NewCylinderSDF(F(0.25), F(1.1))
+    b = TransformSDF.NewTransformSDF(a, Matrix.RotateM(Vector(1, 0, 0), Util.Radians(90)))
+    c = TransformSDF.NewTransformSDF(a, Matrix.RotateM(Vector(0, 0, 1), Util.Radians(90)))
+    difference = DifferenceSDF.NewDifferenceSDF([rounded, a, b, c])
+    shape = TransformSDF.NewTransformSDF(difference, Matrix.RotateM(Vector(0, 0, 1), Util.Radians(30)))
+    scene.Add(SDFShape.NewSDFShape(shape, material))
+    floor = Material.GlossyMaterial(Colour.HexColor(0xFFF0A5), F(1.2), Util.Radians(20))
+    scene.Add(Plane.NewPlane(Vector(0, 0, F(-0.5)), Vector(0, 0, 1), floor))
+    camera = Camera.LookAt(Vector(-3, 0, 1), Vector(0, 0, 0), Vector(0, 0, 1), 35)
+    sampler = DefaultSampler.NewSampler(4, 4)
+    sampler.LightMode = LightMode.LightModeAll
+    sampler.SpecularMode = SpecularMode.SpecularModeAll
+    return scene, camera, sampler
+
+
+def sdf_zoo():
+    """The SDF nodes Example.sdf does not use: CapsuleSDF, TorusSDF (with its flat bounding box,
+    SDF.cs:314-318), ScaleSDF, UnionSDF, RepeatSDF (zero box, so only inside an intersection), a
+    non-2 LengthN exponent, and an emissive SDF shape (a class shape: a real light)."""
+    scene = Scene()
+    scene.Color = Colour(0.05, 0.05, 0.08)
+    glossy = Material.GlossyMaterial(Colour.HexColor(0xBEDB39), F(1.3), Util.Radians(15))
+    capsule = CapsuleSDF.NewCapsuleSDF(Vector(-0.6, -0.3, 0.2), Vector(0.4, 0.5, 0.6), F(0.2))
+    torus = TransformSDF.NewTransformSDF(TorusSDF.NewTorusSDF(F(0.5), F(0.15)), Matrix.TranslateM(Vector(0.3, 0.2, -0.25)))
+    blob = ScaleSDF.NewScaleSDF(SphereSDF(( F(0.5), 3.0)), F(0.8))       # LengthN with exponent 3
+    union = UnionSDF.NewUnionSDF([capsule, torus, TransformSDF.NewTransformSDF(blob, Matrix.TranslateM(Vector(0.6, -0.5, 0.3)))])
+    scene.Add(SDFShape.NewSDFShape(union, glossy))
+    grid = IntersectionSDF.NewIntersectionSDF([CubeSDF.NewCubeSDF(Vector(2.4, 2.4, 0.3)),
+                                               RepeatSDF.NewRepeaterSDF(SphereSDF.NewSphereSDF(F(0.12)), Vector(0.3, 0.3, 0.3))])
+    scene.Add(SDFShape.NewSDFShape(TransformSDF.NewTransformSDF(grid, Matrix.TranslateM(Vector(0, 0, -0.55))),
+                                   Material.DiffuseMaterial(Colour.HexColor(0xFD7400))))
+    lamp = SphereSDF.NewSphereSDF(F(0.3))
+    scene.Add(SDFShape.NewSDFShape(TransformSDF.NewTransformSDF(lamp, Matrix.TranslateM(Vector(-0.5, 1.2, 1.6))),
+                                   Material.LightMaterial(Colour.White, 30)))
+    scene.Add(Plane.NewPlane(Vector(0, 0, -0.8), Vector(0, 0, 1), Material.DiffuseMaterial(Colour(0.6, 0.6, 0.6))))
+    camera = Camera.LookAt(Vector(-3, -1, 1.6), Vector(0, 0, -0.1), Vector(0, 0, 1), 40)
+    sampler = DefaultSampler.NewSampler(4, 3)
+    return scene, camera, sampler
+
+
+def volume_slices(w: int = 48, h: int = 48, d: int = 24, seed: int = 7):
+    """Seeded 8-bit slices standing in for Example.volume's images/ folder: a smooth density
+    blob (rings through every window of the scene) plus noise, as SKBitmap red channels."""
+    rng = np.random.default_rng(seed)
+    z, y, x = np.meshgrid(np.linspace(-1, 1, d), np.linspace(-1, 1, h), np.linspace(-1, 1, w), indexing="ij")
+    r = np.sqrt(x * x + 1.3 * y * y + 0.8 * z * z)
+    dens = 0.75 * np.exp(-1.5 * r * r) + 0.08 * rng.standard_normal((d, h, w))
+    return [np.clip(np.round(sl * 255), 0, 255).astype(np.uint8) for sl in dens]
+
+
+def volume(w: int = 48, h: int = 48, d: int = 24, seed: int = 7):
+    """Example.volume (Example.cs:1426-1471) on volume_slices()."""
+    scene = Scene()
+    scene.Color = Colour.White
+    colors = [Colour.HexColor(c) for c in (0x004358, 0x1F8A70, 0xBEDB39, 0xFFE11A, 0xFD7400)]
+    start, size, step = F(0.2), F(0.01), F(0.1)
+    windows = []
+    for i, col in enumerate(colors):
+        lo = start + step * float(i)
+        windows.append(VolumeWindow(lo, lo + size, Material.GlossyMaterial(col, F(1.3), Util.Radians(0))))
+    box = Box(Vector(-1, -1, F(-0.2)), Vector(1, 1, 1))
+    scene.Add(Volume.NewVolume(box, volume_slices(w, h, d, seed), F(3.4) / F(0.9765625), windows))
+    camera = Camera.LookAt(Vector(0, -3, -3), Vector(0, 0, 0), Vector(0, 0, -1), 35)
+    sampler = DefaultSampler.NewSampler(4, 4)
+    return scene, camera, sampler
+
+
+def transformed():
+    """TransformedShape (TransformedShape.cs) over every inner kind on the GPU path."""
+    scene = Scene()
+    scene.Color = Colour(0.3, 0.3, 0.35)
+    black = Material.GlossyMaterial(Colour.HexColor(0x111111), 1.5, Util.Radians(45))
+    white = Material.GlossyMaterial(Colour.HexColor(0xFFFFFF), 1.6, Util.Radians(20))
+    # Example.go's stones: `new Matrix().Scale(..).Translate(..)` keeps only the translation (Matrix.cs:33-36)
+    for i, (px, pz) in enumerate([(-1.2, 0.3), (0.0, -0.4), (1.1, 0.5), (-0.4, 1.3)]):
+        m = Matrix.TranslateM(Vector(px, 0, pz))
+        scene.Add(TransformedShape.NewTransformedShape(Sphere.NewSphere(Vector(), 0.45, black if i % 2 else white), m))
+    squash = Matrix.ScaleM(Vector(0.9, 0.35, 0.6)).Mul(Matrix.RotateM(Vector(0, 1, 0), Util.Radians(25)))
+    scene.Add(TransformedShape.NewTransformedShape(
+        Sphere.NewSphere(Vector(), 1, Material.SpecularMaterial(Colour.HexColor(0x334D5C), 2)),
+        Matrix.TranslateM(Vector(0.2, 0.35, -1.4)).Mul(squash)))
+    cube_m = Matrix.TranslateM(Vector(1.6, 0.4, -0.6)).Mul(Matrix.RotateM(Vector(1, 1, 0), Util.Radians(35)))
+    scene.Add(TransformedShape.NewTransformedShape(
+        Cube.NewCube(Vector(-0.3, -0.3, -0.3), Vector(0.3, 0.3, 0.3), Material.DiffuseMaterial(Colour.HexColor(0xFFE11A))),
+        cube_m))
+    tor = SDFShape.NewSDFShape(TorusSDF(( F(0.45), F(0.12), 2, 2)), Material.GlossyMaterial(Colour.HexColor(0x1F8A70), 1.4, 0.2))
+    scene.Add(TransformedShape.NewTransformedShape(
+        tor, Matrix.TranslateM(Vector(-1.5, 0.6, -0.9)).Mul(Matrix.RotateM(Vector(1, 0, 0), Util.Radians(70)))))
+    vol, _, _ = volume(16, 16, 8, seed=3)
+    scene.Add(TransformedShape.NewTransformedShape(
+        vol.Shapes[0], Matrix.TranslateM(Vector(0.2, 1.2, 0.9)).Mul(Matrix.ScaleM(Vector(0.4, 0.4, 0.4)))))
+    floor = Plane.NewPlane(Vector(0, 0, 0), Vector(0, 1, 0), Material.GlossyMaterial(Colour.HexColor(0xEFECCA), 1.2,
+                                                                                       Util.Radians(30)))
+    scene.Add(TransformedShape.NewTransformedShape(floor, Matrix.TranslateM(Vector(0, -0.45, 0))
+                                                   .Mul(Matrix.RotateM(Vector(0, 0, 1), Util.Radians(4)))))
+    lamp = Sphere.NewSphere(Vector(), 0.5, Material.LightMaterial(Colour.White, 20))
+    scene.Add(TransformedShape.NewTransformedShape(lamp, Matrix.TranslateM(Vector(-1, 3, 1))))   # phantom light
+    scene.Add(Sphere.NewSphere(Vector(1.5, 3.5, 1.5), 0.5, Material.LightMaterial(Colour.White, 25)))
+    camera = Camera.LookAt(Vector(0, 2.4, 4.2), Vector(0, 0.2, 0), Vector(0, 1, 0), 45)
+    sampler = DefaultSampler.NewSampler(4, 4)
+    sampler.SetSpecularMode(SpecularMode.SpecularModeFirst)
+    return scene, camera, sampler
+
+
 SCENES = {
     "gopher3": gopher3,
     "materialspheres": materialspheres,
@@ -229,4 +351,8 @@ SCENES = {
     "furnace": furnace,
     "emitter": emitter,
     "textured": textured,
+    "sdf": sdf,
+    "sdf_zoo": sdf_zoo,
+    "volume": volume,
+    "transformed": transformed,
 }

@@ -59,6 +59,11 @@ def lib() -> C.CDLL:
         L.or_environment.argtypes = [vp, f3, dp]
         L.or_hit_surface.restype = C.c_int32
         L.or_hit_surface.argtypes = [vp, f3, f3, dp, dp]
+        L.or_sdf_evaluate.restype = C.c_double
+        L.or_sdf_evaluate.argtypes = [vp, C.c_int32, f3]
+        L.or_volume_sample.restype = C.c_double
+        L.or_volume_sample.argtypes = [vp, C.c_int32, C.c_double, C.c_double, C.c_double]
+        L.or_shape_box.argtypes = [vp, C.c_int32, C.c_int32, f3, f3]
         L.or_camera_key.restype = C.c_uint64
         L.or_camera_key.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]
         L.or_child_key.restype = C.c_uint64
@@ -109,6 +114,17 @@ class OracleScene:
         out = (C.c_double * 3)()
         lib().or_environment(self.h, f3(direction), out)
         return tuple(out)
+
+    def sdf_evaluate(self, node: int, p) -> float:
+        return lib().or_sdf_evaluate(self.h, node, f3(p))
+
+    def volume_sample(self, volume: int, x, y, z) -> float:
+        return lib().or_volume_sample(self.h, volume, x, y, z)
+
+    def shape_box(self, kind: int, index: int):
+        mn, mx = (C.c_float * 3)(), (C.c_float * 3)()
+        lib().or_shape_box(self.h, kind, index, mn, mx)
+        return tuple(mn), tuple(mx)
 
     def hit_surface(self, origin, direction):
         col, gloss = (C.c_double * 3)(), C.c_double()

@@ -114,7 +114,7 @@ def _fields_cs(src, name):
     body = re.sub(r"//[^\n]*", "", body)
     out = []
     for decl in body.split(";"):
-        decl = decl.replace("public", "").replace("fixed", "").strip()
+        decl = decl.replace("public", "").replace("fixed", "").replace("@", "").strip()
         if not decl:
             continue
         names = decl.split(None, 1)[1]
@@ -125,7 +125,8 @@ def _fields_cs(src, name):
 
 
 @pytest.mark.parametrize("name", ["pt_pass_params", "pt_stats", "pt_mesh_data", "pt_sampler", "pt_device_opts",
-                                  "pt_camera", "pt_material", "pt_texture", "pt_scene_desc"])
+                                  "pt_camera", "pt_material", "pt_texture", "pt_scene_desc", "pt_sdf_node",
+                                  "pt_sdf_shape", "pt_volume_window", "pt_volume", "pt_transformed_shape"])
 def test_csharp_binding_matches_header(name):
     """csharp/HipRenderer.cs mirrors include/ptsharp_hip.h field for field (the library
     writes pt_stats into the caller's struct, so a stale C# layout would be overrun)."""
@@ -133,3 +134,16 @@ def test_csharp_binding_matches_header(name):
     c = _fields_c(open(HEADER).read(), name)
     cs = _fields_cs(open(os.path.join(root, "csharp", "HipRenderer.cs")).read(), name)
     assert cs == c
+
+
+@pytest.mark.parametrize("name", ["pt_pass_params", "pt_stats", "pt_mesh_data", "pt_sampler", "pt_device_opts",
+                                  "pt_camera", "pt_material", "pt_texture", "pt_scene_desc", "pt_sdf_node",
+                                  "pt_sdf_shape", "pt_volume_window", "pt_volume", "pt_transformed_shape",
+                                  "pt_trace_counters"])
+def test_python_binding_matches_header(name):
+    """ptsharp_amd/_abi.py mirrors include/ptsharp_hip.h field for field (names and array lengths)."""
+    c = _fields_c(open(HEADER).read(), name)
+    py = []
+    for fname, ftype in getattr(_abi, name)._fields_:
+        py.append((fname, getattr(ftype, "_length_", 1)))
+    assert py == c

@@ -1,0 +1,49 @@
+"""§8f row 4 on the GPU (libptsharp_hip.so through the C-ABI) vs the oracle, same seed:
+SDF shapes (every node kind), Volume, TransformedShape over each inner kind.  Same bar
+as tests/test_gpu_parity.py."""
+import numpy as np
+import pytest
+
+from parity import MIN_FRACTION_OK, MIN_PSNR_DB, compare, render_both
+from ptsharp_amd import Cube, Matrix, Scene, TransformedShape, Vector, _abi, scenes
+
+pytestmark = pytest.mark.gpu
+
+ENGINES = pytest.mark.parametrize("engine", [_abi.ENGINE_MEGAKERNEL, _abi.ENGINE_WAVEFRONT], ids=["mega", "wave"])
+
+
+def check(g, grays, o, orays):
+    assert np.array_equal(g.N, o.N)
+    frac, maxerr, psnr = compare(g.M, o.M)
+    assert frac >= MIN_FRACTION_OK, f"only {frac:.5f} of pixels within tolerance (max err {maxerr:.3g})"
+    assert psnr >= MIN_PSNR_DB, f"PSNR {psnr:.2f} dB"
+    assert abs(grays - orays) <= 1e-3 * orays + 2, f"rays gpu {grays} vs oracle {orays}"
+
+
+@ENGINES
+@pytest.mark.parametrize("name", ["sdf", "sdf_zoo", "volume", "transformed"])
+def test_row4_scene(gpu, engine, name):
+    s, c, smp = scenes.SCENES[name]()
+    smp.MaxBounces = min(smp.MaxBounces, 3)
+    g, gr, o, orr = render_both(s, c, smp, 48, 36, spp=2, seed=31, engine=engine)
+    check(g, gr, o, orr)
+
+
+@ENGINES
+def test_transformed_furnace_exact(gpu, engine):
+    s, cam, smp = scenes.furnace(0.5)
+    cube = s.Shapes[0]
+    s2 = Scene()
+    s2.Color = s.Color
+    s2.Add(TransformedShape.NewTransformedShape(Cube.NewCube(cube.Min, cube.Max, cube.Material),
+                                                Matrix.TranslateM(Vector(0, 0, 0))))
+    g, gr, o, orr = render_both(s2, cam, smp, 48, 32, spp=2, seed=32, engine=engine)
+    assert set(np.unique(g.M)) <= {0.5, 1.0}
+    assert np.array_equal(g.M, o.M) and gr == orr
+
+
+def test_row4_adaptive(gpu):
+    s, c, smp = scenes.sdf_zoo()
+    smp.MaxBounces = 2
+    g, gr, o, orr = render_both(s, c, smp, 40, 30, spp=1, seed=33, engine=_abi.ENGINE_WAVEFRONT, adaptive=2)
+    check(g, gr, o, orr)
