@@ -243,6 +243,7 @@ namespace PTSharpCore
             // their fields private in the reference (SDF.cs, Volume.cs:21-27, TransformedShape.cs:11-13):
             // the integration marks them `internal` (INTEGRATION.md), as for Plane.
             var sdfNodes = new List<PtHip.pt_sdf_node>(); var sdfKids = new List<int>(); var sdfIds = new Dictionary<SDF, int>(ReferenceEqualityComparer.Instance);
+            var meshIds = new Dictionary<IShape, int>(ReferenceEqualityComparer.Instance);
             var sdfShapes = new List<PtHip.pt_sdf_shape>(); var vols = new List<PtHip.pt_volume>(); var xfs = new List<PtHip.pt_transformed_shape>();
             void Mat16(double* dst, Matrix m)
             {
@@ -299,6 +300,16 @@ namespace PTSharpCore
                         v.box_max[0] = (float)vo.Box.Max.X; v.box_max[1] = (float)vo.Box.Max.Y; v.box_max[2] = (float)vo.Box.Max.Z;
                         vols.Add(v);
                         return (PtHip.SHAPE_VOLUME, vols.Count - 1);
+                    }
+                    case Mesh me:   // instanced: the mesh's triangles in object space, one BLAS per distinct mesh
+                    {
+                        if (!meshIds.TryGetValue(s, out int id))
+                        {
+                            id = mf.Count; mf.Add(tm.Count); mc.Add(me.Triangles.Length);
+                            foreach (var t in me.Triangles) AddTri(t);
+                            meshIds[s] = id;
+                        }
+                        return (PtHip.SHAPE_MESH, id);
                     }
                     default: throw new NotSupportedException($"{s.GetType().Name} inside a TransformedShape is not on the GPU path");
                 }

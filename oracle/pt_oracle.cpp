@@ -855,6 +855,13 @@ double inner_t(const Scene& s, int kind, int idx, const Ray& ray) {
     }
     return HIT_INF;
 }
+Hit mesh_hit(const Scene& s, int mesh, const Ray& ray);   // Mesh.Intersect through its own tree (below)
+// The inner shape's Hit (a mesh reports the Triangle it hit, as Mesh.Intersect does).
+Hit inner_hit(const Scene& s, int kind, int idx, const Ray& ray) {
+    if (kind == K_MESH) return mesh_hit(s, idx, ray);
+    double t = inner_t(s, kind, idx, ray);
+    return t < HIT_INF ? Hit{t, kind, idx} : NOHIT;
+}
 // TransformedShape.Intersect (TransformedShape.cs:43-73) up to hit.T: the inner shape's hit
 // mapped back to world space, T = |position - origin| (fp32 Length).
 inline Ray xform_shape_ray(const Xform& x, const Ray& r) {  // Matrix.Inverse().MulRay(r)
@@ -862,9 +869,9 @@ inline Ray xform_shape_ray(const Xform& x, const Ray& r) {  // Matrix.Inverse().
 }
 double xform_t(const Scene& s, const Xform& x, const Ray& r) {
     Ray sr = xform_shape_ray(x, r);
-    double t = inner_t(s, x.kind, x.idx, sr);
-    if (!(t < HIT_INF)) return HIT_INF;
-    V position = mat_position(x.M, ray_position(sr, t));
+    Hit h = inner_hit(s, x.kind, x.idx, sr);
+    if (!(h.t < HIT_INF)) return HIT_INF;
+    V position = mat_position(x.M, ray_position(sr, h.t));
     return vlen(vsub(position, r.o));
 }
 
@@ -948,6 +955,8 @@ struct Tracer {
     }
 };
 
+Hit mesh_hit(const Scene& s, int mesh, const Ray& ray) { return Tracer(s, false).tree_intersect(s.mesh_trees[(size_t)mesh], ray); }
+
 struct HitInfo { V position, normal; Ray ray; int mat; bool inside; C color; double gloss; };
 
 V shape_normal(const Scene& s, const Hit& h, V p) {
@@ -985,13 +994,13 @@ HitInfo hit_info(const Scene& s, const Hit& h, const Ray& r) {
     if (h.kind == K_XFORM) {  // the HitInfo TransformedShape.Intersect builds (TransformedShape.cs:52-70)
         const Xform& x = s.xforms[(size_t)h.idx];
         Ray sr = xform_shape_ray(x, r);
-        double t = inner_t(s, x.kind, x.idx, sr);
-        V sp = ray_position(sr, t);
-        V sn = shape_normal(s, Hit{t, x.kind, x.idx}, sp);
+        Hit ih = inner_hit(s, x.kind, x.idx, sr);   // hit.Shape: the inner shape (a mesh's Triangle)
+        V sp = ray_position(sr, ih.t);
+        V sn = shape_normal(s, ih, sp);
         info.position = mat_position(x.M, sp);
         V normal = mat_direction_transposed(x.Inv, sn);   // Matrix.Inverse().Transpose().MulDirection
-        info.mat = material_index_at(s, x.kind, x.idx, sp);
-        Surf sf = material_at(s, x.kind, x.idx, info.mat, sp);
+        info.mat = material_index_at(s, ih.kind, ih.idx, sp);
+        Surf sf = material_at(s, ih.kind, ih.idx, info.mat, sp);
         info.color = sf.color;
         info.gloss = sf.gloss;
         info.inside = false;

@@ -431,7 +431,7 @@ int validate_scene(const pt_scene_desc* d) {
         const pt_transformed_shape& x = d->transformed[i];
         int lim = x.shape_kind == PT_SHAPE_SPHERE ? d->num_spheres : x.shape_kind == PT_SHAPE_CUBE ? d->num_cubes
                 : x.shape_kind == PT_SHAPE_PLANE ? d->num_planes : x.shape_kind == PT_SHAPE_SDF ? d->num_sdf_shapes
-                : x.shape_kind == PT_SHAPE_VOLUME ? d->num_volumes : -1;
+                : x.shape_kind == PT_SHAPE_VOLUME ? d->num_volumes : x.shape_kind == PT_SHAPE_MESH ? d->num_meshes : -1;
         if (lim < 0) return fail(PT_ERR_UNSUPPORTED, "transformed shape " + std::to_string(i) + ": inner kind not on the GPU path");
         if (x.shape_index < 0 || x.shape_index >= lim) return fail(PT_ERR_INVALID_ARG, "transformed shape " + std::to_string(i) + ": inner index out of range");
     }
@@ -614,6 +614,16 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
             case PT_SHAPE_PLANE: return HostBox{pt::mk(-1e9, -1e9, -1e9), pt::mk(1e9, 1e9, 1e9)};
             case PT_SHAPE_SDF: return sdf_boxes[(size_t)j];
             case PT_SHAPE_VOLUME: return HostBox{ld3(d->volumes[j].box_min), ld3(d->volumes[j].box_max)};
+            case PT_SHAPE_MESH: {   // Mesh.BoundingBox (Mesh.cs:88-120)
+                const int f = d->mesh_first[j], n = d->mesh_count[j];
+                if (n <= 0) return HostBox{pt::zero3(), pt::zero3()};
+                HostBox b{ld3(d->tri_v1 + 3 * f), ld3(d->tri_v1 + 3 * f)};
+                for (int t = f; t < f + n; t++) {
+                    b.mn = pt::vmin(pt::vmin(pt::vmin(b.mn, ld3(d->tri_v1 + 3 * t)), ld3(d->tri_v2 + 3 * t)), ld3(d->tri_v3 + 3 * t));
+                    b.mx = pt::vmax(pt::vmax(pt::vmax(b.mx, ld3(d->tri_v1 + 3 * t)), ld3(d->tri_v2 + 3 * t)), ld3(d->tri_v3 + 3 * t));
+                }
+                return b;
+            }
         }
         return HostBox{pt::zero3(), pt::zero3()};
     };
@@ -653,6 +663,50 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
             r[2] = f4(u2f((uint32_t)ext_mat), u2f((uint32_t)j), 0.f, 0.f);
         }
     };
+    // instanced meshes: one object-space BVH4 per distinct inner mesh (BLAS), records in their own arrays
+    std::vector<pt::DevBlas> blas;
+    std::vector<float4> blas_nodes, blas_recs, blas_shade, blas_uv;
+    std::vector<int32_t> blas_of_mesh((size_t)std::max(d->num_meshes, 0), -1);
+    for (int i = 0; i < d->num_transformed; i++) {
+        const pt_transformed_shape& x = d->transformed[i];
+        if (x.shape_kind != PT_SHAPE_MESH || blas_of_mesh[(size_t)x.shape_index] >= 0) continue;
+        const int f = d->mesh_first[x.shape_index], n = d->mesh_count[x.shape_index];
+        std::vector<float> lo((size_t)n * 3), hi((size_t)n * 3);
+        for (int t = 0; t < n; t++)
+            for (int k = 0; k < 3; k++) {
+                float a = d->tri_v1[3 * (f + t) + k], b = d->tri_v2[3 * (f + t) + k], cc = d->tri_v3[3 * (f + t) + k];
+                lo[3 * (size_t)t + k] = std::fmin(std::fmin(a, b), cc);
+                hi[3 * (size_t)t + k] = std::fmax(std::fmax(a, b), cc);
+            }
+        for (int t = 0; t < n; t++) pad_box(&lo[3 * (size_t)t], &hi[3 * (size_t)t]);
+        pt::BvhResult bb;
+        pt::build_bvh(lo.data(), hi.data(), (int64_t)n, 0, bb);
+        std::vector<float4> nodes;
+        int32_t nn = 0;
+        if ((rc = pack_nodes(bb, nodes, nn))) return rc;
+        pt::DevBlas B{(int32_t)(blas_nodes.size() / 8), nn, (int32_t)(blas_recs.size() / 3), 0};
+        blas_nodes.insert(blas_nodes.end(), nodes.begin(), nodes.end());
+        for (int t = 0; t < n; t++) {
+            const int src = f + (int)bb.order[(size_t)t];
+            pt::v3 v1 = ld3(d->tri_v1 + 3 * src), v2 = ld3(d->tri_v2 + 3 * src), v3_ = ld3(d->tri_v3 + 3 * src);
+            pt::v3 e1 = pt::sub(v2, v1), e2 = pt::sub(v3_, v1);
+            blas_recs.push_back(f4(v1.x, v1.y, v1.z, e1.x));
+            blas_recs.push_back(f4(e1.y, e1.z, e2.x, e2.y));
+            blas_recs.push_back(f4(e2.z, 0.f, 0.f, 0.f));
+            const float* n1 = d->tri_n1 + 3 * src; const float* n2 = d->tri_n2 + 3 * src; const float* n3 = d->tri_n3 + 3 * src;
+            blas_shade.push_back(f4(n1[0], n1[1], n1[2], n2[0]));
+            blas_shade.push_back(f4(n2[1], n2[2], n3[0], n3[1]));
+            blas_shade.push_back(f4(n3[2], u2f((uint32_t)d->tri_material[src]), 0.f, 0.f));
+            const float zero[3] = {0.f, 0.f, 0.f};
+            const float* t1 = d->tri_t1 ? d->tri_t1 + 3 * src : zero;
+            const float* t2 = d->tri_t2 ? d->tri_t2 + 3 * src : zero;
+            const float* t3 = d->tri_t3 ? d->tri_t3 + 3 * src : zero;
+            blas_uv.push_back(f4(t1[0], t1[1], t2[0], t2[1]));
+            blas_uv.push_back(f4(t3[0], t3[1], 0.f, 0.f));
+        }
+        blas_of_mesh[(size_t)x.shape_index] = (int32_t)blas.size();
+        blas.push_back(B);
+    }
     std::vector<pt::DevXform> xforms((size_t)std::max(d->num_transformed, 0));
     std::vector<float4> ext_recs(xforms.size() * 3);
     std::vector<HostBox> xform_boxes(xforms.size()), xform_bvh_boxes(xforms.size());
@@ -664,9 +718,11 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         pt::DevXform& o = xforms[i];
         rows12(x.matrix, o.m);
         rows12(x.inverse, o.inv);
-        o.kind = x.shape_kind == PT_SHAPE_SDF ? pt::KIND_SDF : x.shape_kind == PT_SHAPE_VOLUME ? pt::KIND_VOLUME : x.shape_kind;
-        o.rec = (int32_t)i;
-        make_rec(x.shape_kind, x.shape_index, shape_mat(x.shape_kind, x.shape_index, origin), &ext_recs[3 * i]);
+        o.kind = x.shape_kind == PT_SHAPE_SDF ? pt::KIND_SDF : x.shape_kind == PT_SHAPE_VOLUME ? pt::KIND_VOLUME
+               : x.shape_kind == PT_SHAPE_MESH ? pt::KIND_MESH : x.shape_kind;
+        o.rec = x.shape_kind == PT_SHAPE_MESH ? blas_of_mesh[(size_t)x.shape_index] : (int32_t)i;
+        if (x.shape_kind != PT_SHAPE_MESH)
+            make_rec(x.shape_kind, x.shape_index, shape_mat(x.shape_kind, x.shape_index, origin), &ext_recs[3 * i]);
         HostBox ib = shape_box(x.shape_kind, x.shape_index);
         xform_boxes[i] = box_mul(x.matrix, ib);   // TransformedShape.BoundingBox (TransformedShape.cs:36-39)
         const double mp = march_pad(x.shape_kind);
@@ -834,6 +890,11 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, vols, &S.volumes); if (rc) return rc;
     rc = upload(c, xforms, &S.xforms); if (rc) return rc;
     rc = upload(c, ext_recs, &S.ext_recs); if (rc) return rc;
+    rc = upload(c, blas, &S.blas); if (rc) return rc;
+    rc = upload(c, blas_nodes, &S.blas_nodes); if (rc) return rc;
+    rc = upload(c, blas_recs, &S.blas_recs); if (rc) return rc;
+    rc = upload(c, blas_shade, &S.blas_shade); if (rc) return rc;
+    rc = upload(c, blas_uv, &S.blas_uv); if (rc) return rc;
     S.default_mat = default_mat;
     S.full = (d->num_textures > 0 || d->num_sdf_shapes > 0 || d->num_volumes > 0 || d->num_transformed > 0) ? 1 : 0;
     S.tri_num_nodes = tri_num_nodes;

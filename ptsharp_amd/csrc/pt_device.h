@@ -19,6 +19,15 @@ struct HitRec {
     int32_t idx;    // record position: tri_recs / ana_recs / planes
 };
 
+// A whole traversal stack in a private array (scratch): the nested traversal of an instanced mesh.
+struct LocalStack {
+    static constexpr int kLds = kMaxDepth;
+    static constexpr int kStride = 1;
+    uint32_t* lds;
+    __device__ __forceinline__ void put(int i, uint32_t v) const { lds[i] = v; }
+    __device__ __forceinline__ uint32_t get(int i) const { return lds[i]; }
+};
+
 struct Counters {
     uint32_t rays, nodes, prims, shades;
 };
@@ -50,16 +59,12 @@ __device__ __noinline__ double inner_t(const DevScene& S, const float4* r, int32
     }
     return kHitInf;
 }
+struct HitRec;
+__device__ __noinline__ HitRec blas_hit(const DevScene& S, int b, v3 o, v3 d);   // below, after traverse()
+
 // TransformedShape.Intersect (TransformedShape.cs:43-73) up to hit.T: the inner hit mapped
 // back to world space, T = |position - origin| (fp32 Length).
-__device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 o, v3 d) {
-    const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);   // Matrix.Inverse().MulRay
-    const float4* ir = S.ext_recs + 3 * (size_t)X.rec;
-    const double t = inner_t(S, ir, X.kind, so, sd);
-    if (!(t < kHitInf)) return kHitInf;
-    const v3 position = mat_position(X.m, add(so, muls(sd, t)));
-    return (double)lengthf(sub(position, o));
-}
+__device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 o, v3 d);
 
 // Intersect one record; returns t (kHitInf = miss) and the primitive kind.  FULL adds
 // the §8f row 4 kinds of the analytic BVH (SDF, volume, transformed shape).
@@ -210,6 +215,30 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
         ref = stack.get(sp);
     }
     return false;
+}
+
+// Mesh.Intersect of an instanced mesh: its own object-space BVH4 (Mesh.cs:83-86, 122-125);
+// idx is the triangle's position in the mesh's BLAS records.
+__device__ __noinline__ HitRec blas_hit(const DevScene& S, int b, v3 o, v3 d) {
+    const DevBlas B = S.blas[b];
+    uint32_t st[kMaxDepth];
+    const LocalStack stack{st};
+    HitRec best{kHitInf, -1, -1};
+    Counters ctr{0, 0, 0, 0};
+    const v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    traverse<true, false, false, false>(S, S.blas_nodes + 8 * (size_t)B.node_off, B.num_nodes,
+                                        S.blas_recs + 3 * (size_t)B.rec_off, o, d, invd, best, stack, ctr);
+    return best;
+}
+
+__device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 o, v3 d) {
+    const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);   // Matrix.Inverse().MulRay
+    double t;
+    if (X.kind == KIND_MESH) t = blas_hit(S, X.rec, so, sd).t;
+    else t = inner_t(S, S.ext_recs + 3 * (size_t)X.rec, X.kind, so, sd);
+    if (!(t < kHitInf)) return kHitInf;
+    const v3 position = mat_position(X.m, add(so, muls(sd, t)));
+    return (double)lengthf(sub(position, o));
 }
 
 // Scene.Intersect (Scene.cs:75-79): closest hit over planes, analytic BVH, triangle BVH.
@@ -437,6 +466,20 @@ struct Shade {
     double gloss;    // and gloss (gloss texture applied)
 };
 
+// Triangle.NormalAt (maps included) and its material id, for triangle record idx of S.tri_recs / tri_shade.
+__device__ inline v3 tri_normal_at(const DevScene& S, int idx, v3 p, int32_t& mat) {
+    const float4* r = S.tri_recs + 3 * (size_t)idx;
+    const float4* q = S.tri_shade + 3 * (size_t)idx;
+    const float4 a = r[0], b = r[1], c = r[2];
+    const float4 x = q[0], y = q[1], z = q[2];
+    mat = (int32_t)f2u(z.y);
+    const DevMaterial& m = S.mats[mat];
+    const v3 v1{a.x, a.y, a.z}, e1{a.w, b.x, b.y}, e2{b.z, b.w, c.x};
+    const v3 n1{x.x, x.y, x.z}, n2{x.w, y.x, y.y}, n3{y.z, y.w, z.x};
+    if (m.ntex < 0 && m.btex < 0) return tri_normal(v1, e1, e2, n1, n2, n3, p);
+    return tri_normal_mapped(S, m, idx, v1, e1, e2, n1, n2, n3, p);
+}
+
 // NormalAt / MaterialAt of an analytic-format record (kinds that can be a TransformedShape's inner shape).
 __device__ inline v3 inner_normal(const DevScene& S, const float4* r, int32_t kind, v3 p) {
     const float4 a = r[0], b = r[1];
@@ -462,14 +505,27 @@ __device__ __noinline__ void ext_hit_info(const DevScene& S, const HitRec& h, v3
     if (h.kind == KIND_XFORM) {
         const DevXform& X = S.xforms[rec_ext(r)];
         const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
-        const float4* ir = S.ext_recs + 3 * (size_t)X.rec;
-        const double t = inner_t(S, ir, X.kind, so, sd);
-        const v3 sp = add(so, muls(sd, t));
-        const v3 sn = inner_normal(S, ir, X.kind, sp);
+        v3 sp, sn;
+        if (X.kind == KIND_MESH) {   // hit.Shape is the mesh's Triangle: shade it from the BLAS records
+            const HitRec ih = blas_hit(S, X.rec, so, sd);
+            const int off = S.blas[X.rec].rec_off;
+            DevScene T = S;
+            T.tri_recs = S.blas_recs + 3 * (size_t)off;
+            T.tri_shade = S.blas_shade + 3 * (size_t)off;
+            T.tri_uv = S.blas_uv ? S.blas_uv + 2 * (size_t)off : nullptr;
+            sp = add(so, muls(sd, ih.t));
+            sn = tri_normal_at(T, ih.idx, sp, s.mat);
+            surface_at<true>(T, S.mats[s.mat], KIND_TRI, ih.idx, sp, s.col, s.gloss);
+        } else {
+            const float4* ir = S.ext_recs + 3 * (size_t)X.rec;
+            const double t = inner_t(S, ir, X.kind, so, sd);
+            sp = add(so, muls(sd, t));
+            sn = inner_normal(S, ir, X.kind, sp);
+            s.mat = inner_material(S, ir, X.kind, sp);
+            surface_at<true>(S, S.mats[s.mat], X.kind, X.rec, sp, s.col, s.gloss, S.ext_recs);
+        }
         s.pos = mat_position(X.m, sp);
         n = mat_direction_t(X.inv, sn);   // Matrix.Inverse().Transpose().MulDirection
-        s.mat = inner_material(S, ir, X.kind, sp);
-        surface_at<true>(S, S.mats[s.mat], X.kind, X.rec, sp, s.col, s.gloss, S.ext_recs);
         s.inside = 0;
         if (dot(sn, sd) > 0) { n = neg(n); s.inside = 1; }
         s.nrm = n;

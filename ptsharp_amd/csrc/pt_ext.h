@@ -55,11 +55,17 @@ struct DevVolume {
     double zscale;
     float bmin[3], bmax[3];
 };
+struct DevBlas {          // object-space BVH4 of a mesh instanced by TransformedShape
+    int32_t node_off;     // first node in blas_nodes
+    int32_t num_nodes;
+    int32_t rec_off;      // first triangle in blas_recs / blas_shade / blas_uv
+    int32_t _pad;
+};
 struct DevXform {
     double m[12];     // Matrix rows 1-3 (row 4 is 0 0 0 1 for affine transforms; MulPosition ignores it)
     double inv[12];   // Inverse rows 1-3
-    int32_t kind;     // inner shape kind (KIND_SPHERE, KIND_CUBE, KIND_PLANE, KIND_SDF, KIND_VOLUME)
-    int32_t rec;      // its record in ext_recs (analytic-record format)
+    int32_t kind;     // inner shape kind (KIND_SPHERE, KIND_CUBE, KIND_PLANE, KIND_SDF, KIND_VOLUME, KIND_MESH)
+    int32_t rec;      // its record in ext_recs (analytic-record format); KIND_MESH: its DevBlas
 };
 
 // ---------------------------------------------------------------- Matrix (Matrix.cs)

@@ -78,6 +78,11 @@ struct DevScene {
     const DevVolume* volumes;
     const DevXform* xforms;
     const float4* ext_recs;    // object-space records of transformed shapes' inner shapes (ana format)
+    const DevBlas* blas;       // instanced meshes: object-space BVH4s over their own triangle records
+    const float4* blas_nodes;
+    const float4* blas_recs;   // tri_recs / tri_shade / tri_uv formats
+    const float4* blas_shade;
+    const float4* blas_uv;
     int32_t default_mat;       // `new Material()` (Volume.MaterialAt with no window near)
     int32_t full;              // textures or §8f row 4 shapes present: kernels run their FULL instantiation
 };

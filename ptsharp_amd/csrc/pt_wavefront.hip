@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
 // sampling up to the shadow query runs here too, so k_wf_shadow is a lean
 // traversal kernel (ray + stack state only).
 template <bool COUNT, bool FULL>
-__global__ __launch_bounds__(256, PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
+__global__ __launch_bounds__(256, FULL ? 2 : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
     if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + 2 * kParts + threadIdx.x] = 0u;  // k_wf_shadow's
     const Group G = xcd_group();

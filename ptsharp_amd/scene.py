@@ -650,6 +650,7 @@ class FlatScene:
         mesh_first, mesh_count = [], []
         sdf_nodes, sdf_children, sdf_ids = [], [], {}
         sdf_shapes, volumes, vol_keep, xforms = [], [], [], []
+        inner_meshes = {}
 
         def sdf_node(n) -> int:   # post-order: children before their parent
             if id(n) in sdf_ids:
@@ -693,6 +694,15 @@ class FlatScene:
                                               C.cast(wins, C.POINTER(_abi.pt_volume_window)),
                                               (C.c_float * 3)(*s.Box.Min.f32()), (C.c_float * 3)(*s.Box.Max.f32())))
                 return _abi.SHAPE_VOLUME, len(volumes) - 1
+            if isinstance(s, Mesh):   # an instanced mesh: its triangles in object space, not in Scene.Shapes
+                if id(s) not in inner_meshes:
+                    remap = np.array([mid(m) for m in s.materials], np.int32)
+                    tri_parts.append((s.v1, s.v2, s.v3, s.n1, s.n2, s.n3, remap[s.mat_index], s.t1, s.t2, s.t3))
+                    nonlocal ntri
+                    mesh_first.append(ntri); mesh_count.append(len(s))
+                    ntri += len(s)
+                    inner_meshes[id(s)] = len(mesh_first) - 1
+                return _abi.SHAPE_MESH, inner_meshes[id(s)]
             raise _abi.PTError(_abi.PT_ERR_UNSUPPORTED, "Scene.flatten",
                                f"{type(s).__name__} inside a TransformedShape is not on the GPU path")
 

@@ -17,6 +17,7 @@ as PTSharpCore/Example.cs builds them.  No model assets ship with the reference
   volume           Example.volume (Example.cs:1426-1471) on seeded synthetic slices
   transformed      TransformedShape over spheres (Example.go's stones, Translate quirk kept),
                    a cube, a plane, an SDF shape and a volume, and a transformed light
+  instances        one Mesh instanced six times through TransformedShape
 """
 from __future__ import annotations
 
@@ -341,6 +342,27 @@ def transformed():
     return scene, camera, sampler
 
 
+def instances(copies: int = 6, mesh_tris: int = 3000):
+    """TransformedShape over one Mesh, several times (Example.cs:1016, 1274, 1339 instance meshes
+    this way): one object-space BVH shared by every instance."""
+    scene = Scene()
+    scene.Color = Colour(0.4, 0.45, 0.5)
+    mesh = blob_mesh(mesh_tris, seed=21, amplitude=0.15)
+    mesh.SetMaterial(Material.GlossyMaterial(Colour.HexColor(0xBEDB39), 1.4, Util.Radians(10)))
+    mesh.SmoothNormals()
+    rng = np.random.default_rng(5)
+    for i in range(copies):
+        m = Matrix.TranslateM(Vector(rng.uniform(-2, 2), rng.uniform(0.3, 1.2), rng.uniform(-2, 1))).Mul(
+            Matrix.RotateM(Vector(*rng.normal(size=3)), rng.uniform(0, 3))).Mul(
+            Matrix.ScaleM(Vector(*rng.uniform(0.3, 0.6, size=3))))
+        scene.Add(TransformedShape.NewTransformedShape(mesh, m))
+    scene.Add(Cube.NewCube(Vector(-20, -1, -20), Vector(20, 0, 20), Material.DiffuseMaterial(Colour(0.7, 0.7, 0.7))))
+    scene.Add(Sphere.NewSphere(Vector(2, 5, 3), 1, Material.LightMaterial(Colour.White, 15)))
+    camera = Camera.LookAt(Vector(0, 3, 5), Vector(0, 0.6, -0.5), Vector(0, 1, 0), 50)
+    sampler = DefaultSampler.NewSampler(4, 4)
+    return scene, camera, sampler
+
+
 SCENES = {
     "gopher3": gopher3,
     "materialspheres": materialspheres,
@@ -355,4 +377,5 @@ SCENES = {
     "sdf_zoo": sdf_zoo,
     "volume": volume,
     "transformed": transformed,
+    "instances": instances,
 }

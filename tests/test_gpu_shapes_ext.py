@@ -21,7 +21,7 @@ def check(g, grays, o, orays):
 
 
 @ENGINES
-@pytest.mark.parametrize("name", ["sdf", "sdf_zoo", "volume", "transformed"])
+@pytest.mark.parametrize("name", ["sdf", "sdf_zoo", "volume", "transformed", "instances"])
 def test_row4_scene(gpu, engine, name):
     s, c, smp = scenes.SCENES[name]()
     smp.MaxBounces = min(smp.MaxBounces, 3)

@@ -204,7 +204,31 @@ def test_transformed_furnace_exact():
     assert set(np.unique(b.M)) <= {0.5, 1.0} and rays > 0
 
 
-@pytest.mark.parametrize("name", ["sdf", "sdf_zoo", "volume", "transformed"])
+def test_instanced_mesh_matches_world_space_mesh():
+    """A mesh under a pure translation hits where the same mesh moved in world space does
+    (up to the fp32 rounding of the two paths), and reports T as a distance."""
+    from ptsharp_amd import Mesh
+    m = scenes.blob_mesh(800, seed=9)
+    s1, s2 = Scene(), Scene()
+    s1.Add(TransformedShape.NewTransformedShape(m, Matrix.TranslateM(Vector(0.5, 0.25, -3))))
+    moved = m.copy()
+    moved.Transform(Matrix.TranslateM(Vector(0.5, 0.25, -3)))
+    s2.Add(moved)
+    o1, o2 = O.OracleScene(s1), O.OracleScene(s2)
+    rng = np.random.default_rng(8)
+    hits = 0
+    for d in rng.normal(size=(64, 3)) * [0.15, 0.15, 1] - [0, 0, 1]:
+        d = d / np.linalg.norm(d)
+        t1, k1, _ = o1.intersect((0.5, 0.25, 0.0), d)
+        t2, k2, _ = o2.intersect((0.5, 0.25, 0.0), d)
+        assert (k1 == 7) == (k2 == 3)
+        if k1 == 7:
+            hits += 1
+            assert abs(t1 - t2) < 1e-5 * t2
+    assert hits > 20
+
+
+@pytest.mark.parametrize("name", ["sdf", "sdf_zoo", "volume", "transformed", "instances"])
 def test_row4_scenes_render(name):
     s, cam, smp = scenes.SCENES[name]()
     smp.MaxBounces = min(smp.MaxBounces, 2)
