@@ -32,19 +32,16 @@ namespace pt {
 constexpr int kTB = 256;   // threads per block, traversal kernels (LDS stack column stride)
 using WStack = SpillStack<kTB, kLdsStack>;
 
-// Streaming (nt) accesses for queue traffic: read or written once per depth, they
-// should not displace the BVH from L2 / the Infinity Cache.
+// Queue traffic.  Loads are non-temporal (read once per depth; they should not displace
+// the BVH from L2 / the Infinity Cache).  Stores go through the default policy: a shade
+// lane writes its children to consecutive slots, one 16-B field per store instruction,
+// so a 128-B line is completed over several instructions; L2 write-combines them, while
+// non-temporal stores sent the partial lines on (measured: k_wf_shade 67 → 43 ms/step).
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void nt_store(float4* p, float4 v) {
-    f4v x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, (f4v*)p);
-}
-__device__ __forceinline__ void nt_store(uint4* p, uint4 v) {
-    u4v x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, (u4v*)p);
-}
-__device__ __forceinline__ void nt_store(uint64_t* p, uint64_t v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void q_store(float4* p, float4 v) { *p = v; }
+__device__ __forceinline__ void q_store(uint4* p, uint4 v) { *p = v; }
+__device__ __forceinline__ void q_store(uint64_t* p, uint64_t v) { *p = v; }
 __device__ __forceinline__ float4 nt_load(const float4* p) {
     f4v x = __builtin_nontemporal_load((const f4v*)p);
     return make_float4(x.x, x.y, x.z, x.w);
@@ -120,10 +117,10 @@ __device__ __forceinline__ void block_reserve2(unsigned long long* word, uint32_
 
 __device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, float3 thr, uint32_t pixel,
                                           uint32_t meta, uint64_t key) {
-    nt_store(&Q.q_o[q][i], make_float4(o.x, o.y, o.z, __uint_as_float(pixel)));
-    nt_store(&Q.q_d[q][i], make_float4(d.x, d.y, d.z, __uint_as_float(meta)));
-    nt_store(&Q.q_t[q][i], make_float4(thr.x, thr.y, thr.z, 0.f));
-    nt_store(&Q.q_k[q][i], key);
+    q_store(&Q.q_o[q][i], make_float4(o.x, o.y, o.z, __uint_as_float(pixel)));
+    q_store(&Q.q_d[q][i], make_float4(d.x, d.y, d.z, __uint_as_float(meta)));
+    q_store(&Q.q_t[q][i], make_float4(thr.x, thr.y, thr.z, 0.f));
+    q_store(&Q.q_k[q][i], key);
 }
 
 __device__ __forceinline__ void acc_add(double* acc, uint32_t pixel, float r, float g, float b) {
@@ -134,6 +131,37 @@ __device__ __forceinline__ void acc_add(double* acc, uint32_t pixel, float r, fl
     if (r != 0.f) atomicAdd(a + 0, (double)r);
     if (g != 0.f) atomicAdd(a + 1, (double)g);
     if (b != 0.f) atomicAdd(a + 2, (double)b);
+#endif
+}
+
+// Wave-aggregated acc_add: lanes of a wave often add to the same pixel (a camera sample's
+// children and a pixel's samples sit in consecutive queue slots), and same-address fp64
+// atomics serialise at L2.  Lanes are grouped into runs of equal `pixel` (segment ids
+// from a ballot of run heads), each run is summed by a segmented suffix scan over
+// shuffles, and only the run's head issues the three atomics.  Wave-uniform call;
+// lanes with has = false add nothing (their pixel is ignored).
+__device__ __forceinline__ void acc_add_wave(double* acc, uint32_t pixel, bool has, float r, float g, float b) {
+#if defined(PT_ABLATE_ACC) || defined(PT_ACC_DIRECT)
+    if (has) acc_add(acc, pixel, r, g, b);
+#else
+    const int lane = threadIdx.x & 63;
+    const uint32_t pix = has ? pixel : 0xFFFFFFFFu;
+    const uint32_t prev = __shfl_up(pix, 1, 64);
+    const bool head = lane == 0 || prev != pix;
+    const uint64_t heads = __ballot(head);
+    const int seg = __popcll(heads & (~0ull >> (63 - lane)));   // run id: heads at or below this lane
+    double vr = has ? (double)r : 0.0, vg = has ? (double)g : 0.0, vb = has ? (double)b : 0.0;
+    for (int off = 1; off < 64; off <<= 1) {   // suffix sums within a run
+        const int so = __shfl_down(seg, off, 64);
+        const double ur = __shfl_down(vr, off, 64), ug = __shfl_down(vg, off, 64), ub = __shfl_down(vb, off, 64);
+        if (lane + off < 64 && so == seg) { vr += ur; vg += ug; vb += ub; }
+    }
+    if (head && has) {
+        double* a = acc + 3 * (size_t)pixel;
+        if (vr != 0.0) atomicAdd(a + 0, vr);
+        if (vg != 0.0) atomicAdd(a + 1, vg);
+        if (vb != 0.0) atomicAdd(a + 2, vb);
+    }
 #endif
 }
 
@@ -175,8 +203,11 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
 }
 
 // ---------------------------------------------------------------- closest hit
+#ifndef PT_TRACE_WAVES
+#define PT_TRACE_WAVES 7
+#endif
 template <bool COUNT, bool FULL>
-__global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB, FULL ? 2 : PT_TRACE_WAVES) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
@@ -203,7 +234,7 @@ __global__ __launch_bounds__(kTB) void k_wf_trace(DevScene S, WfQueues Q, int qi
         float4 a = nt_load(&Q.q_o[qi][i]);
         HitRec h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
         unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
-        nt_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
+        q_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
     }
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
@@ -344,9 +375,9 @@ __global__ __launch_bounds__(256, FULL ? 2 : PT_SHADE_WAVES) void k_wf_shade(Dev
                                                       all_lights ? light_key(E, (uint32_t)li) : E, ldir, lc);
                         if (nj < Q.spcap) {
                             const uint32_t at = G.g * Q.spcap + nj;
-                            nt_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
-                            nt_store(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
-                            nt_store(&Q.n_w[at], make_float4((t2[0] * w[0]) * (lc.x * scale), (t2[1] * w[1]) * (lc.y * scale),
+                            q_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
+                            q_store(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
+                            q_store(&Q.n_w[at], make_float4((t2[0] * w[0]) * (lc.x * scale), (t2[1] * w[1]) * (lc.y * scale),
                                                              (t2[2] * w[2]) * (lc.z * scale), 0.f));
                         }
                         nj++;
@@ -373,10 +404,13 @@ __global__ __launch_bounds__(256, FULL ? 2 : PT_SHADE_WAVES) void k_wf_shade(Dev
 }
 
 // ---------------------------------------------------------------- shadow rays
+#ifndef PT_SHADOW_WAVES
+#define PT_SHADOW_WAVES 7
+#endif
 // One thread per shadow ray that k_wf_shade set up (light, direction, the colour the
 // light adds if it is the nearest hit): the visibility query of Sampler.cs:261-265.
 template <bool COUNT, bool FULL>
-__global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB, FULL ? 1 : PT_SHADOW_WAVES) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + threadIdx.x] = 0u;  // next k_wf_trace's
@@ -391,17 +425,20 @@ __global__ __launch_bounds__(kTB) void k_wf_shadow(DevScene S, WfQueues Q, int q
         if (lane == 0) k0 = atomicAdd(cursor, 64u);
         k0 = __shfl(k0, 0, 64);
         if (k0 >= n) break;
-        if (k0 + lane >= n) continue;
         const uint32_t i = base + k0 + lane;
-        const float4 b = nt_load(&Q.n_n[i]);
-        const uint32_t li = __float_as_uint(b.w);
-        if (li == kDead) continue;
-        const float4 a = nt_load(&Q.n_o[i]);
-        const DevLight L = S.lights[li];
-        if (light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) {
-            const float4 wt = nt_load(&Q.n_w[i]);
-            acc_add(Q.acc, __float_as_uint(a.w), wt.x, wt.y, wt.z);
+        bool lit = false;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), wt = a;
+        if (k0 + lane < n) {
+            const float4 b = nt_load(&Q.n_n[i]);
+            const uint32_t li = __float_as_uint(b.w);
+            if (li != kDead) {
+                a = nt_load(&Q.n_o[i]);
+                const DevLight L = S.lights[li];
+                lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+                if (lit) wt = nt_load(&Q.n_w[i]);
+            }
         }
+        acc_add_wave(Q.acc, __float_as_uint(a.w), lit, wt.x, wt.y, wt.z);
     }
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
