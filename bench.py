@@ -141,8 +141,9 @@ def main():
         return
 
     value = total_rays / elapsed / 1e6
-    names = ["k_wf_camera", "k_wf_trace<false>", "k_wf_shade<false>", "k_wf_shadow<false>", "k_wf_finalize",
-             "k_render_pass<false>"]
+    # kernel names as rocprofv3 reports them (template arguments <COUNT, FULL>)
+    names = ["k_wf_camera", "k_wf_trace<false, false>", "k_wf_shade<false, false>", "k_wf_shadow<false, false>",
+             "k_wf_finalize", "k_render_pass<false, false>"]
     dom = int(np.argmax(kms))
     # algorithmic bytes of the dominant kernel over the timed region: the counted pass' bytes per
     # ray of that kernel's ray class × the rays it traced (same scene/seed/spp → same ray mix)

@@ -20,7 +20,7 @@ kernel = bench["roofline"]["kernel"]
 
 def per_launch(path, counter):
     v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-         if r["Kernel_Name"].startswith("void pt::" + kernel.replace("<false>", "<false>")) and r["Counter_Name"] == counter]
+         if r["Kernel_Name"].startswith("void pt::" + kernel) and r["Counter_Name"] == counter]
     return sum(v), len(v)
 
 fetch, nf = per_launch(f"{src}/fetch/fetch_counter_collection.csv", "FETCH_SIZE")
