@@ -240,6 +240,37 @@ int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_no
     return PT_OK;
 }
 
+// Triangle leaf chunks: every leaf ref of the collapsed triangle BVH4 is re-pointed at a
+// 128-B chunk holding its (<= 3) triangles' {v1, e1, e2} (27 floats, the tri_recs fields)
+// and, in word 27, the first triangle's record position.  A traversal step then loads the
+// same seven 16-B pieces whether the lane is at an inner node or at a leaf (pt_device.h
+// traverse_tri).  Chunks are allocated in node order, so sibling leaves sit together.
+int make_leaf_chunks(std::vector<float4>& nodes, const std::vector<float4>& recs, std::vector<float4>& chunks) {
+    chunks.clear();
+    const size_t nn = nodes.size() / 8;
+    for (size_t n = 0; n < nn; n++) {
+        uint32_t* refs = reinterpret_cast<uint32_t*>(&nodes[8 * n + 6]);
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r = refs[k];
+            if (r == pt::kEmpty4 || !(r & 0x80000000u)) continue;
+            const uint32_t first = r & 0x1FFFFFFFu, cnt = ((r >> 29) & 3u) + 1u;
+            if (cnt > 3) return fail(PT_ERR_UNSUPPORTED, "triangle leaf larger than a chunk");
+            const size_t ci = chunks.size() / 8;
+            if (ci > 0x1FFFFFFFu) return fail(PT_ERR_UNSUPPORTED, "too many triangle leaves");
+            float w[32] = {0.f};
+            for (uint32_t t = 0; t < cnt; t++) {
+                const float* rf = reinterpret_cast<const float*>(&recs[3 * (size_t)(first + t)]);
+                for (int j = 0; j < 9; j++) w[9 * t + j] = rf[j];
+            }
+            std::memcpy(&w[27], &first, 4);
+            const float4* w4 = reinterpret_cast<const float4*>(w);
+            chunks.insert(chunks.end(), w4, w4 + 8);
+            refs[k] = 0x80000000u | ((cnt - 1u) << 29) | (uint32_t)ci;
+        }
+    }
+    return PT_OK;
+}
+
 // Box of a light shape as Box.Center / Box.OuterRadius compute it (Box.cs:316-324).
 void light_sphere_of_box(pt::v3 mn, pt::v3 mx, pt::DevLight& L) {
     pt::v3 center = pt::add(mn, pt::mul(pt::sub(mx, mn), pt::mk(0.5, 0.5, 0.5)));
@@ -748,7 +779,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         pad_box(&bmin[3 * i], &bmax[3 * i]);
     }
     pt::BvhResult tb;
-    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb);
+    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb, 3);   // leaves fit one chunk
     std::vector<float4> tri_recs(nt * 3), tri_shade(nt * 3);
     const bool want_uv = d->num_textures > 0 && nt > 0;   // texture coordinates only matter with textures
     std::vector<float4> tri_uv(want_uv ? nt * 2 : 0);
@@ -775,6 +806,8 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     std::vector<float4> tri_nodes;
     int32_t tri_num_nodes = 0;
     if ((rc = pack_nodes(tb, tri_nodes, tri_num_nodes))) return rc;
+    std::vector<float4> tri_chunks;
+    if ((rc = make_leaf_chunks(tri_nodes, tri_recs, tri_chunks))) return rc;
 
     // --- analytic BVH (spheres, cubes, SDF shapes, volumes, transformed shapes)
     const size_t na = ana_kind.size();
@@ -862,6 +895,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     pt::DevScene S{};
     rc = upload(c, tri_nodes, &S.tri_nodes); if (rc) return rc;
     rc = upload(c, tri_recs, &S.tri_recs); if (rc) return rc;
+    rc = upload(c, tri_chunks, &S.tri_chunks); if (rc) return rc;
     rc = upload(c, tri_shade, &S.tri_shade); if (rc) return rc;
     rc = upload(c, ana_nodes, &S.ana_nodes); if (rc) return rc;
     rc = upload(c, ana_recs, &S.ana_recs); if (rc) return rc;
@@ -906,7 +940,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     c->S = S;
     c->has_scene = true;
     c->stats.bvh_nodes = (uint64_t)tri_num_nodes + (uint64_t)ana_num_nodes;
-    c->stats.bvh_bytes = (tri_nodes.size() + ana_nodes.size()) * sizeof(float4) +
+    c->stats.bvh_bytes = (tri_nodes.size() + tri_chunks.size() + ana_nodes.size()) * sizeof(float4) +
                          (tri_recs.size() + tri_shade.size() + ana_recs.size()) * sizeof(float4);
     c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return PT_OK;

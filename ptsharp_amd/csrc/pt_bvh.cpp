@@ -39,9 +39,10 @@ struct Builder {
     std::atomic<int> leaves{0};
     std::atomic<int> live_threads{1};
     int max_threads;
+    int max_leaf;
 
-    Builder(const float* a, const float* b, int64_t n, std::vector<BvhNode>& out, int threads)
-        : pmin(a), pmax(b), cent((size_t)n * 3), idx((size_t)n), nodes(out), max_threads(threads) {
+    Builder(const float* a, const float* b, int64_t n, std::vector<BvhNode>& out, int threads, int leaf)
+        : pmin(a), pmax(b), cent((size_t)n * 3), idx((size_t)n), nodes(out), max_threads(threads), max_leaf(leaf) {
         for (int64_t i = 0; i < n; i++) {
             idx[(size_t)i] = (uint32_t)i;
             for (int k = 0; k < 3; k++) cent[(size_t)i * 3 + k] = 0.5f * (pmin[i * 3 + k] + pmax[i * 3 + k]);
@@ -85,7 +86,7 @@ struct Builder {
         bool force_median = (kMaxDepth - depth - 1) < 62 && n > ((int64_t)1 << (kMaxDepth - depth - 1));
         if (ext[axis] <= 0.f) {
             // all centroids coincide: split by count (or leaf if small)
-            if (n <= kMaxLeafSize) { make_leaf(ni, begin, end, depth); return; }
+            if (n <= max_leaf) { make_leaf(ni, begin, end, depth); return; }
             mid = begin + n / 2;
         } else if (force_median) {
             mid = begin + n / 2;
@@ -120,8 +121,8 @@ struct Builder {
             }
             float leaf_cost = bounds.area() * (float)n;
             // traversal step ~ 1 box pair, intersection ~ 1: split cost = 1*area + sum(area*count)
-            if (best_axis < 0 || (n <= kMaxLeafSize && best_cost + bounds.area() >= leaf_cost)) {
-                if (n <= kMaxLeafSize) { make_leaf(ni, begin, end, depth); return; }
+            if (best_axis < 0 || (n <= max_leaf && best_cost + bounds.area() >= leaf_cost)) {
+                if (n <= max_leaf) { make_leaf(ni, begin, end, depth); return; }
                 mid = begin + n / 2;
                 std::nth_element(idx.begin() + begin, idx.begin() + mid, idx.begin() + end, [&](uint32_t a, uint32_t b) {
                     return cent[(size_t)a * 3 + axis] < cent[(size_t)b * 3 + axis];
@@ -156,7 +157,7 @@ struct Builder {
 
 }  // namespace
 
-void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out) {
+void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out, int max_leaf) {
     out.nodes.clear();
     out.order.clear();
     out.max_depth = 0;
@@ -164,7 +165,7 @@ void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int thre
     if (n <= 0) return;
     if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
     out.nodes.assign((size_t)(2 * n + 2), BvhNode{});
-    Builder b(prim_min, prim_max, n, out.nodes, threads);
+    Builder b(prim_min, prim_max, n, out.nodes, threads, std::min(std::max(max_leaf, 1), kMaxLeafSize));
     b.build(0, 0, n, 0);
     out.nodes.resize(b.next_pair.load());
     // padding node 1: an empty leaf

@@ -33,8 +33,10 @@ struct BvhResult {
     int leaves = 0;
 };
 
-// prim_min/prim_max: [n][3] AABBs.  Builds with up to `threads` host threads.
-void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out);
+// prim_min/prim_max: [n][3] AABBs.  Builds with up to `threads` host threads; leaves hold
+// at most max_leaf (1..kMaxLeafSize) primitives.
+void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out,
+               int max_leaf = kMaxLeafSize);
 
 // 4-wide BVH collapsed from the BVH2: one 128-byte node (one cache line) per
 // step of the traversal instead of a 64-byte child pair, so a ray makes about

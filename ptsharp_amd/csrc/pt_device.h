@@ -217,6 +217,75 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
     return false;
 }
 
+// Pin loaded values so the compiler keeps each aligned 16-B load whole (left alone it
+// re-splits them along the consumers' 12-B vertex fields into unaligned pieces).
+#define PT_PIN4(q) asm volatile("" : "+v"((q).x), "+v"((q).y), "+v"((q).z), "+v"((q).w))
+
+// Triangle-BVH traversal over leaf chunks (pt_api.hip make_leaf_chunks).  The node step
+// is traverse()'s; a leaf ref points at a 128-B chunk of up to three triangles, so an
+// inner step and a leaf step issue the same seven aligned 16-B loads and a wave whose
+// lanes are split between nodes and leaves pays for one set of load instructions, not
+// for the node loads plus a per-triangle load loop.
+template <bool COUNT, bool ANY, class STK>
+__device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 invd, HitRec& best, const STK& stack,
+                                             Counters& ctr) {
+    if (S.tri_num_nodes <= 0) return false;
+    uint32_t ref = 0;  // root: always an inner node
+    int sp = 0;
+    float tmax = tmax_bound(best.t);
+    for (;;) {
+        const bool leaf = (ref & 0x80000000u) != 0;
+        const float4* c = (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu);
+        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6];
+        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
+        if (!leaf) {
+            if (COUNT) ctr.nodes++;
+            const float inf = __int_as_float(0x7f800000);
+            float k0 = slab1(q0.x, q1.x, q2.x, q3.x, q4.x, q5.x, o, invd, tmax);
+            float k1 = slab1(q0.y, q1.y, q2.y, q3.y, q4.y, q5.y, o, invd, tmax);
+            float k2 = slab1(q0.z, q1.z, q2.z, q3.z, q4.z, q5.z, o, invd, tmax);
+            float k3 = slab1(q0.w, q1.w, q2.w, q3.w, q4.w, q5.w, o, invd, tmax);
+            uint32_t v0 = __float_as_uint(q6.x), v1 = __float_as_uint(q6.y), v2 = __float_as_uint(q6.z),
+                     v3r = __float_as_uint(q6.w);
+            if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
+            if (v2 == kEmpty4) k2 = inf;
+            if (v3r == kEmpty4) k3 = inf;
+            cswap(k0, v0, k1, v1);
+            cswap(k2, v2, k3, v3r);
+            cswap(k0, v0, k2, v2);
+            cswap(k1, v1, k3, v3r);
+            cswap(k1, v1, k2, v2);
+            if (k0 != inf) {
+                push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
+                ref = v0;
+                continue;
+            }
+        } else {
+            const uint32_t cnt = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q6.w);
+            // triangle k = floats 9k..9k+8 of the chunk: {v1, e1, e2}; shifted down after each test
+            v3 a0{q0.x, q0.y, q0.z}, a1{q0.w, q1.x, q1.y}, a2{q1.z, q1.w, q2.x};
+            v3 b0{q2.y, q2.z, q2.w}, b1{q3.x, q3.y, q3.z}, b2{q3.w, q4.x, q4.y};
+            const v3 c0{q4.z, q4.w, q5.x}, c1{q5.y, q5.z, q5.w}, c2{q6.x, q6.y, q6.z};
+#pragma unroll 1
+            for (uint32_t k = 0; k < cnt; k++) {
+                if (COUNT) ctr.prims++;
+                const double t = isect_tri(a0, a1, a2, o, d);
+                if (t < best.t) {
+                    if (ANY) return true;
+                    best.t = t; best.kind = KIND_TRI; best.idx = (int32_t)(first + k);
+                    tmax = tmax_bound(t);
+                }
+                a0 = b0; a1 = b1; a2 = b2;
+                b0 = c0; b1 = c1; b2 = c2;
+            }
+        }
+        if (sp == 0) break;
+        sp--;
+        ref = stack.get(sp);
+    }
+    return false;
+}
+
 // Mesh.Intersect of an instanced mesh: its own object-space BVH4 (Mesh.cs:83-86, 122-125);
 // idx is the triangle's position in the mesh's BLAS records.
 __device__ __noinline__ HitRec blas_hit(const DevScene& S, int b, v3 o, v3 d) {
@@ -253,7 +322,7 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
     traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
-    traverse<true, COUNT, false, FULL>(S, S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr);
+    traverse_tri<COUNT, false>(S, o, d, invd, best, stack, ctr);
     return best;
 }
 
@@ -280,7 +349,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         // traces the ray, so trace it (the answer is "not visible" either way)
         HitRec h{kHitInf, -1, -1};
         v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-        traverse<true, COUNT, true, FULL>(S, S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, h, stack, ctr);
+        traverse_tri<COUNT, true>(S, o, d, invd, h, stack, ctr);
         return false;
     }
     double tl = light_t<FULL>(S, L, o, d);
@@ -293,8 +362,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
     if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr))
         return false;
-    if (traverse<true, COUNT, true, FULL>(S, S.tri_nodes, S.tri_num_nodes, S.tri_recs, o, d, invd, best, stack, ctr))
-        return false;
+    if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return false;
     return true;
 }
 

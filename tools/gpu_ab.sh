@@ -8,7 +8,7 @@ first=1
 for V in "${VS[@]}"; do
   NAME=${V%%:*}; FLAGS=${V#*:}
   make -s -C ptsharp_amd/csrc clean >/dev/null && make -s -j16 -C ptsharp_amd/csrc EXTRA="$FLAGS" > gpurun_out/ab/build_$NAME.log 2>&1 || exit 1
-  if [ $first = 1 ]; then
+  if [ $first = 1 ] || [ -n "$TESTS_ALL" ]; then
     timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q -m gpu > gpurun_out/ab/tests_$NAME.log 2>&1 || exit 1
     first=0
   fi
