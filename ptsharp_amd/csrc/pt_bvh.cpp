@@ -25,7 +25,7 @@ struct Aabb {
     }
 };
 
-constexpr int kBins = 16;
+constexpr int kBins = 32;
 constexpr int64_t kParallelCutoff = 16384;
 
 struct Builder {
