@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -114,6 +115,7 @@ struct Ctx {
     pt::WfQueues Q{};
     std::vector<DeviceArray> wf_arrays;
     uint32_t wf_cap = 0, wf_scap = 0;
+    uint32_t wf_max_cap = 0;       // queue capacity bound (wf_max_cap()), once per context
     // adaptive / firefly phases (allocated on first use, with the queues)
     uint32_t* d_plist = nullptr;   // [P] firefly candidates
     uint32_t* d_fcount = nullptr;
@@ -123,7 +125,33 @@ struct Ctx {
     EventTimer timer;
 };
 
-constexpr uint32_t kWfMaxCap = 1u << 25;   // 32M rays per queue: ~6 GB of queues at most (of 288 GB HBM)
+// Queue capacity bound (entries per queue).  A pass is rendered in chunks of camera
+// samples whose widest depth fits the queues; every chunk pays the fill and drain of
+// 16 persistent launches, so fewer, larger chunks are faster (C4, 16 spp per pass: 8
+// chunks of 32M-entry queues 2574 Mrays/s, 2 chunks 2809, one chunk 2853).  The bound is
+// the largest power of two whose queues (176 B per entry: two extension queues of
+// o, d, throughput, key + hits + one shadow queue) fit a quarter of the device's memory,
+// clamped to [2^20, 2^28] entries (2^28: 47 GB of the MI355X's 288 GB).
+constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
+constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 8) + 16 + 48;
+
+// PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
+uint32_t wf_max_cap(Ctx* c) {
+    if (c->wf_max_cap) return c->wf_max_cap;
+    if (const char* env = std::getenv("PT_WF_MAX_CAP")) {
+        const unsigned long long v = std::strtoull(env, nullptr, 10);
+        uint32_t cap = kWfMaxCapLimit;
+        while (cap > (uint32_t)pt::kParts * 1024u && cap > v) cap >>= 1;
+        return c->wf_max_cap = cap;
+    }
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) total_b = (size_t)kWfMinCapLimit * kWfBytesPerEntry * 4;
+    const size_t budget = total_b / 4;
+    uint32_t cap = kWfMaxCapLimit;
+    while (cap > kWfMinCapLimit && (size_t)cap * kWfBytesPerEntry > budget) cap >>= 1;
+    c->wf_max_cap = cap;
+    return cap;
+}
 
 void free_wavefront(Ctx* c) {
     for (auto& a : c->wf_arrays) a.release();
@@ -1004,7 +1032,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     // Queues are kParts partitions.  Camera samples are dealt to the XCD groups in
     // 256-sample blocks, so a group gets at most ceil(ceil(chunk/256)/kParts)·256 of
     // them, and everything it appends stays in its own partition.
-    const double pmax = (double)(kWfMaxCap / pt::kParts);
+    const double pmax = (double)(wf_max_cap(c) / pt::kParts);
     auto group_max = [](uint64_t ch) { return (double)(((ch + 255) / 256 + pt::kParts - 1) / pt::kParts * 256); };
     uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples,
                                                 std::floor(pmax / per_sample_nee / 256.0) * 256.0 * pt::kParts);

@@ -113,8 +113,10 @@ def test_engines_agree(gpu, name):
     assert np.allclose(a.M, b.M, rtol=2e-5, atol=1e-6)
 
 
-def test_wavefront_many_chunks(gpu):
-    """A 1080p-wide frame at spp 8 with FH 16 needs several queue chunks; results match the megakernel."""
+def test_wavefront_many_chunks(gpu, monkeypatch):
+    """With the queues held to 4M entries (PT_WF_MAX_CAP) a 640x360 frame at spp 8 with FH 16
+    takes ~15 queue chunks; results match the megakernel."""
+    monkeypatch.setenv("PT_WF_MAX_CAP", str(1 << 22))
     s, c, smp = scenes.gopher3()
     smp.MaxBounces = 2
     a, ra = render_gpu(s, c, smp, 640, 360, spp=8, seed=31, engine=_abi.ENGINE_MEGAKERNEL)
