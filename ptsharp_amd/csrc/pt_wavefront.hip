@@ -30,6 +30,11 @@
 namespace pt {
 
 constexpr int kTB = 256;   // threads per block, traversal kernels (LDS stack column stride)
+// Rays a traversal wave claims per fetch atomic, in 64-ray batches.  A wave waits for its
+// claim's return before tracing, and the 8 partition cursors are contended: claiming one
+// batch at a time cost C4 trace 106 ms and shadow 47 ms per pass, four batches 82 and 42
+// (eight: the same; sixteen: a longer tail).
+constexpr uint32_t kFetchBatches = 4;
 using WStack = SpillStack<kTB, kLdsStack>;
 
 // Queue traffic.  Loads are non-temporal (read once per depth; they should not displace
@@ -247,22 +252,24 @@ __global__ __launch_bounds__(kTB, FULL ? 2 : PT_TRACE_WAVES) void k_wf_trace(Dev
     uint32_t* cursor = Q.counts + kFetchWord + G.g;
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
-    // Persistent grid (resident capacity); each wave takes 64 rays of its partition
-    // at a time, so no wave waits for a second dispatch round and the tail is one
-    // traversal long.
+    // Persistent grid (resident capacity); each wave claims kFetchBatches × 64 rays of
+    // its partition with one atomic and traces them 64 at a time, so no wave waits for a
+    // second dispatch round and the tail is a few traversals long.
     for (;;) {
-        uint32_t k0 = 0;
-        if (lane == 0) k0 = atomicAdd(cursor, 64u);
-        k0 = __shfl(k0, 0, 64);
-        if (k0 >= n) break;
-        if (k0 + lane >= n) continue;
-        const uint32_t i = base + k0 + lane;
-        float4 b = nt_load(&Q.q_d[qi][i]);
-        if (__float_as_uint(b.w) == kDead) continue;   // a camera slot outside the image
-        float4 a = nt_load(&Q.q_o[qi][i]);
-        HitRec h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
-        unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
-        q_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
+        uint32_t kc = 0;
+        if (lane == 0) kc = atomicAdd(cursor, 64u * kFetchBatches);
+        kc = __shfl(kc, 0, 64);
+        if (kc >= n) break;
+        for (uint32_t k0 = kc; k0 < kc + 64u * kFetchBatches && k0 < n; k0 += 64u) {
+            if (k0 + lane >= n) continue;
+            const uint32_t i = base + k0 + lane;
+            float4 b = nt_load(&Q.q_d[qi][i]);
+            if (__float_as_uint(b.w) == kDead) continue;   // a camera slot outside the image
+            float4 a = nt_load(&Q.q_o[qi][i]);
+            HitRec h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+            unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
+            q_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
+        }
     }
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
@@ -448,25 +455,27 @@ __global__ __launch_bounds__(kTB, FULL ? 1 : PT_SHADOW_WAVES) void k_wf_shadow(D
     uint32_t* cursor = Q.counts + kFetchWord + 2 * kParts + G.g;
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
-    for (;;) {  // 64 rays per wave at a time (see k_wf_trace)
-        uint32_t k0 = 0;
-        if (lane == 0) k0 = atomicAdd(cursor, 64u);
-        k0 = __shfl(k0, 0, 64);
-        if (k0 >= n) break;
-        const uint32_t i = base + k0 + lane;
-        bool lit = false;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), wt = a;
-        if (k0 + lane < n) {
-            const float4 b = nt_load(&Q.n_n[i]);
-            const uint32_t li = __float_as_uint(b.w);
-            if (li != kDead) {
-                a = nt_load(&Q.n_o[i]);
-                const DevLight L = S.lights[li];
-                lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
-                if (lit) wt = nt_load(&Q.n_w[i]);
+    for (;;) {  // kFetchBatches × 64 rays per claim, 64 at a time (see k_wf_trace)
+        uint32_t kc = 0;
+        if (lane == 0) kc = atomicAdd(cursor, 64u * kFetchBatches);
+        kc = __shfl(kc, 0, 64);
+        if (kc >= n) break;
+        for (uint32_t k0 = kc; k0 < kc + 64u * kFetchBatches && k0 < n; k0 += 64u) {
+            const uint32_t i = base + k0 + lane;
+            bool lit = false;
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f), wt = a;
+            if (k0 + lane < n) {
+                const float4 b = nt_load(&Q.n_n[i]);
+                const uint32_t li = __float_as_uint(b.w);
+                if (li != kDead) {
+                    a = nt_load(&Q.n_o[i]);
+                    const DevLight L = S.lights[li];
+                    lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+                    if (lit) wt = nt_load(&Q.n_w[i]);
+                }
             }
+            acc_add_wave(Q.acc, __float_as_uint(a.w), lit, wt.x, wt.y, wt.z);
         }
-        acc_add_wave(Q.acc, __float_as_uint(a.w), lit, wt.x, wt.y, wt.z);
     }
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
