@@ -922,15 +922,28 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
 
     pt::DevScene S{};
     rc = upload(c, tri_nodes, &S.tri_nodes); if (rc) return rc;
-    rc = upload(c, tri_recs, &S.tri_recs); if (rc) return rc;
+    // one 128-B shading record per triangle (pt_scene.h tri_rstride): what k_wf_shade reads
+    // for a triangle hit is one line instead of two or three
+    std::vector<float4> tri_sh(nt * 8, f4(0.f, 0.f, 0.f, 0.f));
+    for (size_t i = 0; i < nt; i++) {
+        for (int k = 0; k < 3; k++) tri_sh[8 * i + k] = tri_recs[3 * i + k];
+        for (int k = 0; k < 3; k++) tri_sh[8 * i + 3 + k] = tri_shade[3 * i + k];
+        if (want_uv)
+            for (int k = 0; k < 2; k++) tri_sh[8 * i + 6 + k] = tri_uv[2 * i + k];
+    }
+    const float4* d_tri_sh = nullptr;
+    rc = upload(c, tri_sh, &d_tri_sh); if (rc) return rc;
+    S.tri_recs = d_tri_sh;
+    S.tri_shade = d_tri_sh ? d_tri_sh + 3 : nullptr;
+    S.tri_uv = d_tri_sh && want_uv ? d_tri_sh + 6 : nullptr;
+    S.tri_rstride = 8;
+    S.tri_ustride = 8;
     rc = upload(c, tri_chunks, &S.tri_chunks); if (rc) return rc;
-    rc = upload(c, tri_shade, &S.tri_shade); if (rc) return rc;
     rc = upload(c, ana_nodes, &S.ana_nodes); if (rc) return rc;
     rc = upload(c, ana_recs, &S.ana_recs); if (rc) return rc;
     rc = upload(c, planes, &S.planes); if (rc) return rc;
     rc = upload(c, mats, &S.mats); if (rc) return rc;
     rc = upload(c, lights, &S.lights); if (rc) return rc;
-    rc = upload(c, tri_uv, &S.tri_uv); if (rc) return rc;
     const double* d_tex = nullptr;
     rc = upload(c, tex_data, &d_tex); if (rc) return rc;
     std::vector<pt::DevTexture> texs((size_t)std::max(d->num_textures, 0));
@@ -969,7 +982,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     c->has_scene = true;
     c->stats.bvh_nodes = (uint64_t)tri_num_nodes + (uint64_t)ana_num_nodes;
     c->stats.bvh_bytes = (tri_nodes.size() + tri_chunks.size() + ana_nodes.size()) * sizeof(float4) +
-                         (tri_recs.size() + tri_shade.size() + ana_recs.size()) * sizeof(float4);
+                         (tri_sh.size() + ana_recs.size()) * sizeof(float4);
     c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return PT_OK;
 }

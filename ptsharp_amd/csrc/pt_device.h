@@ -423,7 +423,8 @@ __device__ inline v3 tex_bump_sample(const DevTexture& T, double u, double v) {
 __device__ __forceinline__ bool nonzero3(v3 a) { return !(a.x == 0 && a.y == 0 && a.z == 0); }
 
 __device__ __forceinline__ void tri_uvs(const DevScene& S, int idx, v3& t1, v3& t2, v3& t3) {
-    const float4 A = S.tri_uv[2 * (size_t)idx], B = S.tri_uv[2 * (size_t)idx + 1];
+    const float4* u = S.tri_uv + (size_t)S.tri_ustride * idx;
+    const float4 A = u[0], B = u[1];
     t1 = v3{A.x, A.y, 0.f}; t2 = v3{A.z, A.w, 0.f}; t3 = v3{B.x, B.y, 0.f};
 }
 
@@ -432,7 +433,7 @@ __device__ __forceinline__ void tri_uvs(const DevScene& S, int idx, v3& t1, v3& 
 // (default: the analytic records).
 __device__ inline v3 shape_uv(const DevScene& S, int kind, int idx, v3 p, const float4* recs = nullptr) {
     if (kind == KIND_TRI) {
-        const float4* r = S.tri_recs + 3 * (size_t)idx;
+        const float4* r = S.tri_recs + (size_t)S.tri_rstride * idx;
         const float4 a = r[0], b = r[1], c = r[2];
         double u, v, w;
         barycentric(v3{a.x, a.y, a.z}, v3{a.w, b.x, b.y}, v3{b.z, b.w, c.x}, p, u, v, w);
@@ -536,8 +537,8 @@ struct Shade {
 
 // Triangle.NormalAt (maps included) and its material id, for triangle record idx of S.tri_recs / tri_shade.
 __device__ inline v3 tri_normal_at(const DevScene& S, int idx, v3 p, int32_t& mat) {
-    const float4* r = S.tri_recs + 3 * (size_t)idx;
-    const float4* q = S.tri_shade + 3 * (size_t)idx;
+    const float4* r = S.tri_recs + (size_t)S.tri_rstride * idx;
+    const float4* q = S.tri_shade + (size_t)S.tri_rstride * idx;
     const float4 a = r[0], b = r[1], c = r[2];
     const float4 x = q[0], y = q[1], z = q[2];
     mat = (int32_t)f2u(z.y);
@@ -581,6 +582,8 @@ __device__ __noinline__ void ext_hit_info(const DevScene& S, const HitRec& h, v3
             T.tri_recs = S.blas_recs + 3 * (size_t)off;
             T.tri_shade = S.blas_shade + 3 * (size_t)off;
             T.tri_uv = S.blas_uv ? S.blas_uv + 2 * (size_t)off : nullptr;
+            T.tri_rstride = 3;
+            T.tri_ustride = 2;
             sp = add(so, muls(sd, ih.t));
             sn = tri_normal_at(T, ih.idx, sp, s.mat);
             surface_at<true>(T, S.mats[s.mat], KIND_TRI, ih.idx, sp, s.col, s.gloss);
@@ -616,8 +619,8 @@ __device__ __forceinline__ Shade hit_info(const DevScene& S, const HitRec& h, v3
     v3 n;
     if (h.kind == KIND_TRI) {
         if (COUNT) ctr.shades++;
-        const float4* r = S.tri_recs + 3 * (size_t)h.idx;
-        const float4* q = S.tri_shade + 3 * (size_t)h.idx;
+        const float4* r = S.tri_recs + (size_t)S.tri_rstride * h.idx;
+        const float4* q = S.tri_shade + (size_t)S.tri_rstride * h.idx;
         float4 a = r[0], b = r[1], c = r[2];
         float4 x = q[0], y = q[1], z = q[2];
         s.mat = (int32_t)f2u(z.y);

@@ -70,6 +70,10 @@ struct DevScene {
     // textures (§8f row 3)
     const DevTexture* texs;
     const float4* tri_uv;      // 2 float4 per triangle: {t1.xy, t2.xy} {t3.xy, -, -}; null without textured triangles
+    // float4 stride between consecutive triangles of tri_recs / tri_shade / tri_uv: the
+    // world mesh interleaves the three into one 128-B shading record per triangle (8:
+    // recs at +0, shade at +3, uv at +6), a BLAS keeps separate arrays (3, 3, 2)
+    int32_t tri_rstride, tri_ustride;
     int32_t env_tex;           // Scene.Texture (-1 = null)
     double env_angle;          // Scene.TextureAngle
     // SDF shapes, volumes, transformed shapes (§8f row 4; pt_ext.h)
