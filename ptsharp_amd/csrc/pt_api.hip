@@ -65,18 +65,18 @@ struct EventTimer : pt::LaunchTimer {
     hipStream_t stream = nullptr;
     bool failed = false;
     void reset(hipStream_t s) { stream = s; used = 0; cls.clear(); failed = false; }
-    void record(int c, bool is_begin) {
+    void record(int c, bool is_begin, hipStream_t s) {
         if (used == pool.size()) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) { failed = true; return; }
             pool.push_back(e);
         }
-        if (hipEventRecord(pool[used], stream) != hipSuccess) failed = true;
+        if (hipEventRecord(pool[used], s ? s : stream) != hipSuccess) failed = true;
         if (is_begin) cls.push_back(c);
         used++;
     }
-    void begin(int c) override { record(c, true); }
-    void end(int c) override { record(c, false); }
+    void begin(int c, hipStream_t s) override { record(c, true, s); }
+    void end(int c, hipStream_t s) override { record(c, false, s); }
     hipError_t collect(double* ms, uint32_t* launches) {
         for (size_t i = 0; i + 1 < used; i += 2) {
             float t = 0.f;
@@ -94,6 +94,8 @@ struct Ctx {
     int device = 0;
     int width = 0, height = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;                          // shadow passes (pt::WfPlan::side)
+    hipEvent_t ev_main = nullptr, ev_side = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // Welford buffer
     double* d_m = nullptr;
@@ -133,6 +135,10 @@ struct Ctx {
 // o, d, throughput, key + hits + one shadow queue) fit a quarter of the device's memory,
 // clamped to [2^20, 2^28] entries (2^28: 47 GB of the MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
+#ifndef PT_SIDE_MAX_CHUNK
+#define PT_SIDE_MAX_CHUNK (20u << 20)
+#endif
+constexpr uint64_t kSideStreamMaxChunk = PT_SIDE_MAX_CHUNK;   // camera samples
 constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 8) + 16 + 48;
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
@@ -546,6 +552,10 @@ int pt_create(const pt_device_opts* opts, void** out_ctx) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(PT_ERR_HIP, "stream"));
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
         return cleanup(fail(PT_ERR_HIP, "events"));
+    if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming) != hipSuccess)
+        return cleanup(fail(PT_ERR_HIP, "side stream"));
     size_t P = (size_t)c->width * (size_t)c->height;
     if (hipMalloc(&c->d_m, P * 3 * sizeof(double)) != hipSuccess || hipMalloc(&c->d_v, P * 3 * sizeof(double)) != hipSuccess ||
         hipMalloc(&c->d_n, P * sizeof(int32_t)) != hipSuccess ||
@@ -1061,6 +1071,15 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     if (engine != PT_ENGINE_WAVEFRONT && engine != PT_ENGINE_MEGAKERNEL) return fail(PT_ERR_INVALID_ARG, "bad engine");
     if (engine == PT_ENGINE_WAVEFRONT) {
         plan.chunk = chunk;
+        // Shadow passes on the side stream, beside the next depth's closest-hit pass, when a
+        // chunk is small enough for the launches' fill and drain to matter (one rank's
+        // share of a multi-GPU frame: +6.5 % at 1/8 of C4); a full C4 frame runs 0.3 %
+        // slower that way, so it keeps one stream.
+        if (chunk <= kSideStreamMaxChunk) {
+            plan.side = c->side;
+            plan.ev_main = c->ev_main;
+            plan.ev_side = c->ev_side;
+        }
         const double group_samples = group_max(chunk);
         const double need = group_samples * per_sample;   // a partition's widest depth
         const uint32_t pcap = (uint32_t)std::min(pmax, std::max(8192.0, std::max(group_samples, need)));
@@ -1101,9 +1120,9 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
                                        pass->firefly_samples, nsel, c->d_plist, c->d_snap));
         }
     } else {
-        if (timing) c->timer.begin(PT_K_MEGAKERNEL);
+        if (timing) c->timer.begin(PT_K_MEGAKERNEL, c->stream);
         PT_HIP(pt::launch_render_pass(c->S, cam, smp, P, B, num_tiles, counted != nullptr, c->stream));
-        if (timing) c->timer.end(PT_K_MEGAKERNEL);
+        if (timing) c->timer.end(PT_K_MEGAKERNEL, c->stream);
     }
     PT_HIP(hipEventRecord(c->ev1, c->stream));
     if (c->timer.failed) return fail(PT_ERR_HIP, "hipEventRecord (kernel timing) failed");
@@ -1190,6 +1209,9 @@ void pt_destroy(void* ctx) {
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_tiles) (void)hipFree(c->d_tiles);
     c->timer.destroy();
+    if (c->ev_main) (void)hipEventDestroy(c->ev_main);
+    if (c->ev_side) (void)hipEventDestroy(c->ev_side);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);

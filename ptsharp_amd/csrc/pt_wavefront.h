@@ -53,12 +53,18 @@ struct WfPlan {
     uint32_t trace_blocks;     // persistent grids: resident capacity of each kernel
     uint32_t shade_blocks;
     uint32_t shadow_blocks;
+    // Optional second stream: each depth's shadow pass runs there, beside the next depth's
+    // closest-hit pass (independent queues), so one fills the other's ramp and tail.
+    // ev_main / ev_side order shade(d) → shadow(d) → shade(d + 1).  Null: one stream.
+    hipStream_t side;
+    hipEvent_t ev_main, ev_side;
 };
 
-// Optional per-launch timing hook (hipEvent pairs recorded around each kernel; pt_api.hip).
+// Optional per-launch timing hook (hipEvent pairs recorded around each kernel on the
+// stream it runs on; pt_api.hip).
 struct LaunchTimer {
-    virtual void begin(int kernel_class) = 0;
-    virtual void end(int kernel_class) = 0;
+    virtual void begin(int kernel_class, hipStream_t s) = 0;
+    virtual void end(int kernel_class, hipStream_t s) = 0;
     virtual ~LaunchTimer() = default;
 };
 

@@ -297,7 +297,10 @@ __global__ __launch_bounds__(kTB, FULL ? 2 : PT_TRACE_WAVES) void k_wf_trace(Dev
 template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(256, FULL ? 2 : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
-    if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + 2 * kParts + threadIdx.x] = 0u;  // k_wf_shadow's
+    if (blockIdx.x == 0 && threadIdx.x < kParts) {
+        Q.counts[kFetchWord + 2 * kParts + threadIdx.x] = 0u;   // k_wf_shadow's fetch cursors
+        Q.counts[kFetchWord + threadIdx.x] = 0u;                // the next k_wf_trace's (it may run beside k_wf_shadow)
+    }
     const Group G = xcd_group();
     const uint32_t cnt = *ray_count(Q, qi, G.g);
     const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
@@ -448,7 +451,6 @@ template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(kTB, FULL ? 1 : PT_SHADOW_WAVES) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
-    if (blockIdx.x == 0 && threadIdx.x < kParts) Q.counts[kFetchWord + threadIdx.x] = 0u;  // next k_wf_trace's
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
@@ -590,36 +592,48 @@ static unsigned grid_for(uint64_t items, unsigned block, unsigned cap_blocks) {
 // Trace / shade / shadow for every depth of one chunk whose camera rays are queued.
 static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer& B, const WfQueues& Q,
                        const WfPlan& plan, bool count, hipStream_t stream, LaunchTimer* timer, uint64_t bound) {
-    auto begin_k = [&](int cls) { if (timer) timer->begin(cls); };
-    auto end_k = [&](int cls) { if (timer) timer->end(cls); };
-    int qi = 0;
-    for (int depth = 0; depth <= smp.mb; depth++) {
-        const unsigned tg = grid_for(bound, kTB, plan.trace_blocks);
-        begin_k(1);
-        const bool full = S.full != 0;
+    auto begin_k = [&](int cls, hipStream_t s) { if (timer) timer->begin(cls, s); };
+    auto end_k = [&](int cls, hipStream_t s) { if (timer) timer->end(cls, s); };
+    const bool full = S.full != 0;
+    const hipStream_t side = plan.side ? plan.side : stream;
+    auto trace = [&](int qi, uint64_t n) {
+        const unsigned tg = grid_for(n, kTB, plan.trace_blocks);
+        begin_k(1, stream);
         if (count && full) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (full) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-        end_k(1);
+        end_k(1, stream);
+    };
+    int qi = 0;
+    trace(qi, bound);
+    for (int depth = 0; depth <= smp.mb; depth++) {
+        if (plan.side && depth > 0) (void)hipStreamWaitEvent(stream, plan.ev_side, 0);   // shadow(d-1) read its queue
         const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
-        begin_k(2);
+        begin_k(2, stream);
         if (count && full) hipLaunchKernelGGL((k_wf_shade<true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_shade<true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         else if (full) hipLaunchKernelGGL((k_wf_shade<false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shade<false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
-        end_k(2);
+        end_k(2, stream);
+        if (plan.side) {
+            (void)hipEventRecord(plan.ev_main, stream);
+            (void)hipStreamWaitEvent(side, plan.ev_main, 0);
+        }
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
         const unsigned hg = grid_for(children * plan.lights_per_child, kTB, plan.shadow_blocks);
-        begin_k(3);
-        if (count && full) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
-        else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
-        else if (full) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
-        else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, stream, S, Q, 1 - qi, B.counters);
-        end_k(3);
+        begin_k(3, side);
+        if (count && full) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (full) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        end_k(3, side);
+        if (plan.side) (void)hipEventRecord(plan.ev_side, side);
         bound = children < Q.cap ? children : Q.cap;
         qi = 1 - qi;
+        if (depth < smp.mb) trace(qi, bound);
     }
+    if (plan.side) (void)hipStreamWaitEvent(stream, plan.ev_side, 0);   // the chunk ends with its last shadow pass
 }
 
 hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
@@ -630,8 +644,8 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     const int spp_launch = P.stratified ? 1 : P.spp;
     const double inv_spp = 1.0 / (double)spp_launch;
     const uint64_t total = pix_slots * (uint64_t)spp_launch;
-    auto begin_k = [&](int cls) { if (timer) timer->begin(cls); };
-    auto end_k = [&](int cls) { if (timer) timer->end(cls); };
+    auto begin_k = [&](int cls) { if (timer) timer->begin(cls, stream); };
+    auto end_k = [&](int cls) { if (timer) timer->end(cls, stream); };
     for (int r = 0; r < rounds; r++) {
         for (uint64_t begin = 0; begin < total; begin += plan.chunk) {
             const uint32_t cnt = (uint32_t)((total - begin) < plan.chunk ? (total - begin) : plan.chunk);
@@ -655,8 +669,8 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
                            LaunchTimer* timer, int firefly, int32_t K, uint64_t entries, const uint32_t* plist,
                            const double* snap) {
     if (K <= 0 || entries == 0) return hipSuccess;
-    auto begin_k = [&](int cls) { if (timer) timer->begin(cls); };
-    auto end_k = [&](int cls) { if (timer) timer->end(cls); };
+    auto begin_k = [&](int cls) { if (timer) timer->begin(cls, stream); };
+    auto end_k = [&](int cls) { if (timer) timer->end(cls, stream); };
     WfQueues Qx = Q;
     Qx.acc = Q.acc_s;  // per-sample accumulators
     uint64_t per_chunk = plan.chunk / (uint64_t)K;  // entries per chunk (whole pixels)
