@@ -30,6 +30,19 @@
 namespace pt {
 
 constexpr int kTB = 256;   // threads per block, traversal kernels (LDS stack column stride)
+// Occupancy of the FULL instantiations (textures / SDF / volume / transformed shapes),
+// measured with tools/bench_scenes.py: traversal at 4 waves (spilling past the 128-VGPR
+// budget) beat 2/1 by 14-33 % on sdf_zoo / volume / transformed; 5-7 were slower on the
+// SDF scene; shade is fastest at 2.
+#ifndef PT_FULL_TRACE_WAVES
+#define PT_FULL_TRACE_WAVES 4
+#endif
+#ifndef PT_FULL_SHADE_WAVES
+#define PT_FULL_SHADE_WAVES 2
+#endif
+#ifndef PT_FULL_SHADOW_WAVES
+#define PT_FULL_SHADOW_WAVES 4
+#endif
 // Rays a traversal wave claims per fetch atomic, in 64-ray batches.  A wave waits for its
 // claim's return before tracing, and the 8 partition cursors are contended: claiming one
 // batch at a time cost C4 trace 106 ms and shadow 47 ms per pass, four batches 82 and 42
@@ -239,7 +252,7 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
 #define PT_TRACE_WAVES 7
 #endif
 template <bool COUNT, bool FULL>
-__global__ __launch_bounds__(kTB, FULL ? 2 : PT_TRACE_WAVES) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
@@ -295,7 +308,7 @@ __global__ __launch_bounds__(kTB, FULL ? 2 : PT_TRACE_WAVES) void k_wf_trace(Dev
 // sampling up to the shadow query runs here too, so k_wf_shadow is a lean
 // traversal kernel (ray + stack state only).
 template <bool COUNT, bool FULL>
-__global__ __launch_bounds__(256, FULL ? 2 : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
+__global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         Q.counts[kFetchWord + 2 * kParts + threadIdx.x] = 0u;   // k_wf_shadow's fetch cursors
@@ -448,7 +461,7 @@ __global__ __launch_bounds__(256, FULL ? 2 : PT_SHADE_WAVES) void k_wf_shade(Dev
 // One thread per shadow ray that k_wf_shade set up (light, direction, the colour the
 // light adds if it is the nearest hit): the visibility query of Sampler.cs:261-265.
 template <bool COUNT, bool FULL>
-__global__ __launch_bounds__(kTB, FULL ? 1 : PT_SHADOW_WAVES) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
