@@ -981,7 +981,8 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, blas_shade, &S.blas_shade); if (rc) return rc;
     rc = upload(c, blas_uv, &S.blas_uv); if (rc) return rc;
     S.default_mat = default_mat;
-    S.full = (d->num_textures > 0 || d->num_sdf_shapes > 0 || d->num_volumes > 0 || d->num_transformed > 0) ? 1 : 0;
+    S.full_geom = (d->num_sdf_shapes > 0 || d->num_volumes > 0 || d->num_transformed > 0) ? 1 : 0;
+    S.full = (d->num_textures > 0 || S.full_geom) ? 1 : 0;
     S.tri_num_nodes = tri_num_nodes;
     S.ana_num_nodes = ana_num_nodes;
     S.num_planes = (int32_t)plane_scene.size();

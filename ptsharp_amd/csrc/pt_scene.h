@@ -90,6 +90,7 @@ struct DevScene {
     const float4* blas_uv;
     int32_t default_mat;       // `new Material()` (Volume.MaterialAt with no window near)
     int32_t full;              // textures or §8f row 4 shapes present: kernels run their FULL instantiation
+    int32_t full_geom;         // §8f row 4 shapes present: the traversal kernels need FULL (textures alone do not)
 };
 
 struct DevCamera {

@@ -607,14 +607,15 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
                        const WfPlan& plan, bool count, hipStream_t stream, LaunchTimer* timer, uint64_t bound) {
     auto begin_k = [&](int cls, hipStream_t s) { if (timer) timer->begin(cls, s); };
     auto end_k = [&](int cls, hipStream_t s) { if (timer) timer->end(cls, s); };
-    const bool full = S.full != 0;
+    const bool full = S.full != 0;        // shade: textures or row-4 shapes
+    const bool fullg = S.full_geom != 0;  // traversal: row-4 shapes only
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
         const unsigned tg = grid_for(n, kTB, plan.trace_blocks);
         begin_k(1, stream);
-        if (count && full) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-        else if (full) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (fullg) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         end_k(1, stream);
     };
@@ -636,9 +637,9 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
         const unsigned hg = grid_for(children * plan.lights_per_child, kTB, plan.shadow_blocks);
         begin_k(3, side);
-        if (count && full) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-        else if (full) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         end_k(3, side);
         if (plan.side) (void)hipEventRecord(plan.ev_side, side);
