@@ -132,8 +132,9 @@ struct Ctx {
 // 16 persistent launches, so fewer, larger chunks are faster (C4, 16 spp per pass: 8
 // chunks of 32M-entry queues 2574 Mrays/s, 2 chunks 2809, one chunk 2853).  The bound is
 // the largest power of two whose queues (176 B per entry: two extension queues of
-// o, d, throughput, key + hits + one shadow queue) fit a quarter of the device's memory,
-// clamped to [2^20, 2^28] entries (2^28: 47 GB of the MI355X's 288 GB).
+// o, d, throughput, key + hits + one shadow queue) fit a quarter of the device's memory
+// and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
+// MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #ifndef PT_SIDE_MAX_CHUNK
 #define PT_SIDE_MAX_CHUNK (20u << 20)
@@ -151,8 +152,8 @@ uint32_t wf_max_cap(Ctx* c) {
         return c->wf_max_cap = cap;
     }
     size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) total_b = (size_t)kWfMinCapLimit * kWfBytesPerEntry * 4;
-    const size_t budget = total_b / 4;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = total_b = (size_t)kWfMinCapLimit * kWfBytesPerEntry * 4;
+    const size_t budget = std::min(total_b / 4, free_b / 2);   // and at most half of what is free now
     uint32_t cap = kWfMaxCapLimit;
     while (cap > kWfMinCapLimit && (size_t)cap * kWfBytesPerEntry > budget) cap >>= 1;
     c->wf_max_cap = cap;
