@@ -125,6 +125,19 @@ def test_wavefront_many_chunks(gpu, monkeypatch):
     assert np.allclose(a.M, b.M, rtol=2e-5, atol=1e-6)
 
 
+def test_wavefront_full_frame_one_stream(gpu):
+    """1920x1080 at 16 spp with 8 first-bounce children: one 33M-sample chunk, above the side-stream
+    threshold, so shadow passes run on the main stream (the C4 bench's configuration); agrees with
+    the megakernel."""
+    s, c, smp = scenes.bunny_frame(4000, seed=9)
+    smp.MaxBounces = 2
+    a, ra = render_gpu(s, c, smp, 1920, 1080, spp=16, seed=37, engine=_abi.ENGINE_MEGAKERNEL)
+    b, rb = render_gpu(s, c, smp, 1920, 1080, spp=16, seed=37, engine=_abi.ENGINE_WAVEFRONT)
+    assert ra == rb
+    assert np.array_equal(a.N, b.N)
+    assert np.allclose(a.M, b.M, rtol=2e-5, atol=1e-6)
+
+
 # ---- adaptive / firefly phases of RenderParallel (Renderer.cs:340-537), wavefront engine
 def test_adaptive_phase(gpu):
     s, c, smp = scenes.gopher3()
