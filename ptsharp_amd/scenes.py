@@ -363,6 +363,23 @@ def instances(copies: int = 6, mesh_tris: int = 3000):
     return scene, camera, sampler
 
 
+def mixed(n_tris: int = 1_000_000, seed: int = 1234):
+    """BASELINE.json configs[4]'s kind of scene (C5): the C4 mesh frame plus an SDF shape, a
+    voxel Volume (iso-windows) and an environment texture standing in for the HDRI (the
+    reference's environment is an 8-bit ColorTexture lookup, Sampler.cs:177-189)."""
+    scene, camera, sampler = bunny_frame(n_tris, seed=seed)
+    scene.Texture = seeded_texture(512, 256, 21)
+    scene.TextureAngle = Util.Radians(40)
+    ring = TransformSDF.NewTransformSDF(TorusSDF.NewTorusSDF(F(0.45), F(0.12)),
+                                        Matrix.TranslateM(Vector(-1.8, 0.5, 0.4)).Mul(
+                                            Matrix.RotateM(Vector(1, 0, 0), Util.Radians(70))))
+    scene.Add(SDFShape.NewSDFShape(ring, Material.GlossyMaterial(Colour.HexColor(0x1F8A70), F(1.4), Util.Radians(10))))
+    vol, _, _ = volume(32, 32, 16, seed=5)
+    scene.Add(TransformedShape.NewTransformedShape(
+        vol.Shapes[0], Matrix.TranslateM(Vector(1.6, 0.55, -0.6)).Mul(Matrix.ScaleM(Vector(0.5, 0.5, 0.5)))))
+    return scene, camera, sampler
+
+
 SCENES = {
     "gopher3": gopher3,
     "materialspheres": materialspheres,
@@ -378,4 +395,5 @@ SCENES = {
     "volume": volume,
     "transformed": transformed,
     "instances": instances,
+    "mixed": mixed,
 }

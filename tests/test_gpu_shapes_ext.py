@@ -30,6 +30,15 @@ def test_row4_scene(gpu, engine, name):
 
 
 @ENGINES
+def test_mixed_scene(gpu, engine):
+    """The C5-kind scene (mesh + SDF + Volume + environment texture) at a test size."""
+    s, c, smp = scenes.mixed(3000, seed=5)
+    smp.MaxBounces = 3
+    g, gr, o, orr = render_both(s, c, smp, 48, 36, spp=2, seed=33, engine=engine)
+    check(g, gr, o, orr)
+
+
+@ENGINES
 def test_transformed_furnace_exact(gpu, engine):
     s, cam, smp = scenes.furnace(0.5)
     cube = s.Shapes[0]
