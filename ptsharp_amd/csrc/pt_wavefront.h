@@ -24,10 +24,11 @@ struct WfQueues {
     float4* n_o;         // shadow rays (a diffuse child's sampleLights, set up by k_wf_shade): {origin.xyz, pixel}
     float4* n_n;         // {direction.xyz, light index | kDead: no ray cast (diffuse <= 0)}
     float4* n_w;         // {throughput·weight·light colour·coverage.rgb, -}: added if the light is visible
-    uint32_t* counts;    // word (q, g) = {counts[2(q·kParts+g)], +1}: partition g of ray queue q and the
-                         // NEE requests made with it (one packed 64-bit word, reserved together);
-                         // counts[kFetchWord + k·kParts + g] = work-fetch cursor of kernel k
-                         // (0 trace, 1 shade, 2 shadow) in partition g; counts[kFlagWord] = overflow
+    uint32_t* counts;    // counter slots, each kCountStride words apart (see count_word below):
+                         // slot q·kParts+g = {rays, NEE requests} of partition g of ray queue q
+                         // (one packed 64-bit word, reserved together); slot kFetchSlot + k·kParts + g
+                         // = work-fetch cursor of kernel k (0 trace, 1 shade, 2 shadow) in partition
+                         // g; slot kFlagSlot = overflow flag
     uint32_t cap;        // entries per ray queue (kParts partitions of pcap)
     uint32_t s_cap;      // NEE queue entries (kParts partitions of spcap)
     uint32_t pcap, spcap;
@@ -36,10 +37,23 @@ struct WfQueues {
     double* acc_s;       // [cap][3] per-sample accumulators of the adaptive / firefly phases
 };
 
-constexpr int kFetchWord = 4 * kParts;
-constexpr int kFlagWord = 7 * kParts;
-constexpr int kCountWords = 7 * kParts + 2;
-constexpr int kChunkResetWords = 7 * kParts;   // pair words + fetch cursors, zeroed per chunk
+// Every counter sits on a line of its own: returning atomics execute at the memory side,
+// one line at a time, so cursors packed into one 128-B line serialise every partition's
+// claims on one channel.  kCountStride words (4 B each) between slots.
+#ifndef PT_COUNT_STRIDE
+#define PT_COUNT_STRIDE 64
+#endif
+constexpr int kCountStride = PT_COUNT_STRIDE;
+static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
+constexpr int kFetchSlot = 2 * kParts;
+constexpr int kFlagSlot = 5 * kParts;
+constexpr int count_word(int slot) { return slot * kCountStride; }
+constexpr int kFetchWord = count_word(kFetchSlot);
+constexpr int kFlagWord = count_word(kFlagSlot);
+constexpr int kCountWords = count_word(kFlagSlot + 1);
+constexpr int kChunkResetWords = count_word(kFlagSlot);   // pair words + fetch cursors, zeroed per chunk
+// work-fetch cursor of kernel k (0 trace, 1 shade, 2 shadow) in partition g
+constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 
 constexpr int kLdsStack = 16;                    // LDS stack entries per lane (traversal kernels)
 constexpr uint32_t kWfMaxBlocks = 256 * 8;        // grid cap of the traversal kernels

@@ -70,12 +70,12 @@ __device__ __forceinline__ uint4 nt_load(const uint4* p) {
 }
 __device__ __forceinline__ uint64_t nt_load(const uint64_t* p) { return __builtin_nontemporal_load(p); }
 
-__device__ __forceinline__ uint32_t* ray_count(const WfQueues& Q, int q, int g) { return Q.counts + 2 * (q * kParts + g); }
+__device__ __forceinline__ uint32_t* ray_count(const WfQueues& Q, int q, int g) { return Q.counts + count_word(q * kParts + g); }
 __device__ __forceinline__ uint32_t* nee_count(const WfQueues& Q, int q, int g) {
-    return Q.counts + 2 * (q * kParts + g) + 1;
+    return Q.counts + count_word(q * kParts + g) + 1;
 }
 __device__ __forceinline__ unsigned long long* pair_word(const WfQueues& Q, int q, int g) {
-    return reinterpret_cast<unsigned long long*>(Q.counts) + q * kParts + g;
+    return reinterpret_cast<unsigned long long*>(Q.counts + count_word(q * kParts + g));
 }
 
 // XCD group of this block (grids are multiples of kParts): group g = b % kParts,
@@ -257,12 +257,12 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
-        Q.counts[kFetchWord + kParts + threadIdx.x] = 0u;        // k_wf_shade's fetch cursors
+        Q.counts[fetch_word(1, threadIdx.x)] = 0u;               // k_wf_shade's fetch cursors
     }
     const Group G = xcd_group();
     const uint32_t cnt = *ray_count(Q, qi, G.g);
     const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
-    uint32_t* cursor = Q.counts + kFetchWord + G.g;
+    uint32_t* cursor = Q.counts + fetch_word(0, G.g);
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
     // Persistent grid (resident capacity); each wave claims kFetchBatches × 64 rays of
@@ -311,8 +311,8 @@ template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters) {
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
-        Q.counts[kFetchWord + 2 * kParts + threadIdx.x] = 0u;   // k_wf_shadow's fetch cursors
-        Q.counts[kFetchWord + threadIdx.x] = 0u;                // the next k_wf_trace's (it may run beside k_wf_shadow)
+        Q.counts[fetch_word(2, threadIdx.x)] = 0u;              // k_wf_shadow's fetch cursors
+        Q.counts[fetch_word(0, threadIdx.x)] = 0u;              // the next k_wf_trace's (it may run beside k_wf_shadow)
     }
     const Group G = xcd_group();
     const uint32_t cnt = *ray_count(Q, qi, G.g);
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     Counters ctr{0, 0, 0, 0};
     __shared__ uint32_t s_k0;
     for (;;) {  // block-uniform: the block takes 256 vertices of its partition at a time
-        if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + kFetchWord + kParts + G.g, 256u);
+        if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u);
         __syncthreads();
         const uint32_t k0 = s_k0;  // thread 0 rewrites it only after block_reserve2's barriers below
         if (k0 >= n) break;
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
-    uint32_t* cursor = Q.counts + kFetchWord + 2 * kParts + G.g;
+    uint32_t* cursor = Q.counts + fetch_word(2, G.g);
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
     for (;;) {  // kFetchBatches × 64 rays per claim, 64 at a time (see k_wf_trace)

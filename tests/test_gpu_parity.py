@@ -167,3 +167,33 @@ def test_extra_phases_unsupported_on_megakernel(gpu):
     s, c, smp = scenes.gopher3()
     with pytest.raises(_abi.PTError):
         render_gpu(s, c, smp, 32, 32, spp=1, engine=_abi.ENGINE_MEGAKERNEL, adaptive=1)
+
+
+def test_rccl_gather_single_rank(gpu):
+    """pt_comm_unique_id / pt_comm_init / pt_comm_gather (the RCCL ncclReduce of M, V, N that
+    assembles a multi-GPU frame) on a one-rank communicator: the gathered Buffer is the
+    rendered one, bit for bit.  A 1-GPU box cannot host two RCCL ranks; the N-rank sum
+    itself is covered by test_distributed.py (gloo) and test_tiles_shard_equals_full."""
+    from ptsharp_amd import Renderer, tiles_for_rank
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 3
+    w, h = 80, 70
+    r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+    try:
+        r.SamplesPerPixel = 2
+        r.Seed = 31
+        r.Tiles = tiles_for_rank(w, h, 0, 2)   # a rank's share: the other tiles stay zero
+        r.RenderParallel()
+        before = r.ReadBuffer()
+        M, V, N = before.M.copy(), before.V.copy(), before.N.copy()
+        assert (N > 0).any() and (N == 0).any()
+        r.CommInit(1, 0, Renderer.CommUniqueId())
+        r.Gather(0)
+        after = r.ReadBuffer()
+        assert np.array_equal(after.N, N)
+        assert np.array_equal(after.M, M)
+        assert np.array_equal(after.V, V)
+        r.RenderParallel()   # the context keeps rendering after a gather
+        assert (r.ReadBuffer().N == 2 * N).all()
+    finally:
+        r.close()

@@ -12,5 +12,5 @@ for V in "${VS[@]}"; do
     timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q -m gpu > gpurun_out/ab/tests_$NAME.log 2>&1 || exit 1
     first=0
   fi
-  timeout -k 10 300 python bench.py --steps 3 --warmup 1 --spp ${SPP:-16} --cpu-seconds 0 --no-parity --engine wave --json-out gpurun_out/ab/$NAME.json > gpurun_out/ab/$NAME.log 2>&1 || exit 1
+  timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --spp ${SPP:-16} --cpu-seconds 0 --no-parity --engine wave --json-out gpurun_out/ab/$NAME.json > gpurun_out/ab/$NAME.log 2>&1 || exit 1
 done
