@@ -397,14 +397,31 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         uint32_t ebase, nbase;
         block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase);
         if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) Q.counts[kFlagWord] = 1;
-        uint32_t ej = ebase, nj = nbase;
-        for (int c = 0; c < nch; c++) {
+        // Child-major slots: the wave's reservation [ebase of lane 0, + the wave's total) is
+        // filled child index by child index, each live child c of the wave's lanes on
+        // consecutive slots (a ballot prefix).  A 64-ray batch of the next depth then holds the
+        // same stratum and mode of neighbouring camera samples (one direction quadrant, origins
+        // of a few pixels) rather than all children of one sample, and every store instruction
+        // writes whole lines.  Which children exist is unchanged, so is every child's key.
+        const int lane = threadIdx.x & 63;
+        const uint64_t below = (1ull << lane) - 1ull;
+        uint32_t ej = __shfl(ebase, 0, 64), nj = __shfl(nbase, 0, 64);
+        int cmax = nch;
+        for (int off = 32; off > 0; off >>= 1) cmax = max(cmax, __shfl_xor(cmax, off, 64));
+        for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
             const int mode = ma + c % nm;
             const uint64_t E = child_key(node, (uint32_t)c);
-            const bool refl = mode == 2 || (mode == 0 && draw(E, D_REFLECT) < pv);
-            const bool live = mode == 0 || (refl ? pv > 0 : (1 - pv) > 0);
-            if (!live) continue;
+            const bool refl = mode == 2 || (mode == 0 && c < nch && draw(E, D_REFLECT) < pv);
+            const bool live = c < nch && (mode == 0 || (refl ? pv > 0 : (1 - pv) > 0));
             const bool reflected = refl || m.transparent;                 // specular branch (Sampler.cs:109-115)
+            const bool emit_nee = live && !reflected && nee_on;
+            const bool emit_ext = live && ext_on;
+            const uint64_t bn = __ballot(emit_nee), be = __ballot(emit_ext);
+            const uint32_t my_n = nj + (uint32_t)__popcll(bn & below) * rays_per_nee;
+            const uint32_t my_e = ej + (uint32_t)__popcll(be & below);
+            nj += (uint32_t)__popcll(bn) * rays_per_nee;
+            ej += (uint32_t)__popcll(be);
+            if (!live) continue;
             const float fp = mode == 0 ? 1.0f : (float)(refl ? pv : 1 - pv);
             float w[3];
             if (reflected) {
@@ -424,14 +441,13 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                         float3 lc;
                         const bool cast = light_setup<FULL>(S, smp, S.lights[li], sh.pos, sh.nrm,
                                                       all_lights ? light_key(E, (uint32_t)li) : E, ldir, lc);
-                        if (nj < Q.spcap) {
-                            const uint32_t at = G.g * Q.spcap + nj;
+                        if (my_n + j < Q.spcap) {
+                            const uint32_t at = G.g * Q.spcap + my_n + j;
                             q_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
                             q_store(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
                             q_store(&Q.n_w[at], make_float4((t2[0] * w[0]) * (lc.x * scale), (t2[1] * w[1]) * (lc.y * scale),
                                                              (t2[2] * w[2]) * (lc.z * scale), 0.f));
                         }
-                        nj++;
                     }
                 }
             }
@@ -442,10 +458,9 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
             v3 no, nd;
             bounce_dir(m, sh, d, fu, fv, refl, n1, n2, E, no, nd);
-            if (ej < Q.pcap)
-                ray_store(Q, qo, G.g * Q.pcap + ej, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
+            if (my_e < Q.pcap)
+                ray_store(Q, qo, G.g * Q.pcap + my_e, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
                           (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
-            ej++;
         }
     }
     if (COUNT) {
