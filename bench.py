@@ -147,8 +147,9 @@ def main():
         return
 
     value = total_rays / elapsed / 1e6
-    # kernel names as rocprofv3 reports them (template arguments <COUNT, FULL>)
-    names = ["k_wf_camera", "k_wf_trace<false, false>", "k_wf_shade<false, false>", "k_wf_shadow<false, false>",
+    # kernel names as rocprofv3 reports them (template arguments <COUNT, FULL>; the shade
+    # class times both of its forms <COUNT, FULL, SCAN>, one of which returns at once)
+    names = ["k_wf_camera", "k_wf_trace<false, false>", "k_wf_shade<false, false, *>", "k_wf_shadow<false, false>",
              "k_wf_finalize", "k_render_pass<false, false>"]
     # the closest-hit kernel is the dominant one by design (on a multi-GPU shard the shadow
     # passes run beside it on a second stream, so their event spans overlap it)

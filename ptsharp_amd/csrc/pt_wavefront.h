@@ -28,7 +28,8 @@ struct WfQueues {
                          // slot q·kParts+g = {rays, NEE requests} of partition g of ray queue q
                          // (one packed 64-bit word, reserved together); slot kFetchSlot + k·kParts + g
                          // = work-fetch cursor of kernel k (0 trace, 1 shade, 2 shadow) in partition
-                         // g; slot kFlagSlot = overflow flag
+                         // g; slots kKeptSlot + q = rays of queue q with shading work (k_wf_trace);
+                         // slot kFlagSlot = overflow flag
     uint32_t cap;        // entries per ray queue (kParts partitions of pcap)
     uint32_t s_cap;      // NEE queue entries (kParts partitions of spcap)
     uint32_t pcap, spcap;
@@ -46,7 +47,8 @@ struct WfQueues {
 constexpr int kCountStride = PT_COUNT_STRIDE;
 static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
 constexpr int kFetchSlot = 2 * kParts;
-constexpr int kFlagSlot = 5 * kParts;
+constexpr int kKeptSlot = 5 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
+constexpr int kFlagSlot = 5 * kParts + 2;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kFlagWord = count_word(kFlagSlot);
@@ -54,6 +56,7 @@ constexpr int kCountWords = count_word(kFlagSlot + 1);
 constexpr int kChunkResetWords = count_word(kFlagSlot);   // pair words + fetch cursors, zeroed per chunk
 // work-fetch cursor of kernel k (0 trace, 1 shade, 2 shadow) in partition g
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
+constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
 
 constexpr int kLdsStack = 16;                    // LDS stack entries per lane (traversal kernels)
 constexpr uint32_t kWfMaxBlocks = 256 * 8;        // grid cap of the traversal kernels
@@ -67,6 +70,8 @@ struct WfPlan {
     uint32_t trace_blocks;     // persistent grids: resident capacity of each kernel
     uint32_t shade_blocks;
     uint32_t shadow_blocks;
+    int32_t shade_form;        // k_wf_shade form: 0 chosen per depth from the kept count, 1 direct, 2 SCAN
+                               // (PT_SHADE_FORM=direct|scan in the environment; tests)
     // Optional second stream: each depth's shadow pass runs there, beside the next depth's
     // closest-hit pass (independent queues), so one fills the other's ramp and tail.
     // ev_main / ev_side order shade(d) → shadow(d) → shade(d + 1).  Null: one stream.

@@ -92,6 +92,14 @@ __device__ __forceinline__ uint32_t append(uint32_t* counter) {
 }
 
 constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that was not cast
+constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera slot (k_wf_trace)
+#ifndef PT_SHADE_SCAN
+#define PT_SHADE_SCAN 8
+#endif
+constexpr int kShadeScan = PT_SHADE_SCAN;   // 256-vertex groups a SCAN shade block claims and lists
+// The environment may be textured (non-black per direction) only where the shade kernel
+// runs its FULL instantiation; the traversal kernels see S.env_tex either way.
+#define FULL_SHADE_ENV(S) ((S).env_tex >= 0)
 
 __device__ __forceinline__ uint32_t wave_scan(uint32_t n, int lane) {  // inclusive
     uint32_t x = n;
@@ -265,6 +273,8 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
     uint32_t* cursor = Q.counts + fetch_word(0, G.g);
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
+    const bool env_black = (!FULL_SHADE_ENV(S)) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
+    uint32_t kept = 0;   // rays with work for k_wf_shade (its SCAN choice)
     // Persistent grid (resident capacity); each wave claims kFetchBatches × 64 rays of
     // its partition with one atomic and traces them 64 at a time, so no wave waits for a
     // second dispatch round and the tail is a few traversals long.
@@ -277,15 +287,21 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
             if (k0 + lane >= n) continue;
             const uint32_t i = base + k0 + lane;
             float4 b = nt_load(&Q.q_d[qi][i]);
-            if (__float_as_uint(b.w) == kDead) continue;   // a camera slot outside the image
+            if (__float_as_uint(b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
+                q_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
+                continue;
+            }
             float4 a = nt_load(&Q.q_o[qi][i]);
             HitRec h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+            kept += (h.kind >= 0 || !env_black) ? 1u : 0u;
             unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
             q_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
         }
     }
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
+    kept = wave_sum(kept);
+    if (lane == 0 && kept) atomicAdd(Q.counts + kept_word(qi), kept);
     if (COUNT) {
         uint32_t nodes = wave_sum(ctr.nodes), prims = wave_sum(ctr.prims);
         if (lane == 0) {
@@ -307,160 +323,224 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 // word saturates near 88 per µs on MI355X, MI355X_MICROARCH.md "dequeue").  Light
 // sampling up to the shadow query runs here too, so k_wf_shadow is a lean
 // traversal kernel (ray + stack state only).
+// One queued vertex (slot i of partition G.g; `alive` false: the lane only takes part in
+// the block's reservation and ballots).  Block-uniform call.
 template <bool COUNT, bool FULL>
-__global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
-                                                                  unsigned long long* counters) {
-    if (blockIdx.x == 0 && threadIdx.x < kParts) {
-        Q.counts[fetch_word(2, threadIdx.x)] = 0u;              // k_wf_shadow's fetch cursors
-        Q.counts[fetch_word(0, threadIdx.x)] = 0u;              // the next k_wf_trace's (it may run beside k_wf_shadow)
-    }
-    const Group G = xcd_group();
-    const uint32_t cnt = *ray_count(Q, qi, G.g);
-    const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
+__device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler& smp, const WfQueues& Q, int qi,
+                                             const Group& G, uint32_t i, bool alive, Counters& ctr) {
     const int qo = 1 - qi;
     const bool nee_on = smp.dl && S.num_lights > 0;
     const int nl = S.num_lights;
     const bool all_lights = smp.light_mode == 1;
     const uint32_t rays_per_nee = all_lights ? (uint32_t)nl : 1u;   // shadow rays of one sampleLights call
-    Counters ctr{0, 0, 0, 0};
-    __shared__ uint32_t s_k0;
-    for (;;) {  // block-uniform: the block takes 256 vertices of its partition at a time
-        if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u);
-        __syncthreads();
-        const uint32_t k0 = s_k0;  // thread 0 rewrites it only after block_reserve2's barriers below
-        if (k0 >= n) break;
-        const uint32_t i = base + k0 + threadIdx.x;
-        bool alive = k0 + threadIdx.x < n;
-        float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, rt = ro;
-        uint4 hr = make_uint4(0, 0, 0, 0);
-        uint32_t meta = kDead;
-        uint64_t node = 0;
-        if (alive) {  // all loads issued together: one memory round trip
-            rd = nt_load(&Q.q_d[qi][i]);
-            ro = nt_load(&Q.q_o[qi][i]);
-            rt = nt_load(&Q.q_t[qi][i]);
-            hr = nt_load(&Q.hits[i]);
-            node = nt_load(&Q.q_k[qi][i]);
-            meta = __float_as_uint(rd.w);
-            alive = meta != kDead;
-        }
-        const uint32_t pixel = __float_as_uint(ro.w);
-        const int depth = (int)(meta & 0xFF);
-        const bool emission = (meta >> 8) & 1;
-        HitRec h;
-        h.t = __longlong_as_double((long long)(((unsigned long long)hr.y << 32) | hr.x));
-        h.kind = (int32_t)hr.z;
-        h.idx = (int32_t)hr.w;
-        const float thr[3] = {rt.x, rt.y, rt.z};
-        const v3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z};
-        Shade sh{};
-        int mat = 0, nn = 1, nm = 1, nch = 0;
-        float t2[3] = {0.f, 0.f, 0.f};
-        double pv = 0.0, n1 = 1.0, n2 = 1.0;
-        if (alive && !(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67, 177-189)
-            const float3 env = environment<FULL>(S, d);
-            acc_add(Q.acc, pixel, thr[0] * env.x, thr[1] * env.y, thr[2] * env.z);
-            alive = false;
-        }
-        if (alive) {
-            sh = hit_info<COUNT, FULL>(S, h, o, d, ctr);
-            mat = sh.mat;
-            const DevMaterial& m = S.mats[mat];
-            const int samples = depth == 0 ? smp.fh : 1;
-            nn = (int)sqrt((double)samples);
-            const float inv_n2 = 1.0f / (float)(nn * nn);
-            if (m.emittance > 0) {
-                if (smp.dl && !emission) {
-                    alive = false;  // Sampler.cs:75-78
-                } else {
-                    float e = (float)((double)m.emittance * samples) * inv_n2;
-                    acc_add(Q.acc, pixel, thr[0] * sh.col[0] * e, thr[1] * sh.col[1] * e, thr[2] * sh.col[2] * e);
-                }
-            }
-            nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
-            nch = alive ? nn * nn * nm : 0;
-            for (int k = 0; k < 3; k++) t2[k] = thr[k] * inv_n2;
-            pv = vertex_p(m, sh, d, n1, n2);
-        }
+    float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, rt = ro;
+    uint4 hr = make_uint4(0, 0, 0, 0);
+    uint32_t meta = kDead;
+    uint64_t node = 0;
+    if (alive) {  // all loads issued together: one memory round trip
+        rd = nt_load(&Q.q_d[qi][i]);
+        ro = nt_load(&Q.q_o[qi][i]);
+        rt = nt_load(&Q.q_t[qi][i]);
+        hr = nt_load(&Q.hits[i]);
+        node = nt_load(&Q.q_k[qi][i]);
+        meta = __float_as_uint(rd.w);
+        alive = meta != kDead;
+    }
+    const uint32_t pixel = __float_as_uint(ro.w);
+    const int depth = (int)(meta & 0xFF);
+    const bool emission = (meta >> 8) & 1;
+    HitRec h;
+    h.t = __longlong_as_double((long long)(((unsigned long long)hr.y << 32) | hr.x));
+    h.kind = (int32_t)hr.z;
+    h.idx = (int32_t)hr.w;
+    const float thr[3] = {rt.x, rt.y, rt.z};
+    const v3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z};
+    Shade sh{};
+    int mat = 0, nn = 1, nm = 1, nch = 0;
+    float t2[3] = {0.f, 0.f, 0.f};
+    double pv = 0.0, n1 = 1.0, n2 = 1.0;
+    if (alive && !(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67, 177-189)
+        const float3 env = environment<FULL>(S, d);
+        acc_add(Q.acc, pixel, thr[0] * env.x, thr[1] * env.y, thr[2] * env.z);
+        alive = false;
+    }
+    if (alive) {
+        sh = hit_info<COUNT, FULL>(S, h, o, d, ctr);
+        mat = sh.mat;
         const DevMaterial& m = S.mats[mat];
-        const int ma = nm == 2 ? 1 : 0;
-        const bool ext_on = depth + 1 <= smp.mb;   // deeper samples return black without an Intersect
-        // child c: mode, reflect decision, liveness (p > 0 after the Any-mode override)
-        uint32_t n_ext = 0, n_nee = 0;
-        for (int c = 0; c < nch; c++) {
-            const int mode = ma + c % nm;
-            const bool refl = mode == 2 || (mode == 0 && draw(child_key(node, (uint32_t)c), D_REFLECT) < pv);
-            const bool live = mode == 0 || (refl ? pv > 0 : (1 - pv) > 0);
-            n_ext += (live && ext_on) ? 1u : 0u;
-            n_nee += (live && !refl && !m.transparent && nee_on) ? rays_per_nee : 0u;
-        }
-        uint32_t ebase, nbase;
-        block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase);
-        if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) Q.counts[kFlagWord] = 1;
-        // Child-major slots: the wave's reservation [ebase of lane 0, + the wave's total) is
-        // filled child index by child index, each live child c of the wave's lanes on
-        // consecutive slots (a ballot prefix).  A 64-ray batch of the next depth then holds the
-        // same stratum and mode of neighbouring camera samples (one direction quadrant, origins
-        // of a few pixels) rather than all children of one sample, and every store instruction
-        // writes whole lines.  Which children exist is unchanged, so is every child's key.
-        const int lane = threadIdx.x & 63;
-        const uint64_t below = (1ull << lane) - 1ull;
-        uint32_t ej = __shfl(ebase, 0, 64), nj = __shfl(nbase, 0, 64);
-        int cmax = nch;
-        for (int off = 32; off > 0; off >>= 1) cmax = max(cmax, __shfl_xor(cmax, off, 64));
-        for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
-            const int mode = ma + c % nm;
-            const uint64_t E = child_key(node, (uint32_t)c);
-            const bool refl = mode == 2 || (mode == 0 && c < nch && draw(E, D_REFLECT) < pv);
-            const bool live = c < nch && (mode == 0 || (refl ? pv > 0 : (1 - pv) > 0));
-            const bool reflected = refl || m.transparent;                 // specular branch (Sampler.cs:109-115)
-            const bool emit_nee = live && !reflected && nee_on;
-            const bool emit_ext = live && ext_on;
-            const uint64_t bn = __ballot(emit_nee), be = __ballot(emit_ext);
-            const uint32_t my_n = nj + (uint32_t)__popcll(bn & below) * rays_per_nee;
-            const uint32_t my_e = ej + (uint32_t)__popcll(be & below);
-            nj += (uint32_t)__popcll(bn) * rays_per_nee;
-            ej += (uint32_t)__popcll(be);
-            if (!live) continue;
-            const float fp = mode == 0 ? 1.0f : (float)(refl ? pv : 1 - pv);
-            float w[3];
-            if (reflected) {
-                for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * sh.col[k]);
+        const int samples = depth == 0 ? smp.fh : 1;
+        nn = (int)sqrt((double)samples);
+        const float inv_n2 = 1.0f / (float)(nn * nn);
+        if (m.emittance > 0) {
+            if (smp.dl && !emission) {
+                alive = false;  // Sampler.cs:75-78
             } else {
-                for (int k = 0; k < 3; k++) w[k] = fp * sh.col[k];
-                if (nee_on) {
-                    // diffuse child: sampleLights from the normal ray (Sampler.cs:191-296) up to the
-                    // shadow query — light choice, soft-shadow point, coverage — here, so the
-                    // visibility kernel carries only ray + stack state.  One shadow-ray slot per
-                    // light considered; a light with diffuse <= 0 casts no ray (dead slot).
-                    const int first = all_lights ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
-                    const float scale = all_lights ? 1.0f / (float)nl : (float)nl;
-                    for (uint32_t j = 0; j < rays_per_nee; j++) {
-                        const int li = first + (int)j;
-                        v3 ldir;
-                        float3 lc;
-                        const bool cast = light_setup<FULL>(S, smp, S.lights[li], sh.pos, sh.nrm,
-                                                      all_lights ? light_key(E, (uint32_t)li) : E, ldir, lc);
-                        if (my_n + j < Q.spcap) {
-                            const uint32_t at = G.g * Q.spcap + my_n + j;
-                            q_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
-                            q_store(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
-                            q_store(&Q.n_w[at], make_float4((t2[0] * w[0]) * (lc.x * scale), (t2[1] * w[1]) * (lc.y * scale),
-                                                             (t2[2] * w[2]) * (lc.z * scale), 0.f));
-                        }
+                float e = (float)((double)m.emittance * samples) * inv_n2;
+                acc_add(Q.acc, pixel, thr[0] * sh.col[0] * e, thr[1] * sh.col[1] * e, thr[2] * sh.col[2] * e);
+            }
+        }
+        nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
+        nch = alive ? nn * nn * nm : 0;
+        for (int k = 0; k < 3; k++) t2[k] = thr[k] * inv_n2;
+        pv = vertex_p(m, sh, d, n1, n2);
+    }
+    const DevMaterial& m = S.mats[mat];
+    const int ma = nm == 2 ? 1 : 0;
+    const bool ext_on = depth + 1 <= smp.mb;   // deeper samples return black without an Intersect
+    // child c: mode, reflect decision, liveness (p > 0 after the Any-mode override)
+    uint32_t n_ext = 0, n_nee = 0;
+    for (int c = 0; c < nch; c++) {
+        const int mode = ma + c % nm;
+        const bool refl = mode == 2 || (mode == 0 && draw(child_key(node, (uint32_t)c), D_REFLECT) < pv);
+        const bool live = mode == 0 || (refl ? pv > 0 : (1 - pv) > 0);
+        n_ext += (live && ext_on) ? 1u : 0u;
+        n_nee += (live && !refl && !m.transparent && nee_on) ? rays_per_nee : 0u;
+    }
+    uint32_t ebase, nbase;
+    block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase);
+    if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) Q.counts[kFlagWord] = 1;
+    // Child-major slots: the wave's reservation [ebase of lane 0, + the wave's total) is
+    // filled child index by child index, each live child c of the wave's lanes on
+    // consecutive slots (a ballot prefix).  A 64-ray batch of the next depth then holds the
+    // same stratum and mode of neighbouring camera samples (one direction quadrant, origins
+    // of a few pixels) rather than all children of one sample, and every store instruction
+    // writes whole lines.  Which children exist is unchanged, so is every child's key.
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t ej = __shfl(ebase, 0, 64), nj = __shfl(nbase, 0, 64);
+    int cmax = nch;
+    for (int off = 32; off > 0; off >>= 1) cmax = max(cmax, __shfl_xor(cmax, off, 64));
+    for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
+        const int mode = ma + c % nm;
+        const uint64_t E = child_key(node, (uint32_t)c);
+        const bool refl = mode == 2 || (mode == 0 && c < nch && draw(E, D_REFLECT) < pv);
+        const bool live = c < nch && (mode == 0 || (refl ? pv > 0 : (1 - pv) > 0));
+        const bool reflected = refl || m.transparent;                 // specular branch (Sampler.cs:109-115)
+        const bool emit_nee = live && !reflected && nee_on;
+        const bool emit_ext = live && ext_on;
+        const uint64_t bn = __ballot(emit_nee), be = __ballot(emit_ext);
+        const uint32_t my_n = nj + (uint32_t)__popcll(bn & below) * rays_per_nee;
+        const uint32_t my_e = ej + (uint32_t)__popcll(be & below);
+        nj += (uint32_t)__popcll(bn) * rays_per_nee;
+        ej += (uint32_t)__popcll(be);
+        if (!live) continue;
+        const float fp = mode == 0 ? 1.0f : (float)(refl ? pv : 1 - pv);
+        float w[3];
+        if (reflected) {
+            for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * sh.col[k]);
+        } else {
+            for (int k = 0; k < 3; k++) w[k] = fp * sh.col[k];
+            if (nee_on) {
+                // diffuse child: sampleLights from the normal ray (Sampler.cs:191-296) up to the
+                // shadow query — light choice, soft-shadow point, coverage — here, so the
+                // visibility kernel carries only ray + stack state.  One shadow-ray slot per
+                // light considered; a light with diffuse <= 0 casts no ray (dead slot).
+                const int first = all_lights ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
+                const float scale = all_lights ? 1.0f / (float)nl : (float)nl;
+                for (uint32_t j = 0; j < rays_per_nee; j++) {
+                    const int li = first + (int)j;
+                    v3 ldir;
+                    float3 lc;
+                    const bool cast = light_setup<FULL>(S, smp, S.lights[li], sh.pos, sh.nrm,
+                                                  all_lights ? light_key(E, (uint32_t)li) : E, ldir, lc);
+                    if (my_n + j < Q.spcap) {
+                        const uint32_t at = G.g * Q.spcap + my_n + j;
+                        q_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
+                        q_store(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
+                        q_store(&Q.n_w[at], make_float4((t2[0] * w[0]) * (lc.x * scale), (t2[1] * w[1]) * (lc.y * scale),
+                                                         (t2[2] * w[2]) * (lc.z * scale), 0.f));
                     }
                 }
             }
-            if (!ext_on) continue;
-            const int stratum = c / nm;
-            const int u = stratum / nn, v = stratum % nn;
-            const double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)nn;
-            const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
-            v3 no, nd;
-            bounce_dir(m, sh, d, fu, fv, refl, n1, n2, E, no, nd);
-            if (my_e < Q.pcap)
-                ray_store(Q, qo, G.g * Q.pcap + my_e, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
-                          (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
+        }
+        if (!ext_on) continue;
+        const int stratum = c / nm;
+        const int u = stratum / nn, v = stratum % nn;
+        const double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)nn;
+        const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
+        v3 no, nd;
+        bounce_dir(m, sh, d, fu, fv, refl, n1, n2, E, no, nd);
+        if (my_e < Q.pcap)
+            ray_store(Q, qo, G.g * Q.pcap + my_e, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
+                      (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
+    }
+}
+
+// SCAN (one of the two instantiations launched per depth runs; the other returns at
+// once): k_wf_trace counted the rays with work for shade (hits, and misses when the
+// environment is not black; kept_word).  Where fewer than half of the queued rays have
+// work (C4's first bounce: ~77 % escape), a block claims kShadeScan × 256 vertices, reads
+// their hit records and lists the ones with work in slot order, then shades the list 256
+// at a time: each round trip of the chain (claim, queue loads, triangle record,
+// reservation) serves four times as many vertices.  Otherwise the block shades every
+// claimed slot (no extra read of the hit records, fewer live registers).
+template <bool COUNT, bool FULL, bool SCAN>
+__global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
+                                                                  unsigned long long* counters, int form) {
+    uint32_t queued = 0;
+    for (int g = 0; g < kParts; g++) queued += min(*ray_count(Q, qi, g), Q.pcap);
+    const bool scan = form ? form == 2 : 2ull * Q.counts[kept_word(qi)] < (unsigned long long)queued;
+    if (scan != SCAN) return;
+    if (blockIdx.x == 0 && threadIdx.x < kParts) {
+        Q.counts[fetch_word(2, threadIdx.x)] = 0u;              // k_wf_shadow's fetch cursors
+        Q.counts[fetch_word(0, threadIdx.x)] = 0u;              // the next k_wf_trace's (it may run beside k_wf_shadow)
+        if (threadIdx.x == 0) Q.counts[kept_word(1 - qi)] = 0u;   // the next k_wf_trace's kept count
+    }
+    const Group G = xcd_group();
+    const uint32_t cnt = *ray_count(Q, qi, G.g);
+    const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
+    Counters ctr{0, 0, 0, 0};
+    __shared__ uint32_t s_k0;
+    if constexpr (!SCAN) {
+        for (;;) {  // block-uniform: the block takes 256 vertices of its partition at a time
+            if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u);
+            __syncthreads();
+            const uint32_t k0 = s_k0;  // thread 0 rewrites it only after block_reserve2's barriers
+            if (k0 >= n) break;
+            shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + k0 + threadIdx.x, k0 + threadIdx.x < n, ctr);
+        }
+    } else {
+        const bool env_black = (!FULL || S.env_tex < 0) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        const uint64_t below = (1ull << lane) - 1ull;
+        __shared__ uint32_t s_wcnt[kShadeScan * 4];
+        __shared__ uint16_t s_list[kShadeScan * 256];
+        for (;;) {
+            if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u * kShadeScan);
+            __syncthreads();
+            const uint32_t k0 = s_k0;  // thread 0 rewrites it only after the barriers below
+            if (k0 >= n) break;
+            uint32_t keep = 0;
+#pragma unroll
+            for (int j = 0; j < kShadeScan; j++) {
+                const uint32_t sl = k0 + (uint32_t)j * 256u + threadIdx.x;
+                int32_t kind = kDeadKind;
+                if (sl < n) kind = (int32_t)nt_load(&Q.hits[base + sl]).z;
+                keep |= (kind != kDeadKind && (kind >= 0 || !env_black)) ? 1u << j : 0u;
+            }
+            uint64_t bal[kShadeScan];
+#pragma unroll
+            for (int j = 0; j < kShadeScan; j++) {
+                bal[j] = __ballot((keep >> j) & 1u);
+                if (lane == 0) s_wcnt[j * 4 + wid] = (uint32_t)__popcll(bal[j]);
+            }
+            __syncthreads();
+            uint32_t total = 0, pre[kShadeScan];
+#pragma unroll
+            for (int q = 0; q < kShadeScan * 4; q++) {
+                const uint32_t w = s_wcnt[q];
+                if ((q & 3) == wid) pre[q >> 2] = total;
+                total += w;
+            }
+#pragma unroll
+            for (int j = 0; j < kShadeScan; j++)
+                if ((keep >> j) & 1u) s_list[pre[j] + (uint32_t)__popcll(bal[j] & below)] = (uint16_t)(j * 256 + threadIdx.x);
+            __syncthreads();
+            for (uint32_t r = 0; r < total; r += 256u) {   // block-uniform
+                const bool listed = r + threadIdx.x < total;
+                shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + k0 + (listed ? (uint32_t)s_list[r + threadIdx.x] : 0u),
+                                          listed, ctr);
+            }
         }
     }
     if (COUNT) {
@@ -640,10 +720,20 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         if (plan.side && depth > 0) (void)hipStreamWaitEvent(stream, plan.ev_side, 0);   // shadow(d-1) read its queue
         const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
         begin_k(2, stream);
-        if (count && full) hipLaunchKernelGGL((k_wf_shade<true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
-        else if (count) hipLaunchKernelGGL((k_wf_shade<true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
-        else if (full) hipLaunchKernelGGL((k_wf_shade<false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
-        else hipLaunchKernelGGL((k_wf_shade<false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters);
+        // both forms (the one the kept count selects runs, the other returns at once)
+        if (count && full) {
+            hipLaunchKernelGGL((k_wf_shade<true, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+        } else if (count) {
+            hipLaunchKernelGGL((k_wf_shade<true, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+        } else if (full) {
+            hipLaunchKernelGGL((k_wf_shade<false, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+        } else {
+            hipLaunchKernelGGL((k_wf_shade<false, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+        }
         end_k(2, stream);
         if (plan.side) {
             (void)hipEventRecord(plan.ev_main, stream);
@@ -734,7 +824,7 @@ hipError_t wavefront_grids(WfPlan& plan) {
     };
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace<false, false>, kTB, 0);
     if (e == hipSuccess) plan.trace_blocks = resident(nb, kWfMaxBlocks);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shade<false, false>, 256, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shade<false, false, false>, 256, 0);
     if (e == hipSuccess) plan.shade_blocks = resident(nb, 1u << 20);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false, false>, kTB, 0);
     if (e == hipSuccess) plan.shadow_blocks = resident(nb, kWfMaxBlocks);

@@ -197,3 +197,25 @@ def test_rccl_gather_single_rank(gpu):
         assert (r.ReadBuffer().N == 2 * N).all()
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("form", ["direct", "scan"])
+@pytest.mark.parametrize("name", ["mesh", "gopher3", "gopher3_env", "textured"])
+def test_shade_forms(gpu, monkeypatch, form, name):
+    """Both forms of k_wf_shade forced at every depth (PT_SHADE_FORM): the direct form and
+    the SCAN form (claim 8 x 256 slots, list the ones with work, shade the list) agree
+    with the oracle, on a black environment (misses dropped from the list), a constant
+    coloured one and a textured one (misses listed and shaded)."""
+    from ptsharp_amd import Colour
+    monkeypatch.setenv("PT_SHADE_FORM", form)
+    if name == "mesh":
+        s, c, smp = scenes.bunny_frame(4000, seed=9)
+    elif name == "textured":
+        s, c, smp = scenes.textured()
+    else:
+        s, c, smp = scenes.gopher3()
+        smp.MaxBounces = 4
+        if name == "gopher3_env":
+            s.Color = Colour(0.3, 0.5, 0.7)
+    g, gr, o, orr = render_both(s, c, smp, 64, 48, spp=2, passes=2, seed=41, engine=_abi.ENGINE_WAVEFRONT)
+    check(g, gr, o, orr)
