@@ -92,6 +92,9 @@ __device__ __forceinline__ uint32_t append(uint32_t* counter) {
 }
 
 constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that was not cast
+// Block-wide child-major fill (k_wf_shade) up to FirstHitSamples 16: ⌊√16⌋² strata × 2 modes.
+constexpr int kBlockMajorFH = 16;
+constexpr int kBlockMajorChildren = 32;
 constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera slot (k_wf_trace)
 #ifndef PT_SHADE_SCAN
 #define PT_SHADE_SCAN 8
@@ -115,8 +118,9 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t n, int lane) {  // inclus
 // returning atomic on one word saturates near 88 per µs on MI355X,
 // MI355X_MICROARCH.md "dequeue"; per-wave reservation made k_wf_shade wait on it).
 // Block-uniform call sites only.  Returns each lane's first slot in both queues.
+// Optionally also returns the block's first slot in both queues (blk_a, blk_b).
 __device__ __forceinline__ void block_reserve2(unsigned long long* word, uint32_t a, uint32_t b, uint32_t& abase,
-                                               uint32_t& bbase) {
+                                               uint32_t& bbase, uint32_t* blk_a = nullptr, uint32_t* blk_b = nullptr) {
     __shared__ uint32_t s_tot[2][4];
     __shared__ uint32_t s_base[2][4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -137,6 +141,7 @@ __device__ __forceinline__ void block_reserve2(unsigned long long* word, uint32_
         }
     }
     __syncthreads();
+    if (blk_a) { *blk_a = s_base[0][0]; *blk_b = s_base[1][0]; }
     abase = s_base[0][wid] + xa - a;
     bbase = s_base[1][wid] + xb - b;
 }
@@ -388,28 +393,40 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     const int ma = nm == 2 ? 1 : 0;
     const bool ext_on = depth + 1 <= smp.mb;   // deeper samples return black without an Intersect
     // child c: mode, reflect decision, liveness (p > 0 after the Any-mode override)
-    uint32_t n_ext = 0, n_nee = 0;
-    for (int c = 0; c < nch; c++) {
-        const int mode = ma + c % nm;
-        const bool refl = mode == 2 || (mode == 0 && draw(child_key(node, (uint32_t)c), D_REFLECT) < pv);
-        const bool live = mode == 0 || (refl ? pv > 0 : (1 - pv) > 0);
-        n_ext += (live && ext_on) ? 1u : 0u;
-        n_nee += (live && !refl && !m.transparent && nee_on) ? rays_per_nee : 0u;
-    }
-    uint32_t ebase, nbase;
-    block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase);
-    if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) Q.counts[kFlagWord] = 1;
-    // Child-major slots: the wave's reservation [ebase of lane 0, + the wave's total) is
-    // filled child index by child index, each live child c of the wave's lanes on
-    // consecutive slots (a ballot prefix).  A 64-ray batch of the next depth then holds the
-    // same stratum and mode of neighbouring camera samples (one direction quadrant, origins
-    // of a few pixels) rather than all children of one sample, and every store instruction
-    // writes whole lines.  Which children exist is unchanged, so is every child's key.
-    const int lane = threadIdx.x & 63;
+    // Block-wide child-major slots (below): each wave's count of child c's extension rays
+    // and NEE requests goes to LDS here, ahead of the reservation's barriers.
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t below = (1ull << lane) - 1ull;
-    uint32_t ej = __shfl(ebase, 0, 64), nj = __shfl(nbase, 0, 64);
     int cmax = nch;
     for (int off = 32; off > 0; off >>= 1) cmax = max(cmax, __shfl_xor(cmax, off, 64));
+    __shared__ uint32_t s_cc[kBlockMajorChildren][4][2];
+    const bool block_major = smp.fh <= kBlockMajorFH;   // kernel-uniform: every depth's children fit s_cc
+    uint32_t n_ext = 0, n_nee = 0;
+    for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
+        const int mode = ma + c % nm;
+        const bool refl = mode == 2 || (mode == 0 && c < nch && draw(child_key(node, (uint32_t)c), D_REFLECT) < pv);
+        const bool live = c < nch && (mode == 0 || (refl ? pv > 0 : (1 - pv) > 0));
+        const bool ee = live && ext_on, en = live && !refl && !m.transparent && nee_on;
+        n_ext += ee ? 1u : 0u;
+        n_nee += en ? rays_per_nee : 0u;
+        if (block_major) {
+            const uint64_t be = __ballot(ee), bn = __ballot(en);
+            if (lane == 0) { s_cc[c][wid][0] = (uint32_t)__popcll(be); s_cc[c][wid][1] = (uint32_t)__popcll(bn); }
+        }
+    }
+    if (block_major && lane >= cmax && lane < kBlockMajorChildren) { s_cc[lane][wid][0] = 0u; s_cc[lane][wid][1] = 0u; }
+    uint32_t ebase, nbase, blk_e, blk_n;
+    block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase, &blk_e, &blk_n);
+    if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) Q.counts[kFlagWord] = 1;
+    // Child-major slots: the block's reservation is filled child index by child index,
+    // child c of every lane of the block on consecutive slots (waves in order, a ballot
+    // prefix within each), then child c + 1.  A 64-ray batch of the next depth then holds
+    // the same stratum and mode of neighbouring camera samples (one direction quadrant,
+    // origins of a few pixels) rather than all children of one sample, the depth after it
+    // inherits runs of one stratum from 16 pixels, and every store instruction writes
+    // whole lines.  Which children exist is unchanged, so is every child's key.  With
+    // more children per vertex than s_cc holds, each wave fills its own share that way.
+    uint32_t ej = block_major ? blk_e : __shfl(ebase, 0, 64), nj = block_major ? blk_n : __shfl(nbase, 0, 64);
     for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
         const int mode = ma + c % nm;
         const uint64_t E = child_key(node, (uint32_t)c);
@@ -419,10 +436,19 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         const bool emit_nee = live && !reflected && nee_on;
         const bool emit_ext = live && ext_on;
         const uint64_t bn = __ballot(emit_nee), be = __ballot(emit_ext);
-        const uint32_t my_n = nj + (uint32_t)__popcll(bn & below) * rays_per_nee;
-        const uint32_t my_e = ej + (uint32_t)__popcll(be & below);
-        nj += (uint32_t)__popcll(bn) * rays_per_nee;
-        ej += (uint32_t)__popcll(be);
+        uint32_t pe = 0, pn = 0, te = (uint32_t)__popcll(be), tn = (uint32_t)__popcll(bn);
+        if (block_major) {   // waves before this one, and the whole block's total, at child c
+            te = tn = 0;
+            for (int w = 0; w < 4; w++) {
+                const uint32_t ce = s_cc[c][w][0], cn = s_cc[c][w][1];
+                if (w < wid) { pe += ce; pn += cn; }
+                te += ce; tn += cn;
+            }
+        }
+        const uint32_t my_n = nj + (pn + (uint32_t)__popcll(bn & below)) * rays_per_nee;
+        const uint32_t my_e = ej + pe + (uint32_t)__popcll(be & below);
+        nj += tn * rays_per_nee;
+        ej += te;
         if (!live) continue;
         const float fp = mode == 0 ? 1.0f : (float)(refl ? pv : 1 - pv);
         float w[3];
@@ -540,6 +566,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                 const bool listed = r + threadIdx.x < total;
                 shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + k0 + (listed ? (uint32_t)s_list[r + threadIdx.x] : 0u),
                                           listed, ctr);
+                __syncthreads();   // the next round rewrites shade_vertex's LDS child counts
             }
         }
     }
