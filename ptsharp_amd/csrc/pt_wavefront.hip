@@ -316,6 +316,172 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
     }
 }
 
+// Closest hit with per-lane refill (lean scenes: no §8f row 4 shapes).  k_wf_trace runs
+// 64 rays in lockstep until the longest is done: ~10 of 64 lanes are active per node
+// fetch, and every fetch instruction pays the texture-address unit's fixed cost.  Here
+// each lane keeps one ray in flight through ONE step loop: a step is one node (or leaf)
+// of the analytic BVH or of the triangle BVH (the same seven-load 128-B fetch), the
+// analytic phase hands over to the triangle phase at an empty stack, and a lane whose ray
+// is done takes the next one when PT_REFILL_IDLE lanes of the wave are idle (one claim
+// atomic per refill).  A new ray's head work is two queue loads and the planes (none in
+// C4), so a refill holds the busy lanes for one load round trip.  Same visit order,
+// same arithmetic as trace(): bit-identical hits.
+#ifndef PT_REFILL_IDLE
+#define PT_REFILL_IDLE 32
+#endif
+#ifndef PT_LANES_MIN_NODES
+#define PT_LANES_MIN_NODES 64
+#endif
+constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
+template <bool COUNT>
+__global__ __launch_bounds__(kTB, PT_TRACE_WAVES) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+    __shared__ uint32_t s_stack[kLdsStack * kTB];
+    const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
+    if (blockIdx.x == 0 && threadIdx.x < kParts) {
+        *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
+        Q.counts[fetch_word(1, threadIdx.x)] = 0u;               // k_wf_shade's fetch cursors
+    }
+    const Group G = xcd_group();
+    const uint32_t cnt = *ray_count(Q, qi, G.g);
+    const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
+    uint32_t* cursor = Q.counts + fetch_word(0, G.g);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
+    Counters ctr{0, 0, 0, 0};
+    const bool env_black = (!FULL_SHADE_ENV(S)) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
+    uint32_t kept = 0;
+    const float inf = __int_as_float(0x7f800000);
+    bool has = false, tri = false, more = true;
+    uint32_t i = 0, ref = 0;
+    int sp = 0;
+    v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
+    double bt = kHitInf;
+    int32_t bkind = -1, bidx = -1;
+    float tmax = 0.f;
+    auto finish = [&]() {
+        unsigned long long tb = (unsigned long long)__double_as_longlong(bt);
+        q_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
+        kept += (bkind >= 0 || !env_black) ? 1u : 0u;
+        has = false;
+    };
+    for (;;) {
+        const uint64_t idle = __ballot(!has);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (more && (nidle >= PT_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
+            uint32_t kc = 0;
+            if (lane == 0) kc = atomicAdd(cursor, nidle);
+            kc = __shfl(kc, 0, 64);
+            if (kc + nidle >= n) more = false;
+            const uint32_t k = kc + (uint32_t)__popcll(idle & below);
+            if (!has && k < n) {
+                i = base + k;
+                const float4 b = nt_load(&Q.q_d[qi][i]);
+                const float4 a = nt_load(&Q.q_o[qi][i]);
+                if (__float_as_uint(b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
+                    q_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
+                } else {
+                    has = true;
+                    ctr.rays++;
+                    o = v3{a.x, a.y, a.z};
+                    d = v3{b.x, b.y, b.z};
+                    invd = v3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                    bt = kHitInf; bkind = -1; bidx = -1;
+                    for (int p = 0; p < S.num_planes; p++) {   // Scene.Intersect order: planes, analytic BVH, triangles
+                        const float4 pa = S.planes[2 * p], pb = S.planes[2 * p + 1];
+                        const double t = isect_plane(v3{pa.x, pa.y, pa.z}, v3{pb.x, pb.y, pb.z}, o, d);
+                        if (t < bt) { bt = t; bkind = KIND_PLANE; bidx = p; }
+                    }
+                    tmax = tmax_bound(bt);
+                    sp = 0;
+                    ref = 0;
+                    tri = S.ana_num_nodes <= 0;
+                    if (tri && S.tri_num_nodes <= 0) finish();
+                }
+            }
+        }
+        if (!more && __ballot(has) == 0ull) break;
+        if (!has) continue;
+        // one step: inner node or leaf of the current BVH (seven 16-B loads)
+        const bool leaf = (ref & 0x80000000u) != 0;
+        const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
+                              : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
+        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6];
+        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
+        bool pop = true;
+        if (!leaf) {
+            if (COUNT) ctr.nodes++;
+            float k0 = slab1(q0.x, q1.x, q2.x, q3.x, q4.x, q5.x, o, invd, tmax);
+            float k1 = slab1(q0.y, q1.y, q2.y, q3.y, q4.y, q5.y, o, invd, tmax);
+            float k2 = slab1(q0.z, q1.z, q2.z, q3.z, q4.z, q5.z, o, invd, tmax);
+            float k3 = slab1(q0.w, q1.w, q2.w, q3.w, q4.w, q5.w, o, invd, tmax);
+            uint32_t v0 = __float_as_uint(q6.x), v1 = __float_as_uint(q6.y), v2 = __float_as_uint(q6.z),
+                     v3r = __float_as_uint(q6.w);
+            if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
+            if (v2 == kEmpty4) k2 = inf;
+            if (v3r == kEmpty4) k3 = inf;
+            cswap(k0, v0, k1, v1);
+            cswap(k2, v2, k3, v3r);
+            cswap(k0, v0, k2, v2);
+            cswap(k1, v1, k3, v3r);
+            cswap(k1, v1, k2, v2);
+            if (k0 != inf) {
+                push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
+                ref = v0;
+                pop = false;
+            }
+        } else if (tri) {
+            const uint32_t cntl = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q6.w);
+            v3 a0{q0.x, q0.y, q0.z}, a1{q0.w, q1.x, q1.y}, a2{q1.z, q1.w, q2.x};
+            v3 b0{q2.y, q2.z, q2.w}, b1{q3.x, q3.y, q3.z}, b2{q3.w, q4.x, q4.y};
+            const v3 c0{q4.z, q4.w, q5.x}, c1{q5.y, q5.z, q5.w}, c2{q6.x, q6.y, q6.z};
+#pragma unroll 1
+            for (uint32_t k = 0; k < cntl; k++) {
+                if (COUNT) ctr.prims++;
+                const double t = isect_tri(a0, a1, a2, o, d);
+                if (t < bt) {
+                    bt = t; bkind = KIND_TRI; bidx = (int32_t)(first + k);
+                    tmax = tmax_bound(t);
+                }
+                a0 = b0; a1 = b1; a2 = b2;
+                b0 = c0; b1 = c1; b2 = c2;
+            }
+        } else {
+            const uint32_t first = ref & 0x1FFFFFFFu, cntl = ((ref >> 29) & 3u) + 1u;
+            for (uint32_t k = 0; k < cntl; k++) {
+                if (COUNT) ctr.prims++;
+                int32_t kind;
+                const double t = prim_t<false, false>(S, S.ana_recs, first + k, o, d, kind);
+                if (t < bt) {
+                    bt = t; bkind = kind; bidx = (int32_t)(first + k);
+                    tmax = tmax_bound(t);
+                }
+            }
+        }
+        if (pop) {
+            if (sp > 0) {
+                sp--;
+                ref = stack.get(sp);
+            } else if (!tri && S.tri_num_nodes > 0) {
+                tri = true;
+                ref = 0;
+            } else {
+                finish();
+            }
+        }
+    }
+    uint32_t rays = wave_sum(ctr.rays);
+    if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
+    kept = wave_sum(kept);
+    if (lane == 0 && kept) atomicAdd(Q.counts + kept_word(qi), kept);
+    if (COUNT) {
+        uint32_t nodes = wave_sum(ctr.nodes), prims = wave_sum(ctr.prims);
+        if (lane == 0) {
+            atomicAdd(&counters[1], (unsigned long long)nodes);
+            atomicAdd(&counters[2], (unsigned long long)prims);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- shade / bounce
 #ifndef PT_SHADE_WAVES
 #define PT_SHADE_WAVES 3
@@ -731,13 +897,21 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     auto end_k = [&](int cls, hipStream_t s) { if (timer) timer->end(cls, s); };
     const bool full = S.full != 0;        // shade: textures or row-4 shapes
     const bool fullg = S.full_geom != 0;  // traversal: row-4 shapes only
+    // Per-lane refill closest-hit traversal (k_wf_trace_lanes) where rays are long enough
+    // to pay for it: scenes with a triangle BVH of more than kLanesMinNodes nodes
+    // (gopher3's five analytic shapes: trace 16.0 → 23.5 ms with refill).
+    const bool lanes = S.tri_num_nodes > kLanesMinNodes;
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
         const unsigned tg = grid_for(n, kTB, plan.trace_blocks);
         begin_k(1, stream);
         if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-        else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+#ifndef PT_NO_TRACE_LANES
+        else if (lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (lanes) hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+#endif
+        else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         end_k(1, stream);
     };
@@ -770,8 +944,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         const unsigned hg = grid_for(children * plan.lights_per_child, kTB, plan.shadow_blocks);
         begin_k(3, side);
         if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-        else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         end_k(3, side);
         if (plan.side) (void)hipEventRecord(plan.ev_side, side);

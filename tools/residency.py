@@ -9,7 +9,7 @@ import csv
 import glob
 import sys
 
-KERNELS = ("k_wf_trace<false, false>", "k_wf_shade<false, false, false>", "k_wf_shade<false, false, true>",
+KERNELS = ("k_wf_trace_lanes<false>", "k_wf_trace<false, false>", "k_wf_shade<false, false, false>", "k_wf_shade<false, false, true>",
            "k_wf_shadow<false, false>")
 
 
