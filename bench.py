@@ -91,10 +91,12 @@ def main():
     r._ensure_scene()
     st = r.Stats()
     build_ms, bvh_bytes = st.build_ms, st.bvh_bytes
-    # closest-hit kernel the library runs on this scene: per-lane refill (k_wf_trace_lanes)
-    # above 64 triangle-BVH nodes (pt_wavefront.hip kLanesMinNodes); the bench scene's
+    # closest-hit and shadow kernels the library runs on this scene: per-lane refill
+    # (k_wf_*_lanes) above 64 triangle-BVH nodes (pt_wavefront.hip kLanesMinNodes); the bench scene's
     # analytic BVH (floor cube, two light spheres) is one node
-    trace_name = "k_wf_trace_lanes<false>" if st.bvh_nodes - 1 > 64 else "k_wf_trace<false, false>"
+    lanes = st.bvh_nodes - 1 > 64
+    trace_name = "k_wf_trace_lanes<false>" if lanes else "k_wf_trace<false, false>"
+    shadow_name = "k_wf_shadow_lanes<false>" if lanes else "k_wf_shadow<false, false>"
 
     for _ in range(a.warmup):
         r.RenderParallel()
@@ -154,7 +156,7 @@ def main():
     # kernel names as rocprofv3 reports them (template arguments <COUNT, FULL>; the shade
     # class times both of its forms <COUNT, FULL, SCAN>, one of which returns at once; the
     # closest-hit class is k_wf_trace_lanes<COUNT> on triangle scenes)
-    names = ["k_wf_camera", trace_name, "k_wf_shade<false, false, *>", "k_wf_shadow<false, false>",
+    names = ["k_wf_camera", trace_name, "k_wf_shade<false, false, *>", shadow_name,
              "k_wf_finalize", "k_render_pass<false, false>"]
     # the closest-hit kernel is the dominant one by design (on a multi-GPU shard the shadow
     # passes run beside it on a second stream, so their event spans overlap it)

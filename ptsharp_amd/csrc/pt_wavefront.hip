@@ -791,6 +791,154 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
     }
 }
 
+// Shadow visibility with per-lane refill (triangle scenes; see k_wf_trace_lanes): the
+// light's own t and the planes at refill, then one step loop over the analytic BVH and
+// the triangle BVH, any-hit (a primitive strictly nearer than the light ends the ray
+// unlit).  A lit lane holds its colour until the wave's next refill (or the end) and the
+// wave adds all held colours with the run-aggregated acc_add_wave.
+template <bool COUNT>
+__global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+    __shared__ uint32_t s_stack[kLdsStack * kTB];
+    const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
+    const Group G = xcd_group();
+    const uint32_t cnt = *nee_count(Q, qo, G.g);
+    const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
+    uint32_t* cursor = Q.counts + fetch_word(2, G.g);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
+    Counters ctr{0, 0, 0, 0};
+    const float inf = __int_as_float(0x7f800000);
+    bool has = false, tri = false, more = true, phantom = false, pend = false;
+    uint32_t i = 0, ref = 0, pixel = 0;
+    int sp = 0;
+    v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
+    double tl = kHitInf;
+    float tmax = 0.f;
+    float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (;;) {
+        const uint64_t idle = __ballot(!has);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (more && (nidle >= PT_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
+            acc_add_wave(Q.acc, pixel, pend, pw.x, pw.y, pw.z);   // colours of the rays lit since the last refill
+            pend = false;
+            uint32_t kc = 0;
+            if (lane == 0) kc = atomicAdd(cursor, nidle);
+            kc = __shfl(kc, 0, 64);
+            if (kc + nidle >= n) more = false;
+            const uint32_t k = kc + (uint32_t)__popcll(idle & below);
+            if (!has && k < n) {
+                i = base + k;
+                const float4 b = nt_load(&Q.n_n[i]);
+                const float4 a = nt_load(&Q.n_o[i]);
+                const uint32_t li = __float_as_uint(b.w);
+                if (li != kDead) {   // light_visible (pt_device.h), head part
+                    ctr.rays++;
+                    const DevLight L = S.lights[li];
+                    o = v3{a.x, a.y, a.z};
+                    d = v3{b.x, b.y, b.z};
+                    pixel = __float_as_uint(a.w);
+                    invd = v3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                    phantom = L.phantom != 0;
+                    bool run;
+                    if (phantom) {
+                        tl = kHitInf;   // traced like the reference, never lit
+                        run = S.tri_num_nodes > 0;
+                        tri = true;
+                    } else {
+                        tl = light_t<false>(S, L, o, d);
+                        run = tl < kHitInf;
+                        for (int p = 0; run && p < S.num_planes; p++) {
+                            const float4 pa = S.planes[2 * p], pb = S.planes[2 * p + 1];
+                            if (isect_plane(v3{pa.x, pa.y, pa.z}, v3{pb.x, pb.y, pb.z}, o, d) < tl) run = false;
+                        }
+                        tri = S.ana_num_nodes <= 0;
+                    }
+                    tmax = tmax_bound(tl);
+                    sp = 0;
+                    ref = 0;
+                    has = run;
+                }
+            }
+        }
+        if (!more && __ballot(has) == 0ull) break;
+        if (!has) continue;
+        const bool leaf = (ref & 0x80000000u) != 0;
+        const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
+                              : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
+        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6];
+        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
+        bool pop = true, blocked = false;
+        if (!leaf) {
+            if (COUNT) ctr.nodes++;
+            float k0 = slab1(q0.x, q1.x, q2.x, q3.x, q4.x, q5.x, o, invd, tmax);
+            float k1 = slab1(q0.y, q1.y, q2.y, q3.y, q4.y, q5.y, o, invd, tmax);
+            float k2 = slab1(q0.z, q1.z, q2.z, q3.z, q4.z, q5.z, o, invd, tmax);
+            float k3 = slab1(q0.w, q1.w, q2.w, q3.w, q4.w, q5.w, o, invd, tmax);
+            uint32_t v0 = __float_as_uint(q6.x), v1 = __float_as_uint(q6.y), v2 = __float_as_uint(q6.z),
+                     v3r = __float_as_uint(q6.w);
+            if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
+            if (v2 == kEmpty4) k2 = inf;
+            if (v3r == kEmpty4) k3 = inf;
+            cswap(k0, v0, k1, v1);
+            cswap(k2, v2, k3, v3r);
+            cswap(k0, v0, k2, v2);
+            cswap(k1, v1, k3, v3r);
+            cswap(k1, v1, k2, v2);
+            if (k0 != inf) {
+                push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
+                ref = v0;
+                pop = false;
+            }
+        } else if (tri) {
+            const uint32_t cntl = ((ref >> 29) & 3u) + 1u;
+            v3 a0{q0.x, q0.y, q0.z}, a1{q0.w, q1.x, q1.y}, a2{q1.z, q1.w, q2.x};
+            v3 b0{q2.y, q2.z, q2.w}, b1{q3.x, q3.y, q3.z}, b2{q3.w, q4.x, q4.y};
+            const v3 c0{q4.z, q4.w, q5.x}, c1{q5.y, q5.z, q5.w}, c2{q6.x, q6.y, q6.z};
+#pragma unroll 1
+            for (uint32_t k = 0; k < cntl; k++) {
+                if (COUNT) ctr.prims++;
+                if (isect_tri(a0, a1, a2, o, d) < tl) { blocked = true; break; }
+                a0 = b0; a1 = b1; a2 = b2;
+                b0 = c0; b1 = c1; b2 = c2;
+            }
+        } else {
+            const uint32_t first = ref & 0x1FFFFFFFu, cntl = ((ref >> 29) & 3u) + 1u;
+            for (uint32_t k = 0; k < cntl; k++) {
+                if (COUNT) ctr.prims++;
+                int32_t kind;
+                if (prim_t<false, false>(S, S.ana_recs, first + k, o, d, kind) < tl) { blocked = true; break; }
+            }
+        }
+        if (blocked) {
+            has = false;
+        } else if (pop) {
+            if (sp > 0) {
+                sp--;
+                ref = stack.get(sp);
+            } else if (!tri && S.tri_num_nodes > 0) {
+                tri = true;
+                ref = 0;
+            } else {   // no primitive nearer than the light: lit (a phantom light never is)
+                has = false;
+                if (!phantom) {
+                    pw = nt_load(&Q.n_w[i]);
+                    pend = true;
+                }
+            }
+        }
+    }
+    acc_add_wave(Q.acc, pixel, pend, pw.x, pw.y, pw.z);
+    uint32_t rays = wave_sum(ctr.rays);
+    if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
+    if (COUNT) {
+        uint32_t nodes = wave_sum(ctr.nodes), prims = wave_sum(ctr.prims);
+        if (lane == 0) {
+            atomicAdd(&counters[5], (unsigned long long)nodes);
+            atomicAdd(&counters[6], (unsigned long long)prims);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- Welford
 __global__ __launch_bounds__(256) void k_wf_finalize(DevPass P, DevBuffer B, WfQueues Q, double inv_spp) {
     const uint32_t total = (uint32_t)P.num_tiles * 1024u;
@@ -897,8 +1045,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     auto end_k = [&](int cls, hipStream_t s) { if (timer) timer->end(cls, s); };
     const bool full = S.full != 0;        // shade: textures or row-4 shapes
     const bool fullg = S.full_geom != 0;  // traversal: row-4 shapes only
-    // Per-lane refill closest-hit traversal (k_wf_trace_lanes) where rays are long enough
-    // to pay for it: scenes with a triangle BVH of more than kLanesMinNodes nodes
+    // Per-lane refill traversal (k_wf_trace_lanes, k_wf_shadow_lanes) where rays are long
+    // enough to pay for it: scenes with a triangle BVH of more than kLanesMinNodes nodes
     // (gopher3's five analytic shapes: trace 16.0 → 23.5 ms with refill).
     const bool lanes = S.tri_num_nodes > kLanesMinNodes;
     const hipStream_t side = plan.side ? plan.side : stream;
@@ -945,6 +1093,10 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         begin_k(3, side);
         if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+#ifndef PT_NO_SHADOW_LANES
+        else if (lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (lanes) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+#endif
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         end_k(3, side);
