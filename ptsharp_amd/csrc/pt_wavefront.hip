@@ -333,6 +333,9 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 #define PT_LANES_MIN_NODES 64
 #endif
 constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
+#ifndef PT_SHADOW_REFILL_IDLE
+#define PT_SHADOW_REFILL_IDLE PT_REFILL_IDLE
+#endif
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_TRACE_WAVES) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
@@ -818,7 +821,7 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
     for (;;) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (more && (nidle >= PT_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
+        if (more && (nidle >= PT_SHADOW_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
             acc_add_wave(Q.acc, pixel, pend, pw.x, pw.y, pw.z);   // colours of the rays lit since the last refill
             pend = false;
             uint32_t kc = 0;
