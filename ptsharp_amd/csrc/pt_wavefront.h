@@ -72,6 +72,8 @@ struct WfPlan {
     uint32_t shadow_blocks;
     int32_t shade_form;        // k_wf_shade form: 0 chosen per depth from the kept count, 1 direct, 2 SCAN
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
+    int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always
+                               // (PT_LANES=0|1 in the environment; tests)
     // Optional second stream: each depth's shadow pass runs there, beside the next depth's
     // closest-hit pass (independent queues), so one fills the other's ramp and tail.
     // ev_main / ev_side order shade(d) → shadow(d) → shade(d + 1).  Null: one stream.

@@ -1051,7 +1051,7 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     // Per-lane refill traversal (k_wf_trace_lanes, k_wf_shadow_lanes) where rays are long
     // enough to pay for it: scenes with a triangle BVH of more than kLanesMinNodes nodes
     // (gopher3's five analytic shapes: trace 16.0 → 23.5 ms with refill).
-    const bool lanes = S.tri_num_nodes > kLanesMinNodes;
+    const bool lanes = plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes;
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
         const unsigned tg = grid_for(n, kTB, plan.trace_blocks);
