@@ -327,14 +327,14 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 // C4), so a refill holds the busy lanes for one load round trip.  Same visit order,
 // same arithmetic as trace(): bit-identical hits.
 #ifndef PT_REFILL_IDLE
-#define PT_REFILL_IDLE 32
+#define PT_REFILL_IDLE 40   // closest hit: 8 / 16 / 24 / 32 / 40 / 48 measured on C4, 40 best
 #endif
 #ifndef PT_LANES_MIN_NODES
 #define PT_LANES_MIN_NODES 64
 #endif
 constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
 #ifndef PT_SHADOW_REFILL_IDLE
-#define PT_SHADOW_REFILL_IDLE PT_REFILL_IDLE
+#define PT_SHADOW_REFILL_IDLE 32   // shadow: 16 / 24 / 32 / 48 measured, 32 best
 #endif
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_TRACE_WAVES) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
