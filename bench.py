@@ -11,8 +11,17 @@ GPU (torchrun), the image's 32x32 tiles are dealt round-robin to ranks, the
 scene is replicated, and the Welford Buffer is gathered onto rank 0 over RCCL
 at the end of the timed region (strong scaling: the image is fixed).
 
-Rank 0 prints one JSON line (driver contract), with `roofline` for
-k_render_pass and `cpu_baseline` (the oracle port timed on this host).
+Rank 0 prints one JSON line (driver contract), with `roofline` for the closest-hit
+kernel and `cpu_baseline` (the oracle port timed on this host).
+
+Roofline: the closest-hit kernel's algorithmic bytes (per ray: 112 B per
+BVH4 node fetch, 36 B per primitive test, 44 B ray in + hit out) over its HIP-event time,
+against the L2 bandwidth (≈34.5 TB/s, MI355X_MICROARCH.md §L2).  The BVH nodes and leaf
+chunks (79 MB at 1M triangles) live in L2 and the 256 MB Infinity Cache, so HBM is not the
+binding bound (the same bytes over 8 TB/s gave a fraction above 1 in round 1).  `traffic`
+is the measured L2↔fabric bytes per launch (rocprofv3 FETCH_SIZE×2 + WRITE_SIZE, which
+count Infinity-Cache hits too; profiles/pmc_traffic.json), set beside the compulsory bytes
+(every ray's queue entry read once, its hit written once, the traversal footprint once).
 """
 from __future__ import annotations
 
@@ -29,6 +38,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/s (rays×bounces/s) at 1920×1080×1024spp; PSNR vs C# ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2 (per-XCD L2s, aggregate)
 
 # Algorithmic bytes per unit: per ray 112 B per 4-wide BVH node
 # fetched (four child boxes of 24 B + four 4-B child refs), 36 B per primitive
@@ -118,8 +128,8 @@ def main():
     t0 = time.perf_counter()
     rays = 0
     kernel_ms = 0.0
-    kms = np.zeros(6)
-    klaunch = np.zeros(6, np.int64)
+    kms = np.zeros(_abi.K_SLOTS)
+    klaunch = np.zeros(_abi.K_SLOTS, np.int64)
     for _ in range(a.steps):
         r.RenderParallel()
         s = r.Stats()
@@ -157,7 +167,7 @@ def main():
     # class times both of its forms <COUNT, FULL, SCAN>, one of which returns at once; the
     # closest-hit class is k_wf_trace_lanes<COUNT> on triangle scenes)
     names = ["k_wf_camera", trace_name, "k_wf_shade<false, false, *>", shadow_name,
-             "k_wf_finalize", "k_render_pass<false, false>"]
+             "k_wf_finalize", "k_render_pass<false, false>", "k_wf_nee_accum", "-"]
     # the closest-hit kernel is the dominant one by design (on a multi-GPU shard the shadow
     # passes run beside it on a second stream, so their event spans overlap it)
     dom = _abi.K_TRACE if klaunch[_abi.K_TRACE] else int(np.argmax(kms))
@@ -173,13 +183,17 @@ def main():
     dom_bytes = per_ray * rays * frac_rays
     avg_launch_ms = kms[dom] / max(klaunch[dom], 1)
     achieved_gbs = dom_bytes / (kms[dom] * 1e-3) / 1e9
+    rays_per_launch = rays * frac_rays / max(klaunch[dom], 1)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             tj = json.load(f)
         if tj.get("kernel") == names[dom] and tj.get("workload_tris") == a.tris:
-            traffic = round(tj["traffic_bytes_per_ray"] * rays * frac_rays / max(klaunch[dom], 1))
+            traffic = round(tj["traffic_bytes_per_ray"] * rays_per_launch)
+    # compulsory bytes of one launch: each ray's queue entry (origin, direction: 32 B) read and its
+    # hit (16 B) written once, the traversal footprint (BVH nodes + leaf chunks) read once
+    compulsory = rays_per_launch * 48 + st.traversal_bytes
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -200,14 +214,21 @@ def main():
             "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
             "rays_per_camera_sample": round(total_rays / (W * H * a.spp * a.steps), 3),
             "shadow_ray_fraction": round(ctr.shadow_rays / max(ctr.rays, 1), 4),
+            "lit_shadow_rays_per_step": int(ctr.lit_shadow_rays), "accum_runs_per_step": int(ctr.accum_runs),
             "engine": a.engine, "scene_build_s": round(t_scene, 3), "bvh_build_ms": round(build_ms, 1),
             "bvh_bytes": int(bvh_bytes),
-            "kernel_ms_per_step": {names[k]: round(kms[k] / a.steps, 3) for k in range(6) if klaunch[k]},
+            "kernel_ms_per_step": {names[k]: round(kms[k] / a.steps, 3) for k in range(_abi.K_SLOTS) if klaunch[k]},
         },
         "roofline": {
-            "bound": "hbm", "kernel": names[dom],
-            "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "bound": "l2", "kernel": names[dom],
+            "achieved": round(achieved_gbs, 2), "peak": L2_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved_gbs / L2_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_kind": "L2-fabric bytes per launch (FETCH_SIZE x2 + WRITE_SIZE; Infinity-Cache hits included), "
+                            "profiles/pmc_traffic.json, same workload",
+            "compulsory_bytes_per_launch": round(compulsory),
+            "traffic_over_compulsory": None if traffic is None else round(traffic / compulsory, 3),
+            "traffic_frac_of_hbm_peak": None if traffic is None else
+            round(traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "avg_launch_ms": round(float(avg_launch_ms), 4), "launches": int(klaunch[dom]),
             "bytes_per_launch": round(dom_bytes / max(klaunch[dom], 1)),
             "bytes_per_ray": round(per_ray, 2),

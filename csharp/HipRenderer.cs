@@ -14,6 +14,7 @@
 using System;
 using System.Collections.Generic;
 using System.Runtime.InteropServices;
+using System.Threading.Tasks;
 using SkiaSharp;
 
 namespace PTSharpCore
@@ -133,8 +134,16 @@ namespace PTSharpCore
             public ulong rays, rays_total; public double last_pass_ms, total_ms;
             public ulong bvh_nodes, bvh_bytes; public double build_ms; public ulong passes;
             public ulong shadow_rays;
-            public fixed double kernel_ms[6];
-            public fixed uint kernel_launches[6];
+            public fixed double kernel_ms[8];       // PT_K_SLOTS
+            public fixed uint kernel_launches[8];
+            public ulong traversal_bytes;           // BVH nodes + leaf chunks (what traversal reads)
+        }
+
+        [StructLayout(LayoutKind.Sequential)]
+        public struct pt_trace_counters
+        {
+            public ulong rays, nodes_visited, prims_tested, shading_fetches, shadow_rays, shadow_nodes, shadow_prims;
+            public ulong lit_shadow_rays, accum_runs;
         }
 
         [StructLayout(LayoutKind.Sequential)]
@@ -145,14 +154,26 @@ namespace PTSharpCore
         }
 
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_get_version();
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_device_count(out int count);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_create(ref pt_device_opts opts, out IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_upload_scene(IntPtr ctx, ref pt_scene_desc scene);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_render_pass(IntPtr ctx, ref pt_camera cam, ref pt_sampler smp, ref pt_pass_params pass);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_render_pass_counted(IntPtr ctx, ref pt_camera cam, ref pt_sampler smp, ref pt_pass_params pass, out pt_trace_counters counters);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_synchronize(IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_read_buffer(IntPtr ctx, double[] m, double[] v, int[] n);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_write_buffer(IntPtr ctx, double[] m, double[] v, int[] n);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_reset_buffer(IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_stats_get(IntPtr ctx, out pt_stats stats);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern IntPtr pt_last_error();
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern void pt_destroy(IntPtr ctx);
+        // multi-GPU (include/ptsharp_hip.h "Multi-GPU"): one process per GPU (unique id + init per rank) or
+        // one process driving G contexts (init_all / gather_all)
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_unique_id(byte[] id128);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_init(IntPtr ctx, int nranks, int rank, byte[] id128);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_gather(IntPtr ctx, int root);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_destroy(IntPtr ctx);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_init_all(IntPtr[] ctxs, int n);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_gather_all(IntPtr[] ctxs, int n, int root);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl, CharSet = CharSet.Ansi)] public static extern int pt_obj_load(string path, out pt_mesh_data mesh);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern void pt_mesh_free(ref pt_mesh_data mesh);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern IntPtr pt_obj_last_error();
@@ -174,7 +195,10 @@ namespace PTSharpCore
         public int AdaptiveSamples = 0;           // Renderer.cs:23, phase at :340-410
         public int FireflySamples = 0;            // Renderer.cs:26, phase at :412-470
         public ulong Seed = 0;                     // Random.Shared is unseedable; this keys the GPU stream
-        IntPtr ctx;
+        /// <summary>32x32 tiles this renderer draws (tile id = ty * ceil(W/32) + tx); null = the whole
+        /// image.  A multi-GPU rank draws TilesForRank(W, H, rank, world) (SURVEY.md §8e).</summary>
+        public int[] Tiles = null;
+        internal IntPtr ctx;
         int W, H, pass;
         bool uploaded;
         readonly List<GCHandle> pins = new();
@@ -195,6 +219,17 @@ namespace PTSharpCore
         }
 
         IntPtr Pin(Array a) { var g = GCHandle.Alloc(a, GCHandleType.Pinned); pins.Add(g); return g.AddrOfPinnedObject(); }
+
+        /// <summary>Static interleaved tile ownership: tile t belongs to rank t % world.  Every pixel's
+        /// random stream is keyed by the pixel, so the union of the ranks' Buffers is the 1-GPU Buffer, bit
+        /// for bit (pt_comm_gather sums the disjoint tiles).</summary>
+        public static int[] TilesForRank(int w, int h, int rank, int world)
+        {
+            int n = ((w + 31) / 32) * ((h + 31) / 32);
+            var t = new List<int>();
+            for (int i = rank; i < n; i += world) t.Add(i);
+            return t.ToArray();
+        }
 
         // Flatten Scene.Shapes (Scene.cs:19) with a type switch; returns PT_ERR_UNSUPPORTED kinds as exceptions
         // so the caller can fall back to the CPU Renderer.
@@ -388,7 +423,33 @@ namespace PTSharpCore
             var pass = new PtHip.pt_pass_params { spp = SamplesPerPixel, stratified = StratifiedSampling ? 1 : 0,
                 seed = Seed, pass_index = (uint)(++this.pass), adaptive_samples = AdaptiveSamples,
                 firefly_samples = FireflySamples };
-            PtHip.Check(PtHip.pt_render_pass(ctx, ref cam, ref smp, ref pass), "pt_render_pass");
+            GCHandle tiles = default;
+            if (Tiles != null)
+            {
+                tiles = GCHandle.Alloc(Tiles, GCHandleType.Pinned);
+                pass.num_tiles = Tiles.Length; pass.tiles = tiles.AddrOfPinnedObject();
+            }
+            try { PtHip.Check(PtHip.pt_render_pass(ctx, ref cam, ref smp, ref pass), "pt_render_pass"); }
+            finally { if (tiles.IsAllocated) tiles.Free(); }
+        }
+
+        /// <summary>Resume: load a saved Buffer (e.g. Renderer.PBuffer of an earlier IterativeRender) into
+        /// the GPU's Welford state; later passes keep accumulating into it (Renderer.cs:702-765).  `passesDone`
+        /// continues the pass numbering the random streams are keyed by.</summary>
+        public void LoadBuffer(Buffer b, int passesDone)
+        {
+            int P = W * H;
+            var m = new double[3 * P]; var v = new double[3 * P]; var n = new int[P];
+            for (int y = 0; y < H; y++)
+                for (int x = 0; x < W; x++)
+                {
+                    int i = y * W + x; var px = b.Pixels[(x, y)];
+                    n[i] = px.Samples;
+                    m[3 * i] = px.M.r; m[3 * i + 1] = px.M.g; m[3 * i + 2] = px.M.b;
+                    v[3 * i] = px.V.r; v[3 * i + 1] = px.V.g; v[3 * i + 2] = px.V.b;
+                }
+            PtHip.Check(PtHip.pt_write_buffer(ctx, m, v, n), "pt_write_buffer");
+            pass = passesDone;
         }
 
         /// <summary>Copy the HBM Welford state into Renderer.PBuffer's Pixel objects (Buffer.cs:18-58).</summary>
@@ -423,6 +484,72 @@ namespace PTSharpCore
         }
 
         public void Dispose() { if (ctx != IntPtr.Zero) { PtHip.pt_destroy(ctx); ctx = IntPtr.Zero; } }
+    }
+
+    /// <summary>One .NET process driving G GPUs (the reference's Renderer is one process on all cores,
+    /// Renderer.cs:257-333): one HipRenderer per device drawing its interleaved tiles, one RCCL
+    /// communicator over the G contexts (pt_comm_init_all), passes issued from G host threads at once
+    /// (a firefly pass all-reduces its snapshot across the group), the Buffer gathered onto device 0
+    /// (pt_comm_gather_all) and copied into Renderer.PBuffer.</summary>
+    class HipRendererGroup : IDisposable
+    {
+        readonly HipRenderer[] parts;
+        readonly IntPtr[] ctxs;
+
+        HipRendererGroup(HipRenderer[] p)
+        {
+            parts = p;
+            ctxs = Array.ConvertAll(p, r => r.ctx);
+            PtHip.Check(PtHip.pt_comm_init_all(ctxs, ctxs.Length), "pt_comm_init_all");
+        }
+
+        public static HipRendererGroup NewRenderer(Scene scene, Camera camera, DefaultSampler sampler, int firstHitSamples,
+                                                   int maxBounces, int w, int h, int[] devices)
+        {
+            var p = new HipRenderer[devices.Length];
+            for (int i = 0; i < devices.Length; i++)
+            {
+                p[i] = HipRenderer.NewRenderer(scene, camera, sampler, firstHitSamples, maxBounces, w, h, devices[i]);
+                p[i].Tiles = HipRenderer.TilesForRank(w, h, i, devices.Length);
+            }
+            return new HipRendererGroup(p);
+        }
+
+        public int SamplesPerPixel { set { foreach (var r in parts) r.SamplesPerPixel = value; } }
+        public int AdaptiveSamples { set { foreach (var r in parts) r.AdaptiveSamples = value; } }
+        public int FireflySamples { set { foreach (var r in parts) r.FireflySamples = value; } }
+        public bool StratifiedSampling { set { foreach (var r in parts) r.StratifiedSampling = value; } }
+        public ulong Seed { set { foreach (var r in parts) r.Seed = value; } }
+
+        /// <summary>One RenderParallel pass on every GPU, one host thread per context.</summary>
+        public void RenderParallel() => Parallel.For(0, parts.Length, new ParallelOptions { MaxDegreeOfParallelism = parts.Length },
+                                                     i => parts[i].RenderParallel());
+
+        /// <summary>Sum the ranks' disjoint tiles onto device 0 and copy them into Renderer.PBuffer.</summary>
+        public void ReadBuffer()
+        {
+            // device 0 then holds every rank's tiles; its next pass clears the others' pixels again
+            // (ptsharp_hip.h "Multi-GPU"), so the gather can follow every pass
+            PtHip.Check(PtHip.pt_comm_gather_all(ctxs, ctxs.Length, 0), "pt_comm_gather_all");
+            parts[0].ReadBuffer();
+        }
+
+        public SKBitmap IterativeRender(string pathTemplate, int iter)
+        {
+            SKBitmap colour = null;
+            for (int i = 1; i <= iter; i++)
+            {
+                Console.WriteLine("Iteration " + i + " of " + iter);
+                RenderParallel();
+                ReadBuffer();
+                colour = Renderer.PBuffer.Image(Channel.ColorChannel);
+                using var stream = System.IO.File.OpenWrite(string.Format(pathTemplate, i));
+                colour.Encode(SKEncodedImageFormat.Png, 100).SaveTo(stream);
+            }
+            return colour;
+        }
+
+        public void Dispose() { foreach (var r in parts) r.Dispose(); }
     }
 
     /// <summary>OBJ.Load (OBJ.cs:11-165) parsed natively, same quirks; the Triangle[] is then

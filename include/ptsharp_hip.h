@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 3
+#define PT_ABI_VERSION 4
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -257,8 +257,10 @@ typedef struct pt_pass_params {
 /* Kernel classes reported by pt_stats.kernel_ms / kernel_launches. */
 typedef enum pt_kernel_class {
     PT_K_CAMERA = 0, PT_K_TRACE = 1, PT_K_SHADE = 2, PT_K_SHADOW = 3, PT_K_FINALIZE = 4, PT_K_MEGAKERNEL = 5,
-    PT_K_COUNT = 6
+    PT_K_ACCUM = 6,            /* k_wf_nee_accum: the visible shadow rays' light terms into the pixel sums */
+    PT_K_COUNT = 7
 } pt_kernel_class;
+#define PT_K_SLOTS 8           /* length of pt_stats.kernel_ms / kernel_launches */
 
 /* Both engines compute identical per-ray arithmetic; they differ in scheduling. */
 typedef enum pt_engine {
@@ -283,8 +285,9 @@ typedef struct pt_stats {
     double build_ms;         /* host BVH build time of the last upload        */
     uint64_t passes;
     uint64_t shadow_rays;    /* of `rays`: shadow-visibility queries (sampleLight)     */
-    double kernel_ms[6];     /* last pass, device time per pt_kernel_class (flag PT_PASS_KERNEL_TIMING) */
-    uint32_t kernel_launches[6];
+    double kernel_ms[PT_K_SLOTS];     /* last pass, device time per pt_kernel_class (flag PT_PASS_KERNEL_TIMING) */
+    uint32_t kernel_launches[PT_K_SLOTS];
+    uint64_t traversal_bytes; /* of bvh_bytes: BVH nodes + leaf chunks, what the traversal kernels read */
 } pt_stats;
 
 int pt_get_version(void);
@@ -297,6 +300,10 @@ int pt_synchronize(void* ctx);
 int pt_reset_buffer(void* ctx);
 /* Welford state of every pixel, row-major: M,V [H*W][3] (Colour, double), N [H*W]. */
 int pt_read_buffer(void* ctx, double* out_m, double* out_v, int32_t* out_n);
+/* Replace the Welford state (same layout; NULL leaves that array as it is): resume an
+ * IterativeRender from a saved Buffer (Renderer.cs:702-765 keeps accumulating into
+ * Renderer.PBuffer pass after pass; a checkpoint is that Buffer). */
+int pt_write_buffer(void* ctx, const double* m, const double* v, const int32_t* n);
 int pt_stats_get(void* ctx, pt_stats* out_stats);
 const char* pt_last_error(void);
 void pt_destroy(void* ctx);
@@ -318,13 +325,23 @@ const char* pt_obj_last_error(void);
 int pt_mesh_smooth_normals(int32_t n, const float* v1, const float* v2, const float* v3, float* n1, float* n2,
                            float* n3);
 
-/* Multi-GPU: one context per GPU (one process per GPU, or one thread per GPU).
- * Rank 0 creates the id, every rank joins, pt_comm_gather sums the disjoint
- * per-rank tile buffers into rank `root` (grouped RCCL send/recv over xGMI). */
+/* Multi-GPU: one context per GPU.  Each context renders its tile list
+ * (pt_pass_params.tiles), and pt_comm_gather sums the disjoint per-rank tile buffers into
+ * rank `root` (RCCL reduce over xGMI).  Two ways to form the communicator:
+ *   - one process per GPU: rank 0 makes the id (pt_comm_unique_id), ships it to the other
+ *     processes, and every rank calls pt_comm_init (it blocks until all ranks joined);
+ *   - one process driving G GPUs (the .NET host): G contexts on G devices, joined by ONE
+ *     call pt_comm_init_all from any thread, gathered by pt_comm_gather_all.  Render the G
+ *     contexts from G host threads at once (one thread per context): a pass with
+ *     firefly_samples > 0 all-reduces the firefly snapshot across the group.
+ * After a gather, root's pt_read_buffer returns the whole frame; root's next pass first
+ * clears the pixels outside its own tiles again, so gathers can repeat every pass. */
 int pt_comm_unique_id(uint8_t out_id[128]);
 int pt_comm_init(void* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 int pt_comm_gather(void* ctx, int32_t root);
 int pt_comm_destroy(void* ctx);
+int pt_comm_init_all(void* const* ctxs, int32_t n);            /* ncclCommInitAll over the contexts' devices */
+int pt_comm_gather_all(void* const* ctxs, int32_t n, int32_t root);   /* the group's gathers, issued together */
 
 /* Instrumentation (bench / roofline): last pass' traversal counters, summed. */
 typedef struct pt_trace_counters {
@@ -335,6 +352,8 @@ typedef struct pt_trace_counters {
     uint64_t shadow_rays;     /* the shadow-visibility part of the above ...   */
     uint64_t shadow_nodes;
     uint64_t shadow_prims;
+    uint64_t lit_shadow_rays; /* shadow rays whose light was the nearest hit (terms added)   */
+    uint64_t accum_runs;      /* their per-pixel runs after wave aggregation (atomic sets)  */
 } pt_trace_counters;
 int pt_render_pass_counted(void* ctx, const pt_camera* camera, const pt_sampler* sampler,
                            const pt_pass_params* pass, pt_trace_counters* out);

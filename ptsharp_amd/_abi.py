@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptsharp_hip.so")
 
-ABI_VERSION = 3   # PT_ABI_VERSION
+ABI_VERSION = 4   # PT_ABI_VERSION
 PT_OK = 0
 PT_ERR_INVALID_ARG = -1
 PT_ERR_HIP = -2
@@ -24,7 +24,8 @@ PT_ERR_NO_DEVICE = -7
 
 ENGINE_AUTO, ENGINE_MEGAKERNEL, ENGINE_WAVEFRONT = 0, 1, 2
 PASS_KERNEL_TIMING = 1
-K_CAMERA, K_TRACE, K_SHADE, K_SHADOW, K_FINALIZE, K_MEGAKERNEL = range(6)
+K_CAMERA, K_TRACE, K_SHADE, K_SHADOW, K_FINALIZE, K_MEGAKERNEL, K_ACCUM = range(7)
+K_SLOTS = 8   # PT_K_SLOTS
 
 SHAPE_SPHERE, SHAPE_CUBE, SHAPE_PLANE, SHAPE_TRIANGLE, SHAPE_MESH = 0, 1, 2, 3, 4
 SHAPE_SDF, SHAPE_VOLUME, SHAPE_TRANSFORMED = 5, 6, 7
@@ -115,13 +116,14 @@ class pt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("rays_total", C.c_uint64), ("last_pass_ms", C.c_double),
                 ("total_ms", C.c_double), ("bvh_nodes", C.c_uint64), ("bvh_bytes", C.c_uint64),
                 ("build_ms", C.c_double), ("passes", C.c_uint64), ("shadow_rays", C.c_uint64),
-                ("kernel_ms", C.c_double * 6), ("kernel_launches", C.c_uint32 * 6)]
+                ("kernel_ms", C.c_double * K_SLOTS), ("kernel_launches", C.c_uint32 * K_SLOTS),
+                ("traversal_bytes", C.c_uint64)]
 
 
 class pt_trace_counters(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("nodes_visited", C.c_uint64), ("prims_tested", C.c_uint64),
                 ("shading_fetches", C.c_uint64), ("shadow_rays", C.c_uint64), ("shadow_nodes", C.c_uint64),
-                ("shadow_prims", C.c_uint64)]
+                ("shadow_prims", C.c_uint64), ("lit_shadow_rays", C.c_uint64), ("accum_runs", C.c_uint64)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/ptsharp_hip.h
@@ -142,6 +144,7 @@ SIGNATURES = {
     "pt_synchronize": (C.c_int, [C.c_void_p]),
     "pt_reset_buffer": (C.c_int, [C.c_void_p]),
     "pt_read_buffer": (C.c_int, [C.c_void_p, _d, _d, _i]),
+    "pt_write_buffer": (C.c_int, [C.c_void_p, _d, _d, _i]),
     "pt_stats_get": (C.c_int, [C.c_void_p, C.POINTER(pt_stats)]),
     "pt_last_error": (C.c_char_p, []),
     "pt_destroy": (None, [C.c_void_p]),
@@ -149,6 +152,8 @@ SIGNATURES = {
     "pt_comm_init": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]),
     "pt_comm_gather": (C.c_int, [C.c_void_p, C.c_int32]),
     "pt_comm_destroy": (C.c_int, [C.c_void_p]),
+    "pt_comm_init_all": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32]),
+    "pt_comm_gather_all": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32]),
     "pt_render_pass_counted": (C.c_int, [C.c_void_p, C.POINTER(pt_camera), C.POINTER(pt_sampler),
                                          C.POINTER(pt_pass_params), C.POINTER(pt_trace_counters)]),
     "pt_obj_load": (C.c_int, [C.c_char_p, C.POINTER(pt_mesh_data)]),

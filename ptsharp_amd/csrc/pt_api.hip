@@ -30,6 +30,19 @@
 #pragma clang fp contract(off)
 
 namespace pt {
+// After a gather the root's Buffer holds every rank's tiles; before its next pass adds to
+// its own tiles (and before a firefly snapshot is all-reduced) the other ranks' pixels are
+// cleared again, so every context's Buffer holds exactly its own tiles between gathers.
+__global__ __launch_bounds__(256) void k_clear_foreign(DevBuffer B, int32_t width, int32_t height, int32_t tiles_x,
+                                                       const uint8_t* own) {
+    const size_t P = (size_t)width * (size_t)height;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (size_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % (size_t)width), y = (int)(i / (size_t)width);
+        if (own[(y >> 5) * tiles_x + (x >> 5)]) continue;
+        B.n[i] = 0;
+        for (int k = 0; k < 3; k++) { B.m[3 * i + k] = 0.0; B.v[3 * i + k] = 0.0; }
+    }
+}
 hipError_t launch_render_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                               const DevBuffer& B, int num_tiles, bool count, hipStream_t stream);
 }
@@ -113,15 +126,20 @@ struct Ctx {
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    bool gathered = false;          // root of a gather: other ranks' tiles are in the Buffer until the next pass
+    uint8_t* d_own = nullptr;       // [tiles] 1 = a tile of this context's last tile list
     // wavefront queues (allocated on first use, grown on demand)
     pt::WfQueues Q{};
     std::vector<DeviceArray> wf_arrays;
     uint32_t wf_cap = 0, wf_scap = 0;
     uint32_t wf_max_cap = 0;       // queue capacity bound (wf_max_cap()), once per context
     // adaptive / firefly phases (allocated on first use, with the queues)
-    uint32_t* d_plist = nullptr;   // [P] firefly candidates
-    uint32_t* d_fcount = nullptr;
+    uint32_t* d_plist = nullptr;   // [P] firefly candidates (ping-pong with d_plist2 over the rounds)
+    uint32_t* d_plist2 = nullptr;
+    uint32_t* d_fcount = nullptr;  // [2] list lengths
     double* d_snap = nullptr;      // [P][3] M at the start of the firefly phase
+    pt::FixAcc acc_s{};            // [acc_s_cap] per-sample accumulators (own allocation; Q.acc_s points at it)
+    uint64_t acc_s_cap = 0;
     int last_engine = 0;
     pt::WfPlan grids{};            // persistent grid sizes (pt::wavefront_grids), once per context
     EventTimer timer;
@@ -131,8 +149,8 @@ struct Ctx {
 // samples whose widest depth fits the queues; every chunk pays the fill and drain of
 // 16 persistent launches, so fewer, larger chunks are faster (C4, 16 spp per pass: 8
 // chunks of 32M-entry queues 2574 Mrays/s, 2 chunks 2809, one chunk 2853).  The bound is
-// the largest power of two whose queues (176 B per entry: two extension queues of
-// o, d, throughput, key + hits + one shadow queue) fit a quarter of the device's memory
+// the largest power of two whose queues (208 B per entry: two extension queues of
+// o, d, throughput r g, key + throughput b + hits + one shadow queue) fit a quarter of the device's memory
 // and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
 // MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
@@ -140,7 +158,7 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #define PT_SIDE_MAX_CHUNK (20u << 20)
 #endif
 constexpr uint64_t kSideStreamMaxChunk = PT_SIDE_MAX_CHUNK;   // camera samples
-constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 8) + 16 + 48;
+constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 64 + 1;
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
 uint32_t wf_max_cap(Ctx* c) {
@@ -166,8 +184,12 @@ void free_wavefront(Ctx* c) {
     c->Q = pt::WfQueues{};
     c->wf_cap = c->wf_scap = 0;
     c->d_plist = nullptr;
+    c->d_plist2 = nullptr;
     c->d_fcount = nullptr;
     c->d_snap = nullptr;
+    if (c->acc_s.w) { (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.big); }
+    c->acc_s = pt::FixAcc{};
+    c->acc_s_cap = 0;
 }
 
 template <class T>
@@ -182,7 +204,7 @@ int wf_alloc(Ctx* c, T** out, size_t n) {
 }
 
 int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
-    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc) return PT_OK;
+    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w) return PT_OK;
     cap = std::max(cap, c->wf_cap);
     scap = std::max(scap, c->wf_scap);
     free_wavefront(c);
@@ -197,12 +219,19 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
     if ((rc = wf_alloc(c, &Q.hits, cap))) return rc;
     if ((rc = wf_alloc(c, &Q.n_o, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.n_n, scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.n_w, scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.n_w, 2 * (size_t)scap))) return rc;
+    if ((rc = wf_alloc(c, &Q.n_lit, scap))) return rc;
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
-    if ((rc = wf_alloc(c, &Q.ovf, (size_t)(pt::kMaxDepth - pt::kLdsStack) * pt::kWfMaxThreads))) return rc;
+    // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
+    // can run at the same time on the side stream)
+    const size_t ovf_words = (size_t)(pt::kMaxDepth - pt::kLdsStack) * pt::kWfMaxThreads;
+    if ((rc = wf_alloc(c, &Q.ovf, 2 * ovf_words))) return rc;
+    Q.ovf_sh = Q.ovf + ovf_words;
     size_t P = (size_t)c->width * (size_t)c->height;
-    if ((rc = wf_alloc(c, &Q.acc, P * 3))) return rc;
-    PT_HIP(hipMemsetAsync(Q.acc, 0, P * 3 * sizeof(double), c->stream));
+    if ((rc = wf_alloc(c, &Q.acc.w, P * pt::kFixWords))) return rc;
+    if ((rc = wf_alloc(c, &Q.acc.big, P * 3))) return rc;
+    PT_HIP(hipMemsetAsync(Q.acc.w, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
+    PT_HIP(hipMemsetAsync(Q.acc.big, 0, P * 3 * sizeof(double), c->stream));
     PT_HIP(hipMemsetAsync(Q.counts, 0, pt::kCountWords * sizeof(uint32_t), c->stream));
     Q.cap = cap;
     Q.s_cap = scap;
@@ -214,17 +243,31 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
     return PT_OK;
 }
 
-// Buffers of the adaptive / firefly phases: per-sample accumulators for one
-// queue's worth of camera samples, the candidate list and the M snapshot.
-int ensure_extra(Ctx* c) {
-    if (c->Q.acc_s) return PT_OK;
+// Buffers of the adaptive / firefly phases: per-sample accumulators for one chunk
+// of camera samples, the candidate list and the M snapshot.
+int ensure_extra(Ctx* c, uint64_t chunk) {
+    if (c->acc_s.w && c->acc_s_cap >= chunk) { c->Q.acc_s = c->acc_s; return PT_OK; }
     int rc;
     const size_t P = (size_t)c->width * (size_t)c->height;
-    if ((rc = wf_alloc(c, &c->Q.acc_s, (size_t)c->wf_cap * 3))) return rc;
-    if ((rc = wf_alloc(c, &c->d_plist, P))) return rc;
-    if ((rc = wf_alloc(c, &c->d_fcount, 1))) return rc;
-    if ((rc = wf_alloc(c, &c->d_snap, P * 3))) return rc;
-    PT_HIP(hipMemsetAsync(c->Q.acc_s, 0, (size_t)c->wf_cap * 3 * sizeof(double), c->stream));
+    if (!c->d_plist) {
+        if ((rc = wf_alloc(c, &c->d_plist, P))) return rc;
+        if ((rc = wf_alloc(c, &c->d_plist2, P))) return rc;
+        if ((rc = wf_alloc(c, &c->d_fcount, 2))) return rc;
+        if ((rc = wf_alloc(c, &c->d_snap, P * 3))) return rc;
+    }
+    if (c->acc_s.w) { (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.big); c->acc_s = pt::FixAcc{}; c->acc_s_cap = 0; }
+    c->Q.acc_s = pt::FixAcc{};
+    if (hipMalloc(&c->acc_s.w, chunk * pt::kFixWords * sizeof(unsigned long long)) != hipSuccess)
+        return fail(PT_ERR_OUT_OF_MEMORY, "hipMalloc per-sample accumulators");
+    if (hipMalloc(&c->acc_s.big, chunk * 3 * sizeof(double)) != hipSuccess) {
+        (void)hipFree(c->acc_s.w);
+        c->acc_s = pt::FixAcc{};
+        return fail(PT_ERR_OUT_OF_MEMORY, "hipMalloc per-sample accumulators");
+    }
+    c->acc_s_cap = chunk;
+    PT_HIP(hipMemsetAsync(c->acc_s.w, 0, chunk * pt::kFixWords * sizeof(unsigned long long), c->stream));
+    PT_HIP(hipMemsetAsync(c->acc_s.big, 0, chunk * 3 * sizeof(double), c->stream));
+    c->Q.acc_s = c->acc_s;
     return PT_OK;
 }
 
@@ -560,7 +603,7 @@ int pt_create(const pt_device_opts* opts, void** out_ctx) {
     size_t P = (size_t)c->width * (size_t)c->height;
     if (hipMalloc(&c->d_m, P * 3 * sizeof(double)) != hipSuccess || hipMalloc(&c->d_v, P * 3 * sizeof(double)) != hipSuccess ||
         hipMalloc(&c->d_n, P * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess)
+        hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess)
         return cleanup(fail(PT_ERR_OUT_OF_MEMORY, "buffer allocation"));
     int rc = pt_reset_buffer(c);
     if (rc != PT_OK) return cleanup(rc);
@@ -596,9 +639,9 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     for (int i = 0; i < d->num_materials; i++) {
         const pt_material& m = d->materials[i];
         pt::DevMaterial& o = mats[(size_t)i];
-        for (int k = 0; k < 3; k++) o.color[k] = (float)m.color[k];
-        o.emittance = (float)m.emittance;
-        o.tint = (float)m.tint;
+        for (int k = 0; k < 3; k++) o.color[k] = m.color[k];
+        o.emittance = m.emittance;
+        o.tint = m.tint;
         o.transparent = m.transparent;
         o.index = m.index;
         o.gloss = m.gloss;
@@ -634,7 +677,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
 
     // --- §8f row 4 tables: SDF programs, volumes, transformed shapes
     mats.push_back(pt::DevMaterial{});   // `new Material()` (Volume.MaterialAt's fallback)
-    for (auto& m : mats.back().color) m = 0.f;
+    for (auto& m : mats.back().color) m = 0.0;
     mats.back().tex = mats.back().ntex = mats.back().btex = mats.back().gtex = -1;
     const int32_t default_mat = d->num_materials;
     SdfCompiler sdfc{d};
@@ -988,11 +1031,12 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     S.ana_num_nodes = ana_num_nodes;
     S.num_planes = (int32_t)plane_scene.size();
     S.num_lights = (int32_t)lights.size();
-    for (int k = 0; k < 3; k++) S.env[k] = (float)d->env_color[k];
+    for (int k = 0; k < 3; k++) S.env[k] = d->env_color[k];
     PT_HIP(hipStreamSynchronize(c->stream));
     c->S = S;
     c->has_scene = true;
     c->stats.bvh_nodes = (uint64_t)tri_num_nodes + (uint64_t)ana_num_nodes;
+    c->stats.traversal_bytes = (tri_nodes.size() + tri_chunks.size() + ana_nodes.size() + ana_recs.size()) * sizeof(float4);
     c->stats.bvh_bytes = (tri_nodes.size() + tri_chunks.size() + ana_nodes.size()) * sizeof(float4) +
                          (tri_sh.size() + ana_recs.size()) * sizeof(float4);
     c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1080,7 +1124,10 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         // chunk is small enough for the launches' fill and drain to matter (one rank's
         // share of a multi-GPU frame: +6.5 % at 1/8 of C4); a full C4 frame runs 0.3 %
         // slower that way, so it keeps one stream.
-        if (chunk <= kSideStreamMaxChunk) {
+        // PT_SIDE_STREAM=0|1 (environment; tests) forces one stream or the side stream.
+        bool side = chunk <= kSideStreamMaxChunk;
+        if (const char* f = std::getenv("PT_SIDE_STREAM")) side = !std::strcmp(f, "1") ? true : !std::strcmp(f, "0") ? false : side;
+        if (side) {
             plan.side = c->side;
             plan.ev_main = c->ev_main;
             plan.ev_side = c->ev_side;
@@ -1092,14 +1139,28 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         uint32_t cap = pcap * pt::kParts, scap = spcap * pt::kParts;
         int rc = ensure_wavefront(c, cap, scap);
         if (rc) return rc;
-        if (extra && (uint64_t)std::max(pass->adaptive_samples, pass->firefly_samples) > chunk)
-            return fail(PT_ERR_UNSUPPORTED, "adaptive / firefly samples exceed one wavefront chunk");
-        if (extra && (rc = ensure_extra(c))) return rc;
+        if ((uint64_t)pass->adaptive_samples > chunk)
+            return fail(PT_ERR_UNSUPPORTED, "adaptive samples exceed one wavefront chunk");
+        if (extra && (rc = ensure_extra(c, chunk))) return rc;
     }
     c->last_engine = engine;
+    if (c->gathered) {
+        c->gathered = false;
+        if (pass->num_tiles > 0) {
+            const int ntiles = tiles_x * tiles_y;
+            std::vector<uint8_t> own((size_t)ntiles, 0);
+            for (int i = 0; i < pass->num_tiles; i++) own[(size_t)pass->tiles[i]] = 1;
+            if (!c->d_own) PT_HIP(hipMalloc(&c->d_own, (size_t)ntiles));
+            PT_HIP(hipMemcpyAsync(c->d_own, own.data(), (size_t)ntiles, hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(pt::k_clear_foreign, dim3(2048), dim3(256), 0, c->stream, B, c->width, c->height, tiles_x,
+                               (const uint8_t*)c->d_own);
+            PT_HIP(hipGetLastError());
+            PT_HIP(hipStreamSynchronize(c->stream));   // `own` is a host temporary
+        }
+    }
     const bool timing = (pass->flags & PT_PASS_KERNEL_TIMING) != 0;
     c->timer.reset(c->stream);
-    PT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    PT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (engine == PT_ENGINE_WAVEFRONT)
         PT_HIP(hipMemsetAsync(c->Q.counts + pt::kFlagWord, 0, sizeof(uint32_t), c->stream));
     PT_HIP(hipEventRecord(c->ev0, c->stream));
@@ -1108,7 +1169,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm));
         if (pass->adaptive_samples > 0)  // Renderer.cs:340-410
             PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm, 0,
-                                       pass->adaptive_samples, (uint64_t)num_tiles * 1024u, nullptr, nullptr));
+                                       pass->adaptive_samples, pt::kAdaptiveSampleBase, (uint64_t)num_tiles * 1024u,
+                                       nullptr, nullptr, nullptr, nullptr));
         if (pass->firefly_samples > 0) {  // Renderer.cs:412-470
             PT_HIP(pt::firefly_select(P, B, c->d_plist, c->d_fcount, c->stream));
             uint32_t nsel = 0;
@@ -1121,8 +1183,20 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
                 if (r != ncclSuccess) return fail(PT_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
             }
             PT_HIP(hipStreamSynchronize(c->stream));
-            PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm, 1,
-                                       pass->firefly_samples, nsel, c->d_plist, c->d_snap));
+            // Renderer.cs:430-445 traces a candidate's samples one after another and stops at the first
+            // IsFirefly sample: rounds of one sample per still-active pixel, so exactly those samples are
+            // traced (and counted in Scene.rays), no more.
+            uint32_t* list = c->d_plist;
+            uint32_t* next = c->d_plist2;
+            for (int j = 0; j < pass->firefly_samples && nsel > 0; j++) {
+                PT_HIP(hipMemsetAsync(c->d_fcount + 1, 0, sizeof(uint32_t), c->stream));
+                PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm, 1, 1,
+                                           pt::kFireflySampleBase + (uint32_t)j, nsel, list, c->d_snap, next,
+                                           c->d_fcount + 1));
+                PT_HIP(hipMemcpyAsync(&nsel, c->d_fcount + 1, sizeof nsel, hipMemcpyDeviceToHost, c->stream));
+                PT_HIP(hipStreamSynchronize(c->stream));
+                std::swap(list, next);
+            }
         }
     } else {
         if (timing) c->timer.begin(PT_K_MEGAKERNEL, c->stream);
@@ -1131,7 +1205,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     }
     PT_HIP(hipEventRecord(c->ev1, c->stream));
     if (c->timer.failed) return fail(PT_ERR_HIP, "hipEventRecord (kernel timing) failed");
-    unsigned long long ctr[8];
+    unsigned long long ctr[16];
     PT_HIP(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
     if (engine == PT_ENGINE_WAVEFRONT) {
@@ -1149,7 +1223,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     c->stats.last_pass_ms = ms;
     c->stats.total_ms += ms;
     c->stats.passes++;
-    for (int k = 0; k < PT_K_COUNT; k++) { c->stats.kernel_ms[k] = 0.0; c->stats.kernel_launches[k] = 0; }
+    for (int k = 0; k < PT_K_SLOTS; k++) { c->stats.kernel_ms[k] = 0.0; c->stats.kernel_launches[k] = 0; }
     if (timing) PT_HIP(c->timer.collect(c->stats.kernel_ms, c->stats.kernel_launches));
     if (counted) {
         counted->rays = rays;
@@ -1159,6 +1233,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         counted->shadow_rays = ctr[4];
         counted->shadow_nodes = ctr[5];
         counted->shadow_prims = ctr[6];
+        counted->lit_shadow_rays = ctr[7];
+        counted->accum_runs = ctr[8];
     }
     return PT_OK;
 }
@@ -1193,6 +1269,18 @@ int pt_read_buffer(void* ctx, double* out_m, double* out_v, int32_t* out_n) {
     return PT_OK;
 }
 
+int pt_write_buffer(void* ctx, const double* m, const double* v, const int32_t* n) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c) return fail(PT_ERR_INVALID_ARG, "ctx is NULL");
+    PT_HIP(hipSetDevice(c->device));
+    size_t P = (size_t)c->width * (size_t)c->height;
+    if (m) PT_HIP(hipMemcpyAsync(c->d_m, m, P * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (v) PT_HIP(hipMemcpyAsync(c->d_v, v, P * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (n) PT_HIP(hipMemcpyAsync(c->d_n, n, P * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    PT_HIP(hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
 int pt_stats_get(void* ctx, pt_stats* out) {
     Ctx* c = (Ctx*)ctx;
     if (!c || !out) return fail(PT_ERR_INVALID_ARG, "NULL argument");
@@ -1213,6 +1301,7 @@ void pt_destroy(void* ctx) {
     if (c->d_n) (void)hipFree(c->d_n);
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_tiles) (void)hipFree(c->d_tiles);
+    if (c->d_own) (void)hipFree(c->d_own);
     c->timer.destroy();
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->ev_side) (void)hipEventDestroy(c->ev_side);
@@ -1265,6 +1354,66 @@ int pt_comm_gather(void* ctx, int32_t root) {
     if (r != ncclSuccess || r2 != ncclSuccess)
         return fail(PT_ERR_RCCL, std::string("ncclReduce: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
     PT_HIP(hipStreamSynchronize(c->stream));
+    if (c->rank == root) c->gathered = true;
+    return PT_OK;
+}
+
+// One communicator over G contexts of this process (one per device), formed by one call:
+// the single-process multi-GPU form a .NET host uses.
+int pt_comm_init_all(void* const* ctxs, int32_t n) {
+    if (!ctxs || n < 1) return fail(PT_ERR_INVALID_ARG, "bad context list");
+    std::vector<int> devs((size_t)n);
+    for (int i = 0; i < n; i++) {
+        Ctx* c = (Ctx*)ctxs[i];
+        if (!c) return fail(PT_ERR_INVALID_ARG, "NULL context in the list");
+        for (int j = 0; j < i; j++)
+            if (((Ctx*)ctxs[j])->device == c->device) return fail(PT_ERR_INVALID_ARG, "two contexts on one device");
+        devs[(size_t)i] = c->device;
+    }
+    for (int i = 0; i < n; i++) {
+        Ctx* c = (Ctx*)ctxs[i];
+        if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    }
+    std::vector<ncclComm_t> comms((size_t)n, nullptr);
+    ncclResult_t r = ncclCommInitAll(comms.data(), n, devs.data());
+    if (r != ncclSuccess) return fail(PT_ERR_RCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    for (int i = 0; i < n; i++) {
+        Ctx* c = (Ctx*)ctxs[i];
+        c->comm = comms[(size_t)i];
+        c->nranks = n;
+        c->rank = i;
+    }
+    return PT_OK;
+}
+
+// The group's gathers issued from one thread inside one RCCL group (each context's
+// reduce on its own stream), then every stream synchronised.
+int pt_comm_gather_all(void* const* ctxs, int32_t n, int32_t root) {
+    if (!ctxs || n < 1) return fail(PT_ERR_INVALID_ARG, "bad context list");
+    if (root < 0 || root >= n) return fail(PT_ERR_INVALID_ARG, "root out of range");
+    for (int i = 0; i < n; i++) {
+        Ctx* c = (Ctx*)ctxs[i];
+        if (!c || !c->comm || c->nranks != n || c->rank != i)
+            return fail(PT_ERR_RCCL, "contexts are not the group pt_comm_init_all formed (in that order)");
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; i < n && r == ncclSuccess; i++) {
+        Ctx* c = (Ctx*)ctxs[i];
+        if (hipSetDevice(c->device) != hipSuccess) { r = ncclInvalidUsage; break; }
+        const size_t P = (size_t)c->width * (size_t)c->height;
+        r = ncclReduce(c->d_m, c->d_m, P * 3, ncclFloat64, ncclSum, root, c->comm, c->stream);
+        if (r == ncclSuccess) r = ncclReduce(c->d_v, c->d_v, P * 3, ncclFloat64, ncclSum, root, c->comm, c->stream);
+        if (r == ncclSuccess) r = ncclReduce(c->d_n, c->d_n, P, ncclInt32, ncclSum, root, c->comm, c->stream);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return fail(PT_ERR_RCCL, std::string("ncclReduce (group): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    for (int i = 0; i < n; i++) {
+        Ctx* c = (Ctx*)ctxs[i];
+        PT_HIP(hipSetDevice(c->device));
+        PT_HIP(hipStreamSynchronize(c->stream));
+    }
+    ((Ctx*)ctxs[root])->gathered = true;
     return PT_OK;
 }
 

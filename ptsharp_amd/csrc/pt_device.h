@@ -462,7 +462,7 @@ __device__ inline v3 shape_uv(const DevScene& S, int kind, int idx, v3 p, const 
 // shading code without any texture path (no extra registers in the hot kernels).
 template <bool FULL>
 __device__ __forceinline__ void surface_at(const DevScene& S, const DevMaterial& m, int kind, int idx, v3 p,
-                                           float col[3], double& gloss, const float4* recs = nullptr) {
+                                           double col[3], double& gloss, const float4* recs = nullptr) {
     col[0] = m.color[0]; col[1] = m.color[1]; col[2] = m.color[2];
     gloss = m.gloss;
     if (!FULL || (m.tex < 0 && m.gtex < 0)) return;
@@ -470,7 +470,7 @@ __device__ __forceinline__ void surface_at(const DevScene& S, const DevMaterial&
     double c[3];
     if (m.tex >= 0) {
         tex_sample(S.texs[m.tex], uv.x, uv.y, c);
-        col[0] = (float)c[0]; col[1] = (float)c[1]; col[2] = (float)c[2];
+        col[0] = c[0]; col[1] = c[1]; col[2] = c[2];
     }
     if (m.gtex >= 0) {
         tex_sample(S.texs[m.gtex], uv.x, uv.y, c);
@@ -516,22 +516,22 @@ __device__ __noinline__ v3 tri_normal_mapped(const DevScene& S, const DevMateria
 
 // sampleEnvironment (Sampler.cs:177-189)
 template <bool FULL>
-__device__ __forceinline__ float3 environment(const DevScene& S, v3 d) {
-    if (!FULL || S.env_tex < 0) return make_float3(S.env[0], S.env[1], S.env[2]);
+__device__ __forceinline__ double3 environment(const DevScene& S, v3 d) {
+    if (!FULL || S.env_tex < 0) return make_double3(S.env[0], S.env[1], S.env[2]);
     double u = atan2((double)d.z, (double)d.x) + S.env_angle;
     double v = atan2((double)d.y, (double)lengthf(v3{d.x, 0.f, d.z}));
     u = (u + kPi) / (2 * kPi);
     v = (v + kPi / 2) / kPi;
     double c[3];
     tex_sample(S.texs[S.env_tex], u, v, c);
-    return make_float3((float)c[0], (float)c[1], (float)c[2]);
+    return make_double3(c[0], c[1], c[2]);
 }
 
 struct Shade {
     v3 pos, nrm;
     int32_t mat;
     int32_t inside;
-    float col[3];    // Material.MaterialAt colour (texture applied)
+    double col[3];   // Material.MaterialAt colour (texture applied), fp64 Colour
     double gloss;    // and gloss (gloss texture applied)
 };
 
@@ -718,7 +718,7 @@ __device__ __forceinline__ void bounce_dir(const DevMaterial& m, const Shade& sh
 // Returns false when diffuse <= 0 (no shadow ray is cast).
 template <bool FULL>
 __device__ __forceinline__ bool light_setup(const DevScene& S, const DevSampler& smp, const DevLight& L, v3 o, v3 n,
-                                            uint64_t key, v3& dir, float3& contrib) {
+                                            uint64_t key, v3& dir, double3& contrib) {
     v3 center{L.center[0], L.center[1], L.center[2]};
     double radius = L.radius;
     v3 point = center;
@@ -753,11 +753,11 @@ __device__ __forceinline__ bool light_setup(const DevScene& S, const DevSampler&
     if (FULL && L.kind == KIND_VOLUME)
         mat = vol_material(S.volumes[rec_ext(S.ana_recs + 3 * (size_t)L.index)], point, S.default_mat);
     const DevMaterial& m = S.mats[mat];
-    float col[3] = {m.color[0], m.color[1], m.color[2]};
+    double col[3] = {m.color[0], m.color[1], m.color[2]};
     double gl;
     if (!L.phantom) surface_at<FULL>(S, m, L.kind, L.index, point, col, gl);
-    float mm = (float)((double)m.emittance * diffuse * coverage);
-    contrib = make_float3(col[0] * mm, col[1] * mm, col[2] * mm);
+    const double mm = m.emittance * diffuse * coverage;   // material.Color.MulScalar(m) (Sampler.cs:293-295)
+    contrib = make_double3(col[0] * mm, col[1] * mm, col[2] * mm);
     return true;
 }
 

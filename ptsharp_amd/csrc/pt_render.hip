@@ -12,9 +12,12 @@
 // Every Scene.Intersect is a closest-hit query over planes (linear), a 4-wide
 // BVH over spheres/cubes and one over all triangles, with the per-lane traversal
 // stack in LDS.  The Welford update (Pixel.AddSample, Buffer.cs:33-44) is done by the
-// owning lane: no atomics on the Buffer.
+// owning lane: no atomics on the Buffer.  Colour terms are fp64 and summed in the
+// fixed-point form of pt_accum.h, term by term as the wavefront engine adds them, so
+// both engines produce the same bits.
 #include <hip/hip_runtime.h>
 
+#include "pt_accum.h"
 #include "pt_device.h"
 
 #pragma clang fp contract(off)
@@ -26,46 +29,44 @@ using MStack = LdsStack<kBlock>;
 constexpr int kMaxFrames = 34;   // MaxBounces <= 32 under SpecularModeAll (checked on the host)
 
 // Sampler.sampleLight (Sampler.cs:212-296): the megakernel keeps the reference's
-// nearest-hit + identity structure for the shadow query.
+// nearest-hit + identity structure for the shadow query.  Returns false (black) when
+// no ray is cast or the light is not the nearest hit.
 template <bool COUNT, bool FULL>
-__device__ __noinline__ float3 sample_light(const DevScene& S, const DevSampler& smp, const DevLight& L, v3 o, v3 n,
-                                            uint64_t key, MStack stack, Counters& ctr) {
+__device__ __noinline__ bool sample_light(const DevScene& S, const DevSampler& smp, const DevLight& L, v3 o, v3 n,
+                                          uint64_t key, MStack stack, Counters& ctr, double3& contrib) {
     v3 dir;
-    float3 contrib;
-    if (!light_setup<FULL>(S, smp, L, o, n, key, dir, contrib)) return make_float3(0.f, 0.f, 0.f);
+    if (!light_setup<FULL>(S, smp, L, o, n, key, dir, contrib)) return false;
     HitRec h = trace<COUNT, FULL>(S, o, dir, stack, ctr);
     // hit.Shape != light is a reference compare; struct Triangle lights never match.
-    if (!(h.t < kHitInf) || L.phantom || h.kind != L.kind || h.idx != L.index) return make_float3(0.f, 0.f, 0.f);
-    return contrib;
+    return (h.t < kHitInf) && !L.phantom && h.kind == L.kind && h.idx == L.index;
 }
 
-// Sampler.sampleLights (Sampler.cs:191-210)
+// Sampler.sampleLights (Sampler.cs:191-210) times the child's throughput·weight tw, each
+// light's term added to acc on its own, as the wavefront's shadow rays add them.
 template <bool COUNT, bool FULL>
-__device__ __forceinline__ float3 sample_lights(const DevScene& S, const DevSampler& smp, v3 o, v3 n, uint64_t key,
-                                                MStack stack, Counters& ctr) {
-    int nl = S.num_lights;
-    if (nl == 0) return make_float3(0.f, 0.f, 0.f);
-    if (smp.light_mode == 1) {
-        float3 acc = make_float3(0.f, 0.f, 0.f);
-        for (int i = 0; i < nl; i++) {
-            float3 c = sample_light<COUNT, FULL>(S, smp, S.lights[i], o, n, light_key(key, (uint32_t)i), stack, ctr);
-            acc.x += c.x; acc.y += c.y; acc.z += c.z;
-        }
-        float inv = 1.0f / (float)nl;
-        return make_float3(acc.x * inv, acc.y * inv, acc.z * inv);
+__device__ __forceinline__ void sample_lights(const DevScene& S, const DevSampler& smp, v3 o, v3 n, uint64_t key,
+                                              const double tw[3], FixReg& acc, MStack stack, Counters& ctr) {
+    const int nl = S.num_lights;
+    if (nl == 0) return;
+    const bool all = smp.light_mode == 1;
+    const int first = all ? 0 : min((int)(draw(key, D_LIGHT) * nl), nl - 1);
+    const int count = all ? nl : 1;
+    for (int j = 0; j < count; j++) {
+        const int li = first + j;
+        double3 lc;
+        if (!sample_light<COUNT, FULL>(S, smp, S.lights[li], o, n, all ? light_key(key, (uint32_t)li) : key, stack, ctr, lc))
+            continue;
+        if (all) { lc.x /= nl; lc.y /= nl; lc.z /= nl; }
+        else { lc.x *= nl; lc.y *= nl; lc.z *= nl; }
+        fixreg_add3(acc, tw[0] * lc.x, tw[1] * lc.y, tw[2] * lc.z);
     }
-    int idx = (int)(draw(key, D_LIGHT) * nl);
-    if (idx >= nl) idx = nl - 1;
-    float3 c = sample_light<COUNT, FULL>(S, smp, S.lights[idx], o, n, key, stack, ctr);
-    float fn = (float)nl;
-    return make_float3(c.x * fn, c.y * fn, c.z * fn);
 }
 
 // A branching vertex of the sampler tree (pending children).
 struct Frame {
     v3 pos, nrm, indir;
-    float thr[3];        // throughput into this vertex already divided by n²
-    float col[3];        // Material.MaterialAt colour / gloss of the vertex
+    double thr[3];       // throughput into this vertex already divided by n²
+    double col[3];       // Material.MaterialAt colour / gloss of the vertex
     double gloss;
     uint64_t node;
     int32_t mat, inside, depth, n, nm, next;
@@ -75,8 +76,8 @@ struct Frame {
 // Adds the vertex' direct-light term to acc and returns the child's ray/throughput.
 template <bool COUNT, bool FULL>
 __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& smp, const Shade& sh, v3 indir,
-                                           const float thr[3], uint64_t node, int n, int nm, int c, float3& acc,
-                                           v3& no, v3& nd, bool& emission, float nthr[3], uint64_t& nkey,
+                                           const double thr[3], uint64_t node, int n, int nm, int c, FixReg& acc,
+                                           v3& no, v3& nd, bool& emission, double nthr[3], uint64_t& nkey,
                                            MStack stack, Counters& ctr) {
     const DevMaterial& m = S.mats[sh.mat];
     int ma = nm == 2 ? 1 : 0;
@@ -91,18 +92,16 @@ __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& 
     bounce(m, sh, indir, fu, fv, mode, E, no, nd, reflected, p);
     if (mode == 0) p = 1;
     if (!(p > 0)) return false;
-    float fp = (float)p;
-    float w[3];
+    const double fp = p;
+    double w[3];
     if (reflected) {
         // specular: tinted = indirect.Mix(Color*indirect, Tint) (Sampler.cs:112-114)
-        for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * sh.col[k]);
+        for (int k = 0; k < 3; k++) w[k] = fp * ((1.0 - m.tint) + m.tint * sh.col[k]);
     } else {
         for (int k = 0; k < 3; k++) w[k] = fp * sh.col[k];
         if (smp.dl) {
-            float3 dl = sample_lights<COUNT, FULL>(S, smp, sh.pos, sh.nrm, E, stack, ctr);
-            acc.x += thr[0] * w[0] * dl.x;
-            acc.y += thr[1] * w[1] * dl.y;
-            acc.z += thr[2] * w[2] * dl.z;
+            const double tw[3] = {thr[0] * w[0], thr[1] * w[1], thr[2] * w[2]};
+            sample_lights<COUNT, FULL>(S, smp, sh.pos, sh.nrm, E, tw, acc, stack, ctr);
         }
     }
     for (int k = 0; k < 3; k++) nthr[k] = thr[k] * w[k];
@@ -111,18 +110,17 @@ __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& 
     return true;
 }
 
-// DefaultSampler.Sample(scene, ray) for one camera ray; returns the sample colour.
+// DefaultSampler.Sample(scene, ray) for one camera ray; adds the sample's terms to acc.
 template <bool COUNT, bool FULL>
-__device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3 d, uint64_t root_key,
-                              MStack stack, Frame* frames, Counters& ctr) {
-    float3 acc = make_float3(0.f, 0.f, 0.f);
+__device__ void sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3 d, uint64_t root_key,
+                            MStack stack, Frame* frames, Counters& ctr, FixReg& acc) {
     // current vertex to visit
     bool have = true;
     bool emission = true;
     int samples = smp.fh;
     int depth = 0;
     uint64_t node = root_key;
-    float thr[3] = {1.f, 1.f, 1.f};
+    double thr[3] = {1.0, 1.0, 1.0};
     int sp = 0;
     for (;;) {
         if (have) {
@@ -130,32 +128,29 @@ __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3
             if (depth <= smp.mb) {
                 HitRec h = trace<COUNT, FULL>(S, o, d, stack, ctr);
                 if (!(h.t < kHitInf)) {
-                    const float3 env = environment<FULL>(S, d);   // sampleEnvironment (Sampler.cs:177-189)
-                    acc.x += thr[0] * env.x;
-                    acc.y += thr[1] * env.y;
-                    acc.z += thr[2] * env.z;
+                    const double3 env = environment<FULL>(S, d);   // sampleEnvironment (Sampler.cs:177-189)
+                    fixreg_add3(acc, thr[0] * env.x, thr[1] * env.y, thr[2] * env.z);
                 } else {
                     Shade sh = hit_info<COUNT, FULL>(S, h, o, d, ctr);
                     const DevMaterial& m = S.mats[sh.mat];
                     int n = (int)sqrt((double)samples);
-                    float inv_n2 = 1.0f / (float)(n * n);
+                    const double nsq = (double)(n * n);
                     bool alive = true;
                     if (m.emittance > 0) {
                         if (smp.dl && !emission) {
                             alive = false;
                         } else {
-                            float e = (float)((double)m.emittance * samples) * inv_n2;
-                            acc.x += thr[0] * sh.col[0] * e;
-                            acc.y += thr[1] * sh.col[1] * e;
-                            acc.z += thr[2] * sh.col[2] * e;
+                            const double e = m.emittance * samples;
+                            fixreg_add3(acc, thr[0] * ((sh.col[0] * e) / nsq), thr[1] * ((sh.col[1] * e) / nsq),
+                                        thr[2] * ((sh.col[2] * e) / nsq));
                         }
                     }
                     if (alive) {
                         int nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
-                        float t2[3] = {thr[0] * inv_n2, thr[1] * inv_n2, thr[2] * inv_n2};
+                        double t2[3] = {thr[0] / nsq, thr[1] / nsq, thr[2] / nsq};
                         if (n * n * nm == 1) {
                             // chain vertex: its only child is processed inline
-                            float nthr[3];
+                            double nthr[3];
                             uint64_t nkey;
                             v3 no, nd;
                             bool em;
@@ -185,11 +180,11 @@ __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3
             int nch = F.n * F.n * F.nm;
             Shade sh{F.pos, F.nrm, F.mat, F.inside, {F.col[0], F.col[1], F.col[2]}, F.gloss};
             v3 indir = F.indir;
-            float t2[3] = {F.thr[0], F.thr[1], F.thr[2]};
+            double t2[3] = {F.thr[0], F.thr[1], F.thr[2]};
             uint64_t fnode = F.node;
             int fdepth = F.depth, fn = F.n, fnm = F.nm;
             if (F.next >= nch) sp--;
-            float nthr[3];
+            double nthr[3];
             uint64_t nkey;
             v3 no, nd;
             bool em;
@@ -201,7 +196,6 @@ __device__ float3 sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3
         }
         if (!have) break;
     }
-    return acc;
 }
 
 template <bool COUNT, bool FULL>
@@ -228,22 +222,24 @@ __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera ca
                     v3 o, d;
                     cast_ray(cam, x, y, w, h, ((double)u + 0.5) / (double)root, ((double)v + 0.5) / (double)root,
                              K, o, d);
-                    float3 c = sample_path<COUNT, FULL>(S, smp, o, d, K, stack, local_frames, ctr);
-                    welford(B, (size_t)pix, (double)c.x, (double)c.y, (double)c.z);
+                    FixReg acc;
+                    fixreg_clear(acc);
+                    sample_path<COUNT, FULL>(S, smp, o, d, K, stack, local_frames, ctr, acc);
+                    welford(B, (size_t)pix, fixreg_value(acc, 0), fixreg_value(acc, 1), fixreg_value(acc, 2));
                 }
         } else {
-            float cr = 0.f, cg = 0.f, cb = 0.f;
+            FixReg acc;   // the pixel's spp samples (c += sampler.Sample(...), Renderer.cs:304)
+            fixreg_clear(acc);
             for (int p = 0; p < P.spp; p++) {
                 uint64_t K = camera_key(P.seed, P.pass_index, pix, (uint32_t)p);
                 double fu = (x + draw(K, D_JX)) / w;
                 double fv = (y + draw(K, D_JY)) / h;
                 v3 o, d;
                 cast_ray(cam, x, y, w, h, fu, fv, K, o, d);
-                float3 c = sample_path<COUNT, FULL>(S, smp, o, d, K, stack, local_frames, ctr);
-                cr += c.x; cg += c.y; cb += c.z;
+                sample_path<COUNT, FULL>(S, smp, o, d, K, stack, local_frames, ctr, acc);
             }
-            double inv = (double)P.spp;
-            welford(B, (size_t)pix, (double)cr / inv, (double)cg / inv, (double)cb / inv);
+            const double spp = (double)P.spp;   // c /= spp (Renderer.cs:308)
+            welford(B, (size_t)pix, fixreg_value(acc, 0) / spp, fixreg_value(acc, 1) / spp, fixreg_value(acc, 2) / spp);
         }
     }
     uint32_t rays = wave_sum(ctr.rays);

@@ -16,18 +16,19 @@ namespace pt {
 enum PrimKind : int32_t { KIND_SPHERE = 0, KIND_CUBE = 1, KIND_PLANE = 2, KIND_TRI = 3, KIND_MESH = 4,
                           KIND_SDF = 5, KIND_VOLUME = 6, KIND_XFORM = 7 };
 
-// Material (Material.cs:8-62); colour terms in fp32 (they never feed a branch),
-// the terms that feed Fresnel / cone / branch decisions stay fp64.
+// Material (Material.cs:8-62), every scalar fp64 as in the reference (Colour is fp64,
+// Colour.cs:10-12): colour, emittance and tint feed the fp64 path throughput.
 struct DevMaterial {
-    float color[3];
-    float emittance;
-    float tint;
-    int32_t transparent;
+    double color[3];
+    double emittance;
+    double tint;
     double index;
     double gloss;
     double reflectivity;
-    int32_t tex, ntex, btex, gtex;   // Texture / NormalTexture / BumpTexture / GlossTexture (-1 = null)
     double bump_multiplier;
+    int32_t transparent;
+    int32_t tex, ntex, btex, gtex;   // Texture / NormalTexture / BumpTexture / GlossTexture (-1 = null)
+    int32_t _pad[3];
 };
 
 // ColorTexture (Texture.cs:96-252): fp64 Colour texels [h][w][3], exactly the C# Data,
@@ -66,7 +67,7 @@ struct DevScene {
     const DevMaterial* mats;
     const DevLight* lights;
     int32_t num_lights;
-    float env[3];
+    double env[3];              // Scene.Color (fp64 Colour)
     // textures (§8f row 3)
     const DevTexture* texs;
     const float4* tri_uv;      // 2 float4 per triangle: {t1.xy, t2.xy} {t3.xy, -, -}; null without textured triangles
@@ -115,7 +116,8 @@ struct DevBuffer {
     double* m;                 // [P][3] Welford mean   (Pixel.M, Buffer.cs:21)
     double* v;                 // [P][3] Welford M2     (Pixel.V, Buffer.cs:22)
     int32_t* n;                // [P]    sample count   (Pixel.Samples)
-    unsigned long long* counters;  // [0] rays, [1] nodes, [2] prims, [3] shading fetches
+    unsigned long long* counters;  // [0..2] closest-hit rays/nodes/prims, [3] shading fetches, [4..6] shadow
+                                   // rays/nodes/prims, [7] lit shadow rays, [8] their accumulation runs
 };
 
 }  // namespace pt

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pt_accum.h"
 #include "pt_scene.h"
 
 namespace pt {
@@ -18,12 +19,14 @@ constexpr int kParts = 8;
 struct WfQueues {
     float4* q_o[2];      // {origin.xyz, pixel}
     float4* q_d[2];      // {direction.xyz, depth | emission << 8}
-    float4* q_t[2];      // {throughput.rgb, -}
-    uint64_t* q_k[2];    // RNG node key of the vertex the ray leads to
+    double2* q_t[2];     // {throughput.r, throughput.g} (fp64, as the reference's Colour)
+    ulonglong2* q_k[2];  // {RNG node key of the vertex the ray leads to, throughput.b (fp64 bits)}
     uint4* hits;         // {t (fp64 bits), kind, record}
     float4* n_o;         // shadow rays (a diffuse child's sampleLights, set up by k_wf_shade): {origin.xyz, pixel}
     float4* n_n;         // {direction.xyz, light index | kDead: no ray cast (diffuse <= 0)}
-    float4* n_w;         // {throughput·weight·light colour·coverage.rgb, -}: added if the light is visible
+    double2* n_w;        // two per entry, {r, g} {b, -}: throughput·weight·light colour·coverage (fp64),
+                         // added if the light is visible
+    uint8_t* n_lit;      // per entry: 1 = the light is the nearest hit (k_wf_shadow*), read by k_wf_nee_accum
     uint32_t* counts;    // counter slots, each kCountStride words apart (see count_word below):
                          // slot q·kParts+g = {rays, NEE requests} of partition g of ray queue q
                          // (one packed 64-bit word, reserved together); slot kFetchSlot + k·kParts + g
@@ -33,9 +36,10 @@ struct WfQueues {
     uint32_t cap;        // entries per ray queue (kParts partitions of pcap)
     uint32_t s_cap;      // NEE queue entries (kParts partitions of spcap)
     uint32_t pcap, spcap;
-    double* acc;         // [P][3] per-pixel sum of this pass' sample colours
-    uint32_t* ovf;       // traversal stack entries beyond kLdsStack: [kMaxDepth - kLdsStack][kWfMaxThreads]
-    double* acc_s;       // [cap][3] per-sample accumulators of the adaptive / firefly phases
+    FixAcc acc;          // [P] per-pixel sum of this pass' sample colours (pt_accum.h: order-independent)
+    uint32_t* ovf;       // closest-hit traversal stack entries beyond kLdsStack: [kMaxDepth - kLdsStack][kWfMaxThreads]
+    uint32_t* ovf_sh;    // the same for the shadow kernels, which may run beside a closest-hit kernel (side stream)
+    FixAcc acc_s;        // [chunk] per-sample accumulators of the adaptive / firefly phases
 };
 
 // Every counter sits on a line of its own: returning atomics execute at the memory side,
@@ -94,11 +98,13 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
                           LaunchTimer* timer);
 
 // Adaptive (firefly = 0) or firefly (firefly = 1) phase of a pass: `entries` pixels
-// (tile order, or `plist`), K samples each.  `snap`: M at the start of the firefly phase.
+// (tile order, or `plist`), K samples each, sample indices sample_base + 0..K-1.  `snap`: M
+// at the start of the firefly phase.  Firefly: pixels that took all K samples without an
+// IsFirefly stop are appended to next_list (count in *next_count, a device word).
 hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                            const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
-                           LaunchTimer* timer, int firefly, int32_t K, uint64_t entries, const uint32_t* plist,
-                           const double* snap);
+                           LaunchTimer* timer, int firefly, int32_t K, uint32_t sample_base, uint64_t entries,
+                           const uint32_t* plist, const double* snap, uint32_t* next_list, uint32_t* next_count);
 
 // Persistent grid sizes (resident capacity on this device) of the traversal / shade kernels.
 hipError_t wavefront_grids(WfPlan& plan);

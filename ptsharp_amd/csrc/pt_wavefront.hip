@@ -13,13 +13,13 @@
 //                                                                (Sampler.cs:62-131,191-296, Ray.cs:44-85)
 //   k_wf_shadow   shadow visibility (nearest-hit == light ⇔ no primitive nearer
 //                 than the light's own t: any-hit, early exit)   (Sampler.cs:261-265)
+//   k_wf_nee_accum  the visible shadow rays' light terms, in slot order (Sampler.cs:119-127, 292-295)
 //   k_wf_finalize per-pixel mean of the pass → Welford           (Renderer.cs:308-309, Buffer.cs:33-44)
 //
 // The traversal kernels keep only ray + stack state, so they run at the
 // occupancy the LDS stack allows.  Queue appends are wave-aggregated atomics;
-// per-pixel contributions are fp64 atomics into a frame accumulator (a path's
-// contributions are summed in a different order than the recursion, which is
-// linear, so only the last fp64 bits can differ).
+// per-pixel contributions (fp64, as the reference's Colour) go into order-independent
+// fixed-point accumulators (pt_accum.h), so a pass gives the same bits on every run.
 #include <hip/hip_runtime.h>
 
 #include "pt_device.h"
@@ -59,7 +59,8 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void q_store(float4* p, float4 v) { *p = v; }
 __device__ __forceinline__ void q_store(uint4* p, uint4 v) { *p = v; }
-__device__ __forceinline__ void q_store(uint64_t* p, uint64_t v) { *p = v; }
+__device__ __forceinline__ void q_store(double2* p, double2 v) { *p = v; }
+__device__ __forceinline__ void q_store(ulonglong2* p, ulonglong2 v) { *p = v; }
 __device__ __forceinline__ float4 nt_load(const float4* p) {
     f4v x = __builtin_nontemporal_load((const f4v*)p);
     return make_float4(x.x, x.y, x.z, x.w);
@@ -68,7 +69,16 @@ __device__ __forceinline__ uint4 nt_load(const uint4* p) {
     u4v x = __builtin_nontemporal_load((const u4v*)p);
     return make_uint4(x.x, x.y, x.z, x.w);
 }
-__device__ __forceinline__ uint64_t nt_load(const uint64_t* p) { return __builtin_nontemporal_load(p); }
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 nt_load(const double2* p) {
+    d2v x = __builtin_nontemporal_load((const d2v*)p);
+    return make_double2(x.x, x.y);
+}
+__device__ __forceinline__ ulonglong2 nt_load(const ulonglong2* p) {
+    u2v x = __builtin_nontemporal_load((const u2v*)p);
+    return make_ulonglong2(x.x, x.y);
+}
 
 __device__ __forceinline__ uint32_t* ray_count(const WfQueues& Q, int q, int g) { return Q.counts + count_word(q * kParts + g); }
 __device__ __forceinline__ uint32_t* nee_count(const WfQueues& Q, int q, int g) {
@@ -146,54 +156,18 @@ __device__ __forceinline__ void block_reserve2(unsigned long long* word, uint32_
     bbase = s_base[1][wid] + xb - b;
 }
 
-__device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, float3 thr, uint32_t pixel,
-                                          uint32_t meta, uint64_t key) {
+// Throughput (fp64) rides in two 16-B fields: {r, g} and {key, b}.
+__device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, const double thr[3],
+                                          uint32_t pixel, uint32_t meta, uint64_t key) {
     q_store(&Q.q_o[q][i], make_float4(o.x, o.y, o.z, __uint_as_float(pixel)));
     q_store(&Q.q_d[q][i], make_float4(d.x, d.y, d.z, __uint_as_float(meta)));
-    q_store(&Q.q_t[q][i], make_float4(thr.x, thr.y, thr.z, 0.f));
-    q_store(&Q.q_k[q][i], key);
+    q_store(&Q.q_t[q][i], make_double2(thr[0], thr[1]));
+    q_store(&Q.q_k[q][i], make_ulonglong2(key, (unsigned long long)__double_as_longlong(thr[2])));
 }
-
-__device__ __forceinline__ void acc_add(double* acc, uint32_t pixel, float r, float g, float b) {
-    double* a = acc + 3 * (size_t)pixel;
-#ifdef PT_ABLATE_ACC  // timing-only build: plain (racy) adds instead of atomics
-    a[0] += r; a[1] += g; a[2] += b;
-#else
-    if (r != 0.f) atomicAdd(a + 0, (double)r);
-    if (g != 0.f) atomicAdd(a + 1, (double)g);
-    if (b != 0.f) atomicAdd(a + 2, (double)b);
-#endif
-}
-
-// Wave-aggregated acc_add: lanes of a wave often add to the same pixel (a camera sample's
-// children and a pixel's samples sit in consecutive queue slots), and same-address fp64
-// atomics serialise at L2.  Lanes are grouped into runs of equal `pixel` (segment ids
-// from a ballot of run heads), each run is summed by a segmented suffix scan over
-// shuffles, and only the run's head issues the three atomics.  Wave-uniform call;
-// lanes with has = false add nothing (their pixel is ignored).
-__device__ __forceinline__ void acc_add_wave(double* acc, uint32_t pixel, bool has, float r, float g, float b) {
-#if defined(PT_ABLATE_ACC) || defined(PT_ACC_DIRECT)
-    if (has) acc_add(acc, pixel, r, g, b);
-#else
-    const int lane = threadIdx.x & 63;
-    const uint32_t pix = has ? pixel : 0xFFFFFFFFu;
-    const uint32_t prev = __shfl_up(pix, 1, 64);
-    const bool head = lane == 0 || prev != pix;
-    const uint64_t heads = __ballot(head);
-    const int seg = __popcll(heads & (~0ull >> (63 - lane)));   // run id: heads at or below this lane
-    double vr = has ? (double)r : 0.0, vg = has ? (double)g : 0.0, vb = has ? (double)b : 0.0;
-    for (int off = 1; off < 64; off <<= 1) {   // suffix sums within a run
-        const int so = __shfl_down(seg, off, 64);
-        const double ur = __shfl_down(vr, off, 64), ug = __shfl_down(vg, off, 64), ub = __shfl_down(vb, off, 64);
-        if (lane + off < 64 && so == seg) { vr += ur; vg += ug; vb += ub; }
-    }
-    if (head && has) {
-        double* a = acc + 3 * (size_t)pixel;
-        if (vr != 0.0) atomicAdd(a + 0, vr);
-        if (vg != 0.0) atomicAdd(a + 1, vg);
-        if (vb != 0.0) atomicAdd(a + 2, vb);
-    }
-#endif
+__device__ __forceinline__ void ray_store_camera(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, uint32_t pixel,
+                                                 uint64_t key) {
+    const double one[3] = {1.0, 1.0, 1.0};
+    ray_store(Q, q, i, o, d, one, pixel, 0u | (1u << 8), key);
 }
 
 // ---------------------------------------------------------------- camera
@@ -256,7 +230,7 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
             double fv = (y + draw(K, D_JY)) / h;
             cast_ray(cam, x, y, w, h, fu, fv, K, o, d);
         }
-        ray_store(Q, 0, i, o, d, make_float3(1.f, 1.f, 1.f), (uint32_t)pix, 0u | (1u << 8), K);
+        ray_store_camera(Q, 0, i, o, d, (uint32_t)pix, K);
     }
 }
 
@@ -507,19 +481,21 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     const int nl = S.num_lights;
     const bool all_lights = smp.light_mode == 1;
     const uint32_t rays_per_nee = all_lights ? (uint32_t)nl : 1u;   // shadow rays of one sampleLights call
-    float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, rt = ro;
+    float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro;
+    double2 rt = make_double2(0.0, 0.0);
+    ulonglong2 rk = make_ulonglong2(0ull, 0ull);
     uint4 hr = make_uint4(0, 0, 0, 0);
     uint32_t meta = kDead;
-    uint64_t node = 0;
     if (alive) {  // all loads issued together: one memory round trip
         rd = nt_load(&Q.q_d[qi][i]);
         ro = nt_load(&Q.q_o[qi][i]);
         rt = nt_load(&Q.q_t[qi][i]);
         hr = nt_load(&Q.hits[i]);
-        node = nt_load(&Q.q_k[qi][i]);
+        rk = nt_load(&Q.q_k[qi][i]);
         meta = __float_as_uint(rd.w);
         alive = meta != kDead;
     }
+    const uint64_t node = rk.x;
     const uint32_t pixel = __float_as_uint(ro.w);
     const int depth = (int)(meta & 0xFF);
     const bool emission = (meta >> 8) & 1;
@@ -527,15 +503,18 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     h.t = __longlong_as_double((long long)(((unsigned long long)hr.y << 32) | hr.x));
     h.kind = (int32_t)hr.z;
     h.idx = (int32_t)hr.w;
-    const float thr[3] = {rt.x, rt.y, rt.z};
+    const double thr[3] = {rt.x, rt.y, __longlong_as_double((long long)rk.y)};
     const v3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z};
     Shade sh{};
     int mat = 0, nn = 1, nm = 1, nch = 0;
-    float t2[3] = {0.f, 0.f, 0.f};
+    double t2[3] = {0.0, 0.0, 0.0};
     double pv = 0.0, n1 = 1.0, n2 = 1.0;
+    bool has_c = false;   // this vertex' own term: environment (miss) or emission
+    double cc[3] = {0.0, 0.0, 0.0};
     if (alive && !(h.t < kHitInf)) {  // sampleEnvironment (Sampler.cs:64-67, 177-189)
-        const float3 env = environment<FULL>(S, d);
-        acc_add(Q.acc, pixel, thr[0] * env.x, thr[1] * env.y, thr[2] * env.z);
+        const double3 env = environment<FULL>(S, d);
+        cc[0] = thr[0] * env.x; cc[1] = thr[1] * env.y; cc[2] = thr[2] * env.z;
+        has_c = true;
         alive = false;
     }
     if (alive) {
@@ -544,20 +523,22 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         const DevMaterial& m = S.mats[mat];
         const int samples = depth == 0 ? smp.fh : 1;
         nn = (int)sqrt((double)samples);
-        const float inv_n2 = 1.0f / (float)(nn * nn);
+        const double nsq = (double)(nn * nn);   // result.DivScalar(n * n) (Sampler.cs:144)
         if (m.emittance > 0) {
             if (smp.dl && !emission) {
                 alive = false;  // Sampler.cs:75-78
             } else {
-                float e = (float)((double)m.emittance * samples) * inv_n2;
-                acc_add(Q.acc, pixel, thr[0] * sh.col[0] * e, thr[1] * sh.col[1] * e, thr[2] * sh.col[2] * e);
+                const double e = m.emittance * samples;   // Color.MulScalar(Emittance * samples) (Sampler.cs:79)
+                for (int k = 0; k < 3; k++) cc[k] = thr[k] * ((sh.col[k] * e) / nsq);
+                has_c = true;
             }
         }
         nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
         nch = alive ? nn * nn * nm : 0;
-        for (int k = 0; k < 3; k++) t2[k] = thr[k] * inv_n2;
+        for (int k = 0; k < 3; k++) t2[k] = thr[k] / nsq;
         pv = vertex_p(m, sh, d, n1, n2);
     }
+    fix_add_wave(Q.acc, pixel, has_c, cc[0], cc[1], cc[2]);
     const DevMaterial& m = S.mats[mat];
     const int ma = nm == 2 ? 1 : 0;
     const bool ext_on = depth + 1 <= smp.mb;   // deeper samples return black without an Intersect
@@ -619,11 +600,11 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         nj += tn * rays_per_nee;
         ej += te;
         if (!live) continue;
-        const float fp = mode == 0 ? 1.0f : (float)(refl ? pv : 1 - pv);
-        float w[3];
-        if (reflected) {
-            for (int k = 0; k < 3; k++) w[k] = fp * ((1.0f - m.tint) + m.tint * sh.col[k]);
-        } else {
+        const double fp = mode == 0 ? 1.0 : (refl ? pv : 1 - pv);
+        double w[3];
+        if (reflected) {   // indirect.Mix(Color·indirect, Tint)·p (Sampler.cs:112-114)
+            for (int k = 0; k < 3; k++) w[k] = fp * ((1.0 - m.tint) + m.tint * sh.col[k]);
+        } else {           // Color·(direct + indirect)·p (Sampler.cs:119-127)
             for (int k = 0; k < 3; k++) w[k] = fp * sh.col[k];
             if (nee_on) {
                 // diffuse child: sampleLights from the normal ray (Sampler.cs:191-296) up to the
@@ -631,19 +612,21 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
                 // visibility kernel carries only ray + stack state.  One shadow-ray slot per
                 // light considered; a light with diffuse <= 0 casts no ray (dead slot).
                 const int first = all_lights ? 0 : min((int)(draw(E, D_LIGHT) * nl), nl - 1);
-                const float scale = all_lights ? 1.0f / (float)nl : (float)nl;
                 for (uint32_t j = 0; j < rays_per_nee; j++) {
                     const int li = first + (int)j;
                     v3 ldir;
-                    float3 lc;
+                    double3 lc;
                     const bool cast = light_setup<FULL>(S, smp, S.lights[li], sh.pos, sh.nrm,
                                                   all_lights ? light_key(E, (uint32_t)li) : E, ldir, lc);
+                    // sampleLights: ÷ nLights (LightModeAll) or × nLights (random light), Sampler.cs:199-209
+                    if (all_lights) { lc.x /= nl; lc.y /= nl; lc.z /= nl; }
+                    else { lc.x *= nl; lc.y *= nl; lc.z *= nl; }
                     if (my_n + j < Q.spcap) {
                         const uint32_t at = G.g * Q.spcap + my_n + j;
                         q_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
                         q_store(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
-                        q_store(&Q.n_w[at], make_float4((t2[0] * w[0]) * (lc.x * scale), (t2[1] * w[1]) * (lc.y * scale),
-                                                         (t2[2] * w[2]) * (lc.z * scale), 0.f));
+                        q_store(&Q.n_w[2 * (size_t)at], make_double2((t2[0] * w[0]) * lc.x, (t2[1] * w[1]) * lc.y));
+                        q_store(&Q.n_w[2 * (size_t)at + 1], make_double2((t2[2] * w[2]) * lc.z, 0.0));
                     }
                 }
             }
@@ -655,9 +638,11 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
         v3 no, nd;
         bounce_dir(m, sh, d, fu, fv, refl, n1, n2, E, no, nd);
-        if (my_e < Q.pcap)
-            ray_store(Q, qo, G.g * Q.pcap + my_e, no, nd, make_float3(t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]), pixel,
-                      (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8), E);
+        if (my_e < Q.pcap) {
+            const double nthr[3] = {t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]};
+            ray_store(Q, qo, G.g * Q.pcap + my_e, no, nd, nthr, pixel, (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8),
+                      E);
+        }
     }
 }
 
@@ -754,7 +739,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
 template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
-    const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
+    const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
@@ -768,19 +753,16 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
         if (kc >= n) break;
         for (uint32_t k0 = kc; k0 < kc + 64u * kFetchBatches && k0 < n; k0 += 64u) {
             const uint32_t i = base + k0 + lane;
+            if (k0 + lane >= n) continue;
             bool lit = false;
-            float4 a = make_float4(0.f, 0.f, 0.f, 0.f), wt = a;
-            if (k0 + lane < n) {
-                const float4 b = nt_load(&Q.n_n[i]);
-                const uint32_t li = __float_as_uint(b.w);
-                if (li != kDead) {
-                    a = nt_load(&Q.n_o[i]);
-                    const DevLight L = S.lights[li];
-                    lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
-                    if (lit) wt = nt_load(&Q.n_w[i]);
-                }
+            const float4 b = nt_load(&Q.n_n[i]);
+            const uint32_t li = __float_as_uint(b.w);
+            if (li != kDead) {
+                const float4 a = nt_load(&Q.n_o[i]);
+                const DevLight L = S.lights[li];
+                lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
             }
-            acc_add_wave(Q.acc, __float_as_uint(a.w), lit, wt.x, wt.y, wt.z);
+            Q.n_lit[i] = lit ? 1 : 0;   // k_wf_nee_accum adds the lit rays' terms
         }
     }
     uint32_t rays = wave_sum(ctr.rays);
@@ -797,12 +779,11 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // Shadow visibility with per-lane refill (triangle scenes; see k_wf_trace_lanes): the
 // light's own t and the planes at refill, then one step loop over the analytic BVH and
 // the triangle BVH, any-hit (a primitive strictly nearer than the light ends the ray
-// unlit).  A lit lane holds its colour until the wave's next refill (or the end) and the
-// wave adds all held colours with the run-aggregated acc_add_wave.
+// unlit).  The outcome goes to n_lit; k_wf_nee_accum adds the lit rays' terms.
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
-    const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
+    const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
@@ -811,19 +792,16 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
     const uint64_t below = (1ull << lane) - 1ull;
     Counters ctr{0, 0, 0, 0};
     const float inf = __int_as_float(0x7f800000);
-    bool has = false, tri = false, more = true, phantom = false, pend = false;
-    uint32_t i = 0, ref = 0, pixel = 0;
+    bool has = false, tri = false, more = true, phantom = false;
+    uint32_t i = 0, ref = 0;
     int sp = 0;
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
     double tl = kHitInf;
     float tmax = 0.f;
-    float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
     for (;;) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (more && (nidle >= PT_SHADOW_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
-            acc_add_wave(Q.acc, pixel, pend, pw.x, pw.y, pw.z);   // colours of the rays lit since the last refill
-            pend = false;
             uint32_t kc = 0;
             if (lane == 0) kc = atomicAdd(cursor, nidle);
             kc = __shfl(kc, 0, 64);
@@ -834,12 +812,13 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
                 const float4 b = nt_load(&Q.n_n[i]);
                 const float4 a = nt_load(&Q.n_o[i]);
                 const uint32_t li = __float_as_uint(b.w);
-                if (li != kDead) {   // light_visible (pt_device.h), head part
+                if (li == kDead) {
+                    Q.n_lit[i] = 0;
+                } else {   // light_visible (pt_device.h), head part
                     ctr.rays++;
                     const DevLight L = S.lights[li];
                     o = v3{a.x, a.y, a.z};
                     d = v3{b.x, b.y, b.z};
-                    pixel = __float_as_uint(a.w);
                     invd = v3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
                     phantom = L.phantom != 0;
                     bool run;
@@ -860,6 +839,7 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
                     sp = 0;
                     ref = 0;
                     has = run;
+                    if (!run) Q.n_lit[i] = 0;
                 }
             }
         }
@@ -914,6 +894,7 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
         }
         if (blocked) {
             has = false;
+            Q.n_lit[i] = 0;
         } else if (pop) {
             if (sp > 0) {
                 sp--;
@@ -923,14 +904,10 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
                 ref = 0;
             } else {   // no primitive nearer than the light: lit (a phantom light never is)
                 has = false;
-                if (!phantom) {
-                    pw = nt_load(&Q.n_w[i]);
-                    pend = true;
-                }
+                Q.n_lit[i] = phantom ? 0 : 1;
             }
         }
     }
-    acc_add_wave(Q.acc, pixel, pend, pw.x, pw.y, pw.z);
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
     if (COUNT) {
@@ -942,8 +919,45 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
     }
 }
 
+// ---------------------------------------------------------------- direct-light terms
+// The light terms (throughput·weight·light colour·coverage, set up by k_wf_shade) of the
+// shadow rays the visibility kernels found lit, added in slot order after each shadow pass
+// (a pixel's rays sit in runs of consecutive slots, so fix_add_wave sums most of them in
+// registers).  Keeping the accumulation out of the traversal kernels keeps their refill path
+// and registers lean.  Group g takes partition g (written on its XCD by k_wf_shade).
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsigned long long* counters) {
+    const Group G = xcd_group();
+    const uint32_t cnt = *nee_count(Q, qo, G.g);
+    const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap;
+    const size_t base = (size_t)G.g * Q.spcap;
+    const uint32_t lane = threadIdx.x & 63, wave = G.lb * 4u + (threadIdx.x >> 6), nwaves = G.nb * 4u;
+    uint32_t lit_n = 0, runs = 0;
+    for (uint32_t j0 = wave * 64u; j0 < n; j0 += nwaves * 64u) {   // wave-uniform
+        const uint32_t j = j0 + lane;
+        bool lit = false;
+        uint32_t pixel = 0;
+        double2 w01 = make_double2(0.0, 0.0), w2 = w01;
+        if (j < n) {
+            const size_t i = base + j;
+            lit = Q.n_lit[i] != 0;
+            if (lit) {
+                pixel = __float_as_uint(nt_load(&Q.n_o[i]).w);
+                w01 = nt_load(&Q.n_w[2 * i]);
+                w2 = nt_load(&Q.n_w[2 * i + 1]);
+            }
+        }
+        const uint32_t r = fix_add_wave(Q.acc, pixel, lit, w01.x, w01.y, w2.x);
+        if (COUNT) { runs += r; lit_n += (uint32_t)__popcll(__ballot(lit)); }
+    }
+    if (COUNT && lane == 0) {
+        atomicAdd(&counters[7], (unsigned long long)lit_n);
+        atomicAdd(&counters[8], (unsigned long long)runs);
+    }
+}
+
 // ---------------------------------------------------------------- Welford
-__global__ __launch_bounds__(256) void k_wf_finalize(DevPass P, DevBuffer B, WfQueues Q, double inv_spp) {
+__global__ __launch_bounds__(256) void k_wf_finalize(DevPass P, DevBuffer B, WfQueues Q, double spp) {
     const uint32_t total = (uint32_t)P.num_tiles * 1024u;
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < total; s += gridDim.x * blockDim.x) {
         const int tile = P.tiles ? P.tiles[s >> 10] : (int)(s >> 10);
@@ -951,10 +965,10 @@ __global__ __launch_bounds__(256) void k_wf_finalize(DevPass P, DevBuffer B, WfQ
         tile_pixel(tile, (int)(s & 1023), P.tiles_x, x, y);
         if (x >= P.width || y >= P.height) continue;
         const size_t pix = (size_t)y * (size_t)P.width + (size_t)x;
-        double* a = Q.acc + 3 * pix;
+        double c[3];
+        fix_take(Q.acc, pix, c);
         // c /= spp (Renderer.cs:308) then Buffer.AddSample
-        welford(B, pix, a[0] * inv_spp, a[1] * inv_spp, a[2] * inv_spp);
-        a[0] = 0.0; a[1] = 0.0; a[2] = 0.0;
+        welford(B, pix, c[0] / spp, c[1] / spp, c[2] / spp);
     }
 }
 
@@ -994,29 +1008,32 @@ __global__ __launch_bounds__(256) void k_wf_camera_extra(DevCamera cam, DevPass 
         cast_ray(cam, x, y, P.width, P.height, draw(Kc, D_JX), draw(Kc, D_JY), Kc, o, d);
         const uint32_t i = append(ray_count(Q, 0, G.g));
         if (i >= Q.pcap) { Q.counts[kFlagWord] = 1; continue; }
-        ray_store(Q, 0, G.g * Q.pcap + i, o, d, make_float3(1.f, 1.f, 1.f), g, 0u | (1u << 8), Kc);
+        ray_store_camera(Q, 0, G.g * Q.pcap + i, o, d, g, Kc);
     }
 }
 
 // One thread per entry: the K samples in order — AddSample each (adaptive), or stop
-// at the first IsFirefly sample (firefly).  Clears the entry's accumulators.
-__global__ __launch_bounds__(256) void k_wf_finalize_extra(DevPass P, DevBuffer B, double* __restrict__ acc,
+// at the first IsFirefly sample (firefly; a pixel that did not stop goes on next_list for
+// the next round).  Clears the entry's accumulators.
+__global__ __launch_bounds__(256) void k_wf_finalize_extra(DevPass P, DevBuffer B, FixAcc acc,
                                                            uint64_t begin_entry, uint32_t entries, int32_t K,
                                                            const uint32_t* plist, int firefly,
-                                                           const double* __restrict__ snap) {
+                                                           const double* __restrict__ snap, uint32_t* next_list,
+                                                           uint32_t* next_count) {
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < entries; e += gridDim.x * blockDim.x) {
         int x, y;
         const bool in = entry_pixel(P, plist, begin_entry + e, x, y);
         const size_t pix = (size_t)y * (size_t)P.width + (size_t)x;
-        double* a = acc + 3 * (size_t)e * (size_t)K;
         bool stop = !in;
-        for (int j = 0; j < K; j++, a += 3) {
-            const double r = a[0], g = a[1], b = a[2];
-            a[0] = 0.0; a[1] = 0.0; a[2] = 0.0;
+        for (int j = 0; j < K; j++) {
+            double c[3];
+            fix_take(acc, (size_t)e * (size_t)K + (size_t)j, c);
+            const double r = c[0], g = c[1], b = c[2];
             if (stop) continue;
             if (firefly && is_firefly(r, g, b, x, y, P.width, P.height, snap, B.m + 3 * pix)) { stop = true; continue; }
             welford(B, pix, r, g, b);
         }
+        if (next_list && !stop) next_list[atomicAdd(next_count, 1u)] = (uint32_t)pix;
     }
 }
 
@@ -1103,6 +1120,11 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         end_k(3, side);
+        begin_k(6, side);   // PT_K_ACCUM
+        const unsigned ag = grid_for(children * plan.lights_per_child, 256, 8192);
+        if (count) hipLaunchKernelGGL((k_wf_nee_accum<true>), dim3(ag), dim3(256), 0, side, Q, 1 - qi, B.counters);
+        else hipLaunchKernelGGL((k_wf_nee_accum<false>), dim3(ag), dim3(256), 0, side, Q, 1 - qi, B.counters);
+        end_k(6, side);
         if (plan.side) (void)hipEventRecord(plan.ev_side, side);
         bound = children < Q.cap ? children : Q.cap;
         qi = 1 - qi;
@@ -1117,7 +1139,7 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     const uint64_t pix_slots = (uint64_t)P.num_tiles * 1024u;
     const int rounds = P.stratified ? P.spp : 1;        // stratified: one Welford sample per sample index
     const int spp_launch = P.stratified ? 1 : P.spp;
-    const double inv_spp = 1.0 / (double)spp_launch;
+    const double spp_d = (double)spp_launch;
     const uint64_t total = pix_slots * (uint64_t)spp_launch;
     auto begin_k = [&](int cls) { if (timer) timer->begin(cls, stream); };
     auto end_k = [&](int cls) { if (timer) timer->end(cls, stream); };
@@ -1133,7 +1155,7 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
             depth_loop(S, smp, B, Q, plan, count, stream, timer, cnt);
         }
         begin_k(4);
-        hipLaunchKernelGGL(k_wf_finalize, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, Q, inv_spp);
+        hipLaunchKernelGGL(k_wf_finalize, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, Q, spp_d);
         end_k(4);
     }
     return hipGetLastError();
@@ -1141,8 +1163,8 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
 
 hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                            const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
-                           LaunchTimer* timer, int firefly, int32_t K, uint64_t entries, const uint32_t* plist,
-                           const double* snap) {
+                           LaunchTimer* timer, int firefly, int32_t K, uint32_t sample_base, uint64_t entries,
+                           const uint32_t* plist, const double* snap, uint32_t* next_list, uint32_t* next_count) {
     if (K <= 0 || entries == 0) return hipSuccess;
     auto begin_k = [&](int cls) { if (timer) timer->begin(cls, stream); };
     auto end_k = [&](int cls) { if (timer) timer->end(cls, stream); };
@@ -1150,7 +1172,6 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
     Qx.acc = Q.acc_s;  // per-sample accumulators
     uint64_t per_chunk = plan.chunk / (uint64_t)K;  // entries per chunk (whole pixels)
     if (per_chunk < 1) per_chunk = 1;
-    const uint32_t base = firefly ? kFireflySampleBase : kAdaptiveSampleBase;
     for (uint64_t e0 = 0; e0 < entries; e0 += per_chunk) {
         const uint64_t ne = (entries - e0) < per_chunk ? (entries - e0) : per_chunk;
         const uint32_t cnt = (uint32_t)(ne * (uint64_t)K);
@@ -1158,12 +1179,12 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
         if (e != hipSuccess) return e;
         begin_k(0);
         hipLaunchKernelGGL(k_wf_camera_extra, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Qx,
-                           e0 * (uint64_t)K, cnt, K, base, plist);
+                           e0 * (uint64_t)K, cnt, K, sample_base, plist);
         end_k(0);
         depth_loop(S, smp, B, Qx, plan, count, stream, timer, cnt);
         begin_k(4);
         hipLaunchKernelGGL(k_wf_finalize_extra, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, stream, P, B, Q.acc_s,
-                           e0, (uint32_t)ne, K, plist, firefly, snap);
+                           e0, (uint32_t)ne, K, plist, firefly, snap, next_list, next_count);
         end_k(4);
     }
     return hipGetLastError();

@@ -213,6 +213,17 @@ class Renderer:
                                             b.N.ctypes.data_as(C.POINTER(C.c_int32))), "pt_read_buffer")
         return b
 
+    def LoadBuffer(self, buf: Buffer, passes_done: int) -> None:
+        """Resume an IterativeRender from a saved Buffer (pt_write_buffer): later passes keep adding
+        Welford samples to it, numbered from passes_done + 1 (the random streams are keyed by pass)."""
+        M = np.ascontiguousarray(buf.M, np.float64)
+        V = np.ascontiguousarray(buf.V, np.float64)
+        N = np.ascontiguousarray(buf.N, np.int32)
+        _abi.check(self._lib.pt_write_buffer(self._ctx, M.ctypes.data_as(C.POINTER(C.c_double)),
+                                             V.ctypes.data_as(C.POINTER(C.c_double)),
+                                             N.ctypes.data_as(C.POINTER(C.c_int32))), "pt_write_buffer")
+        self._pass = int(passes_done)
+
     def ResetBuffer(self) -> None:
         _abi.check(self._lib.pt_reset_buffer(self._ctx), "pt_reset_buffer")
         self._pass = 0
@@ -245,6 +256,19 @@ class Renderer:
 
     def Gather(self, root: int = 0) -> None:
         _abi.check(self._lib.pt_comm_gather(self._ctx, root), "pt_comm_gather")
+
+    @staticmethod
+    def CommInitAll(renderers: list) -> None:
+        """One communicator over renderers on distinct devices of this process (pt_comm_init_all)."""
+        lib = _abi.load_library()
+        arr = (C.c_void_p * len(renderers))(*[r._ctx.value for r in renderers])
+        _abi.check(lib.pt_comm_init_all(arr, len(renderers)), "pt_comm_init_all")
+
+    @staticmethod
+    def GatherAll(renderers: list, root: int = 0) -> None:
+        lib = _abi.load_library()
+        arr = (C.c_void_p * len(renderers))(*[r._ctx.value for r in renderers])
+        _abi.check(lib.pt_comm_gather_all(arr, len(renderers), root), "pt_comm_gather_all")
 
     @staticmethod
     def CommUniqueId() -> bytes:

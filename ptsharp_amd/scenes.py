@@ -9,6 +9,8 @@ as PTSharpCore/Example.cs builds them.  No model assets ship with the reference
   materialspheres  Example.materialspheres (Example.cs:1204-1227)
   simplesphere     Example.simplesphere (Example.cs:1670-1697)
   example1         Example.example1 (Example.cs:341-359), no adaptive/firefly passes
+  example3         Example.example3 (Example.cs:387-418), the scene Program.cs:97 renders: 840 thin
+                   cubes and a Cube light; the renderer runs AdaptiveSamples 32, FireflySamples 64
   textured         §8f row 3: colour / gloss / normal / bump maps, a textured light and an
                    environment map with TextureAngle, on seeded synthetic textures (no
                    texture assets ship with the reference either)
@@ -91,6 +93,27 @@ def example1():
     camera.SetFocus(Vector(-0.75, 1, -1), 0.1)
     sampler = DefaultSampler.NewSampler(8, 10)
     sampler.SpecularMode = SpecularMode.SpecularModeFirst
+    return scene, camera, sampler
+
+
+def example3():
+    """Example.example3 (Example.cs:387-418): a floor cube, the 840 cubes of the 41x41 grid whose
+    x + z is odd ((x + z) % 2 == 0 skips, C#'s % keeps the sign so odd negatives are kept too), a
+    Cube light, LookAt((20,10,0), (8,0,0), up, 45), NewSampler(4,4).  The reference renders it with
+    AdaptiveSamples = 32 and FireflySamples = 64 (pass those to the Renderer)."""
+    scene = Scene()
+    material = Material.DiffuseMaterial(Colour.HexColor(0xFCFAE1))
+    scene.Add(Cube.NewCube(Vector(-1000, -1, -1000), Vector(1000, 0, 1000), material))
+    for x in range(-20, 21):
+        for z in range(-20, 21):
+            if math.fmod(x + z, 2) == 0:
+                continue
+            sz = 0.1
+            scene.Add(Cube.NewCube(Vector(float(x) - sz, 0, float(z) - sz), Vector(float(x) + sz, 2, float(z) + sz),
+                                   material))
+    scene.Add(Cube.NewCube(Vector(-5, 10, -5), Vector(5, 11, 5), Material.LightMaterial(Colour.White, 5)))
+    camera = Camera.LookAt(Vector(20, 10, 0), Vector(8, 0, 0), Vector(0, 1, 0), 45)
+    sampler = DefaultSampler.NewSampler(4, 4)
     return scene, camera, sampler
 
 
@@ -385,6 +408,7 @@ SCENES = {
     "materialspheres": materialspheres,
     "simplesphere": simplesphere,
     "example1": example1,
+    "example3": example3,
     "bunny70k": lambda: bunny_frame(69_451),
     "mesh1m": lambda: bunny_frame(1_000_000),
     "furnace": furnace,

@@ -133,6 +133,13 @@ class OracleScene:
         return tuple(col), gloss.value
 
 
+def default_threads() -> int:
+    """Host threads for the oracle: OMP_NUM_THREADS (16 on the GPU box, whose os.cpu_count() is
+    the whole machine's), else the CPUs here, at most 16."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    return int(env) if env and env.isdigit() and int(env) > 0 else min(os.cpu_count() or 1, 16)
+
+
 def pass_params(spp, seed=0, pass_index=1, stratified=False, tiles=None, adaptive=0, firefly=0):
     keep = None
     if tiles is not None:
@@ -157,10 +164,11 @@ class OracleBuffer:
 
 
 def render(oscene: OracleScene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None,
-           threads=0, brute=False, buf: OracleBuffer = None, first_pass=1, adaptive=0, firefly=0):
+           threads=None, brute=False, buf: OracleBuffer = None, first_pass=1, adaptive=0, firefly=0):
     """IterativeRender-equivalent on the oracle: `passes` RenderParallel calls."""
     buf = buf or OracleBuffer(w, h)
     cam, smp = camera.to_c(), sampler.to_c()
+    threads = default_threads() if threads is None else threads
     rays = 0
     for p in range(first_pass, first_pass + passes):
         pp = pass_params(spp, seed, p, stratified, tiles, adaptive, firefly)
@@ -170,9 +178,10 @@ def render(oscene: OracleScene, camera, sampler, w, h, spp, passes=1, seed=0, st
 
 
 def render_pixels(oscene: OracleScene, camera, sampler, w, h, spp, pix_begin, pix_end, pix_stride=1, seed=0,
-                  pass_index=1, threads=0, buf: OracleBuffer = None):
+                  pass_index=1, threads=None, buf: OracleBuffer = None):
     buf = buf or OracleBuffer(w, h)
     cam, smp = camera.to_c(), sampler.to_c()
+    threads = default_threads() if threads is None else threads
     pp = pass_params(spp, seed, pass_index)
     rays = lib().or_render_pixels(oscene.h, w, h, C.byref(cam), C.byref(smp), C.byref(pp), pix_begin, pix_end,
                                   pix_stride, *buf.ptrs(), threads)

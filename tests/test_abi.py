@@ -48,8 +48,8 @@ def test_struct_layouts_match_header():
     assert C.sizeof(_abi.pt_camera) == 12 * 4 + 3 * 8
     assert C.sizeof(_abi.pt_sampler) == 24
     assert C.sizeof(_abi.pt_pass_params) == 4 + 4 + 8 + 4 + 4 + 8 + 8 + 8
-    assert C.sizeof(_abi.pt_stats) == 9 * 8 + 6 * 8 + 6 * 4
-    assert C.sizeof(_abi.pt_trace_counters) == 56
+    assert C.sizeof(_abi.pt_stats) == 9 * 8 + 8 * 8 + 8 * 4 + 8
+    assert C.sizeof(_abi.pt_trace_counters) == 72
     assert _abi.pt_scene_desc.env_color.offset % 8 == 0
 
 
@@ -92,20 +92,37 @@ def test_missing_library_fails_loudly(tmp_path):
         _abi.load_library(str(tmp_path / "missing.so"))
 
 
+# canonical field types: C (include/ptsharp_hip.h), C# (csharp/HipRenderer.cs), ctypes (_abi.py)
+_C_TYPES = {"int32_t": "i32", "int": "i32", "uint32_t": "u32", "uint64_t": "u64", "double": "f64", "float": "f32",
+            "uint8_t": "u8"}
+_CS_TYPES = {"int": "i32", "uint": "u32", "ulong": "u64", "long": "i64", "double": "f64", "float": "f32",
+             "byte": "u8", "IntPtr": "ptr"}
+
+
+def _macros(src):
+    return {m.group(1): int(m.group(2)) for m in re.finditer(r"#define (\w+) (\d+)", src)}
+
+
 def _fields_c(src, name):
+    """[(field, type, length)] of a typedef struct in the header (pointer fields: type 'ptr')."""
+    macros = _macros(src)
     body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), src, re.S).group(1)
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
     out = []
     for decl in body.split(";"):
-        decl = decl.strip()
+        decl = " ".join(decl.replace("const ", "").split())
         if not decl:
             continue
-        names = decl.split(None, 1)[1] if " " in decl else ""
-        for n in names.replace("*", " ").split(","):
-            n = n.strip().split()[-1] if n.strip() else ""
-            m = re.match(r"(\w+)(?:\[(\d+)\])?", n)
-            if m:
-                out.append((m.group(1), int(m.group(2) or 1)))
+        base, names = decl.split(None, 1)
+        base_ptr = base.endswith("*")
+        base = base.rstrip("*")
+        for n in names.split(","):
+            n = n.strip()
+            ptr = base_ptr or n.startswith("*")
+            m = re.match(r"\*?\s*(\w+)(?:\[(\w+)\])?", n)
+            ln = m.group(2)
+            ln = 1 if ln is None else int(ln) if ln.isdigit() else macros[ln]
+            out.append((m.group(1), "ptr" if ptr else _C_TYPES[base], ln))
     return out
 
 
@@ -117,19 +134,28 @@ def _fields_cs(src, name):
         decl = decl.replace("public", "").replace("fixed", "").replace("@", "").strip()
         if not decl:
             continue
-        names = decl.split(None, 1)[1]
+        base, names = decl.split(None, 1)
         for n in names.split(","):
             m = re.match(r"\s*(\w+)(?:\[(\d+)\])?", n)
-            out.append((m.group(1), int(m.group(2) or 1)))
+            out.append((m.group(1), _CS_TYPES[base], int(m.group(2) or 1)))
     return out
+
+
+def _ctype_name(t):
+    if isinstance(t, type) and issubclass(t, C._Pointer) or t in (C.c_void_p, C.c_char_p):
+        return "ptr"
+    return {C.c_int32: "i32", C.c_uint32: "u32", C.c_uint64: "u64", C.c_int64: "i64", C.c_double: "f64",
+            C.c_float: "f32", C.c_uint8: "u8"}[t]
 
 
 @pytest.mark.parametrize("name", ["pt_pass_params", "pt_stats", "pt_mesh_data", "pt_sampler", "pt_device_opts",
                                   "pt_camera", "pt_material", "pt_texture", "pt_scene_desc", "pt_sdf_node",
-                                  "pt_sdf_shape", "pt_volume_window", "pt_volume", "pt_transformed_shape"])
+                                  "pt_sdf_shape", "pt_volume_window", "pt_volume", "pt_transformed_shape",
+                                  "pt_trace_counters"])
 def test_csharp_binding_matches_header(name):
-    """csharp/HipRenderer.cs mirrors include/ptsharp_hip.h field for field (the library
-    writes pt_stats into the caller's struct, so a stale C# layout would be overrun)."""
+    """csharp/HipRenderer.cs mirrors include/ptsharp_hip.h field for field: names, types (a float /
+    double drift would corrupt the P/Invoke) and array lengths (the library writes pt_stats into the
+    caller's struct, so a stale C# layout would be overrun)."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     c = _fields_c(open(HEADER).read(), name)
     cs = _fields_cs(open(os.path.join(root, "csharp", "HipRenderer.cs")).read(), name)
@@ -141,9 +167,17 @@ def test_csharp_binding_matches_header(name):
                                   "pt_sdf_shape", "pt_volume_window", "pt_volume", "pt_transformed_shape",
                                   "pt_trace_counters"])
 def test_python_binding_matches_header(name):
-    """ptsharp_amd/_abi.py mirrors include/ptsharp_hip.h field for field (names and array lengths)."""
+    """ptsharp_amd/_abi.py mirrors include/ptsharp_hip.h field for field (names, types, array lengths)."""
     c = _fields_c(open(HEADER).read(), name)
     py = []
     for fname, ftype in getattr(_abi, name)._fields_:
-        py.append((fname, getattr(ftype, "_length_", 1)))
+        n = getattr(ftype, "_length_", 1)
+        py.append((fname, _ctype_name(ftype._type_ if n > 1 or hasattr(ftype, "_length_") else ftype), n))
     assert py == c
+
+
+def test_csharp_declares_every_entry_point():
+    """Every function of the header has a [DllImport] in the C# drop-in (multi-GPU included)."""
+    cs = open(os.path.join(ROOT, "csharp", "HipRenderer.cs")).read()
+    imported = set(re.findall(r"static extern \w+ (pt_\w+)\(", cs))
+    assert imported == set(declared_functions())

@@ -1,10 +1,10 @@
 """§8f row 4 on the GPU (libptsharp_hip.so through the C-ABI) vs the oracle, same seed:
 SDF shapes (every node kind), Volume, TransformedShape over each inner kind.  Same bar
-as tests/test_gpu_parity.py."""
+as tests/test_gpu_parity.py (tests/parity.py check)."""
 import numpy as np
 import pytest
 
-from parity import MIN_FRACTION_OK, MIN_PSNR_DB, compare, render_both
+from parity import check, render_both
 from ptsharp_amd import Cube, Matrix, Scene, TransformedShape, Vector, _abi, scenes
 
 pytestmark = pytest.mark.gpu
@@ -12,12 +12,6 @@ pytestmark = pytest.mark.gpu
 ENGINES = pytest.mark.parametrize("engine", [_abi.ENGINE_MEGAKERNEL, _abi.ENGINE_WAVEFRONT], ids=["mega", "wave"])
 
 
-def check(g, grays, o, orays):
-    assert np.array_equal(g.N, o.N)
-    frac, maxerr, psnr = compare(g.M, o.M)
-    assert frac >= MIN_FRACTION_OK, f"only {frac:.5f} of pixels within tolerance (max err {maxerr:.3g})"
-    assert psnr >= MIN_PSNR_DB, f"PSNR {psnr:.2f} dB"
-    assert abs(grays - orays) <= 1e-3 * orays + 2, f"rays gpu {grays} vs oracle {orays}"
 
 
 @ENGINES
@@ -48,7 +42,7 @@ def test_transformed_furnace_exact(gpu, engine):
                                                 Matrix.TranslateM(Vector(0, 0, 0))))
     g, gr, o, orr = render_both(s2, cam, smp, 48, 32, spp=2, seed=32, engine=engine)
     assert set(np.unique(g.M)) <= {0.5, 1.0}
-    assert np.array_equal(g.M, o.M) and gr == orr
+    check(g, gr, o, orr, exact=True)
 
 
 def test_row4_adaptive(gpu):

@@ -1,6 +1,10 @@
-# parity tests + wavefront bench (short); stops at the first failing GPU step
+# GPU tests (verbose, per-test durations) then the default bench; each step time-limited, stops at the first failure.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 &&
-timeout -k 10 300 python bench.py --steps 4 --warmup 1 --spp ${SPP:-16} --cpu-seconds 0 --no-parity --engine ${ENGINE:-wave} --json-out gpurun_out/quick.json > gpurun_out/quick.log 2>&1
+T=${1:-q}
+timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread --durations=15 ${PYTEST_ARGS:-} > gpurun_out/${T}_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/${T}_tests.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 600 python -u bench.py --cpu-seconds 5 --json-out gpurun_out/${T}_bench.json > gpurun_out/${T}_bench.log 2>&1
