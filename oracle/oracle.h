@@ -146,6 +146,26 @@ double or_volume_sample(void* scene, int32_t volume, double x, double y, double 
 /* Bounding box of scene primitive (kind, index): IShape.BoundingBox. */
 void or_shape_box(void* scene, int32_t kind, int32_t index, float out_min[3], float out_max[3]);
 
+/* Bounce and light-sampling KATs (checked against tests/sampler_ref.py, a separate Python
+ * restatement of the same C# lines). */
+/* Ray.Bounce (Ray.cs:44-85) at the nearest hit of (origin, dir): 0 on a miss. */
+int32_t or_bounce(void* scene, const float origin[3], const float dir[3], double u, double v, int32_t btype,
+                  uint64_t key, float out_origin[3], float out_dir[3], int32_t* out_reflected, double* out_p);
+/* Util.Cone (Util.cs:17-32). */
+void or_cone(const float dir[3], double theta, double u, double v, uint64_t key, float out[3]);
+/* Scene.Lights (Scene.cs:33-37): returns the count, fills (kind, index) of the first `cap`. */
+int32_t or_lights(void* scene, int32_t* kinds, int32_t* indices, int32_t cap);
+/* Sampler.sampleLight (Sampler.cs:212-296) of Scene.Lights[light] from the normal ray
+ * (origin, normal); returns the Scene.Intersect calls made (0 or 1). */
+int64_t or_sample_light(void* scene, const float origin[3], const float normal[3], int32_t light, uint64_t key,
+                        int32_t soft_shadows, double out[3]);
+/* Sampler.sampleLights (Sampler.cs:191-210); returns the Scene.Intersect calls made. */
+int64_t or_sample_lights(void* scene, const float origin[3], const float normal[3], uint64_t key, int32_t light_mode,
+                         int32_t soft_shadows, double out[3]);
+/* The any-hit form of the shadow query the GPU runs: 1 if some scene shape
+ * (brute force) is hit strictly nearer than t_light along (origin, dir). */
+int32_t or_any_nearer(void* scene, const float origin[3], const float dir[3], double t_light);
+
 /* Counter-based RNG that replaces Random.Shared (spec in DESIGN.md §RNG). */
 uint64_t or_camera_key(uint64_t seed, uint32_t pass, uint64_t pixel, uint32_t sample);
 uint64_t or_child_key(uint64_t key, uint32_t child);

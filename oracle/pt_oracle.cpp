@@ -1586,6 +1586,75 @@ void or_prim_normal(int32_t kind, const float* a, const float* b, const float* c
     out_normal[0] = n.x; out_normal[1] = n.y; out_normal[2] = n.z;
 }
 
+int32_t or_bounce(void* scene, const float origin[3], const float dir[3], double u, double v, int32_t btype,
+                  uint64_t key, float out_origin[3], float out_dir[3], int32_t* out_reflected, double* out_p) {
+    const Scene& s = *(Scene*)scene;
+    Tracer tr(s, false);
+    Ray r{vload(origin), vload(dir)};
+    Hit h = tr.intersect(r);
+    if (!(h.t < HIT_INF)) return 0;
+    HitInfo info = hit_info(s, h, r);
+    Sampler smp{1, 0, true, true, 0, 0};
+    Integrator in(s, smp, tr);
+    bool reflected;
+    double p;
+    Ray o = in.bounce(r, info, u, v, btype, key, reflected, p);
+    out_origin[0] = o.o.x; out_origin[1] = o.o.y; out_origin[2] = o.o.z;
+    out_dir[0] = o.d.x; out_dir[1] = o.d.y; out_dir[2] = o.d.z;
+    *out_reflected = reflected ? 1 : 0;
+    *out_p = p;
+    return 1;
+}
+
+void or_cone(const float dir[3], double theta, double u, double v, uint64_t key, float out[3]) {
+    Scene s;
+    Tracer tr(s, true);
+    Sampler smp{1, 0, true, true, 0, 0};
+    Integrator in(s, smp, tr);
+    V d = in.cone(vload(dir), theta, u, v, key);
+    out[0] = d.x; out[1] = d.y; out[2] = d.z;
+}
+
+int32_t or_lights(void* scene, int32_t* kinds, int32_t* indices, int32_t cap) {
+    const Scene& s = *(Scene*)scene;
+    for (int32_t i = 0; i < (int32_t)s.lights.size() && i < cap; i++) {
+        kinds[i] = s.lights[(size_t)i].kind;
+        indices[i] = s.lights[(size_t)i].idx;
+    }
+    return (int32_t)s.lights.size();
+}
+
+int64_t or_sample_light(void* scene, const float origin[3], const float normal[3], int32_t light, uint64_t key,
+                        int32_t soft_shadows, double out[3]) {
+    const Scene& s = *(Scene*)scene;
+    Tracer tr(s, false);
+    Sampler smp{1, 0, true, soft_shadows != 0, 0, 0};
+    Integrator in(s, smp, tr);
+    C c = in.sample_light(Ray{vload(origin), vload(normal)}, s.lights[(size_t)light], key);
+    out[0] = c.r; out[1] = c.g; out[2] = c.b;
+    return (int64_t)tr.rays;
+}
+
+int64_t or_sample_lights(void* scene, const float origin[3], const float normal[3], uint64_t key, int32_t light_mode,
+                         int32_t soft_shadows, double out[3]) {
+    const Scene& s = *(Scene*)scene;
+    Tracer tr(s, false);
+    Sampler smp{1, 0, true, soft_shadows != 0, light_mode, 0};
+    Integrator in(s, smp, tr);
+    C c = in.sample_lights(Ray{vload(origin), vload(normal)}, key);
+    out[0] = c.r; out[1] = c.g; out[2] = c.b;
+    return (int64_t)tr.rays;
+}
+
+int32_t or_any_nearer(void* scene, const float origin[3], const float dir[3], double t_light) {
+    const Scene& s = *(Scene*)scene;
+    Tracer tr(s, true);
+    const Ray r{vload(origin), vload(dir)};
+    for (const ShapeRef& sh : s.shapes)
+        if (tr.shape_intersect(sh, r).t < t_light) return 1;
+    return 0;
+}
+
 void or_texture_sample(void* scene, int32_t texture, int32_t kind, double u, double v, double out[3]) {
     const Scene& s = *(Scene*)scene;
     const Tex& t = s.texs[(size_t)(texture - 1)];

@@ -72,6 +72,17 @@ def lib() -> C.CDLL:
         L.or_light_key.argtypes = [C.c_uint64, C.c_uint32]
         L.or_draw.restype = C.c_double
         L.or_draw.argtypes = [C.c_uint64, C.c_uint32]
+        L.or_bounce.restype = C.c_int32
+        L.or_bounce.argtypes = [vp, f3, f3, C.c_double, C.c_double, C.c_int32, C.c_uint64, f3, f3, i32p, dp]
+        L.or_cone.argtypes = [f3, C.c_double, C.c_double, C.c_double, C.c_uint64, f3]
+        L.or_lights.restype = C.c_int32
+        L.or_lights.argtypes = [vp, i32p, i32p, C.c_int32]
+        L.or_sample_light.restype = C.c_int64
+        L.or_sample_light.argtypes = [vp, f3, f3, C.c_int32, C.c_uint64, C.c_int32, dp]
+        L.or_sample_lights.restype = C.c_int64
+        L.or_sample_lights.argtypes = [vp, f3, f3, C.c_uint64, C.c_int32, C.c_int32, dp]
+        L.or_any_nearer.restype = C.c_int32
+        L.or_any_nearer.argtypes = [vp, f3, f3, C.c_double]
         _lib = L
     return _lib
 
@@ -96,6 +107,31 @@ class OracleScene:
         k, i = C.c_int32(), C.c_int32()
         t = lib().or_intersect(self.h, f3(origin), f3(direction), int(brute), C.byref(k), C.byref(i))
         return t, k.value, i.value
+
+    def bounce(self, origin, direction, u, v, btype, key):
+        """Ray.Bounce at the nearest hit: (origin, direction, reflected, p) or None on a miss."""
+        o, d, refl, p = (C.c_float * 3)(), (C.c_float * 3)(), C.c_int32(), C.c_double()
+        if not lib().or_bounce(self.h, f3(origin), f3(direction), u, v, btype, key, o, d, C.byref(refl), C.byref(p)):
+            return None
+        return tuple(o), tuple(d), bool(refl.value), p.value
+
+    def lights(self):
+        k, i = (C.c_int32 * 64)(), (C.c_int32 * 64)()
+        n = lib().or_lights(self.h, k, i, 64)
+        return [(k[j], i[j]) for j in range(min(n, 64))]
+
+    def sample_light(self, origin, normal, light, key, soft_shadows=True):
+        out = (C.c_double * 3)()
+        rays = lib().or_sample_light(self.h, f3(origin), f3(normal), light, key, int(soft_shadows), out)
+        return tuple(out), rays
+
+    def sample_lights(self, origin, normal, key, light_mode, soft_shadows=True):
+        out = (C.c_double * 3)()
+        rays = lib().or_sample_lights(self.h, f3(origin), f3(normal), key, int(light_mode), int(soft_shadows), out)
+        return tuple(out), rays
+
+    def any_nearer(self, origin, direction, t_light) -> bool:
+        return bool(lib().or_any_nearer(self.h, f3(origin), f3(direction), t_light))
 
     def tree_nodes(self) -> int:
         return lib().or_scene_tree_nodes(self.h)

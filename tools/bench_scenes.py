@@ -34,18 +34,18 @@ def main():
         r.Synchronize()
         t0 = time.perf_counter()
         rays = 0
-        kms = np.zeros(6)
+        kms = np.zeros(_abi.K_SLOTS)
         for _ in range(a.passes):
             r.RenderParallel()
             st = r.Stats()
             rays += st.rays
-            kms += np.array(st.kernel_ms[:6])
+            kms += np.array(st.kernel_ms[:])
         r.Synchronize()
         dt = time.perf_counter() - t0
-        names = ["camera", "trace", "shade", "shadow", "finalize", "mega"]
+        names = ["camera", "trace", "shade", "shadow", "finalize", "mega", "accum", "-"]
         print(json.dumps({"scene": name, "Mrays_per_s": round(rays / dt / 1e6, 1),
                           "rays_per_pass": rays // a.passes,
-                          "ms_per_pass": {names[k]: round(kms[k] / a.passes, 3) for k in range(6) if kms[k]}}),
+                          "ms_per_pass": {names[k]: round(kms[k] / a.passes, 3) for k in range(_abi.K_SLOTS) if kms[k]}}),
               flush=True)
         r.close()
 

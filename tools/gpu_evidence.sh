@@ -1,12 +1,31 @@
-# Round evidence: all GPU tests, smoke, rocprofv3 kernel trace + FETCH/WRITE passes,
-# PMC summary (profiles/pmc_traffic.json, read by the bench), then the default bench.
+# Round evidence, one gpurun call (each GPU step time-limited; stops at the first failure):
+#   GPU tests + smoke; rocprofv3 kernel trace + stats and the FETCH_SIZE / WRITE_SIZE passes of the
+#   bench workload (separate runs, no sys/runtime trace with --pmc) -> profiles/<tag>_* and
+#   profiles/pmc_traffic.json; the default bench; residency / cache counters at the bench's own
+#   configuration (C4, 16 spp, one full pass per step); per-rank shard workloads (N = 2, 4, 8).
+# usage: bash tools/gpu_evidence.sh r02a [quick]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-TAG=${1:-r01}
-mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_all.log 2>&1 && \
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-bash tools/gpu_profile.sh $TAG && \
-python tools/pmc_summary.py gpurun_out/prof_$TAG $TAG > gpurun_out/pmc_summary_$TAG.log 2>&1 && \
-cp profiles/pmc_traffic.json gpurun_out/pmc_traffic_$TAG.json && \
-timeout -k 10 900 python bench.py --json-out gpurun_out/bench_default.json > gpurun_out/bench_default.log 2>&1
+export TMPDIR=/tmp
+TAG=${1:-r02}
+D=gpurun_out/ev_$TAG
+mkdir -p $D
+PROF="--steps 4 --warmup 1 --spp 16 --cpu-seconds 0 --no-parity"
+CTR="--steps 2 --warmup 1 --spp 16 --cpu-seconds 0 --no-parity"
+pmc() { P=$1; shift; timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-trace -d $D/$P -o p --output-format csv -- python3 bench.py $CTR > $D/$P.log 2>&1; }
+timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread > $D/tests.log 2>&1 && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/trace -o trace --output-format csv -- python3 bench.py $PROF --json-out $D/bench_trace.json > $D/trace.log 2>&1 && \
+timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $D/fetch -o fetch --output-format csv -- python3 bench.py $PROF --json-out $D/bench_fetch.json > $D/fetch.log 2>&1 && \
+timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $D/write -o write --output-format csv -- python3 bench.py $PROF --json-out $D/bench_write.json > $D/write.log 2>&1 && \
+python tools/pmc_summary.py $D $TAG > $D/pmc_summary.log 2>&1 && \
+timeout -k 10 900 python -u bench.py --json-out $D/bench_default.json > $D/bench_default.log 2>&1 || exit 1
+[ "$2" = quick ] && exit 0
+pmc p4 SQ_LEVEL_WAVES SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU && \
+pmc p5 TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TA_TA_BUSY_sum TCP_PERF_SEL_TOTAL_HIT_LRU_READ_sum TCP_PERF_SEL_TOTAL_MISS_LRU_READ_sum && \
+pmc p6 TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum && \
+python tools/residency.py $D $TAG > $D/residency.txt 2>&1 || exit 1
+for N in 2 4 8; do
+  timeout -k 10 300 python bench.py --shard 0/$N --steps 16 --warmup 2 --cpu-seconds 0 --no-parity --json-out $D/shard_0of$N.json > $D/shard_0of$N.log 2>&1 || exit 1
+done
+timeout -k 10 600 python tools/bench_scenes.py > $D/scenes.jsonl 2> $D/scenes.log

@@ -23,9 +23,9 @@ for far in (False, True, None):
     r = Renderer.NewRenderer(scene, camera, sampler, 3840, 2160, True)
     r.SamplesPerPixel = 1; r.Seed = 1234; r.Engine = _abi.ENGINE_WAVEFRONT
     r.RenderParallel(); r.Flags = _abi.PASS_KERNEL_TIMING; r.Synchronize()
-    t0 = time.perf_counter(); rays = 0; kms = np.zeros(6)
+    t0 = time.perf_counter(); rays = 0; kms = np.zeros(_abi.K_SLOTS)
     for _ in range(2):
-        r.RenderParallel(); st = r.Stats(); rays += st.rays; kms += np.array(st.kernel_ms[:6])
+        r.RenderParallel(); st = r.Stats(); rays += st.rays; kms += np.array(st.kernel_ms[:])
     r.Synchronize(); dt = time.perf_counter() - t0
     print(json.dumps({"far": far, "Mrays": round(rays/dt/1e6,1), "trace": round(kms[1]/2,1), "shade": round(kms[2]/2,1), "shadow": round(kms[3]/2,1)}), flush=True)
     r.close()

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turn a tools/gpu_profile.sh output directory into committed evidence under profiles/:
+"""Turn a tools/gpu_evidence.sh output directory into committed evidence under profiles/:
 <tag>_kernel_stats.csv (rocprofv3 --stats), <tag>_bench_under_rocprof.json, and
 profiles/pmc_traffic.json: FETCH/WRITE traffic per closest-hit ray of the dominant kernel.
 

@@ -20,12 +20,12 @@ for mb in range(0, 5):
     r.Engine = _abi.ENGINE_WAVEFRONT
     r.RenderParallel()  # warm-up
     r.Flags = _abi.PASS_KERNEL_TIMING
-    ms = np.zeros(6)
+    ms = np.zeros(_abi.K_SLOTS)
     rays = shadow = 0
     for _ in range(3):
         r.RenderParallel()
         st = r.Stats()
-        ms += np.array(st.kernel_ms[:6])
+        ms += np.array(st.kernel_ms[:])
         rays += st.rays - st.shadow_rays
         shadow += st.shadow_rays
     r.close()

@@ -1,6 +1,6 @@
-"""Per-kernel residency / issue / cache figures from tools/gpu_counters2.sh output.
+"""Per-kernel residency / issue / cache figures from tools/gpu_evidence.sh output.
 
-usage: python tools/residency.py gpurun_out/lat_<tag> [label]
+usage: python tools/residency.py gpurun_out/ev_<tag> [label]   (tools/gpu_evidence.sh)
 p4: SQ_WAVE_CYCLES, SQ_INSTS_VALU, GRBM_GUI_ACTIVE; p5: TA / TCP stalls; p6: L2 hit and the
 fabric read-request level (Little's law latency).  cycles = GRBM_GUI_ACTIVE / 8 (the counter
 sums over the 8 XCDs); per-SIMD ratios divide by 1024 SIMDs, per-CU ratios by 256 CUs."""
@@ -31,7 +31,7 @@ label = sys.argv[2] if len(sys.argv) > 2 else d
 p4, t4 = load(d, "p4")
 p5, t5 = load(d, "p5")
 p6, _ = load(d, "p6")
-print(f"# rocprofv3 --pmc passes (kernel-trace only) of `bench.py --steps 2 --warmup 1 --spp 4 --engine wave`, {label}.")
+print(f"# rocprofv3 --pmc passes (kernel-trace only) of `bench.py --steps 2 --warmup 1 --spp 16` (the bench configuration, tools/gpu_evidence.sh), {label}.")
 print("# SQ_WAVE_CYCLES counts quad-cycles; cycles = GRBM_GUI_ACTIVE / 8 (sum over XCDs). Per-CU ratios divide by 256 CUs.")
 for k in KERNELS:
     if k not in p4 or t4.get(k, 0) <= 0:
