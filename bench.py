@@ -232,6 +232,7 @@ def main():
             "avg_launch_ms": round(float(avg_launch_ms), 4), "launches": int(klaunch[dom]),
             "bytes_per_launch": round(dom_bytes / max(klaunch[dom], 1)),
             "bytes_per_ray": round(per_ray, 2),
+            "rays_per_launch": round(rays_per_launch),
             "nodes_per_ray": round((ext_nodes if dom == _abi.K_TRACE else ctr.nodes_visited) /
                                    max(ext_rays if dom == _abi.K_TRACE else ctr.rays, 1), 3),
             "prims_per_ray": round((ext_prims if dom == _abi.K_TRACE else ctr.prims_tested) /
