@@ -61,6 +61,37 @@ __device__ __forceinline__ void q_store(float4* p, float4 v) { *p = v; }
 __device__ __forceinline__ void q_store(uint4* p, uint4 v) { *p = v; }
 __device__ __forceinline__ void q_store(double2* p, double2 v) { *p = v; }
 __device__ __forceinline__ void q_store(ulonglong2* p, ulonglong2 v) { *p = v; }
+// Queue stores are non-temporal (PT_QSTORE_NT=2): with the child-major fill every store
+// instruction writes whole lines, and keeping the streamed queues out of the caches helped
+// k_wf_shade (C4 shade 29.9 → 28.2 ms/step, 4963 → 5040 Mrays/s; 1 = only the data read two
+// kernels later — throughput, key, light terms: 29.2 ms).  3 adds the closest-hit records.
+#ifndef PT_QSTORE_NT
+#define PT_QSTORE_NT 2
+#endif
+typedef float f4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void q_store_nt(double2* p, double2 v) {
+    __builtin_nontemporal_store(__builtin_bit_cast(f4s, v), (f4s*)p);
+}
+__device__ __forceinline__ void q_store_nt(ulonglong2* p, ulonglong2 v) {
+    __builtin_nontemporal_store(__builtin_bit_cast(f4s, v), (f4s*)p);
+}
+__device__ __forceinline__ void q_store_nt(float4* p, float4 v) {
+    __builtin_nontemporal_store(__builtin_bit_cast(f4s, v), (f4s*)p);
+}
+template <class T>
+__device__ __forceinline__ void q_store_late(T* p, T v) {
+    if (PT_QSTORE_NT >= 1) q_store_nt(p, v); else q_store(p, v);
+}
+template <class T>
+__device__ __forceinline__ void q_store_next(T* p, T v) {
+    if (PT_QSTORE_NT >= 2) q_store_nt(p, v); else q_store(p, v);
+}
+__device__ __forceinline__ void q_store_nt(uint4* p, uint4 v) {
+    __builtin_nontemporal_store(__builtin_bit_cast(f4s, v), (f4s*)p);
+}
+__device__ __forceinline__ void hit_store(uint4* p, uint4 v) {
+    if (PT_QSTORE_NT >= 3) q_store_nt(p, v); else q_store(p, v);
+}
 __device__ __forceinline__ float4 nt_load(const float4* p) {
     f4v x = __builtin_nontemporal_load((const f4v*)p);
     return make_float4(x.x, x.y, x.z, x.w);
@@ -159,10 +190,10 @@ __device__ __forceinline__ void block_reserve2(unsigned long long* word, uint32_
 // Throughput (fp64) rides in two 16-B fields: {r, g} and {key, b}.
 __device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, const double thr[3],
                                           uint32_t pixel, uint32_t meta, uint64_t key) {
-    q_store(&Q.q_o[q][i], make_float4(o.x, o.y, o.z, __uint_as_float(pixel)));
-    q_store(&Q.q_d[q][i], make_float4(d.x, d.y, d.z, __uint_as_float(meta)));
-    q_store(&Q.q_t[q][i], make_double2(thr[0], thr[1]));
-    q_store(&Q.q_k[q][i], make_ulonglong2(key, (unsigned long long)__double_as_longlong(thr[2])));
+    q_store_next(&Q.q_o[q][i], make_float4(o.x, o.y, o.z, __uint_as_float(pixel)));
+    q_store_next(&Q.q_d[q][i], make_float4(d.x, d.y, d.z, __uint_as_float(meta)));
+    q_store_late(&Q.q_t[q][i], make_double2(thr[0], thr[1]));
+    q_store_late(&Q.q_k[q][i], make_ulonglong2(key, (unsigned long long)__double_as_longlong(thr[2])));
 }
 __device__ __forceinline__ void ray_store_camera(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, uint32_t pixel,
                                                  uint64_t key) {
@@ -267,14 +298,14 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
             const uint32_t i = base + k0 + lane;
             float4 b = nt_load(&Q.q_d[qi][i]);
             if (__float_as_uint(b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
-                q_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
+                hit_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
                 continue;
             }
             float4 a = nt_load(&Q.q_o[qi][i]);
             HitRec h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
             kept += (h.kind >= 0 || !env_black) ? 1u : 0u;
             unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
-            q_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
+            hit_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
         }
     }
     uint32_t rays = wave_sum(ctr.rays);
@@ -337,7 +368,7 @@ __global__ __launch_bounds__(kTB, PT_TRACE_WAVES) void k_wf_trace_lanes(DevScene
     float tmax = 0.f;
     auto finish = [&]() {
         unsigned long long tb = (unsigned long long)__double_as_longlong(bt);
-        q_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
+        hit_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
         kept += (bkind >= 0 || !env_black) ? 1u : 0u;
         has = false;
     };
@@ -355,7 +386,7 @@ __global__ __launch_bounds__(kTB, PT_TRACE_WAVES) void k_wf_trace_lanes(DevScene
                 const float4 b = nt_load(&Q.q_d[qi][i]);
                 const float4 a = nt_load(&Q.q_o[qi][i]);
                 if (__float_as_uint(b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
-                    q_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
+                    hit_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
                 } else {
                     has = true;
                     ctr.rays++;
@@ -623,10 +654,10 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
                     else { lc.x *= nl; lc.y *= nl; lc.z *= nl; }
                     if (my_n + j < Q.spcap) {
                         const uint32_t at = G.g * Q.spcap + my_n + j;
-                        q_store(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
-                        q_store(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
-                        q_store(&Q.n_w[2 * (size_t)at], make_double2((t2[0] * w[0]) * lc.x, (t2[1] * w[1]) * lc.y));
-                        q_store(&Q.n_w[2 * (size_t)at + 1], make_double2((t2[2] * w[2]) * lc.z, 0.0));
+                        q_store_next(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
+                        q_store_next(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
+                        q_store_late(&Q.n_w[2 * (size_t)at], make_double2((t2[0] * w[0]) * lc.x, (t2[1] * w[1]) * lc.y));
+                        q_store_late(&Q.n_w[2 * (size_t)at + 1], make_double2((t2[2] * w[2]) * lc.z, 0.0));
                     }
                 }
             }
