@@ -20,11 +20,14 @@
  *                        → Buffer.AddSample (Welford)                     Buffer.cs:33-44,94-97
  *   pt_read_buffer     reading Renderer.PBuffer pixels {Samples, M, V}     Buffer.cs:18-58, Renderer.cs:20
  *   pt_reset_buffer    Renderer.PBuffer = new Buffer(w,h)                  Renderer.cs:41
+ *   pt_write_buffer    resuming IterativeRender from a saved PBuffer       Renderer.cs:702-765
  *   pt_stats           Scene.rays (Interlocked counter, never printed)     Scene.cs:70-79
  *                      + the "time elapsed" stopwatch                      Renderer.cs:212-213,470
  *   pt_last_error      oidnGetDeviceError(device, out msg)                 OIDN.cs:85-86
  *   pt_destroy         oidnReleaseDevice                                   OIDN.cs:55-56
  *   pt_comm_*          (new) Buffer gather across GPUs over RCCL/xGMI      SURVEY.md §8e
+ *                      (one process per GPU, or one process on all GPUs:  Renderer.cs:257-333 is one
+ *                       pt_comm_init_all / pt_comm_gather_all)            process on all cores)
  *
  * Conventions: every function returns PT_OK (0) or a negative pt_status; the
  * detail string of the last failure on the calling thread is pt_last_error().

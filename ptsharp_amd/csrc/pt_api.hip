@@ -108,7 +108,7 @@ struct Ctx {
     int width = 0, height = 0;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;                          // shadow passes (pt::WfPlan::side)
-    hipEvent_t ev_main = nullptr, ev_side = nullptr;
+    hipEvent_t ev_main = nullptr, ev_side[2] = {nullptr, nullptr};
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // Welford buffer
     double* d_m = nullptr;
@@ -149,8 +149,8 @@ struct Ctx {
 // samples whose widest depth fits the queues; every chunk pays the fill and drain of
 // 16 persistent launches, so fewer, larger chunks are faster (C4, 16 spp per pass: 8
 // chunks of 32M-entry queues 2574 Mrays/s, 2 chunks 2809, one chunk 2853).  The bound is
-// the largest power of two whose queues (208 B per entry: two extension queues of
-// o, d, throughput r g, key + throughput b + hits + one shadow queue) fit a quarter of the device's memory
+// the largest power of two whose queues (274 B per entry: two extension queues of
+// o, d, throughput r g, key + throughput b + hits + two shadow sets) fit a quarter of the device's memory
 // and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
 // MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
@@ -158,7 +158,7 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #define PT_SIDE_MAX_CHUNK (20u << 20)
 #endif
 constexpr uint64_t kSideStreamMaxChunk = PT_SIDE_MAX_CHUNK;   // camera samples
-constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 64 + 1;
+constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 2 * (64 + 1);
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
 uint32_t wf_max_cap(Ctx* c) {
@@ -217,10 +217,12 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
         if ((rc = wf_alloc(c, &Q.q_k[q], cap))) return rc;
     }
     if ((rc = wf_alloc(c, &Q.hits, cap))) return rc;
-    if ((rc = wf_alloc(c, &Q.n_o, scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.n_n, scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.n_w, 2 * (size_t)scap))) return rc;
-    if ((rc = wf_alloc(c, &Q.n_lit, scap))) return rc;
+    for (int q = 0; q < 2; q++) {   // shadow-ray sets by depth parity
+        if ((rc = wf_alloc(c, &Q.n_o[q], scap))) return rc;
+        if ((rc = wf_alloc(c, &Q.n_n[q], scap))) return rc;
+        if ((rc = wf_alloc(c, &Q.n_w[q], 2 * (size_t)scap))) return rc;
+        if ((rc = wf_alloc(c, &Q.n_lit[q], scap))) return rc;
+    }
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
     // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
     // can run at the same time on the side stream)
@@ -598,7 +600,8 @@ int pt_create(const pt_device_opts* opts, void** out_ctx) {
         return cleanup(fail(PT_ERR_HIP, "events"));
     if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&c->ev_side[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_side[1], hipEventDisableTiming) != hipSuccess)
         return cleanup(fail(PT_ERR_HIP, "side stream"));
     size_t P = (size_t)c->width * (size_t)c->height;
     if (hipMalloc(&c->d_m, P * 3 * sizeof(double)) != hipSuccess || hipMalloc(&c->d_v, P * 3 * sizeof(double)) != hipSuccess ||
@@ -1130,7 +1133,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         if (side) {
             plan.side = c->side;
             plan.ev_main = c->ev_main;
-            plan.ev_side = c->ev_side;
+            plan.ev_side[0] = c->ev_side[0];
+            plan.ev_side[1] = c->ev_side[1];
         }
         const double group_samples = group_max(chunk);
         const double need = group_samples * per_sample;   // a partition's widest depth
@@ -1304,7 +1308,7 @@ void pt_destroy(void* ctx) {
     if (c->d_own) (void)hipFree(c->d_own);
     c->timer.destroy();
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
-    if (c->ev_side) (void)hipEventDestroy(c->ev_side);
+    for (hipEvent_t e : c->ev_side) if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);

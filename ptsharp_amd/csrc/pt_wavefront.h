@@ -22,11 +22,14 @@ struct WfQueues {
     double2* q_t[2];     // {throughput.r, throughput.g} (fp64, as the reference's Colour)
     ulonglong2* q_k[2];  // {RNG node key of the vertex the ray leads to, throughput.b (fp64 bits)}
     uint4* hits;         // {t (fp64 bits), kind, record}
-    float4* n_o;         // shadow rays (a diffuse child's sampleLights, set up by k_wf_shade): {origin.xyz, pixel}
-    float4* n_n;         // {direction.xyz, light index | kDead: no ray cast (diffuse <= 0)}
-    double2* n_w;        // two per entry, {r, g} {b, -}: throughput·weight·light colour·coverage (fp64),
+    // Shadow rays (a diffuse child's sampleLights, set up by k_wf_shade), two sets by depth
+    // parity (set q holds the shadow rays counted in pair word q), so the shadow pass and the
+    // light-term accumulation of depth d can run beside the closest-hit and shade passes of d + 1.
+    float4* n_o[2];      // {origin.xyz, pixel}
+    float4* n_n[2];      // {direction.xyz, light index | kDead: no ray cast (diffuse <= 0)}
+    double2* n_w[2];     // two per entry, {r, g} {b, -}: throughput·weight·light colour·coverage (fp64),
                          // added if the light is visible
-    uint8_t* n_lit;      // per entry: 1 = the light is the nearest hit (k_wf_shadow*), read by k_wf_nee_accum
+    uint8_t* n_lit[2];   // per entry: 1 = the light is the nearest hit (k_wf_shadow*), read by k_wf_nee_accum
     uint32_t* counts;    // counter slots, each kCountStride words apart (see count_word below):
                          // slot q·kParts+g = {rays, NEE requests} of partition g of ray queue q
                          // (one packed 64-bit word, reserved together); slot kFetchSlot + k·kParts + g
@@ -51,14 +54,14 @@ struct WfQueues {
 constexpr int kCountStride = PT_COUNT_STRIDE;
 static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
 constexpr int kFetchSlot = 2 * kParts;
-constexpr int kKeptSlot = 5 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
-constexpr int kFlagSlot = 5 * kParts + 2;
+constexpr int kKeptSlot = 6 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
+constexpr int kFlagSlot = 6 * kParts + 2;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kFlagWord = count_word(kFlagSlot);
 constexpr int kCountWords = count_word(kFlagSlot + 1);
 constexpr int kChunkResetWords = count_word(kFlagSlot);   // pair words + fetch cursors, zeroed per chunk
-// work-fetch cursor of kernel k (0 trace, 1 shade, 2 shadow) in partition g
+// work-fetch cursor of kernel k (0 trace, 1 shade, 2 + q shadow rays of set q) in partition g
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
 
@@ -80,9 +83,10 @@ struct WfPlan {
                                // (PT_LANES=0|1 in the environment; tests)
     // Optional second stream: each depth's shadow pass runs there, beside the next depth's
     // closest-hit pass (independent queues), so one fills the other's ramp and tail.
-    // ev_main / ev_side order shade(d) → shadow(d) → shade(d + 1).  Null: one stream.
+    // ev_main orders shade(d) → shadow(d); ev_side[q], recorded after the light terms of
+    // shadow set q were added, orders them before shade(d + 2) rewrites set q.  Null: one stream.
     hipStream_t side;
-    hipEvent_t ev_main, ev_side;
+    hipEvent_t ev_main, ev_side[2];
 };
 
 // Optional per-launch timing hook (hipEvent pairs recorded around each kernel on the

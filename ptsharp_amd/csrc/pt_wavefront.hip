@@ -654,10 +654,10 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
                     else { lc.x *= nl; lc.y *= nl; lc.z *= nl; }
                     if (my_n + j < Q.spcap) {
                         const uint32_t at = G.g * Q.spcap + my_n + j;
-                        q_store_next(&Q.n_o[at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
-                        q_store_next(&Q.n_n[at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
-                        q_store_late(&Q.n_w[2 * (size_t)at], make_double2((t2[0] * w[0]) * lc.x, (t2[1] * w[1]) * lc.y));
-                        q_store_late(&Q.n_w[2 * (size_t)at + 1], make_double2((t2[2] * w[2]) * lc.z, 0.0));
+                        q_store_next(&Q.n_o[qo][at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
+                        q_store_next(&Q.n_n[qo][at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
+                        q_store_late(&Q.n_w[qo][2 * (size_t)at], make_double2((t2[0] * w[0]) * lc.x, (t2[1] * w[1]) * lc.y));
+                        q_store_late(&Q.n_w[qo][2 * (size_t)at + 1], make_double2((t2[2] * w[2]) * lc.z, 0.0));
                     }
                 }
             }
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     const bool scan = form ? form == 2 : 2ull * Q.counts[kept_word(qi)] < (unsigned long long)queued;
     if (scan != SCAN) return;
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
-        Q.counts[fetch_word(2, threadIdx.x)] = 0u;              // k_wf_shadow's fetch cursors
+        Q.counts[fetch_word(2 + (1 - qi), threadIdx.x)] = 0u;   // the fetch cursors of the shadow rays it writes
         Q.counts[fetch_word(0, threadIdx.x)] = 0u;              // the next k_wf_trace's (it may run beside k_wf_shadow)
         if (threadIdx.x == 0) Q.counts[kept_word(1 - qi)] = 0u;   // the next k_wf_trace's kept count
     }
@@ -774,7 +774,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
-    uint32_t* cursor = Q.counts + fetch_word(2, G.g);
+    uint32_t* cursor = Q.counts + fetch_word(2 + qo, G.g);
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
     for (;;) {  // kFetchBatches × 64 rays per claim, 64 at a time (see k_wf_trace)
@@ -786,14 +786,14 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
             const uint32_t i = base + k0 + lane;
             if (k0 + lane >= n) continue;
             bool lit = false;
-            const float4 b = nt_load(&Q.n_n[i]);
+            const float4 b = nt_load(&Q.n_n[qo][i]);
             const uint32_t li = __float_as_uint(b.w);
             if (li != kDead) {
-                const float4 a = nt_load(&Q.n_o[i]);
+                const float4 a = nt_load(&Q.n_o[qo][i]);
                 const DevLight L = S.lights[li];
                 lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
             }
-            Q.n_lit[i] = lit ? 1 : 0;   // k_wf_nee_accum adds the lit rays' terms
+            Q.n_lit[qo][i] = lit ? 1 : 0;   // k_wf_nee_accum adds the lit rays' terms
         }
     }
     uint32_t rays = wave_sum(ctr.rays);
@@ -818,7 +818,7 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
-    uint32_t* cursor = Q.counts + fetch_word(2, G.g);
+    uint32_t* cursor = Q.counts + fetch_word(2 + qo, G.g);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     Counters ctr{0, 0, 0, 0};
@@ -840,11 +840,11 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
             const uint32_t k = kc + (uint32_t)__popcll(idle & below);
             if (!has && k < n) {
                 i = base + k;
-                const float4 b = nt_load(&Q.n_n[i]);
-                const float4 a = nt_load(&Q.n_o[i]);
+                const float4 b = nt_load(&Q.n_n[qo][i]);
+                const float4 a = nt_load(&Q.n_o[qo][i]);
                 const uint32_t li = __float_as_uint(b.w);
                 if (li == kDead) {
-                    Q.n_lit[i] = 0;
+                    Q.n_lit[qo][i] = 0;
                 } else {   // light_visible (pt_device.h), head part
                     ctr.rays++;
                     const DevLight L = S.lights[li];
@@ -870,7 +870,7 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
                     sp = 0;
                     ref = 0;
                     has = run;
-                    if (!run) Q.n_lit[i] = 0;
+                    if (!run) Q.n_lit[qo][i] = 0;
                 }
             }
         }
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
         }
         if (blocked) {
             has = false;
-            Q.n_lit[i] = 0;
+            Q.n_lit[qo][i] = 0;
         } else if (pop) {
             if (sp > 0) {
                 sp--;
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevSce
                 ref = 0;
             } else {   // no primitive nearer than the light: lit (a phantom light never is)
                 has = false;
-                Q.n_lit[i] = phantom ? 0 : 1;
+                Q.n_lit[qo][i] = phantom ? 0 : 1;
             }
         }
     }
@@ -971,11 +971,11 @@ __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsign
         double2 w01 = make_double2(0.0, 0.0), w2 = w01;
         if (j < n) {
             const size_t i = base + j;
-            lit = Q.n_lit[i] != 0;
+            lit = Q.n_lit[qo][i] != 0;
             if (lit) {
-                pixel = __float_as_uint(nt_load(&Q.n_o[i]).w);
-                w01 = nt_load(&Q.n_w[2 * i]);
-                w2 = nt_load(&Q.n_w[2 * i + 1]);
+                pixel = __float_as_uint(nt_load(&Q.n_o[qo][i]).w);
+                w01 = nt_load(&Q.n_w[qo][2 * i]);
+                w2 = nt_load(&Q.n_w[qo][2 * i + 1]);
             }
         }
         const uint32_t r = fix_add_wave(Q.acc, pixel, lit, w01.x, w01.y, w2.x);
@@ -1117,7 +1117,6 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     int qi = 0;
     trace(qi, bound);
     for (int depth = 0; depth <= smp.mb; depth++) {
-        if (plan.side && depth > 0) (void)hipStreamWaitEvent(stream, plan.ev_side, 0);   // shadow(d-1) read its queue
         const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
         begin_k(2, stream);
         // both forms (the one the kept count selects runs, the other returns at once)
@@ -1156,12 +1155,18 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         if (count) hipLaunchKernelGGL((k_wf_nee_accum<true>), dim3(ag), dim3(256), 0, side, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_nee_accum<false>), dim3(ag), dim3(256), 0, side, Q, 1 - qi, B.counters);
         end_k(6, side);
-        if (plan.side) (void)hipEventRecord(plan.ev_side, side);
+        if (plan.side) (void)hipEventRecord(plan.ev_side[1 - qi], side);
         bound = children < Q.cap ? children : Q.cap;
         qi = 1 - qi;
+        // trace(d + 1) frees pair word 1 - qi and shade(d + 1) rewrites shadow set 1 - qi: the
+        // shadow pass and the light-term accumulation of depth d - 1 read both
+        if (plan.side && depth >= 1) (void)hipStreamWaitEvent(stream, plan.ev_side[1 - qi], 0);
         if (depth < smp.mb) trace(qi, bound);
     }
-    if (plan.side) (void)hipStreamWaitEvent(stream, plan.ev_side, 0);   // the chunk ends with its last shadow pass
+    if (plan.side) {   // the chunk ends with its last two shadow passes
+        (void)hipStreamWaitEvent(stream, plan.ev_side[0], 0);
+        (void)hipStreamWaitEvent(stream, plan.ev_side[1], 0);
+    }
 }
 
 hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
