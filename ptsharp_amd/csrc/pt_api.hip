@@ -114,9 +114,11 @@ struct Ctx {
     double* d_m = nullptr;
     double* d_v = nullptr;
     int32_t* d_n = nullptr;
-    unsigned long long* d_counters = nullptr;
+    unsigned long long* d_counters = nullptr;   // [16] the pass' counters (pt::DevBuffer::counters)
+    unsigned long long* h_counters = nullptr;   // [16] pinned: their read-back
     int32_t* d_tiles = nullptr;
     int32_t tiles_cap = 0;
+    std::vector<int32_t> h_tiles;               // the tile list in d_tiles (uploaded when it changes)
     // scene
     bool has_scene = false;
     std::vector<DeviceArray> scene_arrays;
@@ -224,6 +226,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
         if ((rc = wf_alloc(c, &Q.n_lit[q], scap))) return rc;
     }
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
+    Q.overflow = c->d_counters + pt::kOverflowCounter;
     // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
     // can run at the same time on the side stream)
     const size_t ovf_words = (size_t)(pt::kMaxDepth - pt::kLdsStack) * pt::kWfMaxThreads;
@@ -606,7 +609,8 @@ int pt_create(const pt_device_opts* opts, void** out_ctx) {
     size_t P = (size_t)c->width * (size_t)c->height;
     if (hipMalloc(&c->d_m, P * 3 * sizeof(double)) != hipSuccess || hipMalloc(&c->d_v, P * 3 * sizeof(double)) != hipSuccess ||
         hipMalloc(&c->d_n, P * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess)
+        hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(&c->h_counters, 16 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
         return cleanup(fail(PT_ERR_OUT_OF_MEMORY, "buffer allocation"));
     int rc = pt_reset_buffer(c);
     if (rc != PT_OK) return cleanup(rc);
@@ -1067,11 +1071,17 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         if (pass->num_tiles > c->tiles_cap) {
             if (c->d_tiles) (void)hipFree(c->d_tiles);
             c->d_tiles = nullptr;
+            c->h_tiles.clear();
             PT_HIP(hipMalloc(&c->d_tiles, (size_t)pass->num_tiles * sizeof(int32_t)));
             c->tiles_cap = pass->num_tiles;
         }
-        PT_HIP(hipMemcpyAsync(c->d_tiles, pass->tiles, (size_t)pass->num_tiles * sizeof(int32_t), hipMemcpyHostToDevice,
-                              c->stream));
+        // the same list pass after pass (a rank's tiles): uploaded once
+        if (c->h_tiles.size() != (size_t)pass->num_tiles ||
+            std::memcmp(c->h_tiles.data(), pass->tiles, (size_t)pass->num_tiles * sizeof(int32_t))) {
+            c->h_tiles.assign(pass->tiles, pass->tiles + pass->num_tiles);
+            PT_HIP(hipMemcpyAsync(c->d_tiles, c->h_tiles.data(), (size_t)pass->num_tiles * sizeof(int32_t),
+                                  hipMemcpyHostToDevice, c->stream));
+        }
         d_tiles = c->d_tiles;
         num_tiles = pass->num_tiles;
     }
@@ -1164,9 +1174,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     }
     const bool timing = (pass->flags & PT_PASS_KERNEL_TIMING) != 0;
     c->timer.reset(c->stream);
-    PT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
-    if (engine == PT_ENGINE_WAVEFRONT)
-        PT_HIP(hipMemsetAsync(c->Q.counts + pt::kFlagWord, 0, sizeof(uint32_t), c->stream));
+    PT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));   // and the overflow flag
     PT_HIP(hipEventRecord(c->ev0, c->stream));
     if (engine == PT_ENGINE_WAVEFRONT) {
         pt::LaunchTimer* tm = timing ? &c->timer : nullptr;
@@ -1209,14 +1217,11 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     }
     PT_HIP(hipEventRecord(c->ev1, c->stream));
     if (c->timer.failed) return fail(PT_ERR_HIP, "hipEventRecord (kernel timing) failed");
-    unsigned long long ctr[16];
-    PT_HIP(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
+    const unsigned long long* ctr = c->h_counters;
+    PT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
-    if (engine == PT_ENGINE_WAVEFRONT) {
-        uint32_t flag = 0;
-        PT_HIP(hipMemcpy(&flag, c->Q.counts + pt::kFlagWord, sizeof flag, hipMemcpyDeviceToHost));
-        if (flag) return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
-    }
+    if (engine == PT_ENGINE_WAVEFRONT && ctr[pt::kOverflowCounter])
+        return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
     float ms = 0.f;
     PT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     // counters: [0..2] closest-hit rays/nodes/prims, [3] shading fetches, [4..6] shadow rays/nodes/prims
@@ -1304,6 +1309,7 @@ void pt_destroy(void* ctx) {
     if (c->d_v) (void)hipFree(c->d_v);
     if (c->d_n) (void)hipFree(c->d_n);
     if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->d_tiles) (void)hipFree(c->d_tiles);
     if (c->d_own) (void)hipFree(c->d_own);
     c->timer.destroy();

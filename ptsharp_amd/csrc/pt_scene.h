@@ -117,7 +117,8 @@ struct DevBuffer {
     double* v;                 // [P][3] Welford M2     (Pixel.V, Buffer.cs:22)
     int32_t* n;                // [P]    sample count   (Pixel.Samples)
     unsigned long long* counters;  // [0..2] closest-hit rays/nodes/prims, [3] shading fetches, [4..6] shadow
-                                   // rays/nodes/prims, [7] lit shadow rays, [8] their accumulation runs
+                                   // rays/nodes/prims, [7] lit shadow rays, [8] their accumulation runs,
+                                   // [15] wavefront queue overflow flag
 };
 
 }  // namespace pt

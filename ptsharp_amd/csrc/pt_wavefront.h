@@ -33,9 +33,10 @@ struct WfQueues {
     uint32_t* counts;    // counter slots, each kCountStride words apart (see count_word below):
                          // slot q·kParts+g = {rays, NEE requests} of partition g of ray queue q
                          // (one packed 64-bit word, reserved together); slot kFetchSlot + k·kParts + g
-                         // = work-fetch cursor of kernel k (0 trace, 1 shade, 2 shadow) in partition
-                         // g; slots kKeptSlot + q = rays of queue q with shading work (k_wf_trace);
-                         // slot kFlagSlot = overflow flag
+                         // = work-fetch cursor of kernel k (0 trace, 1 shade, 2 + q shadow set q) in
+                         // partition g; slots kKeptSlot + q = rays of queue q with shading work (k_wf_trace)
+    unsigned long long* overflow;   // set to 1 when a queue overflowed: a word of the pass' counters
+                                    // (DevBuffer::counters[kOverflowCounter]), read back with them
     uint32_t cap;        // entries per ray queue (kParts partitions of pcap)
     uint32_t s_cap;      // NEE queue entries (kParts partitions of spcap)
     uint32_t pcap, spcap;
@@ -55,12 +56,12 @@ constexpr int kCountStride = PT_COUNT_STRIDE;
 static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
 constexpr int kFetchSlot = 2 * kParts;
 constexpr int kKeptSlot = 6 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
-constexpr int kFlagSlot = 6 * kParts + 2;
+constexpr int kEndSlot = 6 * kParts + 2;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
-constexpr int kFlagWord = count_word(kFlagSlot);
-constexpr int kCountWords = count_word(kFlagSlot + 1);
-constexpr int kChunkResetWords = count_word(kFlagSlot);   // pair words + fetch cursors, zeroed per chunk
+constexpr int kCountWords = count_word(kEndSlot);
+constexpr int kChunkResetWords = kCountWords;   // every slot is zeroed per chunk
+constexpr int kOverflowCounter = 15;            // DevBuffer::counters word of WfQueues::overflow
 // work-fetch cursor of kernel k (0 trace, 1 shade, 2 + q shadow rays of set q) in partition g
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }

@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
             c = ((nblk - 1u - g) / kParts + 1u) * 256u;
             if ((nblk - 1u) % kParts == g) c -= nblk * 256u - count;   // the chunk's partial last block
         }
-        if (c > Q.pcap) { Q.counts[kFlagWord] = 1; c = Q.pcap; }
+        if (c > Q.pcap) { *Q.overflow = 1ull; c = Q.pcap; }
         *ray_count(Q, 0, g) = c;
     }
     for (uint32_t g = (G.g + kParts * G.lb) * 256u + threadIdx.x; g < count; g += kParts * G.nb * 256u) {
@@ -598,7 +598,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     if (block_major && lane >= cmax && lane < kBlockMajorChildren) { s_cc[lane][wid][0] = 0u; s_cc[lane][wid][1] = 0u; }
     uint32_t ebase, nbase, blk_e, blk_n;
     block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase, &blk_e, &blk_n);
-    if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) Q.counts[kFlagWord] = 1;
+    if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) *Q.overflow = 1ull;
     // Child-major slots: the block's reservation is filled child index by child index,
     // child c of every lane of the block on consecutive slots (waves in order, a ballot
     // prefix within each), then child c + 1.  A 64-ray batch of the next depth then holds
@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(256) void k_wf_camera_extra(DevCamera cam, DevPass 
         // CastRay(x, y, w, h, NextDouble(), NextDouble()): no jitter bug in these loops
         cast_ray(cam, x, y, P.width, P.height, draw(Kc, D_JX), draw(Kc, D_JY), Kc, o, d);
         const uint32_t i = append(ray_count(Q, 0, G.g));
-        if (i >= Q.pcap) { Q.counts[kFlagWord] = 1; continue; }
+        if (i >= Q.pcap) { *Q.overflow = 1ull; continue; }
         ray_store_camera(Q, 0, G.g * Q.pcap + i, o, d, g, Kc);
     }
 }
