@@ -14,6 +14,13 @@ at the end of the timed region (strong scaling: the image is fixed).
 Rank 0 prints one JSON line (driver contract), with `roofline` for the closest-hit
 kernel and `cpu_baseline` (the oracle port timed on this host).
 
+--workload c3 / c2 measure the other GPU configs of BASELINE.json the same way (not the
+driver's line): C3 = the 69,451-triangle mesh in the same frame (L2 roofline of its dominant
+kernel), C2 = the gopher 3-sphere scene, NewSampler(16,16), no triangle BVH — a latency /
+VALU-bound path, priced as SURVEY.md §8d says against the FP32 vector peak (157 TFLOP/s) with
+F_ray = 80 flops per BVH4 node + 22 per primitive test + 60 per shading fetch, and beside it the
+dominant kernel's measured VALU issue fraction (profiles/pmc_valu_c2.json, when present).
+
 Roofline: the closest-hit kernel's algorithmic bytes (per ray: 112 B per
 BVH4 node fetch, 36 B per primitive test, 44 B ray in + hit out) over its HIP-event time,
 against the L2 bandwidth (≈34.5 TB/s, MI355X_MICROARCH.md §L2).  The BVH nodes and leaf
@@ -39,6 +46,16 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/s (rays×bounces/s) at 1920×1080×1024spp; PSNR vs C# ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2 (per-XCD L2s, aggregate)
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md (FP32 vector peak)
+# C2 flops: slab tests of a BVH4 node's four boxes, a primitive test (gopher3:
+# two cubes ≈30, three spheres ≈14 → 22 on average), and the shading of a closest hit
+F_NODE, F_PRIM, F_SHADE = 80, 22, 60
+WORKLOADS = {
+    "c4": "C4: 1M-triangle mesh in Example.bunny's scene, 1920x1080, NewSampler(4,4) SpecularModeFirst",
+    "c3": "C3: 69,451-triangle mesh in Example.bunny's scene, 1920x1080, NewSampler(4,4) SpecularModeFirst",
+    "c2": "C2: gopher 3-sphere scene (Example.cs:1542-1564, mesh replaced by two spheres), 1920x1080, "
+          "NewSampler(16,16), no triangle BVH",
+}
 
 # Algorithmic bytes per unit: per ray 112 B per 4-wide BVH node
 # fetched (four child boxes of 24 B + four 4-B child refs), 36 B per primitive
@@ -55,7 +72,8 @@ def parse():
     p.add_argument("--spp", type=int, default=16, help="samples per pixel per step (pass)")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--tris", type=int, default=1_000_000)
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
+    p.add_argument("--tris", type=int, default=None, help="mesh triangles (default: 1,000,000 for c4, 69,451 for c3)")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     p.add_argument("--no-parity", action="store_true")
@@ -81,7 +99,12 @@ def main():
     from ptsharp_amd import Renderer, _abi, scenes, tiles_for_rank
 
     t_scene = time.perf_counter()
-    scene, camera, sampler = scenes.bunny_frame(a.tris, seed=a.seed)
+    if a.workload == "c2":
+        scene, camera, sampler = scenes.gopher3()
+    else:
+        if a.tris is None:
+            a.tris = 1_000_000 if a.workload == "c4" else 69_451
+        scene, camera, sampler = scenes.bunny_frame(a.tris, seed=a.seed)
     scene.Compile()
     t_scene = time.perf_counter() - t_scene
 
@@ -170,7 +193,8 @@ def main():
              "k_wf_finalize", "k_render_pass<false, false>", "k_wf_nee_accum", "-"]
     # the closest-hit kernel is the dominant one by design (on a multi-GPU shard the shadow
     # passes run beside it on a second stream, so their event spans overlap it)
-    dom = _abi.K_TRACE if klaunch[_abi.K_TRACE] else int(np.argmax(kms))
+    # (C3 / C2: the kernel with the most time)
+    dom = _abi.K_TRACE if klaunch[_abi.K_TRACE] and a.workload == "c4" else int(np.argmax(kms))
     # algorithmic bytes of the dominant kernel over the timed region: the counted pass' bytes per
     # ray of that kernel's ray class × the rays it traced (same scene/seed/spp → same ray mix)
     if dom == _abi.K_TRACE:
@@ -185,11 +209,11 @@ def main():
     achieved_gbs = dom_bytes / (kms[dom] * 1e-3) / 1e9
     rays_per_launch = rays * frac_rays / max(klaunch[dom], 1)
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if a.workload == "c4" else f"pmc_traffic_{a.workload}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             tj = json.load(f)
-        if tj.get("kernel") == names[dom] and tj.get("workload_tris") == a.tris:
+        if tj.get("kernel") == names[dom] and tj.get("workload_tris") == scene.Compile().num_triangles:
             traffic = round(tj["traffic_bytes_per_ray"] * rays_per_launch)
     # compulsory bytes of one launch: each ray's queue entry (origin, direction: 32 B) read and its
     # hit (16 B) written once, the traversal footprint (BVH nodes + leaf chunks) read once
@@ -206,9 +230,10 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32/f64",
-        "data": "synthetic (seeded 1M-triangle displaced-sphere mesh; no model assets ship with the reference)",
+        "data": "synthetic (seeded displaced-sphere mesh; no model assets ship with the reference)" if a.workload != "c2"
+        else "synthetic (analytic gopher3 scene)",
         "config": {
-            "workload": "C4: 1M-triangle mesh in Example.bunny's scene, 1920x1080, NewSampler(4,4) SpecularModeFirst",
+            "workload": WORKLOADS[a.workload],
             "width": W, "height": H, "spp_per_step": a.spp, "total_spp": a.spp * a.steps,
             "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}" + (f" shard {a.shard}" if a.shard else ""),
             "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
@@ -242,8 +267,28 @@ def main():
         },
     }
 
+    if a.workload == "c2":
+        # C2 is priced in flops against the FP32 vector peak (whole pass), with the
+        # dominant kernel's measured VALU issue fraction beside it
+        flops_ray = (F_NODE * ctr.nodes_visited + F_PRIM * ctr.prims_tested + F_SHADE * ctr.shading_fetches) / max(ctr.rays, 1)
+        tflops = flops_ray * rays / (kernel_ms * 1e-3) / 1e12
+        valu = None
+        pv = os.path.join(ROOT, "profiles", "pmc_valu_c2.json")
+        if os.path.exists(pv):
+            with open(pv) as f:
+                vj = json.load(f)
+            valu = vj.get("kernels", {}).get(names[dom], {}).get("valu_issue_frac")
+        out["roofline"] = {
+            "bound": "valu", "kernel": "whole pass", "achieved": round(tflops, 4), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(tflops / FP32_PEAK_TFLOPS, 6), "traffic": None,
+            "flops_per_ray": round(flops_ray, 2),
+            "dominant_kernel": names[dom], "dominant_kernel_ms_per_step": round(float(kms[dom]) / a.steps, 3),
+            "dominant_kernel_valu_issue_frac": valu,
+            "valu_issue_source": "profiles/pmc_valu_c2.json (SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE))",
+        }
+
     # ---------------- CPU baseline + parity sample (rank 0, N = 1 only)
-    if world == 1 and (a.cpu_seconds > 0 or not a.no_parity):
+    if world == 1 and a.workload == "c4" and (a.cpu_seconds > 0 or not a.no_parity):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         osc = O.OracleScene(scene)
