@@ -25,6 +25,7 @@ namespace PTSharpCore
 
         public const int PT_OK = 0;
         public const int PT_ERR_UNSUPPORTED = -4;
+        public const int PT_PASS_KERNEL_TIMING = 1, PT_PASS_SERIAL = 2;
         public const int SHAPE_SPHERE = 0, SHAPE_CUBE = 1, SHAPE_PLANE = 2, SHAPE_TRIANGLE = 3, SHAPE_MESH = 4;
         public const int SHAPE_SDF = 5, SHAPE_VOLUME = 6, SHAPE_TRANSFORMED = 7;
 
@@ -195,6 +196,7 @@ namespace PTSharpCore
         public int AdaptiveSamples = 0;           // Renderer.cs:23, phase at :340-410
         public int FireflySamples = 0;            // Renderer.cs:26, phase at :412-470
         public ulong Seed = 0;                     // Random.Shared is unseedable; this keys the GPU stream
+        public int NumCPU = Environment.ProcessorCount;   // Renderer.cs:51-54: 1 selects Render() in IterativeRender
         /// <summary>32x32 tiles this renderer draws (tile id = ty * ceil(W/32) + tx); null = the whole
         /// image.  A multi-GPU rank draws TilesForRank(W, H, rank, world) (SURVEY.md §8e).</summary>
         public int[] Tiles = null;
@@ -208,10 +210,11 @@ namespace PTSharpCore
         int firstHit, maxBounces; bool directLighting = true, softShadows = true;
 
         public static HipRenderer NewRenderer(Scene scene, Camera camera, DefaultSampler sampler, int firstHitSamples,
-                                              int maxBounces, int w, int h, int device = 0)
+                                              int maxBounces, int w, int h, int device = 0, bool multithreaded = true)
         {
             var r = new HipRenderer { Scene = scene, Camera = camera, Sampler = sampler, W = w, H = h,
-                                      firstHit = firstHitSamples, maxBounces = maxBounces };
+                                      firstHit = firstHitSamples, maxBounces = maxBounces,
+                                      NumCPU = multithreaded ? Environment.ProcessorCount : 1 };
             Renderer.PBuffer = new Buffer(w, h);
             var opts = new PtHip.pt_device_opts { device = device, width = w, height = h };
             PtHip.Check(PtHip.pt_create(ref opts, out r.ctx), "pt_create");
@@ -413,7 +416,13 @@ namespace PTSharpCore
         }
 
         /// <summary>One Renderer.RenderParallel pass on the GPU (Renderer.cs:199-338).</summary>
-        public void RenderParallel()
+        public void RenderParallel() => Pass(0);
+
+        /// <summary>One Renderer.Render pass (Renderer.cs:80-198, the NumCPU == 1 twin): the same main
+        /// samples, then per pixel its adaptive and firefly samples (PT_PASS_SERIAL).</summary>
+        public void Render() => Pass(PtHip.PT_PASS_SERIAL);
+
+        void Pass(int flags)
         {
             if (!uploaded) Upload();
             var cam = Cam();
@@ -422,7 +431,7 @@ namespace PTSharpCore
                 light_mode = (int)Sampler.LightMode, specular_mode = (int)Sampler.SpecularMode };
             var pass = new PtHip.pt_pass_params { spp = SamplesPerPixel, stratified = StratifiedSampling ? 1 : 0,
                 seed = Seed, pass_index = (uint)(++this.pass), adaptive_samples = AdaptiveSamples,
-                firefly_samples = FireflySamples };
+                firefly_samples = FireflySamples, flags = flags };
             GCHandle tiles = default;
             if (Tiles != null)
             {
@@ -474,7 +483,7 @@ namespace PTSharpCore
             for (int i = 1; i <= iter; i++)
             {
                 Console.WriteLine("Iteration " + i + " of " + iter);
-                RenderParallel();
+                if (NumCPU == 1) Render(); else RenderParallel();   // Renderer.cs:712-719
                 ReadBuffer();
                 colour = Renderer.PBuffer.Image(Channel.ColorChannel);
                 using var stream = System.IO.File.OpenWrite(string.Format(pathTemplate, i));

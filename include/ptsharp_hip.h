@@ -15,6 +15,7 @@
  *   pt_upload_scene    Scene.Compile() → Tree.NewTree / Mesh.Compile        Scene.cs:48-68, Tree.cs:22-29, Mesh.cs:45-57
  *                      (lights registered as in Scene.Add                  Scene.cs:29-38)
  *   pt_render_pass     one Renderer.RenderParallel() pass                  Renderer.cs:199-338
+ *                      (flag PT_PASS_SERIAL: one Renderer.Render() pass  Renderer.cs:80-198)
  *                      = spp × Camera.CastRay → DefaultSampler.Sample      Camera.cs:98-119, Sampler.cs:40-145,191-296
  *                        → Scene.Intersect → Tree/IShape.Intersect        Scene.cs:75-79, Tree.cs:31-128
  *                        → Buffer.AddSample (Welford)                     Buffer.cs:33-44,94-97
@@ -250,12 +251,19 @@ typedef struct pt_pass_params {
     int32_t num_tiles;       /* 0 = whole image; else render only these 32x32 tiles */
     const int32_t* tiles;    /* tile id = ty * ceil(W/32) + tx                   */
     int32_t engine;          /* pt_engine                                        */
-    int32_t flags;           /* PT_PASS_KERNEL_TIMING: per-kernel hipEvent timing */
+    int32_t flags;           /* PT_PASS_KERNEL_TIMING: per-kernel hipEvent timing; PT_PASS_SERIAL */
     int32_t adaptive_samples;/* Renderer.AdaptiveSamples (Renderer.cs:340-410): per-sample AddSample x N */
     int32_t firefly_samples; /* Renderer.FireflySamples (Renderer.cs:412-470, FireflyThreshold = 1) */
 } pt_pass_params;
 
 #define PT_PASS_KERNEL_TIMING 1
+/* Renderer.Render semantics (Renderer.cs:80-198, taken by IterativeRender when NumCPU == 1,
+ * Renderer.cs:712-719) instead of RenderParallel's: the main samples are the same; then per
+ * pixel AdaptiveSamples individual samples when StandardDeviation().MaxComponent() >= 1
+ * (AdaptiveSamples * (int)v, AdaptiveThreshold = AdaptiveExponent = 1, :153-175), then
+ * FireflySamples individual samples when it exceeds 1 (:177-191; no IsFirefly stop, jitter
+ * (x + NextDouble()) * (1.0f / w)). */
+#define PT_PASS_SERIAL 2
 
 /* Kernel classes reported by pt_stats.kernel_ms / kernel_launches. */
 typedef enum pt_kernel_class {

@@ -91,9 +91,11 @@ typedef struct or_pass_params {
     uint32_t pass_index;
     int32_t num_tiles;
     const int32_t* tiles;
-    int32_t engine, flags;  /* product-only (GPU scheduling / timing); ignored by the oracle */
+    int32_t engine, flags;  /* engine, and flags other than OR_PASS_SERIAL: product-only, ignored here */
     int32_t adaptive_samples, firefly_samples;  /* Renderer.AdaptiveSamples / FireflySamples */
 } or_pass_params;
+/* flags: Renderer.Render's extra phases (Renderer.cs:80-198) instead of RenderParallel's */
+#define OR_PASS_SERIAL 2
 
 /* Build the scene (k-d trees as Scene.Compile/Tree.NewTree do).  Returns NULL on error. */
 void* or_scene_create(const or_scene_desc* desc);

@@ -1290,6 +1290,33 @@ C extra_sample(Integrator& in, const or_camera& cam, int x, int y, int w, int h,
     return in.sample(ray, true, in.smp.fh, 0, K);
 }
 
+// Renderer.Render's firefly loop (Renderer.cs:184-186): CastRay(x, y, w, h, fu, fv) with
+// fu = (x + NextDouble()) * invWidth, invWidth = 1.0f / w evaluated in float (:98-99).
+C serial_firefly_sample(Integrator& in, const or_camera& cam, int x, int y, int w, int h, const or_pass_params& pp,
+                        uint32_t sample) {
+    uint64_t pix = (uint64_t)y * (uint64_t)w + (uint64_t)x;
+    uint64_t K = camera_key(pp.seed, pp.pass_index, pix, sample);
+    const double inv_w = (double)(1.0f / (float)w), inv_h = (double)(1.0f / (float)h);
+    double fu = ((double)x + draw(K, D_JX)) * inv_w, fv = ((double)y + draw(K, D_JY)) * inv_h;
+    Ray ray = cast_ray(cam, x, y, w, h, fu, fv, K);
+    return in.sample(ray, true, in.smp.fh, 0, K);
+}
+
+// Renderer.Render's adaptive branch (Renderer.cs:155-160): v = StandardDeviation().MaxComponent(),
+// v = Math.Clamp(v / AdaptiveThreshold, 0, 1), v = Math.Pow(v, AdaptiveExponent), and
+// AdaptiveSamples * (int)v samples.  Both knobs are 1 (Renderer.cs:45-46, private, never set
+// elsewhere), so (int)v is 1 exactly when the deviation reaches 1; NaN gives (int)NaN, whose
+// product with AdaptiveSamples is never positive.
+bool adaptive_serial_candidate(const double* V, int32_t N) {
+    if (N < 2) return false;
+    double r = std::sqrt(V[0] / (double)(N - 1)), g = std::sqrt(V[1] / (double)(N - 1)),
+           b = std::sqrt(V[2] / (double)(N - 1));
+    double v = net_max(net_max(r, g), b) / 1.0;
+    if (!(v >= 0.0)) return false;   // NaN
+    v = std::pow(std::min(v, 1.0), 1.0);
+    return (int)v == 1;
+}
+
 // buf.StandardDeviation(x, y).MaxComponent() > FireflyThreshold (= 1, Renderer.cs:48, 426):
 // Variance() is black below 2 samples, else V / (N-1) (Buffer.cs:48-55); Pow(0.5) is the
 // correctly rounded root, i.e. sqrt.
@@ -1474,7 +1501,22 @@ int64_t or_render_pass(void* scene, int32_t width, int32_t height, const or_came
         });
     };
     for_tiles([&](Integrator& in, int x, int y) { render_pixel(in, *cam, x, y, width, height, *pass, m, v, n); });
-    if (pass->adaptive_samples > 0) {
+    if (pass->flags & OR_PASS_SERIAL) {
+        // Renderer.Render (Renderer.cs:80-198): after a pixel's main samples, its adaptive samples
+        // (:153-175) then its firefly samples (:177-191), each AddSample'd.  The decisions read the
+        // pixel's own Buffer only, so this second sweep over the pixels is the same computation.
+        for_tiles([&](Integrator& in, int x, int y) {
+            size_t i = (size_t)y * (size_t)width + (size_t)x;
+            if (pass->adaptive_samples > 0 && adaptive_serial_candidate(v + 3 * i, n[i]))
+                for (int j = 0; j < pass->adaptive_samples; j++)
+                    welford(m + 3 * i, v + 3 * i, n + i,
+                            extra_sample(in, *cam, x, y, width, height, *pass, kAdaptiveBase + (uint32_t)j));
+            if (pass->firefly_samples > 0 && firefly_candidate(v + 3 * i, n[i]))
+                for (int j = 0; j < pass->firefly_samples; j++)
+                    welford(m + 3 * i, v + 3 * i, n + i,
+                            serial_firefly_sample(in, *cam, x, y, width, height, *pass, kFireflyBase + (uint32_t)j));
+        });
+    } else if (pass->adaptive_samples > 0) {
         // Adaptive phase (Renderer.cs:340-410): every pixel gets AdaptiveSamples
         // individual AddSample calls.  The second loop only feeds pixelVariances,
         // which nothing reads, so it is not traced.
@@ -1485,7 +1527,7 @@ int64_t or_render_pass(void* scene, int32_t width, int32_t height, const or_came
                         extra_sample(in, *cam, x, y, width, height, *pass, kAdaptiveBase + (uint32_t)j));
         });
     }
-    if (pass->firefly_samples > 0) {
+    if (!(pass->flags & OR_PASS_SERIAL) && pass->firefly_samples > 0) {
         // Firefly phase (Renderer.cs:412-470).  skippedPixels is created empty per call
         // and each pixel is visited once, so only its first branch is reachable.
         std::vector<double> snap(m, m + 3 * (size_t)width * (size_t)height);

@@ -24,6 +24,7 @@ PT_ERR_NO_DEVICE = -7
 
 ENGINE_AUTO, ENGINE_MEGAKERNEL, ENGINE_WAVEFRONT = 0, 1, 2
 PASS_KERNEL_TIMING = 1
+PASS_SERIAL = 2  # Renderer.Render semantics (Renderer.cs:80-198)
 K_CAMERA, K_TRACE, K_SHADE, K_SHADOW, K_FINALIZE, K_MEGAKERNEL, K_ACCUM = range(7)
 K_SLOTS = 8   # PT_K_SLOTS
 

@@ -1122,6 +1122,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples,
                                                 std::floor(pmax / per_sample_nee / 256.0) * 256.0 * pt::kParts);
     const bool extra = pass->adaptive_samples > 0 || pass->firefly_samples > 0;
+    const bool serial = (pass->flags & PT_PASS_SERIAL) != 0;   // Renderer.Render's extra phases (NumCPU == 1)
     if (pass->adaptive_samples < 0 || pass->firefly_samples < 0) return fail(PT_ERR_INVALID_ARG, "negative extra samples");
     int engine = pass->engine;
     if (engine == PT_ENGINE_AUTO)
@@ -1155,6 +1156,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         if (rc) return rc;
         if ((uint64_t)pass->adaptive_samples > chunk)
             return fail(PT_ERR_UNSUPPORTED, "adaptive samples exceed one wavefront chunk");
+        if (serial && (uint64_t)pass->firefly_samples > chunk)
+            return fail(PT_ERR_UNSUPPORTED, "firefly samples exceed one wavefront chunk");
         if (extra && (rc = ensure_extra(c, chunk))) return rc;
     }
     c->last_engine = engine;
@@ -1179,12 +1182,30 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     if (engine == PT_ENGINE_WAVEFRONT) {
         pt::LaunchTimer* tm = timing ? &c->timer : nullptr;
         PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm));
-        if (pass->adaptive_samples > 0)  // Renderer.cs:340-410
+        if (serial) {
+            // Renderer.Render (Renderer.cs:80-198): after a pixel's main samples, AdaptiveSamples
+            // individual samples if its σmax ≥ 1 (:153-175), then FireflySamples individual samples
+            // if its σmax then exceeds 1 (:177-191).  Each decision reads the pixel's own Buffer
+            // only, so the phases run over all pixels, one after the other.
+            const int32_t K[2] = {pass->adaptive_samples, pass->firefly_samples};
+            const uint32_t base[2] = {pt::kAdaptiveSampleBase, pt::kFireflySampleBase};
+            for (int ph = 0; ph < 2; ph++) {
+                if (K[ph] <= 0) continue;
+                PT_HIP(pt::select_pixels(P, B, ph == 0 ? 1 : 0, c->d_plist, c->d_fcount, c->stream));
+                uint32_t nsel = 0;
+                PT_HIP(hipMemcpyAsync(&nsel, c->d_fcount, sizeof nsel, hipMemcpyDeviceToHost, c->stream));
+                PT_HIP(hipStreamSynchronize(c->stream));
+                PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm,
+                                           ph == 0 ? pt::EXTRA_ADD : pt::EXTRA_ADD_SCALED, K[ph], base[ph], nsel,
+                                           c->d_plist, nullptr, nullptr, nullptr));
+            }
+        }
+        if (!serial && pass->adaptive_samples > 0)  // Renderer.cs:340-410
             PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm, 0,
                                        pass->adaptive_samples, pt::kAdaptiveSampleBase, (uint64_t)num_tiles * 1024u,
                                        nullptr, nullptr, nullptr, nullptr));
-        if (pass->firefly_samples > 0) {  // Renderer.cs:412-470
-            PT_HIP(pt::firefly_select(P, B, c->d_plist, c->d_fcount, c->stream));
+        if (!serial && pass->firefly_samples > 0) {  // Renderer.cs:412-470
+            PT_HIP(pt::select_pixels(P, B, 0, c->d_plist, c->d_fcount, c->stream));
             uint32_t nsel = 0;
             PT_HIP(hipMemcpyAsync(&nsel, c->d_fcount, sizeof nsel, hipMemcpyDeviceToHost, c->stream));
             const size_t npx = (size_t)c->width * (size_t)c->height;
@@ -1202,7 +1223,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
             uint32_t* next = c->d_plist2;
             for (int j = 0; j < pass->firefly_samples && nsel > 0; j++) {
                 PT_HIP(hipMemsetAsync(c->d_fcount + 1, 0, sizeof(uint32_t), c->stream));
-                PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm, 1, 1,
+                PT_HIP(pt::wavefront_extra(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm,
+                                           pt::EXTRA_FIREFLY_STOP, 1,
                                            pt::kFireflySampleBase + (uint32_t)j, nsel, list, c->d_snap, next,
                                            c->d_fcount + 1));
                 PT_HIP(hipMemcpyAsync(&nsel, c->d_fcount + 1, sizeof nsel, hipMemcpyDeviceToHost, c->stream));

@@ -794,6 +794,17 @@ __device__ __forceinline__ bool firefly_candidate(const DevBuffer& B, size_t i) 
     return net_max(net_max(r, g), b) > 1.0;
 }
 
+// Render's adaptive branch (Renderer.cs:155-158, AdaptiveThreshold = AdaptiveExponent = 1,
+// Renderer.cs:45-46): v = clamp(σmax / 1, 0, 1)^1 and AdaptiveSamples · (int)v samples, so a
+// pixel takes them all when σmax ≥ 1 and none otherwise (NaN: (int)NaN · AdaptiveSamples ≤ 0).
+__device__ __forceinline__ bool adaptive_serial_candidate(const DevBuffer& B, size_t i) {
+    const int32_t n = B.n[i];
+    if (n < 2) return false;
+    const double* V = B.v + 3 * i;
+    double r = sqrt(V[0] / (double)(n - 1)), g = sqrt(V[1] / (double)(n - 1)), b = sqrt(V[2] / (double)(n - 1));
+    return net_max(net_max(r, g), b) >= 1.0;
+}
+
 // IsFirefly + CalculateLocalDeviation (Renderer.cs:473-537): brightness > 0.9 and the
 // 3x3 (image-clipped) neighbourhood mean deviates by > 0.2.  Neighbours from `snap`
 // (M at the start of the firefly phase), the pixel's own M live.

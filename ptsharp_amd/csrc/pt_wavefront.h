@@ -102,10 +102,14 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
                           const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
                           LaunchTimer* timer);
 
-// Adaptive (firefly = 0) or firefly (firefly = 1) phase of a pass: `entries` pixels
-// (tile order, or `plist`), K samples each, sample indices sample_base + 0..K-1.  `snap`: M
-// at the start of the firefly phase.  Firefly: pixels that took all K samples without an
-// IsFirefly stop are appended to next_list (count in *next_count, a device word).
+// Extra-sample phase of a pass: `entries` pixels (tile order, or `plist`), K samples each,
+// sample indices sample_base + 0..K-1.  `firefly`: 0 every sample AddSample'd, camera jitter
+// NextDouble() (RenderParallel's adaptive loop; Render's adaptive loop); 1 RenderParallel's
+// firefly loop: stop at the first IsFirefly sample (`snap`: M at the start of the phase),
+// pixels that took all K samples without a stop are appended to next_list (count in
+// *next_count, a device word); 2 Render's firefly loop: every sample AddSample'd, jitter
+// (x + NextDouble()) · (1.0f / w) (Renderer.cs:184-185).
+enum ExtraMode : int { EXTRA_ADD = 0, EXTRA_FIREFLY_STOP = 1, EXTRA_ADD_SCALED = 2 };
 hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                            const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
                            LaunchTimer* timer, int firefly, int32_t K, uint32_t sample_base, uint64_t entries,
@@ -114,7 +118,11 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
 // Persistent grid sizes (resident capacity on this device) of the traversal / shade kernels.
 hipError_t wavefront_grids(WfPlan& plan);
 
-// Firefly candidates of the pass' pixels into plist; *count = how many (device word).
-hipError_t firefly_select(const DevPass& P, const DevBuffer& B, uint32_t* plist, uint32_t* count, hipStream_t stream);
+// Pixels of the pass whose StandardDeviation().MaxComponent() exceeds 1 (kind 0: the firefly
+// candidates, Renderer.cs:179,426) or is at least 1 (kind 1: Render's adaptive branch, where
+// AdaptiveSamples · (int)clamp(v / 1, 0, 1)^1 is nonzero, Renderer.cs:155-158) into plist;
+// *count = how many (device word).
+hipError_t select_pixels(const DevPass& P, const DevBuffer& B, int kind, uint32_t* plist, uint32_t* count,
+                         hipStream_t stream);
 
 }  // namespace pt

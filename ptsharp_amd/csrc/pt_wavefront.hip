@@ -1022,7 +1022,7 @@ __device__ __forceinline__ bool entry_pixel(const DevPass& P, const uint32_t* pl
 
 __global__ __launch_bounds__(256) void k_wf_camera_extra(DevCamera cam, DevPass P, WfQueues Q, uint64_t begin,
                                                          uint32_t count, int32_t K, uint32_t sample_base,
-                                                         const uint32_t* plist) {
+                                                         const uint32_t* plist, int scaled) {
     // Camera samples are dealt to the XCD groups in interleaved 256-slot blocks
     // (16 pixels' samples): every group gets an even share of sky, floor and mesh.
     const Group G = xcd_group();
@@ -1035,8 +1035,15 @@ __global__ __launch_bounds__(256) void k_wf_camera_extra(DevCamera cam, DevPass 
         const uint64_t pix = (uint64_t)y * (uint64_t)P.width + (uint64_t)x;
         const uint64_t Kc = camera_key(P.seed, P.pass_index, pix, sample_base + j);
         v3 o, d;
-        // CastRay(x, y, w, h, NextDouble(), NextDouble()): no jitter bug in these loops
-        cast_ray(cam, x, y, P.width, P.height, draw(Kc, D_JX), draw(Kc, D_JY), Kc, o, d);
+        // CastRay(x, y, w, h, NextDouble(), NextDouble()): no jitter bug in these loops; Render's
+        // firefly loop passes (x + NextDouble()) · invWidth, invWidth = 1.0f / w in float
+        // (Renderer.cs:98-99, 184-185)
+        double fu = draw(Kc, D_JX), fv = draw(Kc, D_JY);
+        if (scaled) {
+            fu = ((double)x + fu) * (double)(1.0f / (float)P.width);
+            fv = ((double)y + fv) * (double)(1.0f / (float)P.height);
+        }
+        cast_ray(cam, x, y, P.width, P.height, fu, fv, Kc, o, d);
         const uint32_t i = append(ray_count(Q, 0, G.g));
         if (i >= Q.pcap) { *Q.overflow = 1ull; continue; }
         ray_store_camera(Q, 0, G.g * Q.pcap + i, o, d, g, Kc);
@@ -1068,14 +1075,16 @@ __global__ __launch_bounds__(256) void k_wf_finalize_extra(DevPass P, DevBuffer 
     }
 }
 
-// Pixels of the pass whose standard deviation exceeds FireflyThreshold (Renderer.cs:426).
-__global__ __launch_bounds__(256) void k_wf_firefly_select(DevPass P, DevBuffer B, uint32_t* plist, uint32_t* count) {
+// Pixels of the pass whose standard deviation exceeds FireflyThreshold (kind 0, Renderer.cs:179,
+// 426), or reaches AdaptiveThreshold in Render's adaptive branch (kind 1, Renderer.cs:155-158).
+// List order is irrelevant: every later step is per pixel.
+__global__ __launch_bounds__(256) void k_wf_select(DevPass P, DevBuffer B, int kind, uint32_t* plist, uint32_t* count) {
     const uint32_t total = (uint32_t)P.num_tiles * 1024u;
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < total; s += gridDim.x * blockDim.x) {
         int x, y;
         if (!entry_pixel(P, nullptr, s, x, y)) continue;
         const uint32_t pix = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
-        if (firefly_candidate(B, pix)) plist[atomicAdd(count, 1u)] = pix;
+        if (kind ? adaptive_serial_candidate(B, pix) : firefly_candidate(B, pix)) plist[atomicAdd(count, 1u)] = pix;
     }
 }
 
@@ -1215,12 +1224,13 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
         if (e != hipSuccess) return e;
         begin_k(0);
         hipLaunchKernelGGL(k_wf_camera_extra, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Qx,
-                           e0 * (uint64_t)K, cnt, K, sample_base, plist);
+                           e0 * (uint64_t)K, cnt, K, sample_base, plist, firefly == EXTRA_ADD_SCALED ? 1 : 0);
         end_k(0);
         depth_loop(S, smp, B, Qx, plan, count, stream, timer, cnt);
         begin_k(4);
         hipLaunchKernelGGL(k_wf_finalize_extra, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, stream, P, B, Q.acc_s,
-                           e0, (uint32_t)ne, K, plist, firefly, snap, next_list, next_count);
+                           e0, (uint32_t)ne, K, plist, firefly == EXTRA_FIREFLY_STOP ? 1 : 0, snap, next_list,
+                           next_count);
         end_k(4);
     }
     return hipGetLastError();
@@ -1244,11 +1254,12 @@ hipError_t wavefront_grids(WfPlan& plan) {
     return e;
 }
 
-hipError_t firefly_select(const DevPass& P, const DevBuffer& B, uint32_t* plist, uint32_t* count, hipStream_t stream) {
+hipError_t select_pixels(const DevPass& P, const DevBuffer& B, int kind, uint32_t* plist, uint32_t* count,
+                         hipStream_t stream) {
     hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     const uint64_t pix_slots = (uint64_t)P.num_tiles * 1024u;
-    hipLaunchKernelGGL(k_wf_firefly_select, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, plist,
+    hipLaunchKernelGGL(k_wf_select, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, kind, plist,
                        count);
     return hipGetLastError();
 }

@@ -187,7 +187,16 @@ class Renderer:
             print(f"{self.W} x {self.H}, {self.SamplesPerPixel} spp, MI355X device {self.Device}")
             print("time elapsed:", time.perf_counter() - t0)
 
-    Render = RenderParallel
+    def Render(self) -> None:
+        """One pass of Renderer.Render (Renderer.cs:80-198), the NumCPU == 1 twin: the same main
+        samples, then per pixel AdaptiveSamples individual samples when its standard deviation
+        reaches 1 and FireflySamples when it then exceeds 1 (PT_PASS_SERIAL)."""
+        flags = self.Flags
+        self.Flags = flags | _abi.PASS_SERIAL
+        try:
+            self.RenderParallel()
+        finally:
+            self.Flags = flags
 
     def RenderCounted(self) -> _abi.pt_trace_counters:
         """One pass with traversal counters (bench roofline accounting)."""
@@ -234,14 +243,17 @@ class Renderer:
         return s
 
     def IterativeRender(self, pathTemplate: str | None, iterations: int) -> np.ndarray:
-        """Renderer.IterativeRender (Renderer.cs:702-765).  Each iteration is one
-        RenderParallel pass, including its adaptive / firefly phases."""
+        """Renderer.IterativeRender (Renderer.cs:702-765).  Each iteration is one Render
+        (NumCPU == 1) or RenderParallel pass, including its adaptive / firefly phases."""
         self.iterations = iterations
         img = None
         for i in range(1, iterations + 1):
             if self.Verbose:
                 print(f"Iteration {i} of {iterations}")
-            self.RenderParallel()
+            if self.NumCPU == 1:  # Renderer.cs:712-719
+                self.Render()
+            else:
+                self.RenderParallel()
             if pathTemplate:
                 img = self.ReadBuffer().Image(Channel.ColorChannel)
                 write_png(pathTemplate.replace("{0}", str(i)), img)

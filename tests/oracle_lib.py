@@ -176,13 +176,13 @@ def default_threads() -> int:
     return int(env) if env and env.isdigit() and int(env) > 0 else min(os.cpu_count() or 1, 16)
 
 
-def pass_params(spp, seed=0, pass_index=1, stratified=False, tiles=None, adaptive=0, firefly=0):
+def pass_params(spp, seed=0, pass_index=1, stratified=False, tiles=None, adaptive=0, firefly=0, serial=False):
     keep = None
     if tiles is not None:
         keep = np.ascontiguousarray(tiles, np.int32)
     pp = _abi.pt_pass_params(spp, int(stratified), seed, pass_index, 0 if keep is None else len(keep),
                              C.POINTER(C.c_int32)() if keep is None else keep.ctypes.data_as(C.POINTER(C.c_int32)),
-                             0, 0, int(adaptive), int(firefly))
+                             0, _abi.PASS_SERIAL if serial else 0, int(adaptive), int(firefly))
     pp._keep = keep
     return pp
 
@@ -200,14 +200,14 @@ class OracleBuffer:
 
 
 def render(oscene: OracleScene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None,
-           threads=None, brute=False, buf: OracleBuffer = None, first_pass=1, adaptive=0, firefly=0):
-    """IterativeRender-equivalent on the oracle: `passes` RenderParallel calls."""
+           threads=None, brute=False, buf: OracleBuffer = None, first_pass=1, adaptive=0, firefly=0, serial=False):
+    """IterativeRender-equivalent on the oracle: `passes` RenderParallel (serial: Render) calls."""
     buf = buf or OracleBuffer(w, h)
     cam, smp = camera.to_c(), sampler.to_c()
     threads = default_threads() if threads is None else threads
     rays = 0
     for p in range(first_pass, first_pass + passes):
-        pp = pass_params(spp, seed, p, stratified, tiles, adaptive, firefly)
+        pp = pass_params(spp, seed, p, stratified, tiles, adaptive, firefly, serial)
         rays += lib().or_render_pass(oscene.h, w, h, C.byref(cam), C.byref(smp), C.byref(pp), *buf.ptrs(), threads,
                                      int(brute))
     return buf, rays

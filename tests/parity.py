@@ -72,8 +72,9 @@ def same_buffer(a, b):
 
 
 def render_gpu(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None, device=0, engine=0,
-               adaptive=0, firefly=0):
-    r = Renderer.NewRenderer(scene, camera, sampler, w, h, True, device=device)
+               adaptive=0, firefly=0, serial=False):
+    """`passes` RenderParallel calls (serial: Render calls, the NumCPU == 1 twin)."""
+    r = Renderer.NewRenderer(scene, camera, sampler, w, h, not serial, device=device)
     r.SamplesPerPixel = spp
     r.AdaptiveSamples = adaptive
     r.FireflySamples = firefly
@@ -83,7 +84,10 @@ def render_gpu(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=F
     r.Engine = engine
     rays = 0
     for _ in range(passes):
-        r.RenderParallel()
+        if serial:
+            r.Render()
+        else:
+            r.RenderParallel()
         rays += r.Stats().rays
     buf = r.ReadBuffer()
     out = Buffer(w, h)
@@ -93,9 +97,9 @@ def render_gpu(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=F
 
 
 def render_both(scene, camera, sampler, w, h, spp, passes=1, seed=0, stratified=False, tiles=None, engine=0,
-                adaptive=0, firefly=0):
+                adaptive=0, firefly=0, serial=False):
     g, grays = render_gpu(scene, camera, sampler, w, h, spp, passes, seed, stratified, tiles, engine=engine,
-                          adaptive=adaptive, firefly=firefly)
+                          adaptive=adaptive, firefly=firefly, serial=serial)
     o, orays = O.render(O.OracleScene(scene), camera, sampler, w, h, spp, passes=passes, seed=seed,
-                        stratified=stratified, tiles=tiles, adaptive=adaptive, firefly=firefly)
+                        stratified=stratified, tiles=tiles, adaptive=adaptive, firefly=firefly, serial=serial)
     return g, grays, o, orays

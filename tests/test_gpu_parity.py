@@ -212,6 +212,29 @@ def test_firefly_phase(gpu):
     check(g, gr, o, orr)   # candidate choice and the IsFirefly stop: N equal on every pixel
 
 
+def test_serial_render_twin(gpu):
+    """Renderer.Render (NumCPU == 1, Renderer.cs:80-198) on the GPU (PT_PASS_SERIAL): per-pixel
+    adaptive samples when the deviation reaches 1 and firefly samples when it then exceeds 1,
+    against the oracle's Render: M, V, N and the ray count."""
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 4
+    g, gr, o, orr = render_both(s, c, smp, 64, 48, spp=1, passes=3, seed=29, engine=_abi.ENGINE_WAVEFRONT,
+                                adaptive=3, firefly=4, serial=True)
+    plain = render_gpu(s, c, smp, 64, 48, spp=1, passes=3, seed=29, engine=_abi.ENGINE_WAVEFRONT)[0]
+    extra = g.N - plain.N
+    assert (extra > 0).any() and (extra == 0).any(), "the scene must exercise both branches"
+    check(g, gr, o, orr)
+
+
+def test_serial_render_example3(gpu):
+    """The reference's default scene (Example.example3: AdaptiveSamples 32, FireflySamples 64) through
+    Render rather than RenderParallel; 48x32, 2 passes, against the oracle."""
+    s, c, smp = scenes.example3()
+    g, gr, o, orr = render_both(s, c, smp, 48, 32, spp=4, passes=2, seed=5, engine=_abi.ENGINE_WAVEFRONT,
+                                adaptive=32, firefly=64, serial=True)
+    check(g, gr, o, orr)
+
+
 def test_extra_phases_unsupported_on_megakernel(gpu):
     s, c, smp = scenes.gopher3()
     with pytest.raises(_abi.PTError):

@@ -292,6 +292,29 @@ def test_firefly_candidates_and_stop():
     assert (extra[ref.N == 0] == 0).all()
 
 
+def test_serial_render_phases():
+    """Renderer.Render (the NumCPU == 1 twin, Renderer.cs:80-198): per pixel, AdaptiveSamples
+    individual samples exactly when its deviation reaches 1 (AdaptiveSamples * (int)v with
+    threshold and exponent 1), then FireflySamples when it then exceeds 1, with no IsFirefly
+    stop.  With spp 1 (one averaged sample per pass) pass 1 leaves N = 1, so only pass 2
+    decides: each pixel gains 0, 3, 5 or 8 samples over the plain passes."""
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 4
+    osc = O.OracleScene(s)
+    ref, rref = O.render(osc, c, smp, 48, 32, spp=1, passes=2, seed=9)
+    ser, rser = O.render(osc, c, smp, 48, 32, spp=1, passes=2, seed=9, adaptive=3, firefly=5, serial=True)
+    extra = ser.N - ref.N
+    assert set(np.unique(extra)) <= {0, 3, 5, 8}
+    assert (extra == 8).any() and (extra == 0).any()
+    assert rser > rref
+    # pixels without extras are untouched: the main samples are RenderParallel's
+    same = extra == 0
+    assert np.array_equal(ser.M[same], ref.M[same]) and np.array_equal(ser.V[same], ref.V[same])
+    # after a pixel's adaptive samples, firefly samples follow iff its deviation then exceeds 1
+    par, _ = O.render(osc, c, smp, 48, 32, spp=1, passes=2, seed=9, adaptive=3, firefly=5)
+    assert not np.array_equal(par.N, ser.N)   # RenderParallel's phases differ (every pixel adapts)
+
+
 def test_extra_phases_rng_domains_disjoint():
     """Adaptive and firefly samples use their own camera_key sample domains."""
     k = {O.lib().or_camera_key(7, 1, 100, s) for s in (0, 1, 0x40000000, 0x40000001, 0x80000000, 0x80000001)}
