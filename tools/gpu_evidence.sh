@@ -25,7 +25,8 @@ pmc p4 SQ_LEVEL_WAVES SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY
 pmc p5 TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TA_TA_BUSY_sum TCP_PERF_SEL_TOTAL_HIT_LRU_READ_sum TCP_PERF_SEL_TOTAL_MISS_LRU_READ_sum && \
 pmc p6 TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum && \
 python tools/residency.py $D $TAG > $D/residency.txt 2>&1 || exit 1
-for N in 2 4 8; do
-  timeout -k 10 300 python bench.py --shard 0/$N --steps 16 --warmup 2 --cpu-seconds 0 --no-parity --json-out $D/shard_0of$N.json > $D/shard_0of$N.log 2>&1 || exit 1
+for S in 0/2 0/4 0/8 3/8 7/8; do
+  F=shard_${S%/*}of${S#*/}
+  timeout -k 10 300 python bench.py --shard $S --steps 16 --warmup 2 --cpu-seconds 0 --no-parity --json-out $D/$F.json > $D/$F.log 2>&1 || exit 1
 done
 timeout -k 10 600 python tools/bench_scenes.py > $D/scenes.jsonl 2> $D/scenes.log
