@@ -337,8 +337,11 @@ int pt_mesh_smooth_normals(int32_t n, const float* v1, const float* v2, const fl
                            float* n3);
 
 /* Multi-GPU: one context per GPU.  Each context renders its tile list
- * (pt_pass_params.tiles), and pt_comm_gather sums the disjoint per-rank tile buffers into
- * rank `root` (RCCL reduce over xGMI).  Two ways to form the communicator:
+ * (pt_pass_params.tiles; the ranks' lists must be disjoint), and pt_comm_gather assembles
+ * them on rank `root`: every other rank packs the {M, V, N} of its last pass' tiles and sends
+ * them with the tile ids (RCCL send/recv over xGMI, after an all-gather of the tile counts);
+ * root writes them into its Buffer.  For disjoint tiles that is the sum of the ranks'
+ * Buffers, at 1/N of a full frame's bytes per rank.  Two ways to form the communicator:
  *   - one process per GPU: rank 0 makes the id (pt_comm_unique_id), ships it to the other
  *     processes, and every rank calls pt_comm_init (it blocks until all ranks joined);
  *   - one process driving G GPUs (the .NET host): G contexts on G devices, joined by ONE

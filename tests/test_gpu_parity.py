@@ -84,6 +84,18 @@ def test_c4_mesh1m_tiles(gpu):
     check(g, gr, o, orr)
 
 
+def test_c5_mixed_4k_tiles_adaptive(gpu):
+    """C5's kind of workload: the 1M-triangle mesh frame plus an SDF shape, a voxel Volume and an
+    environment texture (scenes.mixed), at 3840x2160 with adaptive sampling, the full default
+    sampler (no MaxBounces cap), on one 512th of the 4K frame's tiles, 2 passes."""
+    s, c, smp = scenes.mixed(1_000_000)
+    tiles = tiles_for_rank(3840, 2160, 3, 512)
+    g, gr, o, orr = render_both(s, c, smp, 3840, 2160, spp=1, passes=2, seed=4096, tiles=tiles,
+                                engine=_abi.ENGINE_WAVEFRONT, adaptive=2)
+    assert (g.N > 0).sum() == len(tiles) * 1024 and (g.N[g.N > 0] == 2 * (1 + 2)).all()
+    check(g, gr, o, orr)
+
+
 def test_c3_mesh70k_tiles(gpu):
     """C3: the ~70k-triangle mesh frame at 1920x1080 on one 64th of the tiles, 2 passes of 2 spp."""
     s, c, smp = scenes.bunny_frame(69_451)
