@@ -163,6 +163,8 @@ namespace PTSharpCore
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_synchronize(IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_read_buffer(IntPtr ctx, double[] m, double[] v, int[] n);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_write_buffer(IntPtr ctx, double[] m, double[] v, int[] n);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_read_tiles(IntPtr ctx, int[] tiles, int num_tiles, double[] m, double[] v, int[] n);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_write_tiles(IntPtr ctx, int[] tiles, int num_tiles, double[] m, double[] v, int[] n);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_reset_buffer(IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_stats_get(IntPtr ctx, out pt_stats stats);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern IntPtr pt_last_error();
@@ -460,6 +462,19 @@ namespace PTSharpCore
             PtHip.Check(PtHip.pt_write_buffer(ctx, m, v, n), "pt_write_buffer");
             pass = passesDone;
         }
+
+        /// <summary>The Buffer pixels of 32x32 tiles, packed row-major inside each tile (pt_read_tiles):
+        /// m, v [tiles][32][32][3], n [tiles][32][32].  With WriteTiles, a host that moves Buffers over
+        /// its own transport assembles a sharded frame (pt_comm_gather's protocol).</summary>
+        public (double[] m, double[] v, int[] n) ReadTiles(int[] tiles)
+        {
+            var m = new double[tiles.Length * 3072]; var v = new double[tiles.Length * 3072]; var n = new int[tiles.Length * 1024];
+            PtHip.Check(PtHip.pt_read_tiles(ctx, tiles, tiles.Length, m, v, n), "pt_read_tiles");
+            return (m, v, n);
+        }
+
+        public void WriteTiles(int[] tiles, double[] m, double[] v, int[] n) =>
+            PtHip.Check(PtHip.pt_write_tiles(ctx, tiles, tiles.Length, m, v, n), "pt_write_tiles");
 
         /// <summary>Copy the HBM Welford state into Renderer.PBuffer's Pixel objects (Buffer.cs:18-58).</summary>
         public void ReadBuffer()

@@ -22,6 +22,8 @@
  *   pt_read_buffer     reading Renderer.PBuffer pixels {Samples, M, V}     Buffer.cs:18-58, Renderer.cs:20
  *   pt_reset_buffer    Renderer.PBuffer = new Buffer(w,h)                  Renderer.cs:41
  *   pt_write_buffer    resuming IterativeRender from a saved PBuffer       Renderer.cs:702-765
+ *   pt_read_tiles /    (new) a tile list's pixels, packed: progressive    SURVEY.md §8e
+ *   pt_write_tiles     display of a rank's tiles, host-side gathers
  *   pt_stats           Scene.rays (Interlocked counter, never printed)     Scene.cs:70-79
  *                      + the "time elapsed" stopwatch                      Renderer.cs:212-213,470
  *   pt_last_error      oidnGetDeviceError(device, out msg)                 OIDN.cs:85-86
@@ -315,6 +317,15 @@ int pt_read_buffer(void* ctx, double* out_m, double* out_v, int32_t* out_n);
  * IterativeRender from a saved Buffer (Renderer.cs:702-765 keeps accumulating into
  * Renderer.PBuffer pass after pass; a checkpoint is that Buffer). */
 int pt_write_buffer(void* ctx, const double* m, const double* v, const int32_t* n);
+
+/* The Buffer pixels of `num_tiles` 32x32 tiles, packed: m, v [num_tiles][32][32][3], n
+ * [num_tiles][32][32], row-major inside a tile (entry (t, r, c) = pixel (32·(tiles[t] mod
+ * ceil(W/32)) + c, 32·(tiles[t] div ceil(W/32)) + r)).  Pixels outside the image read as 0
+ * and are ignored on write.  The same packing carries pt_comm_gather's tiles; a host that
+ * moves Buffers over its own transport (gloo, MPI, sockets) gathers with these two calls. */
+int pt_read_tiles(void* ctx, const int32_t* tiles, int32_t num_tiles, double* out_m, double* out_v, int32_t* out_n);
+int pt_write_tiles(void* ctx, const int32_t* tiles, int32_t num_tiles, const double* m, const double* v,
+                   const int32_t* n);
 int pt_stats_get(void* ctx, pt_stats* out_stats);
 const char* pt_last_error(void);
 void pt_destroy(void* ctx);

@@ -146,6 +146,8 @@ SIGNATURES = {
     "pt_reset_buffer": (C.c_int, [C.c_void_p]),
     "pt_read_buffer": (C.c_int, [C.c_void_p, _d, _d, _i]),
     "pt_write_buffer": (C.c_int, [C.c_void_p, _d, _d, _i]),
+    "pt_read_tiles": (C.c_int, [C.c_void_p, _i, C.c_int32, _d, _d, _i]),
+    "pt_write_tiles": (C.c_int, [C.c_void_p, _i, C.c_int32, _d, _d, _i]),
     "pt_stats_get": (C.c_int, [C.c_void_p, C.POINTER(pt_stats)]),
     "pt_last_error": (C.c_char_p, []),
     "pt_destroy": (None, [C.c_void_p]),

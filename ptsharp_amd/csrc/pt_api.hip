@@ -44,16 +44,16 @@ __global__ __launch_bounds__(256) void k_clear_foreign(DevBuffer B, int32_t widt
         for (int k = 0; k < 3; k++) { B.m[3 * i + k] = 0.0; B.v[3 * i + k] = 0.0; }
     }
 }
-// Tile-compacted gather (pt_comm_gather): entry s of a packed run is slot s & 1023 of tile
-// ids[s >> 10]; pack copies a rank's {M, V, N} out (zeros outside the image), unpack writes a
-// run into the root's Buffer.
+// Packed tiles (pt_read_tiles / pt_write_tiles, the tile-compacted gather): entry s of a run
+// is pixel (s & 31, (s >> 5) & 31) of tile ids[s >> 10], row-major inside the tile; pack
+// copies {M, V, N} out (zeros outside the image), unpack writes a run into the Buffer.
 __global__ __launch_bounds__(256) void k_tiles_pack(DevBuffer B, int32_t width, int32_t height, int32_t tiles_x,
                                                     const int32_t* ids, uint32_t nt, double* pm, double* pv,
                                                     int32_t* pn, int unpack) {
     const size_t total = (size_t)nt * 1024u;
     for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (size_t)gridDim.x * blockDim.x) {
-        int x, y;
-        tile_pixel(ids[s >> 10], (int)(s & 1023u), tiles_x, x, y);
+        const int tile = ids[s >> 10];
+        const int x = (tile % tiles_x) * 32 + (int)(s & 31u), y = (tile / tiles_x) * 32 + (int)((s >> 5) & 31u);
         const bool in = x < width && y < height;
         const size_t i = (size_t)y * (size_t)width + (size_t)x;
         if (unpack) {
@@ -1348,6 +1348,48 @@ int pt_write_buffer(void* ctx, const double* m, const double* v, const int32_t* 
     return PT_OK;
 }
 
+static int tile_workspace(Ctx* c);
+
+// Host copies of a tile list's packed {M, V, N} (see k_tiles_pack for the order).
+static int tiles_io(void* ctx, const int32_t* tiles, int32_t num_tiles, double* m, double* v, int32_t* n, bool write) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c || (num_tiles > 0 && (!tiles || !m || !v || !n))) return fail(PT_ERR_INVALID_ARG, "NULL argument");
+    if (num_tiles < 0) return fail(PT_ERR_INVALID_ARG, "num_tiles < 0");
+    const int32_t all = ((c->width + 31) / 32) * ((c->height + 31) / 32);
+    if (num_tiles > all) return fail(PT_ERR_INVALID_ARG, "more tiles than the image has");
+    for (int32_t i = 0; i < num_tiles; i++)
+        if (tiles[i] < 0 || tiles[i] >= all) return fail(PT_ERR_INVALID_ARG, "tile id out of range");
+    if (num_tiles == 0) return PT_OK;
+    PT_HIP(hipSetDevice(c->device));
+    int rc = tile_workspace(c);
+    if (rc) return rc;
+    const size_t s = (size_t)num_tiles * 1024u;
+    PT_HIP(hipMemcpyAsync(c->g_ids, tiles, (size_t)num_tiles * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    if (write) {
+        PT_HIP(hipMemcpyAsync(c->g_m, m, s * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        PT_HIP(hipMemcpyAsync(c->g_v, v, s * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        PT_HIP(hipMemcpyAsync(c->g_n, n, s * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    }
+    pt::DevBuffer B{c->d_m, c->d_v, c->d_n, c->d_counters};
+    hipLaunchKernelGGL(pt::k_tiles_pack, dim3(2048), dim3(256), 0, c->stream, B, c->width, c->height,
+                       (c->width + 31) / 32, c->g_ids, (uint32_t)num_tiles, c->g_m, c->g_v, c->g_n, write ? 1 : 0);
+    PT_HIP(hipGetLastError());
+    if (!write) {
+        PT_HIP(hipMemcpyAsync(m, c->g_m, s * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        PT_HIP(hipMemcpyAsync(v, c->g_v, s * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        PT_HIP(hipMemcpyAsync(n, c->g_n, s * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    }
+    PT_HIP(hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+int pt_read_tiles(void* ctx, const int32_t* tiles, int32_t num_tiles, double* out_m, double* out_v, int32_t* out_n) {
+    return tiles_io(ctx, tiles, num_tiles, out_m, out_v, out_n, false);
+}
+int pt_write_tiles(void* ctx, const int32_t* tiles, int32_t num_tiles, const double* m, const double* v,
+                   const int32_t* n) {
+    return tiles_io(ctx, tiles, num_tiles, const_cast<double*>(m), const_cast<double*>(v), const_cast<int32_t*>(n), true);
+}
+
 int pt_stats_get(void* ctx, pt_stats* out) {
     Ctx* c = (Ctx*)ctx;
     if (!c || !out) return fail(PT_ERR_INVALID_ARG, "NULL argument");
@@ -1414,7 +1456,7 @@ int pt_comm_init(void* ctx, int32_t nranks, int32_t rank, const uint8_t id[128])
 // its Buffer.  The ranks' tiles are disjoint, so this equals a sum-reduce of the full frames
 // at ≈1/N of their bytes per rank (1080p, 8 ranks: 13.6 MB instead of 108 MB).  Two steps:
 // the tile counts (one all-gather), then the grouped sends and receives.
-static int gather_prepare(Ctx* c) {
+static int tile_workspace(Ctx* c) {
     const int32_t tiles = ((c->width + 31) / 32) * ((c->height + 31) / 32);
     const size_t slots = (size_t)tiles * 1024u;
     if (!c->g_ids) {
@@ -1422,11 +1464,17 @@ static int gather_prepare(Ctx* c) {
         PT_HIP(hipMalloc(&c->g_m, slots * 3 * sizeof(double)));
         PT_HIP(hipMalloc(&c->g_v, slots * 3 * sizeof(double)));
         PT_HIP(hipMalloc(&c->g_n, slots * sizeof(int32_t)));
-        PT_HIP(hipMalloc(&c->g_cnts, (size_t)(c->nranks + 1) * sizeof(int32_t)));
         PT_HIP(hipMalloc(&c->g_all, (size_t)tiles * sizeof(int32_t)));
         hipLaunchKernelGGL(pt::k_iota, dim3(64), dim3(256), 0, c->stream, c->g_all, tiles);
         PT_HIP(hipGetLastError());
     }
+    return PT_OK;
+}
+static int gather_prepare(Ctx* c) {
+    const int32_t tiles = ((c->width + 31) / 32) * ((c->height + 31) / 32);
+    int rc = tile_workspace(c);
+    if (rc) return rc;
+    if (!c->g_cnts) PT_HIP(hipMalloc(&c->g_cnts, (size_t)(c->nranks + 1) * sizeof(int32_t)));
     const int32_t mine = c->pass_tiles > 0 ? c->pass_tiles : tiles;
     PT_HIP(hipMemcpyAsync(c->g_cnts + c->nranks, &mine, sizeof mine, hipMemcpyHostToDevice, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));   // `mine` is a host temporary

@@ -233,6 +233,29 @@ class Renderer:
                                              N.ctypes.data_as(C.POINTER(C.c_int32))), "pt_write_buffer")
         self._pass = int(passes_done)
 
+    def ReadTiles(self, tiles):
+        """The Buffer pixels of 32x32 tiles, packed (pt_read_tiles): M, V [n, 32, 32, 3], N [n, 32, 32],
+        row-major inside a tile; pixels outside the image are 0."""
+        t = np.ascontiguousarray(tiles, np.int32)
+        M = np.zeros((len(t), 32, 32, 3), np.float64)
+        V = np.zeros((len(t), 32, 32, 3), np.float64)
+        N = np.zeros((len(t), 32, 32), np.int32)
+        _abi.check(self._lib.pt_read_tiles(self._ctx, t.ctypes.data_as(C.POINTER(C.c_int32)), len(t),
+                                           M.ctypes.data_as(C.POINTER(C.c_double)), V.ctypes.data_as(C.POINTER(C.c_double)),
+                                           N.ctypes.data_as(C.POINTER(C.c_int32))), "pt_read_tiles")
+        return M, V, N
+
+    def WriteTiles(self, tiles, M, V, N) -> None:
+        """Write packed tiles (ReadTiles' layout) into the Buffer (pt_write_tiles)."""
+        t = np.ascontiguousarray(tiles, np.int32)
+        M = np.ascontiguousarray(M, np.float64)
+        V = np.ascontiguousarray(V, np.float64)
+        N = np.ascontiguousarray(N, np.int32)
+        assert M.size == V.size == 3 * N.size == len(t) * 3 * 1024
+        _abi.check(self._lib.pt_write_tiles(self._ctx, t.ctypes.data_as(C.POINTER(C.c_int32)), len(t),
+                                            M.ctypes.data_as(C.POINTER(C.c_double)), V.ctypes.data_as(C.POINTER(C.c_double)),
+                                            N.ctypes.data_as(C.POINTER(C.c_int32))), "pt_write_tiles")
+
     def ResetBuffer(self) -> None:
         _abi.check(self._lib.pt_reset_buffer(self._ctx), "pt_reset_buffer")
         self._pass = 0

@@ -89,6 +89,35 @@ def _free_port():
         return sk.getsockname()[1]
 
 
+def test_read_write_tiles_layout(gpu):
+    """pt_read_tiles packs a tile row-major (edge tiles: zeros outside the image); pt_write_tiles
+    puts packed tiles back; a render's tiles moved into a fresh context reproduce its Buffer."""
+    w, h = 100, 70                       # 4 x 3 tiles, the last column and row partial
+    s, c, smp = _scene()
+    r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+    q = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+    try:
+        r.SamplesPerPixel, r.Seed = 2, 5
+        r.RenderParallel()
+        b = r.ReadBuffer()
+        full = _Buf(b.M.copy(), b.V.copy(), b.N.copy())
+        tiles = np.array([11, 0, 5, 3], np.int32)
+        M, V, N = r.ReadTiles(tiles)
+        for k, t in enumerate(tiles):
+            x0, y0 = (t % 4) * 32, (t // 4) * 32
+            x1, y1 = min(x0 + 32, w), min(y0 + 32, h)
+            assert np.array_equal(M[k, :y1 - y0, :x1 - x0], full.M[y0:y1, x0:x1])
+            assert np.array_equal(N[k, :y1 - y0, :x1 - x0], full.N[y0:y1, x0:x1])
+            assert (N[k, y1 - y0:, :] == 0).all() and (N[k, :, x1 - x0:] == 0).all()
+        all_t = np.arange(12, dtype=np.int32)
+        q.WriteTiles(all_t, *r.ReadTiles(all_t))
+        b2 = q.ReadBuffer()
+        same_buffer(_Buf(b2.M.copy(), b2.V.copy(), b2.N.copy()), full)
+    finally:
+        r.close()
+        q.close()
+
+
 def _worker(rank, world, port, outdir):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -100,20 +129,45 @@ def _worker(rank, world, port, outdir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         W, H = 200, 120
-        M, V, N = _render(W, H, 2, seed=71, tiles=tiles_for_rank(W, H, rank, world))
-        t = [torch.from_numpy(a) for a in (M, V, N)]
-        for x in t:
-            dist.reduce(x, dst=0, op=dist.ReduceOp.SUM)
-        if rank == 0:
-            np.savez(os.path.join(outdir, "gathered.npz"), M=t[0].numpy(), V=t[1].numpy(), N=t[2].numpy())
+        s, c, smp = _scene()
+        r = Renderer.NewRenderer(s, c, smp, W, H, True, device=0)
+        try:
+            mine = tiles_for_rank(W, H, rank, world)
+            r.SamplesPerPixel, r.Seed, r.Tiles = 2, 71, mine
+            for _ in range(2):
+                r.RenderParallel()
+            # pt_comm_gather's protocol over gloo: tile counts, then each rank's packed tiles to
+            # the root, which writes them into its Buffer
+            cnt = torch.tensor([len(mine)], dtype=torch.int64)
+            cnts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(cnts, cnt)
+            if rank != 0:
+                dist.send(torch.from_numpy(np.ascontiguousarray(mine, np.int32)), dst=0)
+                for a in r.ReadTiles(mine):
+                    dist.send(torch.from_numpy(a), dst=0)
+            else:
+                for p in range(1, world):
+                    n = int(cnts[p][0])
+                    ids = torch.zeros(n, dtype=torch.int32)
+                    dist.recv(ids, src=p)
+                    parts = [torch.zeros((n, 32, 32, 3), dtype=torch.float64), torch.zeros((n, 32, 32, 3), dtype=torch.float64),
+                             torch.zeros((n, 32, 32), dtype=torch.int32)]
+                    for x in parts:
+                        dist.recv(x, src=p)
+                    r.WriteTiles(ids.numpy(), *(x.numpy() for x in parts))
+                b = r.ReadBuffer()
+                np.savez(os.path.join(outdir, "gathered.npz"), M=b.M, V=b.V, N=b.N)
+        finally:
+            r.close()
     finally:
         dist.destroy_process_group()
 
 
 def test_two_ranks_one_gpu_equal_single_render(gpu):
-    """World 2: each process renders its interleaved tiles through libptsharp_hip on the box's GPU,
-    gloo sums the Buffers (the reduce pt_comm_gather does over RCCL between GPUs), and the result
-    is the 1-process render's Buffer bit for bit."""
+    """World 2: each process renders its interleaved tiles through libptsharp_hip on the box's GPU;
+    the root assembles the frame with pt_comm_gather's tile-compacted protocol (counts, then packed
+    tiles via pt_read_tiles / pt_write_tiles) over gloo, and the result is the 1-process render's
+    Buffer bit for bit."""
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
