@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(256) void k_wf_finalize(DevPass P, DevBuffer B, WfQ
 // ---------------------------------------------------------------- adaptive / firefly phases
 // Entry e of a phase is one pixel with K individually accumulated samples
 // (Renderer.cs:340-470): the adaptive phase walks the pass' pixels in tile order,
-// the firefly phase the candidate list of k_wf_firefly_select.  A camera ray's
+// the extra phases the pixel lists of k_wf_select.  A camera ray's
 // accumulator index is its chunk-relative slot e·K + j, not its pixel.
 __device__ __forceinline__ bool entry_pixel(const DevPass& P, const uint32_t* plist, uint64_t e, int& x, int& y) {
     if (plist) {
