@@ -544,10 +544,16 @@ namespace PTSharpCore
         public int FireflySamples { set { foreach (var r in parts) r.FireflySamples = value; } }
         public bool StratifiedSampling { set { foreach (var r in parts) r.StratifiedSampling = value; } }
         public ulong Seed { set { foreach (var r in parts) r.Seed = value; } }
+        public int NumCPU { get => parts[0].NumCPU; set { foreach (var r in parts) r.NumCPU = value; } }
 
         /// <summary>One RenderParallel pass on every GPU, one host thread per context.</summary>
         public void RenderParallel() => Parallel.For(0, parts.Length, new ParallelOptions { MaxDegreeOfParallelism = parts.Length },
                                                      i => parts[i].RenderParallel());
+
+        /// <summary>One Render pass (the NumCPU == 1 twin, Renderer.cs:80-198) on every GPU: its extra
+        /// phases decide per pixel, so the tile split renders exactly the one-GPU frame.</summary>
+        public void Render() => Parallel.For(0, parts.Length, new ParallelOptions { MaxDegreeOfParallelism = parts.Length },
+                                             i => parts[i].Render());
 
         /// <summary>Sum the ranks' disjoint tiles onto device 0 and copy them into Renderer.PBuffer.</summary>
         public void ReadBuffer()
@@ -564,7 +570,7 @@ namespace PTSharpCore
             for (int i = 1; i <= iter; i++)
             {
                 Console.WriteLine("Iteration " + i + " of " + iter);
-                RenderParallel();
+                if (NumCPU == 1) Render(); else RenderParallel();   // Renderer.cs:712-719
                 ReadBuffer();
                 colour = Renderer.PBuffer.Image(Channel.ColorChannel);
                 using var stream = System.IO.File.OpenWrite(string.Format(pathTemplate, i));
