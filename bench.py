@@ -33,6 +33,7 @@ count Infinity-Cache hits too; profiles/pmc_traffic.json), set beside the compul
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -98,6 +99,12 @@ def main():
 
     from ptsharp_amd import Renderer, _abi, scenes, tiles_for_rank
 
+    # A rehearsal of the N-rank path on a box with fewer GPUs than ranks (ranks share devices):
+    # RCCL cannot put two ranks on one GPU, so the gather is skipped there and said so.
+    ndev = C.c_int32(0)
+    _abi.load_library().pt_device_count(C.byref(ndev))
+    shared = world > 1 and ndev.value < world
+    local = local % max(ndev.value, 1)
     t_scene = time.perf_counter()
     if a.workload == "c2":
         scene, camera, sampler = scenes.gopher3()
@@ -118,9 +125,10 @@ def main():
         r.Tiles = tiles_for_rank(W, H, k, nsh)
     if world > 1:
         r.Tiles = tiles_for_rank(W, H, rank, world)
-        obj = [Renderer.CommUniqueId() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        r.CommInit(world, rank, obj[0])
+        if not shared:
+            obj = [Renderer.CommUniqueId() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            r.CommInit(world, rank, obj[0])
     r._ensure_scene()
     st = r.Stats()
     build_ms, bvh_bytes = st.build_ms, st.bvh_bytes
@@ -160,7 +168,7 @@ def main():
         kernel_ms += s.last_pass_ms
         kms += np.array(s.kernel_ms[:])
         klaunch += np.array(s.kernel_launches[:])
-    if world > 1:
+    if world > 1 and not shared:
         r.Gather(0)
     r.Synchronize()
     t1 = time.perf_counter()
@@ -235,7 +243,8 @@ def main():
         "config": {
             "workload": WORKLOADS[a.workload],
             "width": W, "height": H, "spp_per_step": a.spp, "total_spp": a.spp * a.steps,
-            "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}" + (f" shard {a.shard}" if a.shard else ""),
+            "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}" + (f" shard {a.shard}" if a.shard else "")
+            + (f" (rehearsal: {world} ranks on {ndev.value} GPU(s), no gather)" if shared else ""),
             "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
             "rays_per_camera_sample": round(total_rays / (W * H * a.spp * a.steps), 3),
             "shadow_ray_fraction": round(ctr.shadow_rays / max(ctr.rays, 1), 4),
