@@ -264,7 +264,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
     Q.overflow = c->d_counters + pt::kOverflowCounter;
     // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
     // can run at the same time on the side stream)
-    const size_t ovf_words = (size_t)(pt::kMaxDepth - pt::kLdsStack) * pt::kWfMaxThreads;
+    const size_t ovf_words = (size_t)(pt::kStackMax - pt::kLdsStack) * pt::kWfMaxThreads;
     if ((rc = wf_alloc(c, &Q.ovf, 2 * ovf_words))) return rc;
     Q.ovf_sh = Q.ovf + ovf_words;
     size_t P = (size_t)c->width * (size_t)c->height;
@@ -347,11 +347,11 @@ inline void pad_box(float* lo, float* hi) {
 }
 
 // BVH2 → 4-wide nodes (pt_bvh.h collapse_bvh4) as device float4 rows.  The
-// collapse keeps every path's pushes within the kMaxDepth-entry LDS stack.
+// collapse keeps every path's pushes within the kStackMax-entry traversal stack.
 int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_nodes) {
     pt::Bvh4Result r;
-    pt::collapse_bvh4(b, pt::kMaxDepth, r);
-    if (r.stack_need > pt::kMaxDepth) return fail(PT_ERR_UNSUPPORTED, "BVH4 traversal stack bound exceeded");
+    pt::collapse_bvh4(b, pt::kStackMax, r);
+    if (r.stack_need > pt::kStackMax) return fail(PT_ERR_UNSUPPORTED, "BVH4 traversal stack bound exceeded");
     out.resize(r.words.size() / 4);
     std::memcpy(out.data(), r.words.data(), r.words.size() * sizeof(uint32_t));
     num_nodes = (int32_t)r.nodes();

@@ -13,7 +13,16 @@
 
 namespace pt {
 
-constexpr int kMaxDepth = 32;     // = LDS traversal stack entries per lane
+constexpr int kMaxDepth = 32;     // BVH2 depth bound
+// Traversal stack entries per lane: the BVH4 collapse keeps every root-to-leaf path's pushes
+// within it (the traversal kernels hold the first kLdsStack in LDS and the rest in a
+// per-thread global column; the megakernel all in LDS).  A larger budget lets the collapse
+// fill more nodes to four children (fewer, wider steps per ray).
+#ifndef PT_STACK_MAX
+#define PT_STACK_MAX 32
+#endif
+constexpr int kStackMax = PT_STACK_MAX;
+static_assert(kStackMax >= kMaxDepth, "the collapse needs at least the BVH2 depth");
 constexpr int kMaxLeafSize = 4;
 
 // 32-byte node; nodes[0] is the root, nodes[1] is padding, every child pair

@@ -21,7 +21,7 @@ struct HitRec {
 
 // A whole traversal stack in a private array (scratch): the nested traversal of an instanced mesh.
 struct LocalStack {
-    static constexpr int kLds = kMaxDepth;
+    static constexpr int kLds = kStackMax;
     static constexpr int kStride = 1;
     uint32_t* lds;
     __device__ __forceinline__ void put(int i, uint32_t v) const { lds[i] = v; }
@@ -85,7 +85,7 @@ __device__ __forceinline__ double prim_t(const DevScene& S, const float4* __rest
     return inner_t(S, r, kind, o, d);
 }
 
-// Per-lane traversal stacks.  LdsStack: all kMaxDepth entries in LDS (column
+// Per-lane traversal stacks.  LdsStack: all kStackMax entries in LDS (column
 // `lds`, entries STRIDE words apart).  SpillStack: the first LDSN entries in LDS
 // and the rarely used deeper ones in a per-thread global column (entries
 // `ostride` words apart, coalesced across lanes), so a traversal kernel's LDS
@@ -95,7 +95,7 @@ __device__ __forceinline__ double prim_t(const DevScene& S, const float4* __rest
 // unconditionally and advances sp by predicate: no per-push branch.
 template <int STRIDE>
 struct LdsStack {
-    static constexpr int kLds = kMaxDepth;
+    static constexpr int kLds = kStackMax;
     static constexpr int kStride = STRIDE;
     uint32_t* lds;
     __device__ __forceinline__ void put(int i, uint32_t v) const { lds[i * STRIDE] = v; }
@@ -162,7 +162,7 @@ __device__ __forceinline__ void cswap(float& ka, uint32_t& va, float& kb, uint32
 // one 128-byte line fetched with seven independent 16-byte loads; the four
 // child slabs are tested, hits sorted nearest-first with a 5-comparator network,
 // the nearest descended and the others pushed far-to-near on the per-lane stack
-// (LdsStack / SpillStack).  The builder bounds every path's pushes by kMaxDepth.
+// (LdsStack / SpillStack).  The collapse bounds every path's pushes by kStackMax.
 // ANY: stop at the first primitive with t < best.t (shadow visibility).
 template <bool TRI, bool COUNT, bool ANY, bool FULL, class STK>
 __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __restrict__ nodes, int32_t num_nodes,
@@ -290,7 +290,7 @@ __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 i
 // idx is the triangle's position in the mesh's BLAS records.
 __device__ __noinline__ HitRec blas_hit(const DevScene& S, int b, v3 o, v3 d) {
     const DevBlas B = S.blas[b];
-    uint32_t st[kMaxDepth];
+    uint32_t st[kStackMax];
     const LocalStack stack{st};
     HitRec best{kHitInf, -1, -1};
     Counters ctr{0, 0, 0, 0};

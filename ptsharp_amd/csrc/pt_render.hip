@@ -201,7 +201,7 @@ __device__ void sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3 d
 template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera cam, DevSampler smp, DevPass P,
                                                         DevBuffer B) {
-    __shared__ uint32_t s_stack[kMaxDepth * kBlock];
+    __shared__ uint32_t s_stack[kStackMax * kBlock];
     const MStack stack{s_stack + threadIdx.x};
     const int tile_slot = blockIdx.x >> 2;
     const int quarter = blockIdx.x & 3;

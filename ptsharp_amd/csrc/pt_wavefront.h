@@ -41,7 +41,7 @@ struct WfQueues {
     uint32_t s_cap;      // NEE queue entries (kParts partitions of spcap)
     uint32_t pcap, spcap;
     FixAcc acc;          // [P] per-pixel sum of this pass' sample colours (pt_accum.h: order-independent)
-    uint32_t* ovf;       // closest-hit traversal stack entries beyond kLdsStack: [kMaxDepth - kLdsStack][kWfMaxThreads]
+    uint32_t* ovf;       // closest-hit traversal stack entries beyond kLdsStack: [kStackMax - kLdsStack][kWfMaxThreads]
     uint32_t* ovf_sh;    // the same for the shadow kernels, which may run beside a closest-hit kernel (side stream)
     FixAcc acc_s;        // [chunk] per-sample accumulators of the adaptive / firefly phases
 };
