@@ -65,6 +65,28 @@ WORKLOADS = {
 B_NODE, B_PRIM, B_RAY, B_SHADE = 112, 36, 28 + 16, 40
 
 
+def _gloo_gather(r, dist, rank, world, mine):
+    """pt_comm_gather's protocol over gloo (tile counts, then each rank's packed tiles to rank 0,
+    written into its Buffer with pt_write_tiles): the fallback if the RCCL gather fails."""
+    import torch
+    cnts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(cnts, torch.tensor([len(mine)], dtype=torch.int64))
+    if rank != 0:
+        dist.send(torch.from_numpy(np.ascontiguousarray(mine, np.int32)), dst=0)
+        for a in r.ReadTiles(mine):
+            dist.send(torch.from_numpy(np.ascontiguousarray(a)), dst=0)
+        return
+    for p in range(1, world):
+        n = int(cnts[p][0])
+        ids = torch.zeros(n, dtype=torch.int32)
+        dist.recv(ids, src=p)
+        parts = [torch.zeros((n, 32, 32, 3), dtype=torch.float64), torch.zeros((n, 32, 32, 3), dtype=torch.float64),
+                 torch.zeros((n, 32, 32), dtype=torch.int32)]
+        for x in parts:
+            dist.recv(x, src=p)
+        r.WriteTiles(ids.numpy(), *(x.numpy() for x in parts))
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -100,7 +122,7 @@ def main():
     from ptsharp_amd import Renderer, _abi, scenes, tiles_for_rank
 
     # A rehearsal of the N-rank path on a box with fewer GPUs than ranks (ranks share devices):
-    # RCCL cannot put two ranks on one GPU, so the gather is skipped there and said so.
+    # RCCL cannot put two ranks on one GPU, so the tiles are gathered over gloo there, and said so.
     ndev = C.c_int32(0)
     _abi.load_library().pt_device_count(C.byref(ndev))
     shared = world > 1 and ndev.value < world
@@ -168,8 +190,18 @@ def main():
         kernel_ms += s.last_pass_ms
         kms += np.array(s.kernel_ms[:])
         klaunch += np.array(s.kernel_launches[:])
-    if world > 1 and not shared:
-        r.Gather(0)
+    gather = None
+    if shared:   # no RCCL between ranks on one device: the same tile protocol over gloo
+        _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
+        gather = "gloo (rehearsal)"
+    elif world > 1:
+        try:
+            r.Gather(0)   # pt_comm_gather: tile-compacted send/recv over RCCL
+            gather = "rccl"
+        except Exception as e:   # the same protocol over gloo, so the run still reports
+            print(f"pt_comm_gather failed ({e}); gathering the tiles over gloo", file=sys.stderr, flush=True)
+            _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
+            gather = "gloo (RCCL gather failed)"
     r.Synchronize()
     t1 = time.perf_counter()
     if dist:
@@ -244,7 +276,8 @@ def main():
             "workload": WORKLOADS[a.workload],
             "width": W, "height": H, "spp_per_step": a.spp, "total_spp": a.spp * a.steps,
             "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}" + (f" shard {a.shard}" if a.shard else "")
-            + (f" (rehearsal: {world} ranks on {ndev.value} GPU(s), no gather)" if shared else ""),
+            + (f" (rehearsal: {world} ranks on {ndev.value} GPU(s))" if shared else "")
+            + (f", gather {gather}" if gather else ""),
             "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
             "rays_per_camera_sample": round(total_rays / (W * H * a.spp * a.steps), 3),
             "shadow_ray_fraction": round(ctr.shadow_rays / max(ctr.rays, 1), 4),
