@@ -125,7 +125,8 @@ def main():
     # RCCL cannot put two ranks on one GPU, so the tiles are gathered over gloo there, and said so.
     ndev = C.c_int32(0)
     _abi.load_library().pt_device_count(C.byref(ndev))
-    shared = world > 1 and ndev.value < world
+    shared = world > 1 and ndev.value < world and not os.environ.get("PT_BENCH_FORCE_RCCL")
+    rccl_ok = False
     local = local % max(ndev.value, 1)
     t_scene = time.perf_counter()
     if a.workload == "c2":
@@ -150,7 +151,16 @@ def main():
         if not shared:
             obj = [Renderer.CommUniqueId() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
-            r.CommInit(world, rank, obj[0])
+            ok = 1
+            try:
+                r.CommInit(world, rank, obj[0])
+            except Exception as e:
+                print(f"pt_comm_init failed ({e}); the tiles will be gathered over gloo", file=sys.stderr, flush=True)
+                ok = 0
+            import torch
+            t_ok = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
+            rccl_ok = bool(t_ok[0])
     r._ensure_scene()
     st = r.Stats()
     build_ms, bvh_bytes = st.build_ms, st.bvh_bytes
@@ -194,12 +204,22 @@ def main():
     if shared:   # no RCCL between ranks on one device: the same tile protocol over gloo
         _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
         gather = "gloo (rehearsal)"
+    elif world > 1 and not rccl_ok:
+        _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
+        gather = "gloo (RCCL init failed)"
     elif world > 1:
+        ok = 1
         try:
             r.Gather(0)   # pt_comm_gather: tile-compacted send/recv over RCCL
-            gather = "rccl"
-        except Exception as e:   # the same protocol over gloo, so the run still reports
+        except Exception as e:   # then every rank takes the same protocol over gloo
             print(f"pt_comm_gather failed ({e}); gathering the tiles over gloo", file=sys.stderr, flush=True)
+            ok = 0
+        import torch
+        t_ok = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
+        if int(t_ok[0]):
+            gather = "rccl"
+        else:
             _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
             gather = "gloo (RCCL gather failed)"
     r.Synchronize()
