@@ -138,7 +138,7 @@ constexpr int kBlockMajorFH = 16;
 constexpr int kBlockMajorChildren = 32;
 constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera slot (k_wf_trace)
 #ifndef PT_SHADE_SCAN
-#define PT_SHADE_SCAN 8
+#define PT_SHADE_SCAN 16   // 4 / 8 / 16 / 24 / 32 measured on C4 (round 2), 16 best
 #endif
 constexpr int kShadeScan = PT_SHADE_SCAN;   // 256-vertex groups a SCAN shade block claims and lists
 // The environment may be textured (non-black per direction) only where the shade kernel
