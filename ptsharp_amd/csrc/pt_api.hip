@@ -1145,6 +1145,10 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     plan.trace_blocks = c->grids.trace_blocks;
     plan.shade_blocks = c->grids.shade_blocks;
     plan.shadow_blocks = c->grids.shadow_blocks;
+    plan.lanes_trace_blocks = c->grids.lanes_trace_blocks;
+    plan.lanes_shadow_blocks = c->grids.lanes_shadow_blocks;
+    plan.full_trace_blocks = c->grids.full_trace_blocks;
+    plan.full_shadow_blocks = c->grids.full_shadow_blocks;
     const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp);
     double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)
     if (nm == 2) growth = std::ldexp(1.0, std::min(std::max(sampler->max_bounces - 1, 0), 60));

@@ -75,9 +75,10 @@ struct WfPlan {
     uint32_t root_children;    // ⌊√FH⌋² · modes at depth 0
     uint32_t children;         // modes at depth >= 1 (1, or 2 under SpecularModeAll)
     uint32_t lights_per_child; // shadow-ray slots per diffuse child: 1, or #lights under LightModeAll
-    uint32_t trace_blocks;     // persistent grids: resident capacity of each kernel
-    uint32_t shade_blocks;
+    uint32_t trace_blocks;     // persistent grids: resident capacity of each kernel (lockstep traversal,
+    uint32_t shade_blocks;     // shade, lockstep shadow; the refill and FULL traversal kernels below)
     uint32_t shadow_blocks;
+    uint32_t lanes_trace_blocks, lanes_shadow_blocks, full_trace_blocks, full_shadow_blocks;
     int32_t shade_form;        // k_wf_shade form: 0 chosen per depth from the kept count, 1 direct, 2 SCAN
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
     int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always

@@ -266,6 +266,12 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
 }
 
 // ---------------------------------------------------------------- closest hit
+// Waves per SIMD of the lockstep traversal kernels (analytic scenes: gopher3 7 > 6) and of the
+// per-lane refill kernels (C4: 5 / 6 / 7 / 8 measured, 6 best: 80 VGPRs and no spills in the
+// step loop, closest hit 58.3 → 49.5 ms and shadow 25.2 → 22.1 ms per pass against 7).
+#ifndef PT_LANES_WAVES
+#define PT_LANES_WAVES 6
+#endif
 #ifndef PT_TRACE_WAVES
 #define PT_TRACE_WAVES 7
 #endif
@@ -342,7 +348,7 @@ constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
 #define PT_SHADOW_REFILL_IDLE 32   // shadow: 16 / 24 / 32 / 48 measured, 32 best
 #endif
 template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_TRACE_WAVES) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
@@ -763,7 +769,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
 
 // ---------------------------------------------------------------- shadow rays
 #ifndef PT_SHADOW_WAVES
-#define PT_SHADOW_WAVES 7
+#define PT_SHADOW_WAVES 7   // lockstep shadow kernel; the refill one runs PT_LANES_WAVES
 #endif
 // One thread per shadow ray that k_wf_shade set up (light, direction, the colour the
 // light adds if it is the nearest hit): the visibility query of Sampler.cs:261-265.
@@ -812,7 +818,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // the triangle BVH, any-hit (a primitive strictly nearer than the light ends the ray
 // unlit).  The outcome goes to n_lit; k_wf_nee_accum adds the lit rays' terms.
 template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_SHADOW_WAVES) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
@@ -1111,7 +1117,7 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     const bool lanes = plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes;
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
-        const unsigned tg = grid_for(n, kTB, plan.trace_blocks);
+        const unsigned tg = grid_for(n, kTB, fullg ? plan.full_trace_blocks : lanes ? plan.lanes_trace_blocks : plan.trace_blocks);
         begin_k(1, stream);
         if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
@@ -1148,7 +1154,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
             (void)hipStreamWaitEvent(side, plan.ev_main, 0);
         }
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
-        const unsigned hg = grid_for(children * plan.lights_per_child, kTB, plan.shadow_blocks);
+        const unsigned hg = grid_for(children * plan.lights_per_child, kTB,
+                                     fullg ? plan.full_shadow_blocks : lanes ? plan.lanes_shadow_blocks : plan.shadow_blocks);
         begin_k(3, side);
         if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
@@ -1251,6 +1258,14 @@ hipError_t wavefront_grids(WfPlan& plan) {
     if (e == hipSuccess) plan.shade_blocks = resident(nb, 1u << 20);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false, false>, kTB, 0);
     if (e == hipSuccess) plan.shadow_blocks = resident(nb, kWfMaxBlocks);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace_lanes<false>, kTB, 0);
+    if (e == hipSuccess) plan.lanes_trace_blocks = resident(nb, kWfMaxBlocks);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow_lanes<false>, kTB, 0);
+    if (e == hipSuccess) plan.lanes_shadow_blocks = resident(nb, kWfMaxBlocks);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace<false, true>, kTB, 0);
+    if (e == hipSuccess) plan.full_trace_blocks = resident(nb, kWfMaxBlocks);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false, true>, kTB, 0);
+    if (e == hipSuccess) plan.full_shadow_blocks = resident(nb, kWfMaxBlocks);
     return e;
 }
 
