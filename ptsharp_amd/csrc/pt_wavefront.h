@@ -66,7 +66,10 @@ constexpr int kOverflowCounter = 15;            // DevBuffer::counters word of W
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
 
-constexpr int kLdsStack = 16;                    // LDS stack entries per lane (traversal kernels)
+#ifndef PT_LDS_STACK
+#define PT_LDS_STACK 16
+#endif
+constexpr int kLdsStack = PT_LDS_STACK;          // LDS stack entries per lane (traversal kernels)
 constexpr uint32_t kWfMaxBlocks = 256 * 8;        // grid cap of the traversal kernels
 constexpr uint32_t kWfMaxThreads = kWfMaxBlocks * 256;
 
