@@ -233,3 +233,14 @@ def test_exact_t_tie_follows_leaf_order(light_first):
     assert (k, i) in {(kind, idx), (0, other)}
     assert (sum(col) > 0) == ((k, i) == (kind, idx))        # the leaf's first sphere decides
     assert not osc.any_nearer(pos, d.t(), t_twin)            # any-hit: nothing strictly nearer → lit
+
+
+def test_oracle_keeps_sin_and_cos_separate():
+    """.NET's Math.Sin and Math.Cos are two libm calls.  A sincos() fused by the compiler rounds
+    differently in the last ulp on this glibc (e.g. sin(0.15142274361170249)), which surfaced as a
+    rare sampleLight coverage mismatch; oracle/Makefile builds with -fno-builtin-sin/-cos."""
+    import subprocess
+    syms = subprocess.run(["nm", "-D", O.build_oracle()], capture_output=True, text=True).stdout
+    assert "sincos" not in syms
+    L = O.lib()
+    assert L is not None
