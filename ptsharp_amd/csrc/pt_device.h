@@ -655,10 +655,10 @@ __device__ __forceinline__ v3 cone(v3 direction, double theta, double u, double 
     if (theta < kEps) return direction;
     theta = theta * (1 - (2 * acos(u) / kPi));
     double m1, m2;
-    sincos(theta, &m1, &m2);
+    pt_sincos(theta, &m1, &m2);
     double a = v * 2 * kPi;
     double sa, ca;
-    sincos(a, &sa, &ca);
+    pt_sincos(a, &sa, &ca);
     v3 q = random_unit_vector(key, D_RUV_Z, D_RUV_A);
     v3 s = cross(direction, q);
     v3 t = cross(direction, s);
@@ -704,7 +704,7 @@ __device__ __forceinline__ void bounce_dir(const DevMaterial& m, const Shade& sh
         double radius = sqrt(u);
         double theta = 2 * kPi * v;
         double st, ct;
-        sincos(theta, &st, &ct);
+        pt_sincos(theta, &st, &ct);
         v3 s = normalize(cross(sh.nrm, random_unit_vector(key, D_RUV_Z, D_RUV_A)));
         v3 t = cross(sh.nrm, s);
         no = sh.pos;
@@ -776,7 +776,7 @@ __device__ __forceinline__ void cast_ray(const DevCamera& cam, int x, int y, int
         double angle = draw(key, D_LENS_ANGLE) * 2 * kPi;
         double radius = draw(key, D_LENS_RADIUS) * cam.aperture_radius;
         double sa, ca;
-        sincos(angle, &sa, &ca);
+        pt_sincos(angle, &sa, &ca);
         o = add(o, muls(cu, ca * radius));
         o = add(o, muls(cv, sa * radius));
         d = normalize(sub(focal, o));
