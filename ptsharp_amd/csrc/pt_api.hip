@@ -1017,7 +1017,20 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     }
 
     pt::DevScene S{};
-    rc = upload(c, tri_nodes, &S.tri_nodes); if (rc) return rc;
+    {   // the traversal lines: [ana_nodes | tri_nodes | tri_chunks], 8 float4 per node / chunk
+        std::vector<float4> lines;
+        lines.reserve(ana_nodes.size() + tri_nodes.size() + tri_chunks.size());
+        lines.insert(lines.end(), ana_nodes.begin(), ana_nodes.end());
+        lines.insert(lines.end(), tri_nodes.begin(), tri_nodes.end());
+        lines.insert(lines.end(), tri_chunks.begin(), tri_chunks.end());
+        if (lines.size() / 8 >= 0xFFFFFFFFull) return fail(PT_ERR_UNSUPPORTED, "more than 2^32 BVH lines");
+        rc = upload(c, lines, &S.lines); if (rc) return rc;
+        S.tri_node_line0 = (uint32_t)(ana_nodes.size() / 8);
+        S.tri_chunk_line0 = (uint32_t)((ana_nodes.size() + tri_nodes.size()) / 8);
+        S.ana_nodes = ana_nodes.empty() ? nullptr : S.lines;
+        S.tri_nodes = tri_nodes.empty() ? nullptr : S.lines + 8 * (size_t)S.tri_node_line0;
+        S.tri_chunks = tri_chunks.empty() ? nullptr : S.lines + 8 * (size_t)S.tri_chunk_line0;
+    }
     // one 128-B shading record per triangle (pt_scene.h tri_rstride): what k_wf_shade reads
     // for a triangle hit is one line instead of two or three
     std::vector<float4> tri_sh(nt * 8, f4(0.f, 0.f, 0.f, 0.f));
@@ -1034,8 +1047,6 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     S.tri_uv = d_tri_sh && want_uv ? d_tri_sh + 6 : nullptr;
     S.tri_rstride = 8;
     S.tri_ustride = 8;
-    rc = upload(c, tri_chunks, &S.tri_chunks); if (rc) return rc;
-    rc = upload(c, ana_nodes, &S.ana_nodes); if (rc) return rc;
     rc = upload(c, ana_recs, &S.ana_recs); if (rc) return rc;
     rc = upload(c, planes, &S.planes); if (rc) return rc;
     rc = upload(c, mats, &S.mats); if (rc) return rc;

@@ -61,6 +61,10 @@ struct DevScene {
     const float4* ana_nodes;
     int32_t ana_num_nodes;
     const float4* ana_recs;    // 3 float4: {a.xyz,kind} {b.xyz,scene index} {mat, radius(double) | ext index, -}
+    // ana_nodes, tri_nodes and tri_chunks are one allocation of 128-B lines (in that order), so
+    // the cooperative fetch (pt_wavefront.hip coop_line) names any traversal line by a 32-bit index
+    const float4* lines;
+    uint32_t tri_node_line0, tri_chunk_line0;
     // planes (unbounded: tested outside the BVHs)
     const float4* planes;      // 2 float4: {point.xyz, mat} {normal.xyz, scene index}
     int32_t num_planes;

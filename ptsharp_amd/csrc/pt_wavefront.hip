@@ -337,6 +337,74 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 // atomic per refill).  A new ray's head work is two queue loads and the planes (none in
 // C4), so a refill holds the busy lanes for one load round trip.  Same visit order,
 // same arithmetic as trace(): bit-identical hits.
+#ifndef PT_COOP
+#define PT_COOP 0            // 1: the per-lane refill kernels fetch lines cooperatively (measured slower)
+#endif
+#ifndef PT_COOP_STAGE
+#define PT_COOP_STAGE 32     // lines staged in LDS per wave per pass (64: one pass, 32: two)
+#endif
+#ifndef PT_LANES_VGPRS
+// the register budget of the per-lane refill kernels: 512 / waves, rounded down to 8.  Pinned
+// explicitly because the compiler sizes it for the occupancy it computes from LDS, and with the
+// coop staging rows that estimate is below what the CU's 160 KB actually holds
+#define PT_LANES_VGPRS ((512 / PT_LANES_WAVES) & ~7)
+#endif
+constexpr uint32_t kNoLine = 0xFFFFFFFFu;
+constexpr int kCoopStage = PT_COOP_STAGE;
+constexpr int kCoopRows = PT_COOP ? 4 * kCoopStage * 7 : 1;   // float4 of LDS per block
+// Cooperative line fetch.  A traversal step reads one 128-B line per lane (a BVH4 node or a
+// leaf chunk) as seven 16-B loads; with every lane on its own line, each load instruction
+// touches 64 distinct lines and the texture-address path charges per line, ~1 cycle each
+// (the per-lane refill kernels ran at that bound).  Here the 8 lanes of a group
+// load the group's 8 lines, one line per instruction (lanes 0..6 of the group take one 16-B
+// piece each, so an instruction touches 8 lines), stage them in LDS through this wave's rows
+// and each lane reads its own line back: 8 load instructions of 8 lines instead of 7 of 64.
+// Every load is issued before the first LDS hand-off (one memory round trip per step);
+// kCoopStage < 64 stages the groups' lines in 64 / kCoopStage passes through fewer rows.
+// Wave-uniform call: every lane takes part, `line` = kNoLine for a lane with nothing to fetch.
+template <int J>
+__device__ __forceinline__ uint32_t bcast8(uint32_t x) {   // lane J of each group of 8 (ds_swizzle bit mode)
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18 | (J << 5));
+}
+__device__ __forceinline__ void coop_line(const float4* __restrict__ lines, uint32_t line, float4* st, uint32_t lane,
+                                          float4& q0, float4& q1, float4& q2, float4& q3, float4& q4, float4& q5,
+                                          float4& q6) {
+    const uint32_t piece = lane & 7u, g = lane >> 3;
+    float4 v[8];
+    const uint32_t src[8] = {bcast8<0>(line), bcast8<1>(line), bcast8<2>(line), bcast8<3>(line),
+                             bcast8<4>(line), bcast8<5>(line), bcast8<6>(line), bcast8<7>(line)};
+#pragma unroll
+    for (int j = 0; j < 8; j++) {   // lane (g, piece) loads piece `piece` of the line of lane 8g + j
+        v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (src[j] != kNoLine && piece < 7u) v[j] = lines[8 * (size_t)src[j] + piece];   // cached: the tree is reused
+    }
+    constexpr int kPer = kCoopStage / 8;   // lines per group per pass
+#pragma unroll
+    for (int h = 0; h < 8 / kPer; h++) {
+#pragma unroll
+        for (int jj = 0; jj < kPer; jj++)
+            if (piece < 7u) st[(g * kPer + (uint32_t)jj) * 7u + piece] = v[h * kPer + jj];
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes done
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t mj = piece - (uint32_t)(h * kPer);
+        if (mj < (uint32_t)kPer) {
+            const float4* r = st + (g * kPer + mj) * 7u;
+            q0 = r[0]; q1 = r[1]; q2 = r[2]; q3 = r[3]; q4 = r[4]; q5 = r[5]; q6 = r[6];
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // the reads done before the next pass rewrites the rows
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// The line a traversal lane reads at its next step (coop_line's index; the arrays are one
+// allocation, pt_scene.h `lines`); an analytic leaf reads its records instead.
+__device__ __forceinline__ uint32_t step_line(const DevScene& S, bool has, bool tri, uint32_t ref) {
+    const bool leaf = (ref & 0x80000000u) != 0;
+    if (!has) return kNoLine;
+    if (tri) return (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu);
+    return leaf ? kNoLine : ref;
+}
+
 #ifndef PT_REFILL_IDLE
 #define PT_REFILL_IDLE 40   // closest hit: 8 / 16 / 24 / 32 / 40 / 48 measured on C4, 40 best
 #endif
@@ -348,8 +416,9 @@ constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
 #define PT_SHADOW_REFILL_IDLE 32   // shadow: 16 / 24 / 32 / 48 measured, 32 best
 #endif
 template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_LANES_WAVES) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
+    __shared__ float4 s_coop[kCoopRows];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
@@ -414,12 +483,21 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) void k_wf_trace_lanes(DevScene
             }
         }
         if (!more && __ballot(has) == 0ull) break;
-        if (!has) continue;
-        // one step: inner node or leaf of the current BVH (seven 16-B loads)
+        // one step: inner node or leaf of the current BVH (one 128-B line)
         const bool leaf = (ref & 0x80000000u) != 0;
-        const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
-                              : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
-        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6];
+        float4 q0, q1, q2, q3, q4, q5, q6;
+#if PT_COOP
+        coop_line(S.lines, step_line(S, has, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
+                  q3, q4, q5, q6);
+        if (!has) continue;
+#else
+        if (!has) continue;
+        {
+            const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
+                                  : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
+            q0 = c[0]; q1 = c[1]; q2 = c[2]; q3 = c[3]; q4 = c[4]; q5 = c[5]; q6 = c[6];
+        }
+#endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
         bool pop = true;
         if (!leaf) {
@@ -818,8 +896,9 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // the triangle BVH, any-hit (a primitive strictly nearer than the light ends the ray
 // unlit).  The outcome goes to n_lit; k_wf_nee_accum adds the lit rays' terms.
 template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_LANES_WAVES) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
+    __shared__ float4 s_coop[kCoopRows];
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
@@ -881,11 +960,21 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) void k_wf_shadow_lanes(DevScen
             }
         }
         if (!more && __ballot(has) == 0ull) break;
-        if (!has) continue;
+        // one step: inner node or leaf of the current BVH (one 128-B line)
         const bool leaf = (ref & 0x80000000u) != 0;
-        const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
-                              : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
-        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6];
+        float4 q0, q1, q2, q3, q4, q5, q6;
+#if PT_COOP
+        coop_line(S.lines, step_line(S, has, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
+                  q3, q4, q5, q6);
+        if (!has) continue;
+#else
+        if (!has) continue;
+        {
+            const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
+                                  : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
+            q0 = c[0]; q1 = c[1]; q2 = c[2]; q3 = c[3]; q4 = c[4]; q5 = c[5]; q6 = c[6];
+        }
+#endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
         bool pop = true, blocked = false;
         if (!leaf) {
