@@ -351,7 +351,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 #endif
 constexpr uint32_t kNoLine = 0xFFFFFFFFu;
 constexpr int kCoopStage = PT_COOP_STAGE;
-constexpr int kCoopRows = PT_COOP ? 4 * kCoopStage * 7 : 1;   // float4 of LDS per block
+[[maybe_unused]] constexpr int kCoopRows = 4 * kCoopStage * 7;   // float4 of LDS per block (PT_COOP)
 // Cooperative line fetch.  A traversal step reads one 128-B line per lane (a BVH4 node or a
 // leaf chunk) as seven 16-B loads; with every lane on its own line, each load instruction
 // touches 64 distinct lines and the texture-address path charges per line, ~1 cycle each
@@ -412,22 +412,32 @@ __device__ __forceinline__ uint32_t step_line(const DevScene& S, bool has, bool 
 #define PT_LANES_MIN_NODES 64
 #endif
 constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
+#ifndef PT_STEAL
+#define PT_STEAL 0   // 1: a refill wave whose partition is drained claims from the others (measured slower)
+#endif
+#ifndef PT_SHADOW_HELP
+#define PT_SHADOW_HELP 1   // shadow refill kernel: idle lanes help the tail's rays (k_wf_shadow_lanes)
+#endif
 #ifndef PT_SHADOW_REFILL_IDLE
 #define PT_SHADOW_REFILL_IDLE 32   // shadow: 16 / 24 / 32 / 48 measured, 32 best
 #endif
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
+#if PT_COOP
     __shared__ float4 s_coop[kCoopRows];
+#endif
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
         Q.counts[fetch_word(1, threadIdx.x)] = 0u;               // k_wf_shade's fetch cursors
     }
     const Group G = xcd_group();
-    const uint32_t cnt = *ray_count(Q, qi, G.g);
-    const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
-    uint32_t* cursor = Q.counts + fetch_word(0, G.g);
+    // claims start in the XCD's own partition; with PT_STEAL a wave whose partition is drained
+    // goes on to the next ones (hits are stored by slot, so which XCD traces a ray changes nothing)
+    uint32_t part = G.g, hops = 0;
+    uint32_t n = min(*ray_count(Q, qi, part), Q.pcap), base = part * Q.pcap;
+    uint32_t* cursor = Q.counts + fetch_word(0, part);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     Counters ctr{0, 0, 0, 0};
@@ -453,11 +463,20 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
         if (more && (nidle >= PT_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
             uint32_t kc = 0;
             if (lane == 0) kc = atomicAdd(cursor, nidle);
-            kc = __shfl(kc, 0, 64);
-            if (kc + nidle >= n) more = false;
-            const uint32_t k = kc + (uint32_t)__popcll(idle & below);
-            if (!has && k < n) {
-                i = base + k;
+            kc = __builtin_amdgcn_readfirstlane(kc);   // every lane is active here: lane 0's claim, in an SGPR
+            const uint32_t k = kc + (uint32_t)__popcll(idle & below), cn = n, cbase = base;
+            if (kc + nidle >= n) {   // this partition is drained
+                if (PT_STEAL && ++hops < (uint32_t)kParts) {
+                    part = (part + 1u) % (uint32_t)kParts;
+                    n = min(*ray_count(Q, qi, part), Q.pcap);
+                    base = part * Q.pcap;
+                    cursor = Q.counts + fetch_word(0, part);
+                } else {
+                    more = false;
+                }
+            }
+            if (!has && k < cn) {
+                i = cbase + k;
                 const float4 b = nt_load(&Q.q_d[qi][i]);
                 const float4 a = nt_load(&Q.q_o[qi][i]);
                 if (__float_as_uint(b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
@@ -898,12 +917,14 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
+#if PT_COOP
     __shared__ float4 s_coop[kCoopRows];
+#endif
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
-    const uint32_t cnt = *nee_count(Q, qo, G.g);
-    const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
-    uint32_t* cursor = Q.counts + fetch_word(2 + qo, G.g);
+    uint32_t part = G.g, hops = 0;   // as k_wf_trace_lanes: own partition first, then (PT_STEAL) the others
+    uint32_t n = min(*nee_count(Q, qo, part), Q.spcap), base = part * Q.spcap;
+    uint32_t* cursor = Q.counts + fetch_word(2 + qo, part);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     Counters ctr{0, 0, 0, 0};
@@ -914,17 +935,38 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
     double tl = kHitInf;
     float tmax = 0.f;
+    bool waiting = false;   // a root whose traversal is done, waiting for its tail helpers
+#if PT_SHADOW_HELP
+    // The tail (queue drained): idle lanes take stack entries of busy lanes' rays and traverse
+    // those subtrees (any-hit: the ray is blocked iff some subtree holds a blocker, in any order).
+    // s_help[root]: helpers still running on root's ray, bit 31 = blocked.  A root that ends its
+    // own traversal waits for its helpers before it reports the ray lit.
+    __shared__ uint32_t s_help[kTB];
+    __shared__ uint32_t s_map[kTB];   // per wave: donor lane by rank
+    bool helper = false;
+    uint32_t root = threadIdx.x;
+    const uint32_t wbase = threadIdx.x & ~63u;
+#endif
     for (;;) {
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (more && (nidle >= PT_SHADOW_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
             uint32_t kc = 0;
             if (lane == 0) kc = atomicAdd(cursor, nidle);
-            kc = __shfl(kc, 0, 64);
-            if (kc + nidle >= n) more = false;
-            const uint32_t k = kc + (uint32_t)__popcll(idle & below);
-            if (!has && k < n) {
-                i = base + k;
+            kc = __builtin_amdgcn_readfirstlane(kc);   // every lane is active here: lane 0's claim, in an SGPR
+            const uint32_t k = kc + (uint32_t)__popcll(idle & below), cn = n, cbase = base;
+            if (kc + nidle >= n) {
+                if (PT_STEAL && ++hops < (uint32_t)kParts) {
+                    part = (part + 1u) % (uint32_t)kParts;
+                    n = min(*nee_count(Q, qo, part), Q.spcap);
+                    base = part * Q.spcap;
+                    cursor = Q.counts + fetch_word(2 + qo, part);
+                } else {
+                    more = false;
+                }
+            }
+            if (!has && k < cn) {
+                i = cbase + k;
                 const float4 b = nt_load(&Q.n_n[qo][i]);
                 const float4 a = nt_load(&Q.n_o[qo][i]);
                 const uint32_t li = __float_as_uint(b.w);
@@ -956,19 +998,72 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                     ref = 0;
                     has = run;
                     if (!run) Q.n_lit[qo][i] = 0;
+#if PT_SHADOW_HELP
+                    s_help[threadIdx.x] = 0u;
+#endif
                 }
             }
         }
         if (!more && __ballot(has) == 0ull) break;
+#if PT_SHADOW_HELP
+        if (!COUNT && !more) {   // wave-uniform: the tail (not in the counting pass: its node counts stay sequential)
+            if (has) {
+                const uint32_t st = s_help[root];
+                if (st & 0x80000000u) {   // a helper found a blocker: the root ends unlit, its helpers stop
+                    if (!helper) Q.n_lit[qo][i] = 0;
+                    has = false;
+                } else if (waiting && st == 0u) {   // the root's own traversal and every helper done
+                    Q.n_lit[qo][i] = phantom ? 0 : 1;
+                    has = false;
+                }
+            }
+            const uint64_t idle = __ballot(!has), don = __ballot(has && !waiting && sp > 0);
+            if (idle != 0ull && don != 0ull) {
+                const uint32_t nd = min((uint32_t)__popcll(idle), (uint32_t)__popcll(don));
+                const uint32_t rd = (uint32_t)__popcll(don & below), ri = (uint32_t)__popcll(idle & below);
+                uint32_t top = 0;
+                if (has && !waiting && sp > 0 && rd < nd) {   // give the top entry (what this lane would pop next)
+                    sp--;
+                    top = stack.get(sp);
+                    s_map[wbase + rd] = lane;
+                    atomicAdd(&s_help[root], 1u);
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
+                const bool take = !has && ri < nd;
+                const int src = take ? (int)s_map[wbase + ri] : (int)lane;
+                const float ox = __shfl(o.x, src, 64), oy = __shfl(o.y, src, 64), oz = __shfl(o.z, src, 64);
+                const float dx = __shfl(d.x, src, 64), dy = __shfl(d.y, src, 64), dz = __shfl(d.z, src, 64);
+                const double tls = __shfl(tl, src, 64);
+                const uint32_t rt = __shfl(root, src, 64), tp = __shfl(top, src, 64);
+                const int fl = __shfl((tri ? 1 : 0) | (phantom ? 2 : 0), src, 64);
+                if (take) {
+                    o = v3{ox, oy, oz};
+                    d = v3{dx, dy, dz};
+                    invd = v3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                    tl = tls;
+                    tmax = tmax_bound(tl);
+                    root = rt;
+                    ref = tp;
+                    sp = 0;
+                    tri = (fl & 1) != 0;
+                    phantom = (fl & 2) != 0;
+                    helper = true;
+                    waiting = false;
+                    has = true;
+                }
+            }
+        }
+#endif
         // one step: inner node or leaf of the current BVH (one 128-B line)
         const bool leaf = (ref & 0x80000000u) != 0;
         float4 q0, q1, q2, q3, q4, q5, q6;
 #if PT_COOP
-        coop_line(S.lines, step_line(S, has, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
+        coop_line(S.lines, step_line(S, has && !waiting, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
                   q3, q4, q5, q6);
-        if (!has) continue;
+        if (!has || waiting) continue;
 #else
-        if (!has) continue;
+        if (!has || waiting) continue;
         {
             const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
                                   : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
@@ -1018,6 +1113,32 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                 if (prim_t<false, false>(S, S.ana_recs, first + k, o, d, kind) < tl) { blocked = true; break; }
             }
         }
+#if PT_SHADOW_HELP
+        if (blocked) {
+            has = false;
+            if (helper) atomicOr(&s_help[root], 0x80000000u);
+            else {
+                Q.n_lit[qo][i] = 0;
+                if (!more) atomicOr(&s_help[root], 0x80000000u);   // its helpers stop
+            }
+        } else if (pop) {
+            if (sp > 0) {
+                sp--;
+                ref = stack.get(sp);
+            } else if (helper) {   // a donated subtree done, nothing nearer than the light in it
+                has = false;
+                atomicSub(&s_help[root], 1u);
+            } else if (!tri && S.tri_num_nodes > 0) {
+                tri = true;
+                ref = 0;
+            } else if (s_help[root] == 0u) {   // no primitive nearer than the light: lit (a phantom light never is)
+                has = false;
+                Q.n_lit[qo][i] = phantom ? 0 : 1;
+            } else {
+                waiting = true;   // the tail block above decides once the helpers are done
+            }
+        }
+#else
         if (blocked) {
             has = false;
             Q.n_lit[qo][i] = 0;
@@ -1033,6 +1154,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                 Q.n_lit[qo][i] = phantom ? 0 : 1;
             }
         }
+#endif
     }
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
