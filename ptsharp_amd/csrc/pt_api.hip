@@ -375,12 +375,14 @@ int make_leaf_chunks(std::vector<float4>& nodes, const std::vector<float4>& recs
             if (cnt > 3) return fail(PT_ERR_UNSUPPORTED, "triangle leaf larger than a chunk");
             const size_t ci = chunks.size() / 8;
             if (ci > 0x1FFFFFFFu) return fail(PT_ERR_UNSUPPORTED, "too many triangle leaves");
+            // word 0 = the first triangle record, triangle t = words 1 + 9t .. 9 + 9t, so a chunk of
+            // cnt triangles is read with 1 + 2·cnt of its 16-B pieces (3 / 5 / 7)
             float w[32] = {0.f};
+            std::memcpy(&w[0], &first, 4);
             for (uint32_t t = 0; t < cnt; t++) {
                 const float* rf = reinterpret_cast<const float*>(&recs[3 * (size_t)(first + t)]);
-                for (int j = 0; j < 9; j++) w[9 * t + j] = rf[j];
+                for (int j = 0; j < 9; j++) w[1 + 9 * t + j] = rf[j];
             }
-            std::memcpy(&w[27], &first, 4);
             const float4* w4 = reinterpret_cast<const float4*>(w);
             chunks.insert(chunks.end(), w4, w4 + 8);
             refs[k] = 0x80000000u | ((cnt - 1u) << 29) | (uint32_t)ci;
@@ -1023,8 +1025,9 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         lines.insert(lines.end(), ana_nodes.begin(), ana_nodes.end());
         lines.insert(lines.end(), tri_nodes.begin(), tri_nodes.end());
         lines.insert(lines.end(), tri_chunks.begin(), tri_chunks.end());
-        if (lines.size() / 8 >= 0xFFFFFFFFull) return fail(PT_ERR_UNSUPPORTED, "more than 2^32 BVH lines");
+        if (lines.size() >= 0xFFFFFFFFull) return fail(PT_ERR_UNSUPPORTED, "more than 2^29 BVH lines");   // 32-bit piece offsets
         rc = upload(c, lines, &S.lines); if (rc) return rc;
+        S.lines_n = (uint32_t)(lines.size() / 8);
         S.tri_node_line0 = (uint32_t)(ana_nodes.size() / 8);
         S.tri_chunk_line0 = (uint32_t)((ana_nodes.size() + tri_nodes.size()) / 8);
         S.ana_nodes = ana_nodes.empty() ? nullptr : S.lines;

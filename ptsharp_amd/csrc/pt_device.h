@@ -221,6 +221,15 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
 // re-splits them along the consumers' 12-B vertex fields into unaligned pieces).
 #define PT_PIN4(q) asm volatile("" : "+v"((q).x), "+v"((q).y), "+v"((q).z), "+v"((q).w))
 
+// The triangles of a leaf chunk (pt_api.hip make_leaf_chunks): word 0 = the first triangle
+// record, triangle k = words 1 + 9k .. 9 + 9k as {v1, e1, e2}; a0..a2 is the first, b the
+// second, c the third (shifted down after each test).  A chunk of cnt triangles is read with its
+// first 1 + 2·cnt 16-B pieces; the rest of q is stale and never tested.
+#define PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6)                                          \
+    v3 a0{q0.y, q0.z, q0.w}, a1{q1.x, q1.y, q1.z}, a2{q1.w, q2.x, q2.y};                  \
+    v3 b0{q2.z, q2.w, q3.x}, b1{q3.y, q3.z, q3.w}, b2{q4.x, q4.y, q4.z};                  \
+    const v3 c0{q4.w, q5.x, q5.y}, c1{q5.z, q5.w, q6.x}, c2{q6.y, q6.z, q6.w}
+
 // Triangle-BVH traversal over leaf chunks (pt_api.hip make_leaf_chunks).  The node step
 // is traverse()'s; a leaf ref points at a 128-B chunk of up to three triangles, so an
 // inner step and a leaf step issue the same seven aligned 16-B loads and a wave whose
@@ -261,11 +270,8 @@ __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 i
                 continue;
             }
         } else {
-            const uint32_t cnt = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q6.w);
-            // triangle k = floats 9k..9k+8 of the chunk: {v1, e1, e2}; shifted down after each test
-            v3 a0{q0.x, q0.y, q0.z}, a1{q0.w, q1.x, q1.y}, a2{q1.z, q1.w, q2.x};
-            v3 b0{q2.y, q2.z, q2.w}, b1{q3.x, q3.y, q3.z}, b2{q3.w, q4.x, q4.y};
-            const v3 c0{q4.z, q4.w, q5.x}, c1{q5.y, q5.z, q5.w}, c2{q6.x, q6.y, q6.z};
+            const uint32_t cnt = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q0.x);
+            PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6);
 #pragma unroll 1
             for (uint32_t k = 0; k < cnt; k++) {
                 if (COUNT) ctr.prims++;

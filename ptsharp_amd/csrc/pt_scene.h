@@ -64,7 +64,7 @@ struct DevScene {
     // ana_nodes, tri_nodes and tri_chunks are one allocation of 128-B lines (in that order), so
     // the cooperative fetch (pt_wavefront.hip coop_line) names any traversal line by a 32-bit index
     const float4* lines;
-    uint32_t tri_node_line0, tri_chunk_line0;
+    uint32_t tri_node_line0, tri_chunk_line0, lines_n;   // lines_n: 128-B lines in `lines`
     // planes (unbounded: tested outside the BVHs)
     const float4* planes;      // 2 float4: {point.xyz, mat} {normal.xyz, scene index}
     int32_t num_planes;

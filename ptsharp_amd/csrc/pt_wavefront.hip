@@ -504,17 +504,20 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
         if (!more && __ballot(has) == 0ull) break;
         // one step: inner node or leaf of the current BVH (one 128-B line)
         const bool leaf = (ref & 0x80000000u) != 0;
-        float4 q0, q1, q2, q3, q4, q5, q6;
+        float4 q0, q1, q2, q3, q4, q5, q6;   // the step's line
 #if PT_COOP
         coop_line(S.lines, step_line(S, has, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
                   q3, q4, q5, q6);
         if (!has) continue;
 #else
         if (!has) continue;
-        {
-            const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
-                                  : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
-            q0 = c[0]; q1 = c[1]; q2 = c[2]; q3 = c[3]; q4 = c[4]; q5 = c[5]; q6 = c[6];
+        {   // one 128-B line, seven 16-B pieces, by a 32-bit offset into the one allocation of all
+            // traversal lines (no per-BVH 64-bit base: the step loop then holds its state without
+            // spilling).  An analytic leaf reads its records in prim_t; its line is not used.
+            const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
+                                          : (leaf ? 0u : ref));
+            q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
+            q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u];
         }
 #endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
@@ -541,10 +544,8 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                 pop = false;
             }
         } else if (tri) {
-            const uint32_t cntl = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q6.w);
-            v3 a0{q0.x, q0.y, q0.z}, a1{q0.w, q1.x, q1.y}, a2{q1.z, q1.w, q2.x};
-            v3 b0{q2.y, q2.z, q2.w}, b1{q3.x, q3.y, q3.z}, b2{q3.w, q4.x, q4.y};
-            const v3 c0{q4.z, q4.w, q5.x}, c1{q5.y, q5.z, q5.w}, c2{q6.x, q6.y, q6.z};
+            const uint32_t cntl = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q0.x);
+            PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6);
 #pragma unroll 1
             for (uint32_t k = 0; k < cntl; k++) {
                 if (COUNT) ctr.prims++;
@@ -1057,17 +1058,20 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
 #endif
         // one step: inner node or leaf of the current BVH (one 128-B line)
         const bool leaf = (ref & 0x80000000u) != 0;
-        float4 q0, q1, q2, q3, q4, q5, q6;
+        float4 q0, q1, q2, q3, q4, q5, q6;   // the step's line
 #if PT_COOP
         coop_line(S.lines, step_line(S, has && !waiting, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
                   q3, q4, q5, q6);
         if (!has || waiting) continue;
 #else
         if (!has || waiting) continue;
-        {
-            const float4* c = tri ? (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu)
-                                  : S.ana_nodes + 8 * (size_t)(leaf ? 0u : ref);
-            q0 = c[0]; q1 = c[1]; q2 = c[2]; q3 = c[3]; q4 = c[4]; q5 = c[5]; q6 = c[6];
+        {   // one 128-B line, seven 16-B pieces, by a 32-bit offset into the one allocation of all
+            // traversal lines (no per-BVH 64-bit base: the step loop then holds its state without
+            // spilling).  An analytic leaf reads its records in prim_t; its line is not used.
+            const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
+                                          : (leaf ? 0u : ref));
+            q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
+            q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u];
         }
 #endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
@@ -1095,9 +1099,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
             }
         } else if (tri) {
             const uint32_t cntl = ((ref >> 29) & 3u) + 1u;
-            v3 a0{q0.x, q0.y, q0.z}, a1{q0.w, q1.x, q1.y}, a2{q1.z, q1.w, q2.x};
-            v3 b0{q2.y, q2.z, q2.w}, b1{q3.x, q3.y, q3.z}, b2{q3.w, q4.x, q4.y};
-            const v3 c0{q4.z, q4.w, q5.x}, c1{q5.y, q5.z, q5.w}, c2{q6.x, q6.y, q6.z};
+            PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6);
 #pragma unroll 1
             for (uint32_t k = 0; k < cntl; k++) {
                 if (COUNT) ctr.prims++;
