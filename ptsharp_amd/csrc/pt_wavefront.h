@@ -27,7 +27,7 @@ struct WfQueues {
     // light-term accumulation of depth d can run beside the closest-hit and shade passes of d + 1.
     float4* n_o[2];      // {origin.xyz, pixel}
     float4* n_n[2];      // {direction.xyz, light index | kDead: no ray cast (diffuse <= 0)}
-    double2* n_w[2];     // two per entry, {r, g} {b, -}: throughput·weight·light colour·coverage (fp64),
+    double2* n_w[2];     // two per entry, {r, g} {b, pixel (bits)}: throughput·weight·light colour·coverage (fp64),
                          // added if the light is visible
     uint8_t* n_lit[2];   // per entry: 1 = the light is the nearest hit (k_wf_shadow*), read by k_wf_nee_accum
     uint32_t* counts;    // counter slots, each kCountStride words apart (see count_word below):

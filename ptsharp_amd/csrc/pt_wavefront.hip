@@ -761,7 +761,8 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
                         q_store_next(&Q.n_o[qo][at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
                         q_store_next(&Q.n_n[qo][at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
                         q_store_late(&Q.n_w[qo][2 * (size_t)at], make_double2((t2[0] * w[0]) * lc.x, (t2[1] * w[1]) * lc.y));
-                        q_store_late(&Q.n_w[qo][2 * (size_t)at + 1], make_double2((t2[2] * w[2]) * lc.z, 0.0));
+                        q_store_late(&Q.n_w[qo][2 * (size_t)at + 1],   // {b, pixel}: k_wf_nee_accum reads only n_w
+                                     make_double2((t2[2] * w[2]) * lc.z, __longlong_as_double((long long)pixel)));
                     }
                 }
             }
@@ -1192,9 +1193,9 @@ __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsign
             const size_t i = base + j;
             lit = Q.n_lit[qo][i] != 0;
             if (lit) {
-                pixel = __float_as_uint(nt_load(&Q.n_o[qo][i]).w);
                 w01 = nt_load(&Q.n_w[qo][2 * i]);
                 w2 = nt_load(&Q.n_w[qo][2 * i + 1]);
+                pixel = (uint32_t)__double_as_longlong(w2.y);
             }
         }
         const uint32_t r = fix_add_wave(Q.acc, pixel, lit, w01.x, w01.y, w2.x);
