@@ -106,21 +106,49 @@ __device__ __forceinline__ void fix_add_lane(const FixAcc& A, size_t i, double r
 // order inside a run does not matter) and the run's head issues the atomics.  A lane with
 // a term of 2^13 or more adds it on its own (a run's sum must stay inside 63 bits).
 // Wave-uniform call; lanes with has = false add nothing.  Returns the runs issued.
-__device__ __forceinline__ uint32_t fix_add_wave(const FixAcc& A, uint32_t idx, bool has, double r, double g, double b) {
+// A block's LDS table of run sums (k_wf_nee_accum): open addressing on the accumulator index,
+// TABLE entries of {key, three 64-bit sums}.  Terms below kFixLds (|V| < 2^50) only, so a
+// window of up to 2^12 of them per key sums without overflow; the block flushes the table
+// into the 128-bit accumulators (fix_atomic) after each window.
+constexpr double kFixLds = 64.0;
+constexpr uint32_t kLdsFree = 0xFFFFFFFFu;
+struct LdsFix {
+    uint32_t* key;               // [n], kLdsFree = free
+    unsigned long long* sum;     // [n][3]
+    uint32_t mask;               // n - 1 (n a power of two)
+};
+// A run's sums into the table; false if its probe sequence is full (the caller adds globally).
+__device__ __forceinline__ bool lds_fix_add(const LdsFix& T, uint32_t idx, const long long v[3]) {
+    const uint32_t h = idx * 0x9E3779B1u;
+    for (uint32_t p = 0; p < 8u; p++) {
+        const uint32_t sl = ((h >> 16) + p) & T.mask;
+        const uint32_t k = atomicCAS(T.key + sl, kLdsFree, idx);
+        if (k == kLdsFree || k == idx) {
+            for (int c = 0; c < 3; c++)
+                if (v[c]) atomicAdd(T.sum + 3u * sl + c, (unsigned long long)v[c]);
+            return true;
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ uint32_t fix_add_wave(const FixAcc& A, uint32_t idx, bool has, double r, double g, double b,
+                                                 const LdsFix* T = nullptr) {
     if (__ballot(has) == 0ull) return 0u;   // wave-uniform: nothing to add
     const int lane = threadIdx.x & 63;
     const double x[3] = {r, g, b};
+    const double lim = T ? kFixLds : kFixWave;
     bool alone = false;
     long long v[3];
     for (int k = 0; k < 3; k++) {
         v[k] = 0;
         if (!has || x[k] == 0.0) continue;
-        if (!(fabs(x[k]) < kFixWave)) { alone = true; continue; }
+        if (!(fabs(x[k]) < lim)) { alone = true; continue; }
         v[k] = to_fix(x[k]);
     }
     if (alone) {   // rare: large (or side-sum) terms, added per lane
         for (int k = 0; k < 3; k++)
-            if (x[k] != 0.0 && !(fabs(x[k]) < kFixWave)) {
+            if (x[k] != 0.0 && !(fabs(x[k]) < lim)) {
                 if (!fix_ok(x[k])) atomicAdd(A.big + 3 * (size_t)idx + k, x[k]);
                 else fix_atomic(A.w + kFixWords * (size_t)idx, k, to_fix(x[k]));
             }
@@ -148,7 +176,7 @@ __device__ __forceinline__ uint32_t fix_add_wave(const FixAcc& A, uint32_t idx, 
             if (take) v[k] += u;
         }
     }
-    if (head) {
+    if (head && (v[0] | v[1] | v[2]) && !(T && lds_fix_add(*T, idx, v))) {
         unsigned long long* w = A.w + kFixWords * (size_t)idx;
         for (int k = 0; k < 3; k++)
             if (v[k]) fix_atomic(w, k, v[k]);

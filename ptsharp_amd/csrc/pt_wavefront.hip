@@ -1176,16 +1176,21 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
 // (a pixel's rays sit in runs of consecutive slots, so fix_add_wave sums most of them in
 // registers).  Keeping the accumulation out of the traversal kernels keeps their refill path
 // and registers lean.  Group g takes partition g (written on its XCD by k_wf_shade).
+#ifndef PT_ACCUM_LDS
+#define PT_ACCUM_LDS 1   // k_wf_nee_accum sums a window's runs per pixel in LDS before the atomics
+#endif
+constexpr uint32_t kAccWin = 16;       // 256-slot rows per block window (one shade block's child-major region
+                                       // of FirstHitSamples 16 children)
+constexpr uint32_t kAccTable = 512;    // LDS table entries
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsigned long long* counters) {
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap;
     const size_t base = (size_t)G.g * Q.spcap;
-    const uint32_t lane = threadIdx.x & 63, wave = G.lb * 4u + (threadIdx.x >> 6), nwaves = G.nb * 4u;
+    const uint32_t lane = threadIdx.x & 63;
     uint32_t lit_n = 0, runs = 0;
-    for (uint32_t j0 = wave * 64u; j0 < n; j0 += nwaves * 64u) {   // wave-uniform
-        const uint32_t j = j0 + lane;
+    auto row = [&](uint32_t j, const LdsFix* T) {   // slots j .. j + 63 of this wave (wave-uniform)
         bool lit = false;
         uint32_t pixel = 0;
         double2 w01 = make_double2(0.0, 0.0), w2 = w01;
@@ -1198,9 +1203,42 @@ __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsign
                 pixel = (uint32_t)__double_as_longlong(w2.y);
             }
         }
-        const uint32_t r = fix_add_wave(Q.acc, pixel, lit, w01.x, w01.y, w2.x);
+        const uint32_t r = fix_add_wave(Q.acc, pixel, lit, w01.x, w01.y, w2.x, T);
         if (COUNT) { runs += r; lit_n += (uint32_t)__popcll(__ballot(lit)); }
+    };
+#if PT_ACCUM_LDS
+    // A pixel's light terms of one depth sit in runs of consecutive slots, one run per child index
+    // of its vertex (the child-major fill): a block takes windows of kAccWin·256 slots, sums the
+    // wave runs of a window per pixel in LDS and flushes one atomic set per pixel (for
+    // FirstHitSamples 16, 16 runs of a pixel become one).  Integer sums: the order is free.
+    __shared__ uint32_t s_key[kAccTable];
+    __shared__ unsigned long long s_sum[kAccTable * 3];
+    const LdsFix T{s_key, s_sum, kAccTable - 1u};
+    for (uint32_t e = threadIdx.x; e < kAccTable; e += 256u) {
+        s_key[e] = kLdsFree;
+        s_sum[3 * e] = 0ull; s_sum[3 * e + 1] = 0ull; s_sum[3 * e + 2] = 0ull;
     }
+    __syncthreads();
+    for (uint32_t w0 = G.lb * 256u * kAccWin; w0 < n; w0 += G.nb * 256u * kAccWin) {   // block-uniform
+        for (uint32_t r = 0; r < kAccWin; r++) row(w0 + r * 256u + threadIdx.x, &T);
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < kAccTable; e += 256u) {
+            const uint32_t k = s_key[e];
+            if (k == kLdsFree) continue;
+            unsigned long long* w = Q.acc.w + kFixWords * (size_t)k;
+            for (int c = 0; c < 3; c++) {
+                const long long v = (long long)s_sum[3 * e + c];
+                if (v) fix_atomic(w, c, v);
+                s_sum[3 * e + c] = 0ull;
+            }
+            s_key[e] = kLdsFree;
+        }
+        __syncthreads();
+    }
+#else
+    const uint32_t wave = G.lb * 4u + (threadIdx.x >> 6), nwaves = G.nb * 4u;
+    for (uint32_t j0 = wave * 64u; j0 < n; j0 += nwaves * 64u) row(j0 + lane, nullptr);   // wave-uniform
+#endif
     if (COUNT && lane == 0) {
         atomicAdd(&counters[7], (unsigned long long)lit_n);
         atomicAdd(&counters[8], (unsigned long long)runs);
@@ -1381,7 +1419,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         end_k(3, side);
         begin_k(6, side);   // PT_K_ACCUM
-        const unsigned ag = grid_for(children * plan.lights_per_child, 256, 8192);
+        const unsigned ag = PT_ACCUM_LDS ? grid_for(children * plan.lights_per_child, 256u * kAccWin, 4096)
+                                         : grid_for(children * plan.lights_per_child, 256, 8192);
         if (count) hipLaunchKernelGGL((k_wf_nee_accum<true>), dim3(ag), dim3(256), 0, side, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_nee_accum<false>), dim3(ag), dim3(256), 0, side, Q, 1 - qi, B.counters);
         end_k(6, side);
