@@ -137,6 +137,9 @@ constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that
 constexpr int kBlockMajorFH = 16;
 constexpr int kBlockMajorChildren = 32;
 constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera slot (k_wf_trace)
+#ifndef PT_SCAN_MOST
+#define PT_SCAN_MOST 1   // lean shade kernels take the SCAN form below 31/32 kept (0: below half, round 1)
+#endif
 #ifndef PT_SHADE_SCAN
 #define PT_SHADE_SCAN 16   // 4 / 8 / 16 / 24 / 32 measured on C4 (round 2), 16 best
 #endif
@@ -795,7 +798,13 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                                                                   unsigned long long* counters, int form) {
     uint32_t queued = 0;
     for (int g = 0; g < kParts; g++) queued += min(*ray_count(Q, qi, g), Q.pcap);
-    const bool scan = form ? form == 2 : 2ull * Q.counts[kept_word(qi)] < (unsigned long long)queued;
+    // SCAN unless (nearly) every queued ray has work: with its partial rounds carried over it
+    // beat the direct form down to ~92 % kept in the lean kernels (C4 +1.6 %, C2 +9.8 %); the
+    // FULL kernels keep the round-1 rule (SCAN below half kept; forcing it cost them 8-10 %).
+    const unsigned long long kept = Q.counts[kept_word(qi)];
+    const bool scan = form ? form == 2
+                           : (FULL || !PT_SCAN_MOST) ? 2ull * kept < (unsigned long long)queued
+                                                     : 32ull * kept < 31ull * (unsigned long long)queued;
     if (scan != SCAN) return;
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         Q.counts[fetch_word(2 + (1 - qi), threadIdx.x)] = 0u;   // the fetch cursors of the shadow rays it writes
@@ -820,44 +829,57 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
         const uint64_t below = (1ull << lane) - 1ull;
         __shared__ uint32_t s_wcnt[kShadeScan * 4];
-        __shared__ uint16_t s_list[kShadeScan * 256];
+        // the listed vertices (partition-local slots) of this claim, after the < 256 held over from
+        // the last one: every round but the kernel's last shades a full 256 (round 1 shaded each
+        // claim's partial last round, a quarter to a half of the rounds at C4's first bounce)
+        __shared__ uint32_t s_list[kShadeScan * 256 + 256];
+        uint32_t carry = 0;   // block-uniform
         for (;;) {
             if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u * kShadeScan);
             __syncthreads();
             const uint32_t k0 = s_k0;  // thread 0 rewrites it only after the barriers below
-            if (k0 >= n) break;
-            uint32_t keep = 0;
+            const bool last = k0 >= n;   // block-uniform: nothing claimed, shade what is held over
+            uint32_t total = carry;
+            if (!last) {
+                uint32_t keep = 0;
 #pragma unroll
-            for (int j = 0; j < kShadeScan; j++) {
-                const uint32_t sl = k0 + (uint32_t)j * 256u + threadIdx.x;
-                int32_t kind = kDeadKind;
-                if (sl < n) kind = (int32_t)nt_load(&Q.hits[base + sl]).z;
-                keep |= (kind != kDeadKind && (kind >= 0 || !env_black)) ? 1u << j : 0u;
+                for (int j = 0; j < kShadeScan; j++) {
+                    const uint32_t sl = k0 + (uint32_t)j * 256u + threadIdx.x;
+                    int32_t kind = kDeadKind;
+                    if (sl < n) kind = (int32_t)nt_load(&Q.hits[base + sl]).z;
+                    keep |= (kind != kDeadKind && (kind >= 0 || !env_black)) ? 1u << j : 0u;
+                }
+                uint64_t bal[kShadeScan];
+#pragma unroll
+                for (int j = 0; j < kShadeScan; j++) {
+                    bal[j] = __ballot((keep >> j) & 1u);
+                    if (lane == 0) s_wcnt[j * 4 + wid] = (uint32_t)__popcll(bal[j]);
+                }
+                __syncthreads();
+                uint32_t pre[kShadeScan];
+#pragma unroll
+                for (int q = 0; q < kShadeScan * 4; q++) {
+                    const uint32_t w = s_wcnt[q];
+                    if ((q & 3) == wid) pre[q >> 2] = total;
+                    total += w;
+                }
+#pragma unroll
+                for (int j = 0; j < kShadeScan; j++)
+                    if ((keep >> j) & 1u) s_list[pre[j] + (uint32_t)__popcll(bal[j] & below)] = k0 + (uint32_t)j * 256u + threadIdx.x;
+                __syncthreads();
             }
-            uint64_t bal[kShadeScan];
-#pragma unroll
-            for (int j = 0; j < kShadeScan; j++) {
-                bal[j] = __ballot((keep >> j) & 1u);
-                if (lane == 0) s_wcnt[j * 4 + wid] = (uint32_t)__popcll(bal[j]);
-            }
-            __syncthreads();
-            uint32_t total = 0, pre[kShadeScan];
-#pragma unroll
-            for (int q = 0; q < kShadeScan * 4; q++) {
-                const uint32_t w = s_wcnt[q];
-                if ((q & 3) == wid) pre[q >> 2] = total;
-                total += w;
-            }
-#pragma unroll
-            for (int j = 0; j < kShadeScan; j++)
-                if ((keep >> j) & 1u) s_list[pre[j] + (uint32_t)__popcll(bal[j] & below)] = (uint16_t)(j * 256 + threadIdx.x);
-            __syncthreads();
-            for (uint32_t r = 0; r < total; r += 256u) {   // block-uniform
-                const bool listed = r + threadIdx.x < total;
-                shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + k0 + (listed ? (uint32_t)s_list[r + threadIdx.x] : 0u),
-                                          listed, ctr);
+            const uint32_t full = last ? total : total & ~255u;
+            for (uint32_t r = 0; r < full; r += 256u) {   // block-uniform
+                const bool listed = r + threadIdx.x < full;
+                shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed, ctr);
                 __syncthreads();   // the next round rewrites shade_vertex's LDS child counts
             }
+            if (last) break;
+            carry = total - full;   // < 256: to the front of the list
+            const uint32_t held = threadIdx.x < carry ? s_list[full + threadIdx.x] : 0u;
+            __syncthreads();
+            if (threadIdx.x < carry) s_list[threadIdx.x] = held;
+            __syncthreads();
         }
     }
     if (COUNT) {
