@@ -137,11 +137,15 @@ constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that
 constexpr int kBlockMajorFH = 16;
 constexpr int kBlockMajorChildren = 32;
 constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera slot (k_wf_trace)
+#ifndef PT_SCAN_CLAIMS
+#define PT_SCAN_CLAIMS 1   // SCAN claims per block at least (the claim shrinks for small partitions; 4 and 8 measured, no better)
+#endif
 #ifndef PT_SCAN_MOST
 #define PT_SCAN_MOST 1   // lean shade kernels take the SCAN form below 31/32 kept (0: below half, round 1)
 #endif
 #ifndef PT_SHADE_SCAN
-#define PT_SHADE_SCAN 16   // 4 / 8 / 16 / 24 / 32 measured on C4 (round 2), 16 best
+#define PT_SHADE_SCAN 8    // rows of 256 per SCAN claim: 16 best before claims carried their partial round, 8 since
+                           // (C4 5836 / 5885 / 5743 for 16 / 8 / 32; the 1/8 share 5099 / 5208 / 4735)
 #endif
 constexpr int kShadeScan = PT_SHADE_SCAN;   // 256-vertex groups a SCAN shade block claims and lists
 // The environment may be textured (non-black per direction) only where the shade kernel
@@ -834,8 +838,11 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         // claim's partial last round, a quarter to a half of the rounds at C4's first bounce)
         __shared__ uint32_t s_list[kShadeScan * 256 + 256];
         uint32_t carry = 0;   // block-uniform
+        // rows of 256 slots per claim: kShadeScan, fewer when the partition would give a block
+        // fewer than PT_SCAN_CLAIMS claims (small chunks: one rank's share of a multi-GPU frame)
+        const uint32_t rows = max(1u, min((uint32_t)kShadeScan, n / (G.nb * 256u * (uint32_t)PT_SCAN_CLAIMS)));
         for (;;) {
-            if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u * kShadeScan);
+            if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u * rows);
             __syncthreads();
             const uint32_t k0 = s_k0;  // thread 0 rewrites it only after the barriers below
             const bool last = k0 >= n;   // block-uniform: nothing claimed, shade what is held over
@@ -846,7 +853,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                 for (int j = 0; j < kShadeScan; j++) {
                     const uint32_t sl = k0 + (uint32_t)j * 256u + threadIdx.x;
                     int32_t kind = kDeadKind;
-                    if (sl < n) kind = (int32_t)nt_load(&Q.hits[base + sl]).z;
+                    if ((uint32_t)j < rows && sl < n) kind = (int32_t)nt_load(&Q.hits[base + sl]).z;
                     keep |= (kind != kDeadKind && (kind >= 0 || !env_black)) ? 1u << j : 0u;
                 }
                 uint64_t bal[kShadeScan];
