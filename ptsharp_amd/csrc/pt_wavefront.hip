@@ -137,6 +137,9 @@ constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that
 constexpr int kBlockMajorFH = 16;
 constexpr int kBlockMajorChildren = 32;
 constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera slot (k_wf_trace)
+#ifndef PT_SCAN_HIT_LDS
+#define PT_SCAN_HIT_LDS 1   // SCAN: the shade rounds take the hit records the scan read (LDS) instead of reloading them
+#endif
 #ifndef PT_SCAN_CLAIMS
 #define PT_SCAN_CLAIMS 1   // SCAN claims per block at least (the claim shrinks for small partitions; 4 and 8 measured, no better)
 #endif
@@ -617,7 +620,8 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
 // the block's reservation and ballots).  Block-uniform call.
 template <bool COUNT, bool FULL>
 __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler& smp, const WfQueues& Q, int qi,
-                                             const Group& G, uint32_t i, bool alive, Counters& ctr) {
+                                             const Group& G, uint32_t i, bool alive, Counters& ctr,
+                                             const uint4* hl = nullptr) {   // hl: the hit record, already in LDS
     const int qo = 1 - qi;
     const bool nee_on = smp.dl && S.num_lights > 0;
     const int nl = S.num_lights;
@@ -632,7 +636,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         rd = nt_load(&Q.q_d[qi][i]);
         ro = nt_load(&Q.q_o[qi][i]);
         rt = nt_load(&Q.q_t[qi][i]);
-        hr = nt_load(&Q.hits[i]);
+        hr = hl ? *hl : nt_load(&Q.hits[i]);
         rk = nt_load(&Q.q_k[qi][i]);
         meta = __float_as_uint(rd.w);
         alive = meta != kDead;
@@ -837,6 +841,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         // the last one: every round but the kernel's last shades a full 256 (round 1 shaded each
         // claim's partial last round, a quarter to a half of the rounds at C4's first bounce)
         __shared__ uint32_t s_list[kShadeScan * 256 + 256];
+        __shared__ uint4 s_hit[kShadeScan * 256 + 256];   // their hit records (read once, by the scan)
         uint32_t carry = 0;   // block-uniform
         // rows of 256 slots per claim: kShadeScan, fewer when the partition would give a block
         // fewer than PT_SCAN_CLAIMS claims (small chunks: one rank's share of a multi-GPU frame)
@@ -849,11 +854,13 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             uint32_t total = carry;
             if (!last) {
                 uint32_t keep = 0;
+                uint4 hv[kShadeScan];
 #pragma unroll
                 for (int j = 0; j < kShadeScan; j++) {
                     const uint32_t sl = k0 + (uint32_t)j * 256u + threadIdx.x;
-                    int32_t kind = kDeadKind;
-                    if ((uint32_t)j < rows && sl < n) kind = (int32_t)nt_load(&Q.hits[base + sl]).z;
+                    hv[j] = make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u);
+                    if ((uint32_t)j < rows && sl < n) hv[j] = nt_load(&Q.hits[base + sl]);
+                    const int32_t kind = (int32_t)hv[j].z;
                     keep |= (kind != kDeadKind && (kind >= 0 || !env_black)) ? 1u << j : 0u;
                 }
                 uint64_t bal[kShadeScan];
@@ -872,20 +879,26 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                 }
 #pragma unroll
                 for (int j = 0; j < kShadeScan; j++)
-                    if ((keep >> j) & 1u) s_list[pre[j] + (uint32_t)__popcll(bal[j] & below)] = k0 + (uint32_t)j * 256u + threadIdx.x;
+                    if ((keep >> j) & 1u) {
+                        const uint32_t at = pre[j] + (uint32_t)__popcll(bal[j] & below);
+                        s_list[at] = k0 + (uint32_t)j * 256u + threadIdx.x;
+                        s_hit[at] = hv[j];
+                    }
                 __syncthreads();
             }
             const uint32_t full = last ? total : total & ~255u;
             for (uint32_t r = 0; r < full; r += 256u) {   // block-uniform
                 const bool listed = r + threadIdx.x < full;
-                shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed, ctr);
+                shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed, ctr,
+                                          PT_SCAN_HIT_LDS ? &s_hit[r + threadIdx.x] : nullptr);
                 __syncthreads();   // the next round rewrites shade_vertex's LDS child counts
             }
             if (last) break;
             carry = total - full;   // < 256: to the front of the list
             const uint32_t held = threadIdx.x < carry ? s_list[full + threadIdx.x] : 0u;
+            const uint4 hheld = threadIdx.x < carry ? s_hit[full + threadIdx.x] : make_uint4(0u, 0u, 0u, 0u);
             __syncthreads();
-            if (threadIdx.x < carry) s_list[threadIdx.x] = held;
+            if (threadIdx.x < carry) { s_list[threadIdx.x] = held; s_hit[threadIdx.x] = hheld; }
             __syncthreads();
         }
     }
