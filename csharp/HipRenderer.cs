@@ -177,6 +177,8 @@ namespace PTSharpCore
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_destroy(IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_init_all(IntPtr[] ctxs, int n);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_comm_gather_all(IntPtr[] ctxs, int n, int root);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_gather_layout(int nranks, int root, int[] counts, int imageTiles, long[] offsets, out long total);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_tile_lists_check(int[] ids, long n, int imageTiles);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl, CharSet = CharSet.Ansi)] public static extern int pt_obj_load(string path, out pt_mesh_data mesh);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern void pt_mesh_free(ref pt_mesh_data mesh);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern IntPtr pt_obj_last_error();
@@ -204,6 +206,8 @@ namespace PTSharpCore
         public int[] Tiles = null;
         internal IntPtr ctx;
         int W, H, pass;
+        internal int Width => W;
+        internal int Height => H;
         bool uploaded;
         readonly List<GCHandle> pins = new();
 
@@ -524,6 +528,11 @@ namespace PTSharpCore
         {
             parts = p;
             ctxs = Array.ConvertAll(p, r => r.ctx);
+            // the ranks' tile lists must be disjoint: checked once, before any RCCL call
+            var all = new System.Collections.Generic.List<int>();
+            foreach (var r in p) if (r.Tiles != null) all.AddRange(r.Tiles);
+            PtHip.Check(PtHip.pt_tile_lists_check(all.ToArray(), all.Count, ((p[0].Width + 31) / 32) * ((p[0].Height + 31) / 32)),
+                        "pt_tile_lists_check");
             PtHip.Check(PtHip.pt_comm_init_all(ctxs, ctxs.Length), "pt_comm_init_all");
         }
 

@@ -360,13 +360,25 @@ int pt_mesh_smooth_normals(int32_t n, const float* v1, const float* v2, const fl
  *     contexts from G host threads at once (one thread per context): a pass with
  *     firefly_samples > 0 all-reduces the firefly snapshot across the group.
  * After a gather, root's pt_read_buffer returns the whole frame; root's next pass first
- * clears the pixels outside its own tiles again, so gathers can repeat every pass. */
+ * clears the pixels outside its own tiles again, so gathers can repeat every pass (so does any
+ * rank's next tile-subset pass after pt_write_buffer or pt_write_tiles put other ranks' pixels in
+ * its Buffer, e.g. every rank resuming from the whole checkpoint).  Root refuses a gather whose
+ * tile ids repeat (two ranks rendered one tile) before it writes anything. */
 int pt_comm_unique_id(uint8_t out_id[128]);
 int pt_comm_init(void* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 int pt_comm_gather(void* ctx, int32_t root);
 int pt_comm_destroy(void* ctx);
 int pt_comm_init_all(void* const* ctxs, int32_t n);            /* ncclCommInitAll over the contexts' devices */
 int pt_comm_gather_all(void* const* ctxs, int32_t n, int32_t root);   /* the group's gathers, issued together */
+/* The gather's host-side arithmetic, exported so a host can check its tile assignment before any
+ * RCCL call (pure functions: no device, no context).  pt_gather_layout: where rank p's packed
+ * tiles land in root's receive buffers (tile offset; -1 for root and for ranks with no tiles),
+ * and the tiles root receives; PT_ERR_INVALID_ARG if a count is out of range or the counts sum
+ * past image_tiles (overlapping lists).  pt_tile_lists_check: every id in [0, image_tiles), none
+ * twice.  (Renderer.cs:257-333 deals disjoint sub-tiles to tasks; these keep the ranks disjoint.) */
+int pt_gather_layout(int32_t nranks, int32_t root, const int32_t* counts, int32_t image_tiles,
+                     int64_t* out_offsets, int64_t* out_total);
+int pt_tile_lists_check(const int32_t* ids, int64_t n, int32_t image_tiles);
 
 /* Instrumentation (bench / roofline): last pass' traversal counters, summed. */
 typedef struct pt_trace_counters {

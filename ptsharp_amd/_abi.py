@@ -157,6 +157,9 @@ SIGNATURES = {
     "pt_comm_destroy": (C.c_int, [C.c_void_p]),
     "pt_comm_init_all": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32]),
     "pt_comm_gather_all": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_int32]),
+    "pt_gather_layout": (C.c_int, [C.c_int32, C.c_int32, _i, C.c_int32, C.POINTER(C.c_int64),
+                                   C.POINTER(C.c_int64)]),
+    "pt_tile_lists_check": (C.c_int, [_i, C.c_int64, C.c_int32]),
     "pt_render_pass_counted": (C.c_int, [C.c_void_p, C.POINTER(pt_camera), C.POINTER(pt_sampler),
                                          C.POINTER(pt_pass_params), C.POINTER(pt_trace_counters)]),
     "pt_obj_load": (C.c_int, [C.c_char_p, C.POINTER(pt_mesh_data)]),

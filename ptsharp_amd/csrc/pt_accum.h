@@ -50,8 +50,12 @@ __device__ __forceinline__ long long to_fix(double x) {
     return (long long)(int)f * 4294967296ll + lo;
 }
 
-// T = hi·2^64 + lo (hi signed) → T·2^-44.
+// T = hi·2^64 + lo (hi signed) → T·2^-44.  When T fits 64 signed bits (hi is lo's sign
+// extension: every sum of a few terms, negative ones included) it is converted in one step; the
+// two-word form would round a negative T's lo (near 2^64) to a multiple of 2^11 first and then
+// cancel it against hi·2^64, losing most of the 2^-44 resolution.
 __device__ __forceinline__ double fix_value(long long hi, unsigned long long lo) {
+    if (hi == ((long long)lo >> 63)) return (double)(long long)lo * (1.0 / 17592186044416.0);
     return (double)hi * 1048576.0 + (double)lo * (1.0 / 17592186044416.0);
 }
 

@@ -154,7 +154,7 @@ struct Ctx {
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
-    bool gathered = false;          // root of a gather: other ranks' tiles are in the Buffer until the next pass
+    bool gathered = false;          // other ranks' tiles are in the Buffer (a gather, pt_write_buffer, pt_write_tiles) until the next pass
     uint8_t* d_own = nullptr;       // [tiles] 1 = a tile of this context's last tile list
     int32_t pass_tiles = 0;         // tiles of the last pass (0: the whole image); their ids are in d_tiles
     // tile-compacted gather workspace (allocated by the first gather): ids, M, V, N of up to
@@ -1115,8 +1115,6 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     const int32_t* d_tiles = nullptr;
     if (pass->num_tiles > 0) {
         if (!pass->tiles) return fail(PT_ERR_INVALID_ARG, "tiles is NULL");
-        for (int i = 0; i < pass->num_tiles; i++)
-            if (pass->tiles[i] < 0 || pass->tiles[i] >= tiles_x * tiles_y) return fail(PT_ERR_INVALID_ARG, "tile id out of range");
         if (pass->num_tiles > c->tiles_cap) {
             if (c->d_tiles) (void)hipFree(c->d_tiles);
             c->d_tiles = nullptr;
@@ -1127,6 +1125,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         // the same list pass after pass (a rank's tiles): uploaded once
         if (c->h_tiles.size() != (size_t)pass->num_tiles ||
             std::memcmp(c->h_tiles.data(), pass->tiles, (size_t)pass->num_tiles * sizeof(int32_t))) {
+            // ids in range, none twice (a tile listed twice would be rendered into its pixels twice)
+            if (int rc = pt_tile_lists_check(pass->tiles, pass->num_tiles, tiles_x * tiles_y)) return rc;
             c->h_tiles.assign(pass->tiles, pass->tiles + pass->num_tiles);
             PT_HIP(hipMemcpyAsync(c->d_tiles, c->h_tiles.data(), (size_t)pass->num_tiles * sizeof(int32_t),
                                   hipMemcpyHostToDevice, c->stream));
@@ -1363,6 +1363,10 @@ int pt_write_buffer(void* ctx, const double* m, const double* v, const int32_t* 
     if (v) PT_HIP(hipMemcpyAsync(c->d_v, v, P * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
     if (n) PT_HIP(hipMemcpyAsync(c->d_n, n, P * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
+    // The loaded Buffer may hold other ranks' pixels (every rank loads the whole checkpoint): the
+    // next tile-subset pass clears them first, as after a gather, so a firefly snapshot's
+    // all-reduce and a later gather see each pixel on its owner only.
+    c->gathered = true;
     return PT_OK;
 }
 
@@ -1387,6 +1391,7 @@ static int tiles_io(void* ctx, const int32_t* tiles, int32_t num_tiles, double* 
         PT_HIP(hipMemcpyAsync(c->g_m, m, s * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
         PT_HIP(hipMemcpyAsync(c->g_v, v, s * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
         PT_HIP(hipMemcpyAsync(c->g_n, n, s * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        c->gathered = true;   // foreign tiles written (a host-transport gather): cleared before the next subset pass
     }
     pt::DevBuffer B{c->d_m, c->d_v, c->d_n, c->d_counters};
     hipLaunchKernelGGL(pt::k_tiles_pack, dim3(2048), dim3(256), 0, c->stream, B, c->width, c->height,
@@ -1467,6 +1472,51 @@ int pt_comm_init(void* ctx, int32_t nranks, int32_t rank, const uint8_t id[128])
     return PT_OK;
 }
 
+// ---- the gather's host-side arithmetic (pure functions, exported: hosts and CPU tests check them)
+// Where each rank's packed tiles land in the root's receive buffers: rank p (not the root, with
+// tiles) at tile offset out_offsets[p] (entries × 1024 pixels; M/V × 3072 doubles), in rank order;
+// −1 for the root and for ranks with no tiles.  The counts are one pass' tile lists, which the
+// ranks keep disjoint, so they cannot sum past the image's tiles.
+int pt_gather_layout(int32_t nranks, int32_t root, const int32_t* counts, int32_t image_tiles,
+                     int64_t* out_offsets, int64_t* out_total) {
+    if (nranks < 1 || !counts || !out_offsets || !out_total || image_tiles < 0)
+        return fail(PT_ERR_INVALID_ARG, "gather layout: bad arguments");
+    if (root < 0 || root >= nranks) return fail(PT_ERR_INVALID_ARG, "gather layout: root out of range");
+    int64_t sum = 0;
+    for (int32_t p = 0; p < nranks; p++) {
+        if (counts[p] < 0 || counts[p] > image_tiles)
+            return fail(PT_ERR_INVALID_ARG, "gather layout: rank " + std::to_string(p) + " reports " +
+                                                std::to_string(counts[p]) + " tiles of " + std::to_string(image_tiles));
+        sum += counts[p];
+    }
+    if (sum > image_tiles)   // disjoint lists never hold more tiles than the image
+        return fail(PT_ERR_INVALID_ARG, "gather: the ranks' tile lists overlap (more tiles than the image has)");
+    int64_t off = 0;
+    for (int32_t p = 0; p < nranks; p++) {
+        if (p == root || counts[p] == 0) { out_offsets[p] = -1; continue; }
+        out_offsets[p] = off;
+        off += counts[p];
+    }
+    *out_total = off;
+    return PT_OK;
+}
+
+// Every id in [0, image_tiles) and none twice (a tile on two ranks would be written twice, the
+// last sender's copy replacing the others).
+int pt_tile_lists_check(const int32_t* ids, int64_t n, int32_t image_tiles) {
+    if (n < 0 || (n > 0 && !ids) || image_tiles < 0) return fail(PT_ERR_INVALID_ARG, "tile list: bad arguments");
+    std::vector<uint8_t> seen((size_t)image_tiles, 0);
+    for (int64_t i = 0; i < n; i++) {
+        const int32_t t = ids[i];
+        if (t < 0 || t >= image_tiles)
+            return fail(PT_ERR_INVALID_ARG, "tile id " + std::to_string(t) + " out of range [0, " +
+                                                std::to_string(image_tiles) + ")");
+        if (seen[(size_t)t]) return fail(PT_ERR_INVALID_ARG, "tile " + std::to_string(t) + " listed twice");
+        seen[(size_t)t] = 1;
+    }
+    return PT_OK;
+}
+
 // Every rank rendered a disjoint tile set into a zero-initialised full-frame
 // buffer, so a sum-reduce onto `root` is the gather.
 // Tile-compacted gather: every rank but the root packs the {M, V, N} of its
@@ -1504,7 +1554,8 @@ static int32_t own_count(Ctx* c) {
 }
 // The rank's sends (not root) or receives (root) of step 2; inside a group.  Non-root ranks
 // pack first (same stream, so the sends follow the packing).
-static ncclResult_t gather_issue(Ctx* c, int32_t root, const std::vector<int32_t>& cnts) {
+static ncclResult_t gather_issue(Ctx* c, int32_t root, const std::vector<int32_t>& cnts,
+                                 const std::vector<int64_t>& offs) {
     const int tiles_x = (c->width + 31) / 32;
     if (c->rank != root) {
         const int32_t nt = own_count(c);
@@ -1520,26 +1571,30 @@ static ncclResult_t gather_issue(Ctx* c, int32_t root, const std::vector<int32_t
         if (r == ncclSuccess) r = ncclSend(c->g_n, s, ncclInt32, root, c->comm, c->stream);
         return r;
     }
-    size_t off = 0;   // tiles
     for (int p = 0; p < c->nranks; p++) {
-        if (p == root || cnts[(size_t)p] == 0) continue;
-        const size_t nt = (size_t)cnts[(size_t)p], s = nt * 1024u;
+        if (offs[(size_t)p] < 0) continue;   // the root, or a rank without tiles (pt_gather_layout)
+        const size_t off = (size_t)offs[(size_t)p], nt = (size_t)cnts[(size_t)p], s = nt * 1024u;
         ncclResult_t r = ncclRecv(c->g_ids + off, nt, ncclInt32, p, c->comm, c->stream);
         if (r == ncclSuccess) r = ncclRecv(c->g_m + off * 3072u, s * 3, ncclFloat64, p, c->comm, c->stream);
         if (r == ncclSuccess) r = ncclRecv(c->g_v + off * 3072u, s * 3, ncclFloat64, p, c->comm, c->stream);
         if (r == ncclSuccess) r = ncclRecv(c->g_n + off * 1024u, s, ncclInt32, p, c->comm, c->stream);
         if (r != ncclSuccess) return r;
-        off += nt;
     }
     return ncclSuccess;
 }
-// The root writes what it received into its Buffer.
-static int gather_finish(Ctx* c, int32_t root, const std::vector<int32_t>& cnts) {
+// The root checks the received tile ids against each other and its own list (a duplicate means
+// two ranks rendered one tile: refused before anything is written), then writes them into its Buffer.
+static int gather_finish(Ctx* c, int32_t root, int64_t total) {
     if (c->rank == root) {
-        size_t total = 0;
-        for (int p = 0; p < c->nranks; p++)
-            if (p != root) total += (size_t)cnts[(size_t)p];
         if (total > 0) {
+            std::vector<int32_t> ids((size_t)total);
+            PT_HIP(hipMemcpyAsync(ids.data(), c->g_ids, (size_t)total * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+            PT_HIP(hipStreamSynchronize(c->stream));
+            const int32_t image = ((c->width + 31) / 32) * ((c->height + 31) / 32);
+            if (c->pass_tiles > 0) ids.insert(ids.end(), c->h_tiles.begin(), c->h_tiles.end());
+            else for (int32_t t = 0; t < image; t++) ids.push_back(t);   // the root rendered the whole image
+            if (pt_tile_lists_check(ids.data(), (int64_t)ids.size(), image))
+                return fail(PT_ERR_INVALID_ARG, std::string("gather: the ranks' tile lists overlap (") + g_last_error + ")");
             pt::DevBuffer B{c->d_m, c->d_v, c->d_n, c->d_counters};
             hipLaunchKernelGGL(pt::k_tiles_pack, dim3(2048), dim3(256), 0, c->stream, B, c->width, c->height,
                                (c->width + 31) / 32, c->g_ids, (uint32_t)total, c->g_m, c->g_v, c->g_n, 1);
@@ -1550,15 +1605,12 @@ static int gather_finish(Ctx* c, int32_t root, const std::vector<int32_t>& cnts)
     PT_HIP(hipStreamSynchronize(c->stream));
     return PT_OK;
 }
-static int gather_counts(Ctx* c, std::vector<int32_t>& cnts) {
+static int gather_counts(Ctx* c, int32_t root, std::vector<int32_t>& cnts, std::vector<int64_t>& offs, int64_t& total) {
     cnts.assign((size_t)c->nranks, 0);
+    offs.assign((size_t)c->nranks, -1);
     PT_HIP(hipMemcpy(cnts.data(), c->g_cnts, (size_t)c->nranks * sizeof(int32_t), hipMemcpyDeviceToHost));
     const int32_t tiles = ((c->width + 31) / 32) * ((c->height + 31) / 32);
-    int64_t sum = 0;
-    for (int32_t v : cnts) sum += v;
-    if (sum > tiles)   // disjoint lists never hold more tiles than the image
-        return fail(PT_ERR_INVALID_ARG, "gather: the ranks' tile lists overlap (more tiles than the image has)");
-    return PT_OK;
+    return pt_gather_layout(c->nranks, root, cnts.data(), tiles, offs.data(), &total);
 }
 
 int pt_comm_gather(void* ctx, int32_t root) {
@@ -1573,13 +1625,15 @@ int pt_comm_gather(void* ctx, int32_t root) {
     if (r != ncclSuccess) return fail(PT_ERR_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
     PT_HIP(hipStreamSynchronize(c->stream));
     std::vector<int32_t> cnts;
-    if ((rc = gather_counts(c, cnts))) return rc;
+    std::vector<int64_t> offs;
+    int64_t total = 0;
+    if ((rc = gather_counts(c, root, cnts, offs, total))) return rc;   // every rank sees the same counts
     r = ncclGroupStart();
-    if (r == ncclSuccess) r = gather_issue(c, root, cnts);
+    if (r == ncclSuccess) r = gather_issue(c, root, cnts, offs);
     ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
         return fail(PT_ERR_RCCL, std::string("gather send/recv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-    return gather_finish(c, root, cnts);
+    return gather_finish(c, root, total);
 }
 
 // One communicator over G contexts of this process (one per device), formed by one call:
@@ -1636,17 +1690,19 @@ int pt_comm_gather_all(void* const* ctxs, int32_t n, int32_t root) {
     if (r != ncclSuccess || r2 != ncclSuccess)
         return fail(PT_ERR_RCCL, std::string("ncclAllGather (group): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
     std::vector<std::vector<int32_t>> cnts((size_t)n);
+    std::vector<std::vector<int64_t>> offs((size_t)n);
+    std::vector<int64_t> total((size_t)n, 0);
     for (int i = 0; i < n; i++) {
         Ctx* c = (Ctx*)ctxs[i];
         PT_HIP(hipSetDevice(c->device));
         PT_HIP(hipStreamSynchronize(c->stream));
-        if ((rc = gather_counts(c, cnts[(size_t)i]))) return rc;
+        if ((rc = gather_counts(c, root, cnts[(size_t)i], offs[(size_t)i], total[(size_t)i]))) return rc;
     }
     r = ncclGroupStart();   // step 2: the sends and receives
     for (int i = 0; i < n && r == ncclSuccess; i++) {
         Ctx* c = (Ctx*)ctxs[i];
         if (hipSetDevice(c->device) != hipSuccess) { r = ncclInvalidUsage; break; }
-        r = gather_issue(c, root, cnts[(size_t)i]);
+        r = gather_issue(c, root, cnts[(size_t)i], offs[(size_t)i]);
     }
     r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
@@ -1654,7 +1710,7 @@ int pt_comm_gather_all(void* const* ctxs, int32_t n, int32_t root) {
     for (int i = 0; i < n; i++) {
         Ctx* c = (Ctx*)ctxs[i];
         PT_HIP(hipSetDevice(c->device));
-        if ((rc = gather_finish(c, root, cnts[(size_t)i]))) return rc;
+        if ((rc = gather_finish(c, root, total[(size_t)i]))) return rc;
     }
     return PT_OK;
 }

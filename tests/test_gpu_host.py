@@ -1,12 +1,7 @@
 """Host-side paths of the drop-in on the GPU: resuming from a saved Buffer (pt_write_buffer),
 the single-process communicator (pt_comm_init_all / pt_comm_gather_all) and repeated
-gathers, and a world-2 multi-process render through libptsharp_hip (two ranks on the one
-GPU of the box, their tile Buffers summed over gloo) that must equal the 1-process render
-bit for bit (pixel-keyed random streams + order-independent accumulation)."""
-import os
-import socket
-import tempfile
-
+gathers, and the tile read/write layout.  The world-2 multi-process render lives in
+test_zz_gpu_multiprocess.py, which collects last (it spawns processes)."""
 import numpy as np
 import pytest
 
@@ -83,12 +78,6 @@ def test_comm_init_all_and_repeated_gathers(gpu):
     assert (got.N == 0).any() and (got.N == 2).any()
 
 
-def _free_port():
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        return sk.getsockname()[1]
-
-
 def test_read_write_tiles_layout(gpu):
     """pt_read_tiles packs a tile row-major (edge tiles: zeros outside the image); pt_write_tiles
     puts packed tiles back; a render's tiles moved into a fresh context reproduce its Buffer."""
@@ -116,62 +105,3 @@ def test_read_write_tiles_layout(gpu):
     finally:
         r.close()
         q.close()
-
-
-def _worker(rank, world, port, outdir):
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    sys.path.insert(0, here)
-    sys.path.insert(0, os.path.dirname(here))
-    os.environ["PT_WF_MAX_CAP"] = str(1 << 22)   # two contexts share the card: small queues
-    import torch
-    import torch.distributed as dist
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    try:
-        W, H = 200, 120
-        s, c, smp = _scene()
-        r = Renderer.NewRenderer(s, c, smp, W, H, True, device=0)
-        try:
-            mine = tiles_for_rank(W, H, rank, world)
-            r.SamplesPerPixel, r.Seed, r.Tiles = 2, 71, mine
-            for _ in range(2):
-                r.RenderParallel()
-            # pt_comm_gather's protocol over gloo: tile counts, then each rank's packed tiles to
-            # the root, which writes them into its Buffer
-            cnt = torch.tensor([len(mine)], dtype=torch.int64)
-            cnts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-            dist.all_gather(cnts, cnt)
-            if rank != 0:
-                dist.send(torch.from_numpy(np.ascontiguousarray(mine, np.int32)), dst=0)
-                for a in r.ReadTiles(mine):
-                    dist.send(torch.from_numpy(a), dst=0)
-            else:
-                for p in range(1, world):
-                    n = int(cnts[p][0])
-                    ids = torch.zeros(n, dtype=torch.int32)
-                    dist.recv(ids, src=p)
-                    parts = [torch.zeros((n, 32, 32, 3), dtype=torch.float64), torch.zeros((n, 32, 32, 3), dtype=torch.float64),
-                             torch.zeros((n, 32, 32), dtype=torch.int32)]
-                    for x in parts:
-                        dist.recv(x, src=p)
-                    r.WriteTiles(ids.numpy(), *(x.numpy() for x in parts))
-                b = r.ReadBuffer()
-                np.savez(os.path.join(outdir, "gathered.npz"), M=b.M, V=b.V, N=b.N)
-        finally:
-            r.close()
-    finally:
-        dist.destroy_process_group()
-
-
-def test_two_ranks_one_gpu_equal_single_render(gpu):
-    """World 2: each process renders its interleaved tiles through libptsharp_hip on the box's GPU;
-    the root assembles the frame with pt_comm_gather's tile-compacted protocol (counts, then packed
-    tiles via pt_read_tiles / pt_write_tiles) over gloo, and the result is the 1-process render's
-    Buffer bit for bit."""
-    import torch.multiprocessing as mp
-    with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
-        g = np.load(os.path.join(d, "gathered.npz"))
-        got = _Buf(g["M"], g["V"], g["N"])
-    ref = _Buf(*_render(200, 120, 2, seed=71))
-    same_buffer(got, ref)
