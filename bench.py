@@ -87,6 +87,53 @@ def _gloo_gather(r, dist, rank, world, mine):
         r.WriteTiles(ids.numpy(), *(x.numpy() for x in parts))
 
 
+GATHER_WATCHDOG_S = 300.0
+
+
+def _watchdog(seconds, what):
+    """Ends the process with status 3 if `what` has not finished within `seconds` (cancel() when it has)."""
+    import threading
+
+    def fire():
+        print(f"{what} did not finish within {seconds:.0f} s on this rank; exiting", file=sys.stderr, flush=True)
+        os._exit(3)
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def _gather_check(r, dist, rank, world, mine):
+    """Every rank's own tiles (pt_read_tiles, as it rendered them) to rank 0 over gloo; rank 0 reads
+    the same tiles from its gathered Buffer and compares bit for bit.  Returns the verdict on rank 0."""
+    import torch
+    parts = [np.ascontiguousarray(a) for a in r.ReadTiles(mine)] if len(mine) else []
+    cnts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(cnts, torch.tensor([len(mine)], dtype=torch.int64))
+    if rank != 0:
+        if len(mine):
+            dist.send(torch.from_numpy(np.ascontiguousarray(mine, np.int32)), dst=0)
+            for a in parts:
+                dist.send(torch.from_numpy(a), dst=0)
+        return None
+    bad, checked = 0, len(mine)
+    for p in range(1, world):
+        n = int(cnts[p][0])
+        if n == 0:
+            continue
+        ids = torch.zeros(n, dtype=torch.int32)
+        dist.recv(ids, src=p)
+        sent = [torch.zeros((n, 32, 32, 3), dtype=torch.float64), torch.zeros((n, 32, 32, 3), dtype=torch.float64),
+                torch.zeros((n, 32, 32), dtype=torch.int32)]
+        for x in sent:
+            dist.recv(x, src=p)
+        got = r.ReadTiles(ids.numpy())
+        bad += sum(int(not np.array_equal(g, x.numpy())) for g, x in zip(got, sent))
+        checked += n
+    return {"tiles": checked, "bit_exact": bad == 0,
+            "what": "rank 0's Buffer after the gather vs each rank's own pt_read_tiles, {M, V, N}"}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -98,6 +145,8 @@ def parse():
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     p.add_argument("--tris", type=int, default=None, help="mesh triangles (default: 1,000,000 for c4, 69,451 for c3)")
     p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--mesh-source", choices=["obj", "generator"], default="obj",
+                   help="c3/c4 mesh: written as OBJ and loaded through pt_obj_load (default), or in memory")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--engine", choices=["auto", "mega", "wave"], default="auto")
@@ -129,14 +178,39 @@ def main():
     rccl_ok = False
     local = local % max(ndev.value, 1)
     t_scene = time.perf_counter()
+    obj_info = None
     if a.workload == "c2":
         scene, camera, sampler = scenes.gopher3()
     else:
         if a.tris is None:
             a.tris = 1_000_000 if a.workload == "c4" else 69_451
-        scene, camera, sampler = scenes.bunny_frame(a.tris, seed=a.seed)
+        if a.mesh_source == "obj":
+            # Example.bunny loads its mesh with OBJ.Load (Example.cs:1088): the seeded mesh is written as
+            # an OBJ file and read back through pt_obj_load (OBJ.cs's quirks), as SURVEY.md §8d specifies
+            import tempfile
+            from ptsharp_amd.scene import OBJ
+            with tempfile.TemporaryDirectory() as d:
+                path = os.path.join(d, f"mesh{a.tris}.obj")
+                tw = time.perf_counter()
+                scenes.write_blob_obj(path, a.tris, seed=a.seed)
+                tw = time.perf_counter() - tw
+                size = os.path.getsize(path)
+                t_scene = tl = time.perf_counter()   # scene setup from the OBJ load on (not the writer)
+                mesh = OBJ.Load(path)
+                tl = time.perf_counter() - tl
+            obj_info = {"obj_bytes": size, "obj_write_s": round(tw, 3), "obj_load_s": round(tl, 3),
+                   "obj_triangles": len(mesh.v1)}
+            raw = {k: getattr(mesh, k).copy() for k in ("v1", "v2", "v3", "n1", "n2", "n3", "t1", "t2", "t3")}
+            scene, camera, sampler = scenes.bunny_frame(a.tris, seed=a.seed, mesh=mesh)
+        else:
+            scene, camera, sampler = scenes.bunny_frame(a.tris, seed=a.seed)
     scene.Compile()
     t_scene = time.perf_counter() - t_scene
+    if obj_info is not None:   # the OBJ round trip is exact: the loaded Triangle[] is the generator's, bit for bit
+        gen = scenes.blob_mesh(a.tris, a.seed)
+        obj_info["obj_equals_generator"] = all(np.array_equal(raw[k].view(np.uint32), getattr(gen, k).view(np.uint32))
+                                          for k in raw)
+        del gen, raw
 
     W, H = a.width, a.height
     r = Renderer.NewRenderer(scene, camera, sampler, W, H, True, device=local)
@@ -208,6 +282,10 @@ def main():
         _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
         gather = "gloo (RCCL init failed)"
     elif world > 1:
+        # A failure inside the RCCL group on one rank would leave its peers blocked in the group:
+        # the watchdog ends this process (non-zero) instead of letting the job hang.  A failure
+        # every rank sees alike (the MIN below) falls back to the same protocol over gloo.
+        dog = _watchdog(GATHER_WATCHDOG_S, "pt_comm_gather")
         ok = 1
         try:
             r.Gather(0)   # pt_comm_gather: tile-compacted send/recv over RCCL
@@ -222,6 +300,7 @@ def main():
         else:
             _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
             gather = "gloo (RCCL gather failed)"
+        dog.cancel()
     r.Synchronize()
     t1 = time.perf_counter()
     if dist:
@@ -237,6 +316,14 @@ def main():
         total_rays = int(rr[0])
     else:
         total_rays = rays
+
+    gather_check = None
+    if world > 1:
+        # after the timed region: rank 0's gathered Buffer must hold every rank's tiles as that rank
+        # rendered them (each rank's pt_read_tiles of its own list, sent over gloo), bit for bit
+        dog = _watchdog(GATHER_WATCHDOG_S, "gather check")
+        gather_check = _gather_check(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
+        dog.cancel()
 
     if rank != 0:
         r.close()
@@ -290,7 +377,9 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32/f64",
-        "data": "synthetic (seeded displaced-sphere mesh; no model assets ship with the reference)" if a.workload != "c2"
+        "data": ("synthetic (seeded displaced-sphere mesh" + (", written as OBJ and loaded through pt_obj_load"
+                                                               if obj_info else "")
+                 + "; no model assets ship with the reference)") if a.workload != "c2"
         else "synthetic (analytic gopher3 scene)",
         "config": {
             "workload": WORKLOADS[a.workload],
@@ -298,11 +387,13 @@ def main():
             "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}" + (f" shard {a.shard}" if a.shard else "")
             + (f" (rehearsal: {world} ranks on {ndev.value} GPU(s))" if shared else "")
             + (f", gather {gather}" if gather else ""),
+            "gather_check": gather_check,
             "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
             "rays_per_camera_sample": round(total_rays / (W * H * a.spp * a.steps), 3),
             "shadow_ray_fraction": round(ctr.shadow_rays / max(ctr.rays, 1), 4),
             "lit_shadow_rays_per_step": int(ctr.lit_shadow_rays), "accum_runs_per_step": int(ctr.accum_runs),
             "engine": a.engine, "scene_build_s": round(t_scene, 3), "bvh_build_ms": round(build_ms, 1),
+            "mesh_source": None if a.workload == "c2" else a.mesh_source, **(obj_info or {}),
             "bvh_bytes": int(bvh_bytes),
             "kernel_ms_per_step": {names[k]: round(kms[k] / a.steps, 3) for k in range(_abi.K_SLOTS) if klaunch[k]},
         },

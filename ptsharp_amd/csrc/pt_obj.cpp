@@ -29,7 +29,7 @@
 
 #include "../../include/ptsharp_hip.h"
 
-#pragma STDC FP_CONTRACT OFF
+// Built with -ffp-contract=off (Makefile): the face normal is FixNormals' fp32 sequence, unfused.
 
 namespace {
 
@@ -45,26 +45,40 @@ int obj_fail(const std::string& m) {
 }
 
 // float.Parse / int.Parse (invariant culture) allow surrounding white space.
-std::string trim(const std::string& s) {
-    const char* ws = " \t\n\v\f\r";
-    size_t a = s.find_first_not_of(ws), b = s.find_last_not_of(ws);
-    return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+// A word of a line: [p, p + n) (no allocation; lines are parsed in place).
+struct Word {
+    const char* p;
+    size_t n;
+    bool eq(const char* lit) const { return std::strlen(lit) == n && std::memcmp(p, lit, n) == 0; }
+};
+
+Word trim(Word w) {
+    auto ws = [](char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; };
+    while (w.n && ws(w.p[0])) { w.p++; w.n--; }
+    while (w.n && ws(w.p[w.n - 1])) w.n--;
+    return w;
 }
 
-bool parse_float(const std::string& w, float& out) {
-    const std::string s = trim(w);
-    if (s.empty()) return false;
+// strtof / strtol need a terminated string: words are copied to a stack buffer (a longer word,
+// which no number is, goes through a std::string).
+template <class T, class F>
+bool parse_num(Word w, T& out, F conv) {
+    w = trim(w);
+    if (!w.n) return false;
+    char buf[64];
+    std::string big;
+    const char* s = buf;
+    if (w.n < sizeof buf) { std::memcpy(buf, w.p, w.n); buf[w.n] = 0; }
+    else { big.assign(w.p, w.n); s = big.c_str(); }
     char* end = nullptr;
-    out = std::strtof(s.c_str(), &end);
-    return end == s.c_str() + s.size();
+    out = conv(s, &end);
+    return end == s + w.n;
 }
-
-bool parse_int(const std::string& w, long& out) {
-    const std::string s = trim(w);
-    if (s.empty()) return false;
-    char* end = nullptr;
-    out = std::strtol(s.c_str(), &end, 10);
-    return end == s.c_str() + s.size();
+bool parse_float(Word w, float& out) {
+    return parse_num(w, out, [](const char* s, char** e) { return std::strtof(s, e); });
+}
+bool parse_int(Word w, long& out) {
+    return parse_num(w, out, [](const char* s, char** e) { return std::strtol(s, e, 10); });
 }
 
 // Vector.Sub / Cross / Normalize in fp32 (Vector.cs; pt_math.h has the same ops).
@@ -76,26 +90,28 @@ F3 normalize(F3 a) {
 }
 bool is_zero(F3 a) { return a.x == 0.f && a.y == 0.f && a.z == 0.f; }
 
-// String.Split(new[] {"//", "/"}, RemoveEmptyEntries)
-std::vector<std::string> split_slashes(const std::string& s) {
-    std::vector<std::string> out;
-    std::string cur;
-    for (size_t i = 0; i < s.size();) {
-        if (s[i] == '/') {
-            if (!cur.empty()) out.push_back(cur);
-            cur.clear();
-            i += (i + 1 < s.size() && s[i + 1] == '/') ? 2 : 1;
+// String.Split(new[] {"//", "/"}, RemoveEmptyEntries): at most `max` parts kept (the rest are unused)
+size_t split_slashes(Word s, Word* out, size_t max) {
+    size_t k = 0, start = 0;
+    for (size_t i = 0; i <= s.n;) {
+        if (i == s.n || s.p[i] == '/') {
+            if (i > start && k < max) out[k] = Word{s.p + start, i - start};
+            if (i > start) k++;
+            if (i == s.n) break;
+            i += (i + 1 < s.n && s.p[i + 1] == '/') ? 2 : 1;
+            start = i;
         } else {
-            cur.push_back(s[i++]);
+            i++;
         }
     }
-    if (!cur.empty()) out.push_back(cur);
-    return out;
+    return k;
 }
 
 struct Loader {
     std::vector<F3> vs, vts, vns{F3{0.f, 0.f, 0.f}};
     std::vector<float> v1, v2, v3, n1, n2, n3, t1, t2, t3;
+    std::vector<Word> words;             // reused per line
+    std::vector<long> fv, ft, fn;
 
     template <class Vec>
     bool at(const Vec& list, long idx, F3& out) const {
@@ -109,42 +125,42 @@ struct Loader {
         a.push_back(v.z);
     }
 
-    int line(std::string ln, size_t lineno) {
-        for (char& c : ln) c = (char)std::tolower((unsigned char)c);  // ToLower (invariant for ASCII)
-        std::vector<std::string> words;
+    // One line, lower-cased in place (ToLower is invariant for ASCII), split on ' ' (OBJ.cs:33-35).
+    int line(char* ln, size_t len, size_t lineno) {
+        for (size_t i = 0; i < len; i++) ln[i] = (char)std::tolower((unsigned char)ln[i]);
+        words.clear();
         size_t start = 0;
-        for (size_t i = 0; i <= ln.size(); i++) {
-            if (i == ln.size() || ln[i] == ' ') {
-                if (i > start) words.push_back(ln.substr(start, i - start));
+        for (size_t i = 0; i <= len; i++) {
+            if (i == len || ln[i] == ' ') {
+                if (i > start) words.push_back(Word{ln + start, i - start});
                 start = i + 1;
             }
         }
         if (words.empty()) return PT_OK;
-        const std::string type = words[0];
-        words.erase(words.begin());
+        const Word type = words[0];
+        const Word* w = words.data() + 1;
+        const size_t nw = words.size() - 1;
         auto where = [&]() { return " (line " + std::to_string(lineno) + ")"; };
-        if (type == "v" || type == "vn") {
+        if (type.eq("v") || type.eq("vn")) {
             F3 v;
-            if (words.size() < 3 || !parse_float(words[0], v.x) || !parse_float(words[1], v.y) ||
-                !parse_float(words[2], v.z))
-                return obj_fail("bad " + type + where());
-            (type == "v" ? vs : vns).push_back(v);
-        } else if (type == "vt") {
+            if (nw < 3 || !parse_float(w[0], v.x) || !parse_float(w[1], v.y) || !parse_float(w[2], v.z))
+                return obj_fail("bad " + std::string(type.p, type.n) + where());
+            (type.eq("v") ? vs : vns).push_back(v);
+        } else if (type.eq("vt")) {
             F3 v{0.f, 0.f, 0.f};
-            if (words.size() < 2 || !parse_float(words[0], v.x) || !parse_float(words[1], v.y))
+            if (nw < 2 || !parse_float(w[0], v.x) || !parse_float(w[1], v.y))
                 return obj_fail("bad vt" + where());
             vts.push_back(v);
-        } else if (type == "f") {
-            const size_t n = words.size();
-            std::vector<long> fv(n, 0), ft(n, 0), fn(n, 0);
-            size_t count = 0;
-            for (const std::string& arg : words) {
-                std::vector<std::string> p = split_slashes(arg);
+        } else if (type.eq("f")) {
+            const size_t n = nw;
+            fv.assign(n, 0); ft.assign(n, 0); fn.assign(n, 0);
+            for (size_t count = 0; count < n; count++) {
+                Word p[3];
+                const size_t np = split_slashes(w[count], p, 3);
                 long x;
-                if (p.size() > 0) { if (!parse_int(p[0], x)) return obj_fail("bad face index" + where()); fv[count] = x - 1; }
-                if (p.size() > 1) { if (!parse_int(p[1], x)) return obj_fail("bad face index" + where()); ft[count] = x - 1; }
-                if (p.size() > 2) { if (!parse_int(p[2], x)) return obj_fail("bad face index" + where()); fn[count] = x - 1; }
-                count++;
+                if (np > 0) { if (!parse_int(p[0], x)) return obj_fail("bad face index" + where()); fv[count] = x - 1; }
+                if (np > 1) { if (!parse_int(p[1], x)) return obj_fail("bad face index" + where()); ft[count] = x - 1; }
+                if (np > 2) { if (!parse_int(p[2], x)) return obj_fail("bad face index" + where()); fn[count] = x - 1; }
             }
             for (size_t i = 1; i + 1 < n; i++) {
                 const size_t c[3] = {0, i, i + 1};
@@ -203,22 +219,35 @@ int pt_obj_load(const char* path, pt_mesh_data* out) {
     std::string ln;
     size_t lineno = 0;
     int rc = PT_OK;
-    // StreamReader.ReadLine: "\n", "\r\n" and "\r" end a line
-    for (int ch = std::fgetc(f);; ch = std::fgetc(f)) {
-        if (ch == EOF || ch == '\n' || ch == '\r') {
-            if (ch == '\r') {
-                int nx = std::fgetc(f);
-                if (nx != '\n' && nx != EOF) std::ungetc(nx, f);
+    // StreamReader.ReadLine: "\n", "\r\n" and "\r" end a line.  The file is read in 1-MB blocks.
+    std::vector<char> blk(1u << 20);
+    bool cr = false;   // the previous block ended on '\r': a '\n' starting this one belongs to it
+    for (;;) {
+        const size_t got = std::fread(blk.data(), 1, blk.size(), f);
+        size_t i = 0;
+        if (cr && got > 0 && blk[0] == '\n') i = 1;
+        cr = false;
+        for (; i < got && rc == PT_OK; i++) {
+            const char ch = blk[i];
+            if (ch == '\n' || ch == '\r') {
+                rc = L.line(ln.data(), ln.size(), ++lineno);
+                ln.clear();
+                if (ch == '\r') {
+                    if (i + 1 < got) { if (blk[i + 1] == '\n') i++; }
+                    else cr = true;
+                }
+            } else {
+                // the run up to the next line end in one append
+                size_t j = i;
+                while (j < got && blk[j] != '\n' && blk[j] != '\r') j++;
+                ln.append(blk.data() + i, j - i);
+                i = j - 1;
             }
-            if (ch != EOF || !ln.empty()) {
-                if ((rc = L.line(ln, ++lineno)) != PT_OK) break;
-            }
-            ln.clear();
-            if (ch == EOF) break;
-        } else {
-            ln.push_back((char)ch);
         }
+        if (rc != PT_OK || got < blk.size()) break;
     }
+    if (rc == PT_OK && std::ferror(f)) rc = obj_fail(std::string("read error on \"") + path + "\"");
+    if (rc == PT_OK && !ln.empty()) rc = L.line(ln.data(), ln.size(), ++lineno);
     std::fclose(f);
     if (rc != PT_OK) return rc;
     const size_t n = L.v1.size() / 3;

@@ -117,9 +117,9 @@ def example3():
     return scene, camera, sampler
 
 
-def blob_mesh(n_target: int, seed: int = 1234, amplitude: float = 0.05) -> Mesh:
-    """Seeded displaced UV sphere with ~n_target triangles (fan caps + quad bands), per-vertex
-    radius 1 + amplitude·noise, zero normals (FixNormals → face normals), consistent winding."""
+def _blob_geometry(n_target: int, seed: int = 1234, amplitude: float = 0.05):
+    """blob_mesh's shared vertex list (float32 [V,3]), per-vertex texture coordinates (float32 [V,3])
+    and triangle vertex indices ([T,3], 0-based)."""
     # tris = 2*ns + 2*ns*(nr-2) = 2*ns*(nr-1);  choose nr ≈ ns/2
     ns = max(8, int(round(math.sqrt(n_target))))
     nr = max(3, int(round(n_target / (2 * ns))) + 1)
@@ -152,14 +152,46 @@ def blob_mesh(n_target: int, seed: int = 1234, amplitude: float = 0.05) -> Mesh:
         tris.append(np.stack([a, d, c], axis=1))
     tris.append(np.stack([np.full(ns, south), ring(nr - 2, j), ring(nr - 2, j + 1)], axis=1))
     t = np.concatenate(tris)
-    z = np.zeros((len(t), 3), np.float32)
     # texture coordinates: the sphere parametrisation (u = φ/2π, v = θ/π), poles at the ring's u
     uv = np.stack([ph.reshape(-1) / (2 * np.pi), th.reshape(-1) / np.pi, np.zeros(th.size)], axis=-1)
     uv = np.concatenate([uv, [[0.5, 0, 0], [0.5, 1, 0]]]).astype(np.float32)
+    return verts, uv, t
+
+
+def blob_mesh(n_target: int, seed: int = 1234, amplitude: float = 0.05) -> Mesh:
+    """Seeded displaced UV sphere with ~n_target triangles (fan caps + quad bands), per-vertex
+    radius 1 + amplitude·noise, zero normals (FixNormals → face normals), consistent winding."""
+    verts, uv, t = _blob_geometry(n_target, seed, amplitude)
+    z = np.zeros((len(t), 3), np.float32)
     m = Mesh(verts[t[:, 0]], verts[t[:, 1]], verts[t[:, 2]], z, z, z, t1=uv[t[:, 0]], t2=uv[t[:, 1]], t3=uv[t[:, 2]])
     from .scene import fix_normals_arrays
     m.n1, m.n2, m.n3 = fix_normals_arrays(m.v1, m.v2, m.v3, m.n1, m.n2, m.n3)
     return m
+
+
+def blob_obj_text(n_target: int, seed: int = 1234, amplitude: float = 0.05) -> str:
+    """blob_mesh's mesh as Wavefront OBJ text, the form Example.bunny loads (OBJ.Load("models/bunny.obj"),
+    Example.cs:1088): one `v` per vertex and one `vt` per vertex (the same index), faces
+    `f a/a b/b c/c` (1-based, no normal index: OBJ.cs:104 then reads the dummy normal and
+    Triangle.FixNormals puts the face normal in, as blob_mesh does).  Numbers are written with 9
+    significant digits, which float.Parse / strtof read back to the same float32 bits."""
+    verts, uv, t = _blob_geometry(n_target, seed, amplitude)
+    out = [f"# seeded displaced sphere: {len(t)} triangles, blob_mesh({n_target}, seed={seed})\n"]
+
+    def rows(fmt, a, k=8192):   # one %-format call per block of rows
+        for i in range(0, len(a), k):
+            blk = a[i:i + k]
+            out.append((fmt * len(blk)) % tuple(blk.reshape(-1).tolist()))
+    rows("v %.9g %.9g %.9g\n", verts.astype(np.float64))
+    rows("vt %.9g %.9g\n", uv[:, :2].astype(np.float64))
+    rows("f %d/%d %d/%d %d/%d\n", np.repeat(t + 1, 2, axis=1))
+    return "".join(out)
+
+
+def write_blob_obj(path: str, n_target: int, seed: int = 1234) -> str:
+    with open(path, "w") as f:
+        f.write(blob_obj_text(n_target, seed))
+    return path
 
 
 def bunny_frame(n_tris: int = 69_451, seed: int = 1234, mesh: Mesh = None):
