@@ -151,6 +151,9 @@ def parse():
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--engine", choices=["auto", "mega", "wave"], default="auto")
     p.add_argument("--json-out", default=None)
+    p.add_argument("--passes-per-call", type=int, default=0,
+                   help="passes per pt_render_pass call (pt_pass_params.passes; 0 = auto: the number of tile "
+                        "shares, so one rank's share of an N-GPU frame is batched N passes at a time)")
     p.add_argument("--shard", default=None, metavar="K/N",
                    help="render only rank K's tiles of an N-way split, in this one process (profiling the "
                         "per-rank workload of an N-GPU run on one GPU; value then counts this shard only)")
@@ -245,8 +248,27 @@ def main():
     trace_name = "k_wf_trace_lanes<false>" if lanes else "k_wf_trace<false, false>"
     shadow_name = "k_wf_shadow_lanes<false>" if lanes else "k_wf_shadow<false, false>"
 
-    for _ in range(a.warmup):
-        r.RenderParallel()
+    # Passes per call: a rank's 1/N share of the frame is batched N passes per call (the Buffer is
+    # the one separate passes leave, bit for bit), so every launch sees a whole frame's worth of
+    # camera samples; a whole frame already fills the GPU (and the queues) in one pass.
+    shares = world if world > 1 else (int(a.shard.split("/")[1]) if a.shard else 1)
+    ppc = a.passes_per_call or max(1, min(shares, 8))
+    while a.steps % ppc:
+        ppc -= 1
+
+    def passes(k):   # k passes, ppc per call
+        done = 0
+        while done < k:
+            m = min(ppc, k - done)
+            if m == 1:
+                r.RenderParallel()
+            else:
+                r.RenderPasses(m)
+            done += m
+            yield m
+
+    for _ in passes(max(a.warmup, ppc if a.warmup else 0)):   # warm-up includes one full batch (its accumulators)
+        pass
     # one instrumented (untimed) pass: traversal counters → algorithmic bytes per ray, per kernel
     ctr = r.RenderCounted()
     ext_rays = ctr.rays - ctr.shadow_rays
@@ -267,8 +289,7 @@ def main():
     kernel_ms = 0.0
     kms = np.zeros(_abi.K_SLOTS)
     klaunch = np.zeros(_abi.K_SLOTS, np.int64)
-    for _ in range(a.steps):
-        r.RenderParallel()
+    for _ in passes(a.steps):
         s = r.Stats()
         rays += s.rays
         kernel_ms += s.last_pass_ms
@@ -388,6 +409,7 @@ def main():
             + (f" (rehearsal: {world} ranks on {ndev.value} GPU(s))" if shared else "")
             + (f", gather {gather}" if gather else ""),
             "gather_check": gather_check,
+            "passes_per_call": ppc,
             "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
             "rays_per_camera_sample": round(total_rays / (W * H * a.spp * a.steps), 3),
             "shadow_ray_fraction": round(ctr.shadow_rays / max(ctr.rays, 1), 4),

@@ -124,6 +124,7 @@ namespace PTSharpCore
             public IntPtr tiles;
             public int engine, flags;
             public int adaptive_samples, firefly_samples;   // Renderer.AdaptiveSamples / FireflySamples
+            public int passes;                              // K consecutive passes in one call (0/1: one)
         }
 
         [StructLayout(LayoutKind.Sequential)]
@@ -428,7 +429,12 @@ namespace PTSharpCore
         /// samples, then per pixel its adaptive and firefly samples (PT_PASS_SERIAL).</summary>
         public void Render() => Pass(PtHip.PT_PASS_SERIAL);
 
-        void Pass(int flags)
+        /// <summary>k consecutive RenderParallel passes in one call (pt_pass_params.passes): the Buffer
+        /// k RenderParallel() calls leave, bit for bit; plain passes run as one GPU batch, so a rank's
+        /// tile share fills the device like a whole frame.  (IterativeRender keeps one pass per PNG.)</summary>
+        public void RenderPasses(int k) => Pass(0, k);
+
+        void Pass(int flags, int passes = 1)
         {
             if (!uploaded) Upload();
             var cam = Cam();
@@ -436,8 +442,9 @@ namespace PTSharpCore
                 direct_lighting = directLighting ? 1 : 0, soft_shadows = softShadows ? 1 : 0,
                 light_mode = (int)Sampler.LightMode, specular_mode = (int)Sampler.SpecularMode };
             var pass = new PtHip.pt_pass_params { spp = SamplesPerPixel, stratified = StratifiedSampling ? 1 : 0,
-                seed = Seed, pass_index = (uint)(++this.pass), adaptive_samples = AdaptiveSamples,
-                firefly_samples = FireflySamples, flags = flags };
+                seed = Seed, pass_index = (uint)(this.pass + 1), adaptive_samples = AdaptiveSamples,
+                firefly_samples = FireflySamples, flags = flags, passes = passes };
+            this.pass += passes;
             GCHandle tiles = default;
             if (Tiles != null)
             {

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 4
+#define PT_ABI_VERSION 5
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -256,6 +256,13 @@ typedef struct pt_pass_params {
     int32_t flags;           /* PT_PASS_KERNEL_TIMING: per-kernel hipEvent timing; PT_PASS_SERIAL */
     int32_t adaptive_samples;/* Renderer.AdaptiveSamples (Renderer.cs:340-410): per-sample AddSample x N */
     int32_t firefly_samples; /* Renderer.FireflySamples (Renderer.cs:412-470, FireflyThreshold = 1) */
+    int32_t passes;          /* 0 or 1: one pass.  K > 1: K consecutive IterativeRender passes
+                              * (pass_index .. pass_index + K - 1) in one call, the Buffer as after K
+                              * separate calls, bit for bit.  Plain RenderParallel passes on the
+                              * wavefront engine run as one batch: every pass' samples in one launch
+                              * sequence, each pass' Welford update applied per pixel in order (a
+                              * small tile share fills the GPU like a whole frame); other passes run
+                              * one by one.  pt_stats then covers the K passes. */
 } pt_pass_params;
 
 #define PT_PASS_KERNEL_TIMING 1

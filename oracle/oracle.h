@@ -93,6 +93,7 @@ typedef struct or_pass_params {
     const int32_t* tiles;
     int32_t engine, flags;  /* engine, and flags other than OR_PASS_SERIAL: product-only, ignored here */
     int32_t adaptive_samples, firefly_samples;  /* Renderer.AdaptiveSamples / FireflySamples */
+    int32_t passes;  /* product-only (a batch of passes in one call); the oracle renders one pass per call */
 } or_pass_params;
 /* flags: Renderer.Render's extra phases (Renderer.cs:80-198) instead of RenderParallel's */
 #define OR_PASS_SERIAL 2

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptsharp_hip.so")
 
-ABI_VERSION = 4   # PT_ABI_VERSION
+ABI_VERSION = 5   # PT_ABI_VERSION
 PT_OK = 0
 PT_ERR_INVALID_ARG = -1
 PT_ERR_HIP = -2
@@ -106,7 +106,7 @@ class pt_sampler(C.Structure):
 class pt_pass_params(C.Structure):
     _fields_ = [("spp", C.c_int32), ("stratified", C.c_int32), ("seed", C.c_uint64), ("pass_index", C.c_uint32),
                 ("num_tiles", C.c_int32), ("tiles", _i), ("engine", C.c_int32), ("flags", C.c_int32),
-                ("adaptive_samples", C.c_int32), ("firefly_samples", C.c_int32)]
+                ("adaptive_samples", C.c_int32), ("firefly_samples", C.c_int32), ("passes", C.c_int32)]
 
 
 class pt_device_opts(C.Structure):

@@ -169,6 +169,7 @@ struct Ctx {
     pt::WfQueues Q{};
     std::vector<DeviceArray> wf_arrays;
     uint32_t wf_cap = 0, wf_scap = 0;
+    int32_t acc_passes = 0;        // passes of per-pixel accumulators allocated (a batch needs one set per pass)
     uint32_t wf_max_cap = 0;       // queue capacity bound (wf_max_cap()), once per context
     // adaptive / firefly phases (allocated on first use, with the queues)
     uint32_t* d_plist = nullptr;   // [P] firefly candidates (ping-pong with d_plist2 over the rounds)
@@ -220,6 +221,7 @@ void free_wavefront(Ctx* c) {
     c->wf_arrays.clear();
     c->Q = pt::WfQueues{};
     c->wf_cap = c->wf_scap = 0;
+    c->acc_passes = 0;
     c->d_plist = nullptr;
     c->d_plist2 = nullptr;
     c->d_fcount = nullptr;
@@ -240,10 +242,11 @@ int wf_alloc(Ctx* c, T** out, size_t n) {
     return PT_OK;
 }
 
-int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
-    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w) return PT_OK;
+int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
+    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes) return PT_OK;
     cap = std::max(cap, c->wf_cap);
     scap = std::max(scap, c->wf_scap);
+    acc_passes = std::max(acc_passes, c->acc_passes);
     free_wavefront(c);
     pt::WfQueues Q{};
     int rc;
@@ -267,7 +270,8 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
     const size_t ovf_words = (size_t)(pt::kStackMax - pt::kLdsStack) * pt::kWfMaxThreads;
     if ((rc = wf_alloc(c, &Q.ovf, 2 * ovf_words))) return rc;
     Q.ovf_sh = Q.ovf + ovf_words;
-    size_t P = (size_t)c->width * (size_t)c->height;
+    // per-pixel accumulators of one pass, or of each pass of a batch (pt_pass_params.passes)
+    size_t P = (size_t)c->width * (size_t)c->height * (size_t)acc_passes;
     if ((rc = wf_alloc(c, &Q.acc.w, P * pt::kFixWords))) return rc;
     if ((rc = wf_alloc(c, &Q.acc.big, P * 3))) return rc;
     PT_HIP(hipMemsetAsync(Q.acc.w, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
@@ -280,6 +284,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap) {
     c->Q = Q;
     c->wf_cap = cap;
     c->wf_scap = scap;
+    c->acc_passes = acc_passes;
     return PT_OK;
 }
 
@@ -1143,6 +1148,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
                        sampler->light_mode, sampler->specular_mode};
     pt::DevPass P{c->width, c->height, pass->spp, pass->stratified, pass->seed, pass->pass_index, tiles_x, d_tiles,
                   num_tiles};
+    P.acc_stride = (uint32_t)((size_t)c->width * (size_t)c->height);
     pt::DevBuffer B{c->d_m, c->d_v, c->d_n, c->d_counters};
     // ---- engine choice and wavefront plan
     const int n_root = (int)std::sqrt((double)sampler->first_hit_samples);
@@ -1163,7 +1169,18 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     plan.lanes_shadow_blocks = c->grids.lanes_shadow_blocks;
     plan.full_trace_blocks = c->grids.full_trace_blocks;
     plan.full_shadow_blocks = c->grids.full_shadow_blocks;
-    const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp);
+    const bool extra = pass->adaptive_samples > 0 || pass->firefly_samples > 0;
+    const bool serial = (pass->flags & PT_PASS_SERIAL) != 0;   // Renderer.Render's extra phases (NumCPU == 1)
+    // pt_pass_params.passes: K consecutive passes.  Plain RenderParallel passes run as one batch
+    // (one launch sequence over all K passes' camera samples, so a small share — one rank's tiles
+    // of a multi-GPU frame — fills the GPU like a whole frame); the others pass by pass.
+    const int32_t batch = pass->passes > 1 ? pass->passes : 1;
+    if (batch > 1 && counted) return fail(PT_ERR_INVALID_ARG, "counted passes run one at a time (passes = 1)");
+    const bool batchable = batch > 1 && !extra && !serial && !pass->stratified && pass->engine != PT_ENGINE_MEGAKERNEL &&
+                           (uint64_t)P.acc_stride * (uint64_t)batch <= 0xFFFFFFFFull;
+    if (batchable) P.passes = batch;
+    const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp) *
+                                 (uint64_t)P.passes;
     double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)
     if (nm == 2) growth = std::ldexp(1.0, std::min(std::max(sampler->max_bounces - 1, 0), 60));
     const double per_sample = (double)plan.root_children * growth;   // extension rays per camera sample (widest depth)
@@ -1175,8 +1192,6 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     auto group_max = [](uint64_t ch) { return (double)(((ch + 255) / 256 + pt::kParts - 1) / pt::kParts * 256); };
     uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples,
                                                 std::floor(pmax / per_sample_nee / 256.0) * 256.0 * pt::kParts);
-    const bool extra = pass->adaptive_samples > 0 || pass->firefly_samples > 0;
-    const bool serial = (pass->flags & PT_PASS_SERIAL) != 0;   // Renderer.Render's extra phases (NumCPU == 1)
     if (pass->adaptive_samples < 0 || pass->firefly_samples < 0) return fail(PT_ERR_INVALID_ARG, "negative extra samples");
     int engine = pass->engine;
     if (engine == PT_ENGINE_AUTO)
@@ -1186,6 +1201,31 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     if (engine == PT_ENGINE_WAVEFRONT && chunk < 1)
         return fail(PT_ERR_UNSUPPORTED, "wavefront queues cannot hold one camera sample of this sampler (use the megakernel)");
     if (engine != PT_ENGINE_WAVEFRONT && engine != PT_ENGINE_MEGAKERNEL) return fail(PT_ERR_INVALID_ARG, "bad engine");
+    if (batch > 1 && !(P.passes > 1 && engine == PT_ENGINE_WAVEFRONT)) {
+        // not one batch: the K passes one after another, the stats summed
+        pt_pass_params one = *pass;
+        one.passes = 1;
+        pt_stats sum = c->stats;
+        uint64_t rays = 0, shadow = 0;
+        double ms = 0.0;
+        for (int32_t k = 0; k < batch; k++) {
+            one.pass_index = pass->pass_index + (uint32_t)k;
+            if (int rc = render_pass_impl(c, camera, sampler, &one, nullptr)) return rc;
+            rays += c->stats.rays;
+            shadow += c->stats.shadow_rays;
+            ms += c->stats.last_pass_ms;
+            for (int j = 0; j < PT_K_SLOTS; j++) {
+                sum.kernel_ms[j] = (k ? sum.kernel_ms[j] : 0.0) + c->stats.kernel_ms[j];
+                sum.kernel_launches[j] = (k ? sum.kernel_launches[j] : 0) + c->stats.kernel_launches[j];
+            }
+        }
+        std::memcpy(c->stats.kernel_ms, sum.kernel_ms, sizeof sum.kernel_ms);
+        std::memcpy(c->stats.kernel_launches, sum.kernel_launches, sizeof sum.kernel_launches);
+        c->stats.rays = rays;
+        c->stats.shadow_rays = shadow;
+        c->stats.last_pass_ms = ms;
+        return PT_OK;
+    }
     if (engine == PT_ENGINE_WAVEFRONT) {
         plan.chunk = chunk;
         // Shadow passes on the side stream, beside the next depth's closest-hit pass, when a
@@ -1206,7 +1246,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         const uint32_t pcap = (uint32_t)std::min(pmax, std::max(8192.0, std::max(group_samples, need)));
         const uint32_t spcap = (uint32_t)std::min(pmax, std::max(8192.0, group_samples * per_sample_nee));
         uint32_t cap = pcap * pt::kParts, scap = spcap * pt::kParts;
-        int rc = ensure_wavefront(c, cap, scap);
+        int rc = ensure_wavefront(c, cap, scap, P.passes);
         if (rc) return rc;
         if ((uint64_t)pass->adaptive_samples > chunk)
             return fail(PT_ERR_UNSUPPORTED, "adaptive samples exceed one wavefront chunk");
@@ -1307,7 +1347,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     c->stats.rays_total += rays;
     c->stats.last_pass_ms = ms;
     c->stats.total_ms += ms;
-    c->stats.passes++;
+    c->stats.passes += (uint64_t)P.passes;
     for (int k = 0; k < PT_K_SLOTS; k++) { c->stats.kernel_ms[k] = 0.0; c->stats.kernel_launches[k] = 0; }
     if (timing) PT_HIP(c->timer.collect(c->stats.kernel_ms, c->stats.kernel_launches));
     if (counted) {

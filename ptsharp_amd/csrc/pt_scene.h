@@ -114,6 +114,11 @@ struct DevPass {
     int32_t tiles_x;           // ceil(W/32)
     const int32_t* tiles;      // nullptr: tile = blockIdx.x / 4
     int32_t num_tiles;
+    // A batch of `passes` consecutive passes (pass_index .. pass_index + passes - 1) in one
+    // launch sequence (wavefront engine): pass p's samples add into accumulator p·acc_stride +
+    // pixel, and k_wf_finalize applies the passes' Welford updates per pixel in pass order.
+    int32_t passes = 1;
+    uint32_t acc_stride = 0;   // accumulators per pass (W·H)
 };
 
 struct DevBuffer {

@@ -247,6 +247,13 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
             pslot = slot / (uint64_t)spp_launch;
             s = (int)(slot % (uint64_t)spp_launch);
         }
+        // a batch of passes: pass p of the batch covers pixel slots p·num_tiles·1024 ..
+        uint32_t bp = 0;
+        if (P.passes > 1) {
+            const uint64_t per = (uint64_t)P.num_tiles * 1024u;
+            bp = (uint32_t)(pslot / per);
+            pslot -= (uint64_t)bp * per;
+        }
         const int tile_slot = (int)(pslot >> 10);
         const int tile = P.tiles ? P.tiles[tile_slot] : tile_slot;
         int x, y;
@@ -263,15 +270,16 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
             const int sample = sample_base + s;
             const int root = (int)sqrt((double)P.spp);
             const int u = sample / root, v = sample % root;
-            K = camera_key(P.seed, P.pass_index, pix, (uint32_t)sample);
+            K = camera_key(P.seed, P.pass_index + bp, pix, (uint32_t)sample);
             cast_ray(cam, x, y, w, h, ((double)u + 0.5) / (double)root, ((double)v + 0.5) / (double)root, K, o, d);
         } else {
-            K = camera_key(P.seed, P.pass_index, pix, (uint32_t)s);
+            K = camera_key(P.seed, P.pass_index + bp, pix, (uint32_t)s);
             double fu = (x + draw(K, D_JX)) / w;   // RenderParallel's jitter (Renderer.cs:297-302)
             double fv = (y + draw(K, D_JY)) / h;
             cast_ray(cam, x, y, w, h, fu, fv, K, o, d);
         }
-        ray_store_camera(Q, 0, i, o, d, (uint32_t)pix, K);
+        // the queue's "pixel" word is the accumulator the path's terms go to
+        ray_store_camera(Q, 0, i, o, d, (uint32_t)pix + bp * P.acc_stride, K);
     }
 }
 
@@ -1296,10 +1304,12 @@ __global__ __launch_bounds__(256) void k_wf_finalize(DevPass P, DevBuffer B, WfQ
         tile_pixel(tile, (int)(s & 1023), P.tiles_x, x, y);
         if (x >= P.width || y >= P.height) continue;
         const size_t pix = (size_t)y * (size_t)P.width + (size_t)x;
-        double c[3];
-        fix_take(Q.acc, pix, c);
-        // c /= spp (Renderer.cs:308) then Buffer.AddSample
-        welford(B, pix, c[0] / spp, c[1] / spp, c[2] / spp);
+        for (int p = 0; p < P.passes; p++) {   // a batch's passes in order: the Welford sequence of separate passes
+            double c[3];
+            fix_take(Q.acc, pix + (size_t)p * P.acc_stride, c);
+            // c /= spp (Renderer.cs:308) then Buffer.AddSample
+            welford(B, pix, c[0] / spp, c[1] / spp, c[2] / spp);
+        }
     }
 }
 
@@ -1487,7 +1497,7 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     const int rounds = P.stratified ? P.spp : 1;        // stratified: one Welford sample per sample index
     const int spp_launch = P.stratified ? 1 : P.spp;
     const double spp_d = (double)spp_launch;
-    const uint64_t total = pix_slots * (uint64_t)spp_launch;
+    const uint64_t total = pix_slots * (uint64_t)spp_launch * (uint64_t)(P.passes > 1 ? P.passes : 1);
     auto begin_k = [&](int cls) { if (timer) timer->begin(cls, stream); };
     auto end_k = [&](int cls) { if (timer) timer->end(cls, stream); };
     for (int r = 0; r < rounds; r++) {

@@ -172,7 +172,7 @@ class Renderer:
                                  0 if tiles is None else len(tiles),
                                  C.POINTER(C.c_int32)() if tiles is None else tiles.ctypes.data_as(C.POINTER(C.c_int32)),
                                  int(self.Engine), int(self.Flags), int(self.AdaptiveSamples),
-                                 int(self.FireflySamples))
+                                 int(self.FireflySamples), 1)
         return pp
 
     def RenderParallel(self) -> None:
@@ -186,6 +186,19 @@ class Renderer:
         if self.Verbose:
             print(f"{self.W} x {self.H}, {self.SamplesPerPixel} spp, MI355X device {self.Device}")
             print("time elapsed:", time.perf_counter() - t0)
+
+    def RenderPasses(self, k: int) -> None:
+        """k consecutive RenderParallel passes in one call (pt_pass_params.passes): the Buffer is the
+        one k RenderParallel() calls leave, bit for bit; plain passes run as one batch on the GPU."""
+        k = int(k)
+        if k < 1:
+            raise ValueError("k must be >= 1")
+        self._ensure_scene()
+        cam, smp = self.Camera.to_c(), self.Sampler.to_c()
+        pp = self._pass_params(pass_index=self._pass + 1)
+        pp.passes = k
+        _abi.check(self._lib.pt_render_pass(self._ctx, C.byref(cam), C.byref(smp), C.byref(pp)), "pt_render_pass")
+        self._pass += k
 
     def Render(self) -> None:
         """One pass of Renderer.Render (Renderer.cs:80-198), the NumCPU == 1 twin: the same main

@@ -105,3 +105,52 @@ def test_read_write_tiles_layout(gpu):
     finally:
         r.close()
         q.close()
+
+
+def test_resume_then_firefly_pass_clears_foreign_pixels(gpu):
+    """A rank that resumes from the whole checkpoint (LoadBuffer of the full frame) and then runs a
+    firefly pass on its tile subset: the other ranks' pixels are cleared before the pass, so the
+    firefly snapshot (all-reduced over the communicator) and the Buffer hold each pixel on its owner
+    only — the same bits as a rank that rendered its tiles all along (pt_write_buffer
+    never marked the Buffer as holding foreign pixels, and the snapshot then counted them twice)."""
+    w, h = 64, 48
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 4
+    tiles = tiles_for_rank(w, h, 0, 2)
+
+    def ctx():
+        r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+        r.SamplesPerPixel, r.Seed, r.Engine = 1, 23, _abi.ENGINE_WAVEFRONT
+        return r
+
+    full = ctx()
+    try:
+        full.RenderParallel()
+        full.RenderParallel()
+        b = full.ReadBuffer()
+        ck = _Buf(b.M.copy(), b.V.copy(), b.N.copy())
+    finally:
+        full.close()
+    out = []
+    for resume in (False, True):
+        r = ctx()
+        try:
+            r.Tiles = tiles
+            r.CommInit(1, 0, Renderer.CommUniqueId())
+            if resume:
+                r.LoadBuffer(ck, passes_done=2)
+            else:
+                r.RenderParallel()
+                r.RenderParallel()
+            r.FireflySamples = 4
+            r.RenderParallel()
+            b = r.ReadBuffer()
+            out.append(_Buf(b.M.copy(), b.V.copy(), b.N.copy()))
+        finally:
+            r.close()
+    own = np.zeros((h, w), bool)
+    for t in tiles:
+        own[(t // 2) * 32:(t // 2) * 32 + 32, (t % 2) * 32:(t % 2) * 32 + 32] = True
+    assert (out[1].N[~own] == 0).all(), "foreign pixels survived the resume"
+    assert (out[0].N[own] > 3).any(), "no firefly samples: the test exercises nothing"
+    same_buffer(out[1], out[0])

@@ -278,3 +278,87 @@ def test_refill_kernels_match_lockstep(gpu, monkeypatch, name):
         s, c, smp = scene()
         o, orr = O.render(O.OracleScene(s), c, smp, 64, 48, 2, passes=2, seed=43)
         check(b, rb, o, orr)
+
+
+# ---- pass batches (pt_pass_params.passes): K passes in one call == K calls, bit for bit
+def _batched_vs_separate(s, c, smp, w, h, spp, k, tiles=None, engine=_abi.ENGINE_WAVEFRONT, **kw):
+    from ptsharp_amd import Renderer
+    out = []
+    for batched in (False, True):
+        r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+        try:
+            r.SamplesPerPixel, r.Seed, r.Tiles, r.Engine = spp, 97, tiles, engine
+            for name, v in kw.items():
+                setattr(r, name, v)
+            r.RenderParallel()   # one plain pass first: the batch continues the pass numbering
+            rays = r.Stats().rays
+            if batched:
+                r.RenderPasses(k)
+                rays += r.Stats().rays
+            else:
+                for _ in range(k):
+                    r.RenderParallel()
+                    rays += r.Stats().rays
+            b = r.ReadBuffer()
+            out.append((b.M.copy(), b.V.copy(), b.N.copy(), rays, r.Stats().passes))
+        finally:
+            r.close()
+    (m0, v0, n0, r0, p0), (m1, v1, n1, r1, p1) = out
+    assert r0 == r1 and p0 == p1 == k + 1
+    assert np.array_equal(n0, n1) and np.array_equal(m0, m1) and np.array_equal(v0, v1)
+    return n1
+
+
+def test_pass_batch_equals_separate_passes(gpu):
+    s, c, smp = scenes.bunny_frame(4000, seed=9)
+    smp.MaxBounces = 3
+    n = _batched_vs_separate(s, c, smp, 160, 120, 4, 5)
+    assert (n == 6).all()
+
+
+def test_pass_batch_tile_share_and_oracle(gpu):
+    """One rank's eighth of a frame, 8 passes as one batch: the separate passes' bits, and the
+    oracle's Buffer (the pass numbering of the batch is the reference's pass loop, Renderer.cs:709)."""
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 4
+    w, h = 96, 64
+    tiles = tiles_for_rank(w, h, 3, 8)
+    _batched_vs_separate(s, c, smp, w, h, 1, 8, tiles=tiles)
+    from parity import check
+    from ptsharp_amd import Renderer
+    r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+    try:
+        r.SamplesPerPixel, r.Seed, r.Tiles, r.Engine = 1, 5, tiles, _abi.ENGINE_WAVEFRONT
+        r.RenderPasses(3)
+        rays = r.Stats().rays
+        g = r.ReadBuffer()
+    finally:
+        r.close()
+    o, orays = O.render(O.OracleScene(s), c, smp, w, h, 1, passes=3, seed=5, tiles=tiles)
+    check(g, rays, o, orays)
+
+
+def test_pass_batch_many_chunks(gpu, monkeypatch):
+    """A batch larger than the queues: several chunks, each holding parts of several passes."""
+    monkeypatch.setenv("PT_WF_MAX_CAP", str(1 << 20))
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 2
+    _batched_vs_separate(s, c, smp, 320, 180, 4, 6)
+
+
+@pytest.mark.parametrize("case", ["megakernel", "stratified", "adaptive", "firefly"])
+def test_pass_batch_fallbacks(gpu, case):
+    """Passes that cannot share one batch (megakernel engine, stratified, adaptive / firefly phases)
+    run one by one inside the call: still the separate calls' bits."""
+    s, c, smp = scenes.gopher3()
+    smp.MaxBounces = 3
+    kw, engine, spp = {}, _abi.ENGINE_WAVEFRONT, 2
+    if case == "megakernel":
+        engine = _abi.ENGINE_MEGAKERNEL
+    elif case == "stratified":
+        kw, spp = {"StratifiedSampling": True}, 4
+    elif case == "adaptive":
+        kw = {"AdaptiveSamples": 2}
+    else:
+        kw = {"FireflySamples": 3}
+    _batched_vs_separate(s, c, smp, 64, 48, spp, 3, engine=engine, **kw)
