@@ -253,8 +253,6 @@ def main():
     # camera samples; a whole frame already fills the GPU (and the queues) in one pass.
     shares = world if world > 1 else (int(a.shard.split("/")[1]) if a.shard else 1)
     ppc = a.passes_per_call or max(1, min(shares, 8))
-    while a.steps % ppc:
-        ppc -= 1
 
     def passes(k):   # k passes, ppc per call
         done = 0

@@ -192,10 +192,10 @@ struct Ctx {
 // and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
 // MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
-#ifndef PT_SIDE_MAX_CHUNK
-#define PT_SIDE_MAX_CHUNK (20u << 20)
+#ifndef PT_SIDE_MAX_RAYS
+#define PT_SIDE_MAX_RAYS (64ull << 20)
 #endif
-constexpr uint64_t kSideStreamMaxChunk = PT_SIDE_MAX_CHUNK;   // camera samples
+constexpr double kSideStreamMaxRays = (double)PT_SIDE_MAX_RAYS;   // a chunk's widest depth, extension rays
 constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 2 * (64 + 1);
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
@@ -1189,9 +1189,18 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     // 256-sample blocks, so a group gets at most ceil(ceil(chunk/256)/kParts)·256 of
     // them, and everything it appends stays in its own partition.
     const double pmax = (double)(wf_max_cap(c) / pt::kParts);
-    auto group_max = [](uint64_t ch) { return (double)(((ch + 255) / 256 + pt::kParts - 1) / pt::kParts * 256); };
+    const int32_t spp_launch = pass->stratified ? 1 : pass->spp;
+    auto group_max = [&](uint64_t ch) { return (double)pt::deal_group_max(ch, spp_launch); };
     uint64_t chunk = (uint64_t)std::min<double>((double)cam_samples,
                                                 std::floor(pmax / per_sample_nee / 256.0) * 256.0 * pt::kParts);
+    // the deal's runs can give one partition a little more than an eighth: shrink until it fits
+    {
+        const uint64_t step = (uint64_t)pt::deal_run(spp_launch) * 256u * pt::kParts;
+        while (chunk > step && group_max(chunk) * std::max(1.0, per_sample_nee) > pmax) chunk -= step;
+        while (chunk > 256 && group_max(chunk) * std::max(1.0, per_sample_nee) > pmax) chunk -= 256;
+        const uint64_t tile = (uint64_t)pt::deal_run(spp_launch) * 256u;   // chunks of whole tiles where they fit
+        if (chunk < cam_samples && chunk >= tile) chunk = chunk / tile * tile;
+    }
     if (pass->adaptive_samples < 0 || pass->firefly_samples < 0) return fail(PT_ERR_INVALID_ARG, "negative extra samples");
     int engine = pass->engine;
     if (engine == PT_ENGINE_AUTO)
@@ -1229,11 +1238,13 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     if (engine == PT_ENGINE_WAVEFRONT) {
         plan.chunk = chunk;
         // Shadow passes on the side stream, beside the next depth's closest-hit pass, when a
-        // chunk is small enough for the launches' fill and drain to matter (one rank's
-        // share of a multi-GPU frame: +6.5 % at 1/8 of C4); a full C4 frame runs 0.3 %
-        // slower that way, so it keeps one stream.
+        // chunk's widest depth is small enough for the launches' fill and drain to matter (one
+        // rank's 1/8 share of C4 passed one at a time, 33M rays: +6.5 %); a full C4 frame (265M)
+        // runs 0.3 % slower that way and C2's 16-child chunks (268M) 6.2 % slower (10632 vs 11332
+        // Mrays/s, profiles/r03c_c2_*.json): they keep one stream.  The bound is on rays, not
+        // camera samples (round 2 used 20M camera samples, which sent C2 to the side stream).
         // PT_SIDE_STREAM=0|1 (environment; tests) forces one stream or the side stream.
-        bool side = chunk <= kSideStreamMaxChunk;
+        bool side = (double)chunk * per_sample <= kSideStreamMaxRays;
         if (const char* f = std::getenv("PT_SIDE_STREAM")) side = !std::strcmp(f, "1") ? true : !std::strcmp(f, "0") ? false : side;
         if (side) {
             plan.side = c->side;

@@ -71,6 +71,21 @@ constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
 #endif
 constexpr int kLdsStack = PT_LDS_STACK;          // LDS stack entries per lane (traversal kernels)
 constexpr uint32_t kWfMaxBlocks = 256 * 8;        // grid cap of the traversal kernels
+
+// k_wf_camera deals a chunk's camera samples to the partitions in runs of deal_run 256-sample
+// blocks, the runs round-robin (pt_wavefront.hip).  PT_DEAL_TILES=1: a run is one 32x32 tile's
+// samples (1024·spp / 256 blocks), so each XCD traces compact patches of the scene; measured
+// slower (C4 5899 → 5831 Mrays/s, closest hit 47.96 → 48.65 ms per pass, the 1/8 share and C2
+// unchanged; profiles/r03e_ab_deal.txt), so runs are one block (16 pixels' samples).
+#ifndef PT_DEAL_TILES
+#define PT_DEAL_TILES 0
+#endif
+__host__ __device__ inline uint32_t deal_run(int32_t spp_launch) { return PT_DEAL_TILES ? 4u * (uint32_t)spp_launch : 1u; }
+// Camera samples the fullest partition receives from a chunk of `samples`.
+__host__ __device__ inline uint64_t deal_group_max(uint64_t samples, int32_t spp_launch) {
+    const uint64_t run = deal_run(spp_launch), nblk = (samples + 255) / 256, nruns = (nblk + run - 1) / run;
+    return (nruns + kParts - 1) / kParts * run * 256;
+}
 constexpr uint32_t kWfMaxThreads = kWfMaxBlocks * 256;
 
 struct WfPlan {

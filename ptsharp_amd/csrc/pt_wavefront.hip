@@ -212,28 +212,45 @@ __device__ __forceinline__ void ray_store_camera(const WfQueues& Q, int q, uint3
 }
 
 // ---------------------------------------------------------------- camera
+// Camera samples go to the XCD partitions in runs of `run` 256-sample blocks, the runs dealt
+// round-robin.  PT_DEAL_TILES=1: a run is one 32x32 tile's samples of the pass (4·spp blocks),
+// so each XCD traces whole tiles — 1/8 of the frame's tiles, each a compact patch of the scene
+// whose BVH nodes and shading records its own L2 then holds (measured 1.2 % slower on C4, see
+// pt_wavefront.h); 0 (default): runs of one block (16 pixels' samples), every XCD touching every
+// tile, the finest balance.
 __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQueues Q, uint64_t begin,
                                                    uint32_t count, int32_t spp_launch, int32_t sample_base) {
-    // Camera samples are dealt to the XCD groups in interleaved 256-slot blocks
-    // (16 pixels' samples): every group gets an even share of sky, floor and mesh.
-    // The deal is fixed, so each sample's queue slot is too: block b of the chunk goes to
-    // partition b mod kParts at local block b / kParts, and no slot needs an atomic (one
+    // The deal is fixed, so each sample's queue slot is too: no slot needs an atomic (one
     // returning atomic per wave on the partition counters held this kernel to their
     // ~88-per-µs rate: 5.9 ms per C4 pass).  Samples of pixels outside the image (edge
-    // tiles) leave dead slots that k_wf_trace and k_wf_shade skip.
+    // tiles) leave dead slots that k_wf_trace and k_wf_shade skip.  Every run is whole blocks
+    // (a tile's samples are a multiple of 256), and a chunk may start inside a run: the deal
+    // counts blocks from the chunk's start.
     const Group G = xcd_group();
+    const uint32_t run = deal_run(spp_launch);
+    const uint32_t nblk = (count + 255u) / 256u;
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
-        const uint32_t nblk = (count + 255u) / 256u, g = threadIdx.x;
+        const uint32_t g = threadIdx.x;
+        // blocks of partition g: runs g, g + kParts, ... of `run` blocks, the last one cut at nblk
+        const uint32_t nruns = (nblk + run - 1u) / run;
         uint32_t c = 0;
-        if (g < nblk) {
-            c = ((nblk - 1u - g) / kParts + 1u) * 256u;
-            if ((nblk - 1u) % kParts == g) c -= nblk * 256u - count;   // the chunk's partial last block
+        if (g < nruns) {
+            const uint32_t mine = (nruns - 1u - g) / kParts + 1u;   // runs of partition g
+            c = mine * run;
+            if ((nruns - 1u) % kParts == g) c -= nruns * run - nblk;   // the cut last run
+            c *= 256u;
+            if ((nblk - 1u) / run % kParts == g) c -= nblk * 256u - count;   // the chunk's partial last block
         }
         if (c > Q.pcap) { *Q.overflow = 1ull; c = Q.pcap; }
         *ray_count(Q, 0, g) = c;
     }
-    for (uint32_t g = (G.g + kParts * G.lb) * 256u + threadIdx.x; g < count; g += kParts * G.nb * 256u) {
-        const uint32_t local = (g / 256u / kParts) * 256u + (g & 255u);
+    // this block's share of partition G.g: local blocks lb, lb + nb, ...
+    for (uint32_t lblk = G.lb;; lblk += G.nb) {
+        const uint32_t blk = ((lblk / run) * kParts + G.g) * run + lblk % run;   // chunk block of local block lblk
+        if (blk >= nblk) break;
+        const uint32_t g = blk * 256u + threadIdx.x;   // chunk-relative sample
+        if (g >= count) continue;
+        const uint32_t local = lblk * 256u + threadIdx.x;
         if (local >= Q.pcap) continue;   // flagged above
         const uint32_t i = G.g * Q.pcap + local;
         const uint64_t slot = begin + g;
