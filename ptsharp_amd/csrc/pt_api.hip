@@ -351,6 +351,14 @@ inline void pad_box(float* lo, float* hi) {
     }
 }
 
+// Triangle BVH leaves: 1 makes every node of at most 3 triangles one leaf chunk (pt_bvh.h
+// build_bvh fill_leaves).  Measured slower on C4 (5915 → 5839 Mrays/s: nodes per ray 9.98 → 9.87,
+// triangle tests 2.96 → 3.23, closest hit 47.85 → 48.60 ms per pass; profiles/r03g_ab_leaves.txt):
+// the extra tests cost more than the saved steps, so SAH's own leaf decision stays (0).
+#ifndef PT_BVH_FILL_LEAVES
+#define PT_BVH_FILL_LEAVES 0
+#endif
+
 // BVH2 → 4-wide nodes (pt_bvh.h collapse_bvh4) as device float4 rows.  The
 // collapse keeps every path's pushes within the kStackMax-entry traversal stack.
 int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_nodes) {
@@ -910,7 +918,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         pad_box(&bmin[3 * i], &bmax[3 * i]);
     }
     pt::BvhResult tb;
-    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb, 3);   // leaves fit one chunk
+    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb, 3, PT_BVH_FILL_LEAVES != 0);   // leaves fit one chunk
     std::vector<float4> tri_recs(nt * 3), tri_shade(nt * 3);
     const bool want_uv = d->num_textures > 0 && nt > 0;   // texture coordinates only matter with textures
     std::vector<float4> tri_uv(want_uv ? nt * 2 : 0);

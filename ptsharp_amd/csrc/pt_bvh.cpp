@@ -40,9 +40,11 @@ struct Builder {
     std::atomic<int> live_threads{1};
     int max_threads;
     int max_leaf;
+    bool fill_leaves;
 
-    Builder(const float* a, const float* b, int64_t n, std::vector<BvhNode>& out, int threads, int leaf)
-        : pmin(a), pmax(b), cent((size_t)n * 3), idx((size_t)n), nodes(out), max_threads(threads), max_leaf(leaf) {
+    Builder(const float* a, const float* b, int64_t n, std::vector<BvhNode>& out, int threads, int leaf, bool fill)
+        : pmin(a), pmax(b), cent((size_t)n * 3), idx((size_t)n), nodes(out), max_threads(threads), max_leaf(leaf),
+          fill_leaves(fill) {
         for (int64_t i = 0; i < n; i++) {
             idx[(size_t)i] = (uint32_t)i;
             for (int k = 0; k < 3; k++) cent[(size_t)i * 3 + k] = 0.5f * (pmin[i * 3 + k] + pmax[i * 3 + k]);
@@ -73,7 +75,7 @@ struct Builder {
         }
         for (int k = 0; k < 3; k++) { nodes[ni].bmin[k] = bounds.lo[k]; nodes[ni].bmax[k] = bounds.hi[k]; }
         int64_t n = end - begin;
-        if (n <= 1 || depth >= kMaxDepth) { make_leaf(ni, begin, end, depth); return; }
+        if (n <= 1 || depth >= kMaxDepth || (fill_leaves && n <= max_leaf)) { make_leaf(ni, begin, end, depth); return; }
 
         int axis = 0;
         float ext[3];
@@ -157,7 +159,8 @@ struct Builder {
 
 }  // namespace
 
-void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out, int max_leaf) {
+void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out, int max_leaf,
+               bool fill_leaves) {
     out.nodes.clear();
     out.order.clear();
     out.max_depth = 0;
@@ -165,7 +168,7 @@ void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int thre
     if (n <= 0) return;
     if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
     out.nodes.assign((size_t)(2 * n + 2), BvhNode{});
-    Builder b(prim_min, prim_max, n, out.nodes, threads, std::min(std::max(max_leaf, 1), kMaxLeafSize));
+    Builder b(prim_min, prim_max, n, out.nodes, threads, std::min(std::max(max_leaf, 1), kMaxLeafSize), fill_leaves);
     b.build(0, 0, n, 0);
     out.nodes.resize(b.next_pair.load());
     // padding node 1: an empty leaf

@@ -44,8 +44,12 @@ struct BvhResult {
 
 // prim_min/prim_max: [n][3] AABBs.  Builds with up to `threads` host threads; leaves hold
 // at most max_leaf (1..kMaxLeafSize) primitives.
+// fill_leaves: a node of at most max_leaf primitives is always a leaf.  The triangle BVH's leaves
+// are 128-B chunks that one traversal step reads whole (7 loads for 1, 2 or 3 triangles), so a
+// leaf of three costs about what a leaf of one does, and SAH's per-primitive cost (which splits
+// most 3-triangle nodes) only adds steps.
 void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out,
-               int max_leaf = kMaxLeafSize);
+               int max_leaf = kMaxLeafSize, bool fill_leaves = false);
 
 // 4-wide BVH collapsed from the BVH2: one 128-byte node (one cache line) per
 // step of the traversal instead of a 64-byte child pair, so a ray makes about

@@ -100,10 +100,12 @@ enum : uint32_t { D_STRATUM_U = 0, D_STRATUM_V = 1, D_REFLECT = 2, D_RUV_Z = 3, 
                   D_LIGHT = 5, D_SS_RUV_Z = 6, D_SS_RUV_A = 7, D_SS_XY = 8 };
 enum : uint32_t { D_JX = 0, D_JY = 1, D_LENS_ANGLE = 2, D_LENS_RADIUS = 3 };
 
-#ifdef __HIP_DEVICE_COMPILE__
+// PT_DEVICE_SINCOS: the device's reduction and kernels on the host too (tools/sincos_flip_rate.cpp
+// compares them with glibc's sin and cos at the call sites).
+#if defined(__HIP_DEVICE_COMPILE__) || defined(PT_DEVICE_SINCOS)
 // fdlibm's __kernel_sin / __kernel_cos (k_sin.c, k_cos.c: degree-13 / -14 minimax on
 // [-π/4, π/4]) on the reduced argument y0 + y1.
-__device__ __forceinline__ void sincos_kernel(double x, double y, double& s, double& c) {
+PT_HD void sincos_kernel(double x, double y, double& s, double& c) {
     const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
                  S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
     const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
@@ -125,7 +127,7 @@ __device__ __forceinline__ void sincos_kernel(double x, double y, double& s, dou
 // path alone took the shade kernel from 11 to 34 spilled VGPRs.  No large-argument path here:
 // the reduction stays accurate to ~1e-29 absolute for |x| up to ~1e4, far beyond any caller.
 PT_HD void pt_sincos(double x, double* s, double* c) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(PT_LIB_SINCOS)
+#if (defined(__HIP_DEVICE_COMPILE__) || defined(PT_DEVICE_SINCOS)) && !defined(PT_LIB_SINCOS)
     const double hi = 1.5707963267948966, lo = 6.123233995736766e-17, two_over_pi = 0.63661977236758134;
     const double k = rint(x * two_over_pi);
     const double ph = k * hi;

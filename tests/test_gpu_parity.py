@@ -27,6 +27,21 @@ def test_furnace_exact(gpu, engine):
 
 
 @ENGINES
+def test_furnace_negative_albedo(gpu, engine):
+    """A negative colour (legal in the reference's fp64 Colour): every floor pixel's fixed-point sum is
+    negative.  pt_accum.h fix_value converts a total that fits 64 signed bits in one step (ADVICE r02:
+    the two-word form rounded the low word of a negative total to 2^11 ulps, ~6e-11 absolute)."""
+    s, c, smp = scenes.furnace(-0.3)
+    g, gr, o, orr = render_both(s, c, smp, 64, 48, spp=2, passes=2, seed=3, engine=engine)
+    assert gr == orr and np.array_equal(g.N, o.N)
+    floor = o.M[..., 0] < 0
+    assert floor.any() and (~floor).any()
+    assert np.abs(g.M[floor] - o.M[floor]).max() <= 1e-12
+    assert np.array_equal(g.M[~floor], o.M[~floor])
+    assert np.abs(g.V - o.V).max() <= 1e-12
+
+
+@ENGINES
 @pytest.mark.parametrize("fh", [16, 8, 1])
 def test_emitter_exact(gpu, fh, engine):
     s, c, smp = scenes.emitter(fh)
