@@ -146,9 +146,6 @@ constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera sl
 #ifndef PT_SCAN_MOST
 #define PT_SCAN_MOST 1   // lean shade kernels take the SCAN form below 31/32 kept (0: below half, round 1)
 #endif
-#ifndef PT_SCAN_STAGE
-#define PT_SCAN_STAGE 1   // SCAN listing stages the hit records in LDS (round 3); 0: in registers (round 2)
-#endif
 #ifndef PT_SHADE_SCAN
 #define PT_SHADE_SCAN 8    // rows of 256 per SCAN claim: 16 best before claims carried their partial round, 8 since
                            // (C4 5836 / 5885 / 5743 for 16 / 8 / 32; the 1/8 share 5099 / 5208 / 4735)
@@ -880,50 +877,6 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             const uint32_t k0 = s_k0;  // thread 0 rewrites it only after the barriers below
             const bool last = k0 >= n;   // block-uniform: nothing claimed, shade what is held over
             uint32_t total = carry;
-#if PT_SCAN_STAGE
-            if (!last) {
-                // The claim's hit records go to LDS as they arrive, above the held-over list (rows at
-                // carry + j·256 + tid), and are compacted in place row by row: an entry only moves
-                // down (its list position never exceeds its staging position), and a row's writes stay
-                // below the next row's staging.  Holding the rows in registers across the prefix
-                // (round 2) spilled the per-row prefixes to scratch at the kernel's 168-VGPR budget.
-                uint32_t keep = 0;
-#pragma unroll
-                for (int j = 0; j < kShadeScan; j++) {
-                    const uint32_t sl = k0 + (uint32_t)j * 256u + threadIdx.x;
-                    uint4 hv = make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u);
-                    if ((uint32_t)j < rows && sl < n) hv = nt_load(&Q.hits[base + sl]);
-                    const int32_t kind = (int32_t)hv.z;
-                    const bool kp = kind != kDeadKind && (kind >= 0 || !env_black);
-                    keep |= kp ? 1u << j : 0u;
-                    if (kp) s_hit[carry + (uint32_t)j * 256u + threadIdx.x] = hv;
-                    const uint64_t bal = __ballot(kp);
-                    if (lane == 0) s_wcnt[j * 4 + wid] = (uint32_t)__popcll(bal);
-                }
-                __syncthreads();
-#pragma unroll 1
-                for (int j = 0; j < kShadeScan; j++) {
-                    uint32_t before = 0, rowtot = 0;   // kept entries of the waves before this one; the row's
-                    for (int w = 0; w < 4; w++) {
-                        const uint32_t c = s_wcnt[j * 4 + w];
-                        before += w < wid ? c : 0u;
-                        rowtot += c;
-                    }
-                    const bool kp = (keep >> j) & 1u;
-                    const uint64_t bal = __ballot(kp);
-                    uint4 h = make_uint4(0u, 0u, 0u, 0u);
-                    if (kp) h = s_hit[carry + (uint32_t)j * 256u + threadIdx.x];
-                    __syncthreads();   // the row's reads before its writes (a write may land on another entry's source)
-                    if (kp) {
-                        const uint32_t at = total + before + (uint32_t)__popcll(bal & below);
-                        s_list[at] = k0 + (uint32_t)j * 256u + threadIdx.x;
-                        s_hit[at] = h;
-                    }
-                    total += rowtot;
-                }
-                __syncthreads();
-            }
-#else
             if (!last) {
                 uint32_t keep = 0;
                 uint4 hv[kShadeScan];
@@ -958,7 +911,6 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                     }
                 __syncthreads();
             }
-#endif
             const uint32_t full = last ? total : total & ~255u;
             for (uint32_t r = 0; r < full; r += 256u) {   // block-uniform
                 const bool listed = r + threadIdx.x < full;
