@@ -359,6 +359,12 @@ inline void pad_box(float* lo, float* hi) {
 #define PT_BVH_FILL_LEAVES 0
 #endif
 
+// Analytic shapes tested linearly by the refill traversal kernels when there are at most this many
+// (pt_scene.h ana_linear); 0: always through the analytic BVH.
+#ifndef PT_ANA_LINEAR
+#define PT_ANA_LINEAR 8
+#endif
+
 // BVH2 → 4-wide nodes (pt_bvh.h collapse_bvh4) as device float4 rows.  The
 // collapse keeps every path's pushes within the kStackMax-entry traversal stack.
 int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_nodes) {
@@ -1042,6 +1048,18 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         rc = upload(c, lines, &S.lines); if (rc) return rc;
         S.lines_n = (uint32_t)(lines.size() / 8);
         S.tri_node_line0 = (uint32_t)(ana_nodes.size() / 8);
+        if (!tri_nodes.empty()) {   // root box = union of the root node's used child slots (pt_bvh.h layout)
+            const float* w = reinterpret_cast<const float*>(tri_nodes.data());
+            const uint32_t* refs = reinterpret_cast<const uint32_t*>(w + 24);
+            for (int ax = 0; ax < 3; ax++) { S.tri_box[ax] = INFINITY; S.tri_box[3 + ax] = -INFINITY; }
+            for (int k = 0; k < 4; k++) {
+                if (refs[k] == pt::kEmpty4) continue;
+                for (int ax = 0; ax < 3; ax++) {
+                    S.tri_box[ax] = std::min(S.tri_box[ax], w[8 * ax + k]);
+                    S.tri_box[3 + ax] = std::max(S.tri_box[3 + ax], w[8 * ax + 4 + k]);
+                }
+            }
+        }
         S.tri_chunk_line0 = (uint32_t)((ana_nodes.size() + tri_nodes.size()) / 8);
         S.ana_nodes = ana_nodes.empty() ? nullptr : S.lines;
         S.tri_nodes = tri_nodes.empty() ? nullptr : S.lines + 8 * (size_t)S.tri_node_line0;
@@ -1098,6 +1116,10 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     S.full = (d->num_textures > 0 || S.full_geom) ? 1 : 0;
     S.tri_num_nodes = tri_num_nodes;
     S.ana_num_nodes = ana_num_nodes;
+    S.ana_count = (int32_t)na;
+    // C4's floor cube and two light spheres: a linear test of 3 records at refill costs less than a BVH
+    // node step (seven loads through the texture path) and leaf record loads per ray
+    S.ana_linear = (na > 0 && na <= (size_t)PT_ANA_LINEAR && !S.full_geom) ? 1 : 0;
     S.num_planes = (int32_t)plane_scene.size();
     S.num_lights = (int32_t)lights.size();
     for (int k = 0; k < 3; k++) S.env[k] = d->env_color[k];

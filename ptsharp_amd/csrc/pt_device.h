@@ -327,7 +327,16 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         if (t < best.t) { best.t = t; best.kind = KIND_PLANE; best.idx = i; }
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
+    if (S.ana_linear) {   // a few analytic shapes, one by one (as the refill kernels test them; pt_scene.h)
+        for (int p = 0; p < S.ana_count; p++) {
+            if (COUNT) ctr.prims++;
+            int32_t kind;
+            const double t = prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind);
+            if (t < best.t) { best.t = t; best.kind = kind; best.idx = p; }
+        }
+    } else {
+        traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
+    }
     traverse_tri<COUNT, false>(S, o, d, invd, best, stack, ctr);
     return best;
 }
@@ -366,8 +375,16 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr))
+    if (S.ana_linear) {
+        for (int p = 0; p < S.ana_count; p++) {
+            if (COUNT) ctr.prims++;
+            int32_t kind;
+            if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return false;
+        }
+    } else if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack,
+                                                 ctr)) {
         return false;
+    }
     if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return false;
     return true;
 }

@@ -65,6 +65,9 @@ struct DevScene {
     // the cooperative fetch (pt_wavefront.hip coop_line) names any traversal line by a 32-bit index
     const float4* lines;
     uint32_t tri_node_line0, tri_chunk_line0, lines_n;   // lines_n: 128-B lines in `lines`
+    // the triangle BVH's root box (the union of the root node's child boxes): a refill traversal
+    // whose ray misses it skips the triangle phase instead of spending a step on the root node
+    float tri_box[6];          // lo.xyz, hi.xyz
     // planes (unbounded: tested outside the BVHs)
     const float4* planes;      // 2 float4: {point.xyz, mat} {normal.xyz, scene index}
     int32_t num_planes;
@@ -96,6 +99,10 @@ struct DevScene {
     int32_t default_mat;       // `new Material()` (Volume.MaterialAt with no window near)
     int32_t full;              // textures or §8f row 4 shapes present: kernels run their FULL instantiation
     int32_t full_geom;         // §8f row 4 shapes present: the traversal kernels need FULL (textures alone do not)
+    // a few analytic shapes (spheres / cubes only): the per-lane refill kernels test them one by one at
+    // refill, every lane the same record (scalar loads), instead of an analytic-BVH phase
+    int32_t ana_count;         // records in ana_recs
+    int32_t ana_linear;        // 1: test ana_recs linearly in the refill kernels
 };
 
 struct DevCamera {

@@ -440,6 +440,19 @@ __device__ __forceinline__ uint32_t step_line(const DevScene& S, bool has, bool 
     return leaf ? kNoLine : ref;
 }
 
+// Does the ray reach the triangle BVH at all (its root box within tmax)?  A child box lies inside
+// the root box and the fp32 slab arithmetic is monotone in the bounds, so a miss here is a miss of
+// every root child: skipping the root step changes no hit, only the step count.
+#ifndef PT_ROOT_CULL
+#define PT_ROOT_CULL 1
+#endif
+__device__ __forceinline__ bool tri_reach(const DevScene& S, v3 o, v3 invd, float tmax) {
+    if (S.tri_num_nodes <= 0) return false;
+    if (!PT_ROOT_CULL) return true;
+    return slab1(S.tri_box[0], S.tri_box[3], S.tri_box[1], S.tri_box[4], S.tri_box[2], S.tri_box[5], o, invd, tmax) !=
+           __int_as_float(0x7f800000);
+}
+
 #ifndef PT_REFILL_IDLE
 #define PT_REFILL_IDLE 40   // closest hit: 8 / 16 / 24 / 32 / 40 / 48 measured on C4, 40 best
 #endif
@@ -480,7 +493,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
     uint32_t kept = 0;
     const float inf = __int_as_float(0x7f800000);
     bool has = false, tri = false, more = true;
-    uint32_t i = 0, ref = 0;
+    uint32_t i = 0, ref = 0;   // i: the ray's slot; bit 31 set = the ray misses the triangle BVH's root box
     int sp = 0;
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
     double bt = kHitInf;
@@ -488,7 +501,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
     float tmax = 0.f;
     auto finish = [&]() {
         unsigned long long tb = (unsigned long long)__double_as_longlong(bt);
-        hit_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
+        hit_store(&Q.hits[i & 0x7FFFFFFFu], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
         kept += (bkind >= 0 || !env_black) ? 1u : 0u;
         has = false;
     };
@@ -528,11 +541,21 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                         const double t = isect_plane(v3{pa.x, pa.y, pa.z}, v3{pb.x, pb.y, pb.z}, o, d);
                         if (t < bt) { bt = t; bkind = KIND_PLANE; bidx = p; }
                     }
+                    if (S.ana_linear) {   // a few analytic shapes: every lane the same record (one line per load)
+                        for (int p = 0; p < S.ana_count; p++) {
+                            if (COUNT) ctr.prims++;
+                            int32_t kind;
+                            const double t = prim_t<false, false>(S, S.ana_recs, (uint32_t)p, o, d, kind);
+                            if (t < bt) { bt = t; bkind = kind; bidx = p; }
+                        }
+                    }
                     tmax = tmax_bound(bt);
                     sp = 0;
                     ref = 0;
-                    tri = S.ana_num_nodes <= 0;
-                    if (tri && S.tri_num_nodes <= 0) finish();
+                    // tested at the refill's bound (planes only), kept as a bit of i: no register for it
+                    if (!tri_reach(S, o, invd, tmax)) i |= 0x80000000u;
+                    tri = S.ana_linear || S.ana_num_nodes <= 0;
+                    if (tri && (i >> 31)) finish();
                 }
             }
         }
@@ -608,7 +631,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
             if (sp > 0) {
                 sp--;
                 ref = stack.get(sp);
-            } else if (!tri && S.tri_num_nodes > 0) {
+            } else if (!tri && !(i >> 31)) {
                 tri = true;
                 ref = 0;
             } else {
@@ -1060,13 +1083,24 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                             const float4 pa = S.planes[2 * p], pb = S.planes[2 * p + 1];
                             if (isect_plane(v3{pa.x, pa.y, pa.z}, v3{pb.x, pb.y, pb.z}, o, d) < tl) run = false;
                         }
-                        tri = S.ana_num_nodes <= 0;
+                        if (S.ana_linear)   // the light itself gives t == tl, never nearer
+                            for (int p = 0; p < S.ana_count; p++) {
+                                if (COUNT) ctr.prims++;
+                                int32_t kind;
+                                if (prim_t<false, false>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) run = false;
+                            }
+                        tri = S.ana_linear || S.ana_num_nodes <= 0;
                     }
                     tmax = tmax_bound(tl);
                     sp = 0;
                     ref = 0;
+                    if (run && tri && !tri_reach(S, o, invd, tmax)) {   // nothing of the mesh before the light
+                        run = false;
+                        Q.n_lit[qo][i] = phantom ? 0 : 1;
+                    } else if (!run) {
+                        Q.n_lit[qo][i] = 0;
+                    }
                     has = run;
-                    if (!run) Q.n_lit[qo][i] = 0;
 #if PT_SHADOW_HELP
                     s_help[threadIdx.x] = 0u;
 #endif
@@ -1198,7 +1232,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
             } else if (helper) {   // a donated subtree done, nothing nearer than the light in it
                 has = false;
                 atomicSub(&s_help[root], 1u);
-            } else if (!tri && S.tri_num_nodes > 0) {
+            } else if (!tri && tri_reach(S, o, invd, tmax)) {
                 tri = true;
                 ref = 0;
             } else if (s_help[root] == 0u) {   // no primitive nearer than the light: lit (a phantom light never is)
@@ -1216,7 +1250,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
             if (sp > 0) {
                 sp--;
                 ref = stack.get(sp);
-            } else if (!tri && S.tri_num_nodes > 0) {
+            } else if (!tri && tri_reach(S, o, invd, tmax)) {
                 tri = true;
                 ref = 0;
             } else {   // no primitive nearer than the light: lit (a phantom light never is)
