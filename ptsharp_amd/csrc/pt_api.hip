@@ -377,6 +377,69 @@ int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_no
     return PT_OK;
 }
 
+// ---- PT_NODE16 node lines (pt_device.h node4_test): child bounds as binary16 offsets from the node's
+// origin (the per-axis minimum of its children's lower bounds), rounded outward under the kernels' own
+// fp32 arithmetic `origin + (float)half`, so each decoded child box still contains its subtree.
+float half_to_float(uint16_t h) {
+    const uint32_t e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+    float v = e == 0 ? std::ldexp((float)m, -24) : e == 31 ? (m ? NAN : INFINITY) : std::ldexp((float)(m | 0x400u), (int)e - 25);
+    return (h & 0x8000u) ? -v : v;
+}
+// the largest non-negative half h (finite) with fl32(origin + h) <= bound
+uint16_t half_lo(float origin, float bound) {
+    uint32_t lo = 0, hi = 0x7BFFu;   // fl(origin + 0) = origin <= bound
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if ((float)(origin + half_to_float((uint16_t)mid)) <= bound) lo = mid; else hi = mid - 1;
+    }
+    return (uint16_t)lo;
+}
+// the smallest non-negative half h with fl32(origin + h) >= bound (+inf if no finite half reaches it)
+uint16_t half_hi(float origin, float bound) {
+    if (!((float)(origin + half_to_float(0x7BFFu)) >= bound)) return 0x7C00u;
+    uint32_t lo = 0, hi = 0x7BFFu;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) / 2;
+        if ((float)(origin + half_to_float((uint16_t)mid)) >= bound) hi = mid; else lo = mid + 1;
+    }
+    return (uint16_t)lo;
+}
+// Old layout (pt_bvh.h: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4]) → PT_NODE16 layout, in place.
+int encode_nodes16(std::vector<float4>& nodes) {
+    if (!PT_NODE16) return PT_OK;
+    const size_t nn = nodes.size() / 8;
+    for (size_t n = 0; n < nn; n++) {
+        float* w = reinterpret_cast<float*>(&nodes[8 * n]);
+        uint32_t refs[4];
+        std::memcpy(refs, w + 24, sizeof refs);
+        float org[3];
+        for (int ax = 0; ax < 3; ax++) {
+            org[ax] = INFINITY;
+            for (int k = 0; k < 4; k++)
+                if (refs[k] != pt::kEmpty4) org[ax] = std::min(org[ax], w[8 * ax + k]);
+            if (!std::isfinite(org[ax]))
+                return fail(PT_ERR_UNSUPPORTED, "BVH node with a non-finite bound (binary16 node encoding)");
+        }
+        uint32_t out[32] = {0u};
+        std::memcpy(&out[0], org, sizeof org);
+        out[3] = refs[0]; out[4] = refs[1]; out[5] = refs[2]; out[6] = refs[3];
+        for (int ax = 0; ax < 3; ax++) {
+            uint16_t hl[4] = {0, 0, 0, 0}, hh[4] = {0, 0, 0, 0};
+            for (int k = 0; k < 4; k++) {
+                if (refs[k] == pt::kEmpty4) continue;
+                hl[k] = half_lo(org[ax], w[8 * ax + k]);
+                hh[k] = half_hi(org[ax], w[8 * ax + 4 + k]);
+            }
+            out[8 + 4 * ax + 0] = (uint32_t)hl[0] | ((uint32_t)hl[1] << 16);
+            out[8 + 4 * ax + 1] = (uint32_t)hl[2] | ((uint32_t)hl[3] << 16);
+            out[8 + 4 * ax + 2] = (uint32_t)hh[0] | ((uint32_t)hh[1] << 16);
+            out[8 + 4 * ax + 3] = (uint32_t)hh[2] | ((uint32_t)hh[3] << 16);
+        }
+        std::memcpy(w, out, sizeof out);
+    }
+    return PT_OK;
+}
+
 // Triangle leaf chunks: every leaf ref of the collapsed triangle BVH4 is re-pointed at a
 // 128-B chunk holding its (<= 3) triangles' {v1, e1, e2} (27 floats, the tri_recs fields)
 // and, in word 27, the first triangle's record position.  A traversal step then loads the
@@ -860,6 +923,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         std::vector<float4> nodes;
         int32_t nn = 0;
         if ((rc = pack_nodes(bb, nodes, nn))) return rc;
+        if ((rc = encode_nodes16(nodes))) return rc;
         pt::DevBlas B{(int32_t)(blas_nodes.size() / 8), nn, (int32_t)(blas_recs.size() / 3), 0};
         blas_nodes.insert(blas_nodes.end(), nodes.begin(), nodes.end());
         for (int t = 0; t < n; t++) {
@@ -953,6 +1017,20 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     if ((rc = pack_nodes(tb, tri_nodes, tri_num_nodes))) return rc;
     std::vector<float4> tri_chunks;
     if ((rc = make_leaf_chunks(tri_nodes, tri_recs, tri_chunks))) return rc;
+    float tri_box[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (!tri_nodes.empty()) {   // root box = union of the root node's used child slots (pt_bvh.h layout)
+        const float* w = reinterpret_cast<const float*>(tri_nodes.data());
+        const uint32_t* refs = reinterpret_cast<const uint32_t*>(w + 24);
+        for (int ax = 0; ax < 3; ax++) { tri_box[ax] = INFINITY; tri_box[3 + ax] = -INFINITY; }
+        for (int k = 0; k < 4; k++) {
+            if (refs[k] == pt::kEmpty4) continue;
+            for (int ax = 0; ax < 3; ax++) {
+                tri_box[ax] = std::min(tri_box[ax], w[8 * ax + k]);
+                tri_box[3 + ax] = std::max(tri_box[3 + ax], w[8 * ax + 4 + k]);
+            }
+        }
+    }
+    if ((rc = encode_nodes16(tri_nodes))) return rc;
 
     // --- analytic BVH (spheres, cubes, SDF shapes, volumes, transformed shapes)
     const size_t na = ana_kind.size();
@@ -993,6 +1071,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     std::vector<float4> ana_nodes;
     int32_t ana_num_nodes = 0;
     if ((rc = pack_nodes(ab, ana_nodes, ana_num_nodes))) return rc;
+    if ((rc = encode_nodes16(ana_nodes))) return rc;
 
     // --- planes
     std::vector<float4> planes(plane_scene.size() * 2);
@@ -1038,6 +1117,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     }
 
     pt::DevScene S{};
+    std::memcpy(S.tri_box, tri_box, sizeof tri_box);
     {   // the traversal lines: [ana_nodes | tri_nodes | tri_chunks], 8 float4 per node / chunk
         std::vector<float4> lines;
         lines.reserve(ana_nodes.size() + tri_nodes.size() + tri_chunks.size());
@@ -1048,18 +1128,6 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         rc = upload(c, lines, &S.lines); if (rc) return rc;
         S.lines_n = (uint32_t)(lines.size() / 8);
         S.tri_node_line0 = (uint32_t)(ana_nodes.size() / 8);
-        if (!tri_nodes.empty()) {   // root box = union of the root node's used child slots (pt_bvh.h layout)
-            const float* w = reinterpret_cast<const float*>(tri_nodes.data());
-            const uint32_t* refs = reinterpret_cast<const uint32_t*>(w + 24);
-            for (int ax = 0; ax < 3; ax++) { S.tri_box[ax] = INFINITY; S.tri_box[3 + ax] = -INFINITY; }
-            for (int k = 0; k < 4; k++) {
-                if (refs[k] == pt::kEmpty4) continue;
-                for (int ax = 0; ax < 3; ax++) {
-                    S.tri_box[ax] = std::min(S.tri_box[ax], w[8 * ax + k]);
-                    S.tri_box[3 + ax] = std::max(S.tri_box[3 + ax], w[8 * ax + 4 + k]);
-                }
-            }
-        }
         S.tri_chunk_line0 = (uint32_t)((ana_nodes.size() + tri_nodes.size()) / 8);
         S.ana_nodes = ana_nodes.empty() ? nullptr : S.lines;
         S.tri_nodes = tri_nodes.empty() ? nullptr : S.lines + 8 * (size_t)S.tri_node_line0;

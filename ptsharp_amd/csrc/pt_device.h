@@ -158,6 +158,54 @@ __device__ __forceinline__ void cswap(float& ka, uint32_t& va, float& kb, uint32
     va = v;
 }
 
+// The four child slabs of a BVH4 node line (pt_bvh.h; PT_NODE16: pt_api.hip encode_nodes16) →
+// entry distances k0..k3 (+inf = miss or empty slot) and child refs v0..v3.
+//   PT_NODE16 = 0: 7 pieces, lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4] (round 2).
+//   PT_NODE16 = 1: 5 pieces, {origin.xyz, ref0} {ref1, ref2, ref3, -} and the child bounds as
+//   binary16 offsets from the origin, x / y / z rows of {lo c0|c1, lo c2|c3, hi c0|c1, hi c2|c3};
+//   bound = origin + offset in fp32, rounded outward on the host under this same arithmetic, so
+//   every child box contains its subtree (a step reads 80 B of its line instead of 112 B).
+//   Measured slower (C4 6124 → 5825 Mrays/s, closest hit 46.1 → 49.9 ms per pass; the decode's
+//   24 conversions and adds per node cost more than the two loads it saves;
+//   profiles/r03n_ab_node16.txt), so the default stays 0.
+#ifndef PT_NODE16
+#define PT_NODE16 0
+#endif
+constexpr int kNodePieces = PT_NODE16 ? 5 : 7;
+__device__ __forceinline__ float h16lo(float w) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(__float_as_uint(w) & 0xFFFFu));
+}
+__device__ __forceinline__ float h16hi(float w) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(__float_as_uint(w) >> 16));
+}
+__device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, float4 q3, float4 q4, float4 q5, float4 q6,
+                                           v3 o, v3 invd, float tmax, float& k0, float& k1, float& k2, float& k3,
+                                           uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& v3r) {
+#if PT_NODE16
+    (void)q5; (void)q6;
+    const float ox = q0.x, oy = q0.y, oz = q0.z;
+    k0 = slab1(ox + h16lo(q2.x), ox + h16lo(q2.z), oy + h16lo(q3.x), oy + h16lo(q3.z), oz + h16lo(q4.x), oz + h16lo(q4.z),
+               o, invd, tmax);
+    k1 = slab1(ox + h16hi(q2.x), ox + h16hi(q2.z), oy + h16hi(q3.x), oy + h16hi(q3.z), oz + h16hi(q4.x), oz + h16hi(q4.z),
+               o, invd, tmax);
+    k2 = slab1(ox + h16lo(q2.y), ox + h16lo(q2.w), oy + h16lo(q3.y), oy + h16lo(q3.w), oz + h16lo(q4.y), oz + h16lo(q4.w),
+               o, invd, tmax);
+    k3 = slab1(ox + h16hi(q2.y), ox + h16hi(q2.w), oy + h16hi(q3.y), oy + h16hi(q3.w), oz + h16hi(q4.y), oz + h16hi(q4.w),
+               o, invd, tmax);
+    v0 = __float_as_uint(q0.w); v1 = __float_as_uint(q1.x); v2 = __float_as_uint(q1.y); v3r = __float_as_uint(q1.z);
+#else
+    k0 = slab1(q0.x, q1.x, q2.x, q3.x, q4.x, q5.x, o, invd, tmax);
+    k1 = slab1(q0.y, q1.y, q2.y, q3.y, q4.y, q5.y, o, invd, tmax);
+    k2 = slab1(q0.z, q1.z, q2.z, q3.z, q4.z, q5.z, o, invd, tmax);
+    k3 = slab1(q0.w, q1.w, q2.w, q3.w, q4.w, q5.w, o, invd, tmax);
+    v0 = __float_as_uint(q6.x); v1 = __float_as_uint(q6.y); v2 = __float_as_uint(q6.z); v3r = __float_as_uint(q6.w);
+#endif
+    const float inf = __int_as_float(0x7f800000);
+    if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
+    if (v2 == kEmpty4) k2 = inf;
+    if (v3r == kEmpty4) k3 = inf;
+}
+
 // Stack-based BVH4 traversal (node layout: pt_bvh.h, collapse_bvh4).  A node is
 // one 128-byte line fetched with seven independent 16-byte loads; the four
 // child slabs are tested, hits sorted nearest-first with a 5-comparator network,
@@ -175,18 +223,14 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
     for (;;) {
         if (!(ref & 0x80000000u)) {
             const float4* c = nodes + 8 * (size_t)ref;
-            const float4 lx = c[0], hx = c[1], ly = c[2], hy = c[3], lz = c[4], hz = c[5];
-            const uint4 rf = *reinterpret_cast<const uint4*>(c + 6);
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4];
+            const float4 q5 = kNodePieces > 5 ? c[5] : z4, q6 = kNodePieces > 6 ? c[6] : z4;
             if (COUNT) ctr.nodes++;
             const float inf = __int_as_float(0x7f800000);
-            float k0 = slab1(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, o, invd, tmax);
-            float k1 = slab1(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, o, invd, tmax);
-            float k2 = slab1(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, o, invd, tmax);
-            float k3 = slab1(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, o, invd, tmax);
-            uint32_t v0 = rf.x, v1 = rf.y, v2 = rf.z, v3r = rf.w;
-            if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
-            if (v2 == kEmpty4) k2 = inf;
-            if (v3r == kEmpty4) k3 = inf;
+            float k0, k1, k2, k3;
+            uint32_t v0, v1, v2, v3r;
+            node4_test(q0, q1, q2, q3, q4, q5, q6, o, invd, tmax, k0, k1, k2, k3, v0, v1, v2, v3r);
             cswap(k0, v0, k1, v1);
             cswap(k2, v2, k3, v3r);
             cswap(k0, v0, k2, v2);
@@ -221,6 +265,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
 // re-splits them along the consumers' 12-B vertex fields into unaligned pieces).
 #define PT_PIN4(q) asm volatile("" : "+v"((q).x), "+v"((q).y), "+v"((q).z), "+v"((q).w))
 
+
 // The triangles of a leaf chunk (pt_api.hip make_leaf_chunks): word 0 = the first triangle
 // record, triangle k = words 1 + 9k .. 9 + 9k as {v1, e1, e2}; a0..a2 is the first, b the
 // second, c the third (shifted down after each test).  A chunk of cnt triangles is read with its
@@ -250,15 +295,9 @@ __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 i
         if (!leaf) {
             if (COUNT) ctr.nodes++;
             const float inf = __int_as_float(0x7f800000);
-            float k0 = slab1(q0.x, q1.x, q2.x, q3.x, q4.x, q5.x, o, invd, tmax);
-            float k1 = slab1(q0.y, q1.y, q2.y, q3.y, q4.y, q5.y, o, invd, tmax);
-            float k2 = slab1(q0.z, q1.z, q2.z, q3.z, q4.z, q5.z, o, invd, tmax);
-            float k3 = slab1(q0.w, q1.w, q2.w, q3.w, q4.w, q5.w, o, invd, tmax);
-            uint32_t v0 = __float_as_uint(q6.x), v1 = __float_as_uint(q6.y), v2 = __float_as_uint(q6.z),
-                     v3r = __float_as_uint(q6.w);
-            if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
-            if (v2 == kEmpty4) k2 = inf;
-            if (v3r == kEmpty4) k3 = inf;
+            float k0, k1, k2, k3;
+            uint32_t v0, v1, v2, v3r;
+            node4_test(q0, q1, q2, q3, q4, q5, q6, o, invd, tmax, k0, k1, k2, k3, v0, v1, v2, v3r);
             cswap(k0, v0, k1, v1);
             cswap(k2, v2, k3, v3r);
             cswap(k0, v0, k2, v2);

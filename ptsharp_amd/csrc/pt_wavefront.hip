@@ -375,6 +375,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 #ifndef PT_COOP
 #define PT_COOP 0            // 1: the per-lane refill kernels fetch lines cooperatively (measured slower)
 #endif
+static_assert(!(PT_COOP && PT_NODE16), "the cooperative fetch stages the 7-piece node layout only");
 #ifndef PT_COOP_STAGE
 #define PT_COOP_STAGE 32     // lines staged in LDS per wave per pass (64: one pass, 32: two)
 #endif
@@ -575,22 +576,18 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
             const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
                                           : (leaf ? 0u : ref));
             q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
-            q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u];
+            q4 = S.lines[at + 4u];
+            if (kNodePieces > 5 || (tri && leaf)) { q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; }   // a chunk's last two
+            else { q5 = make_float4(0.f, 0.f, 0.f, 0.f); q6 = q5; }
         }
 #endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
         bool pop = true;
         if (!leaf) {
             if (COUNT) ctr.nodes++;
-            float k0 = slab1(q0.x, q1.x, q2.x, q3.x, q4.x, q5.x, o, invd, tmax);
-            float k1 = slab1(q0.y, q1.y, q2.y, q3.y, q4.y, q5.y, o, invd, tmax);
-            float k2 = slab1(q0.z, q1.z, q2.z, q3.z, q4.z, q5.z, o, invd, tmax);
-            float k3 = slab1(q0.w, q1.w, q2.w, q3.w, q4.w, q5.w, o, invd, tmax);
-            uint32_t v0 = __float_as_uint(q6.x), v1 = __float_as_uint(q6.y), v2 = __float_as_uint(q6.z),
-                     v3r = __float_as_uint(q6.w);
-            if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
-            if (v2 == kEmpty4) k2 = inf;
-            if (v3r == kEmpty4) k3 = inf;
+            float k0, k1, k2, k3;
+            uint32_t v0, v1, v2, v3r;
+            node4_test(q0, q1, q2, q3, q4, q5, q6, o, invd, tmax, k0, k1, k2, k3, v0, v1, v2, v3r);
             cswap(k0, v0, k1, v1);
             cswap(k2, v2, k3, v3r);
             cswap(k0, v0, k2, v2);
@@ -1173,22 +1170,18 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
             const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
                                           : (leaf ? 0u : ref));
             q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
-            q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u];
+            q4 = S.lines[at + 4u];
+            if (kNodePieces > 5 || (tri && leaf)) { q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; }   // a chunk's last two
+            else { q5 = make_float4(0.f, 0.f, 0.f, 0.f); q6 = q5; }
         }
 #endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
         bool pop = true, blocked = false;
         if (!leaf) {
             if (COUNT) ctr.nodes++;
-            float k0 = slab1(q0.x, q1.x, q2.x, q3.x, q4.x, q5.x, o, invd, tmax);
-            float k1 = slab1(q0.y, q1.y, q2.y, q3.y, q4.y, q5.y, o, invd, tmax);
-            float k2 = slab1(q0.z, q1.z, q2.z, q3.z, q4.z, q5.z, o, invd, tmax);
-            float k3 = slab1(q0.w, q1.w, q2.w, q3.w, q4.w, q5.w, o, invd, tmax);
-            uint32_t v0 = __float_as_uint(q6.x), v1 = __float_as_uint(q6.y), v2 = __float_as_uint(q6.z),
-                     v3r = __float_as_uint(q6.w);
-            if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
-            if (v2 == kEmpty4) k2 = inf;
-            if (v3r == kEmpty4) k3 = inf;
+            float k0, k1, k2, k3;
+            uint32_t v0, v1, v2, v3r;
+            node4_test(q0, q1, q2, q3, q4, q5, q6, o, invd, tmax, k0, k1, k2, k3, v0, v1, v2, v3r);
             cswap(k0, v0, k1, v1);
             cswap(k2, v2, k3, v3r);
             cswap(k0, v0, k2, v2);
