@@ -48,6 +48,14 @@ METRIC = "Msamples/s (rays×bounces/s) at 1920×1080×1024spp; PSNR vs C# ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2 (per-XCD L2s, aggregate)
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md (FP32 vector peak)
+# FP64 vector peak: half the FP32 rate (a wave64 fp64 FMA issues over 4 cycles against 2 for
+# fp32, MI355X_MICROARCH.md "issue cost"; AMD's MI355X specification: 78.6 TFLOP/s)
+FP64_PEAK_TFLOPS = 78.6
+# C5 march steps (algorithmic fp64 flops): one Volume.Sample of Volume.Intersect (Volume.cs:73-131:
+# the coordinate maps 10, seven trilinear lerps 28, the window test 2, the step position 6) and one
+# SDF evaluation of SDFShape.Intersect (SDF.cs:32-76, the C5 torus: TransformSDF's MulPosition 18,
+# TorusSDF's two LengthN 14 + 2, the step 3 + position 6)
+F_VOX, F_SDF = 46, 43
 # C2 flops: slab tests of a BVH4 node's four boxes, a primitive test (gopher3:
 # two cubes ≈30, three spheres ≈14 → 22 on average), and the shading of a closest hit
 F_NODE, F_PRIM, F_SHADE = 80, 22, 60
@@ -56,7 +64,13 @@ WORKLOADS = {
     "c3": "C3: 69,451-triangle mesh in Example.bunny's scene, 1920x1080, NewSampler(4,4) SpecularModeFirst",
     "c2": "C2: gopher 3-sphere scene (Example.cs:1542-1564, mesh replaced by two spheres), 1920x1080, "
           "NewSampler(16,16), no triangle BVH",
+    "c5": "C5: mixed scene (the C4 1M-triangle frame + SDF torus + voxel Volume + environment texture), "
+          "3840x2160, RenderParallel with AdaptiveSamples",
 }
+# per-workload defaults of --steps / --warmup / --spp / --width / --height / --adaptive: C5's 4K pass
+# with AdaptiveSamples 32 traces 33 camera samples per pixel (≈5 G rays) per step
+DEFAULTS = {"c5": dict(steps=2, warmup=1, spp=1, width=3840, height=2160, adaptive=32)}
+DEFAULT = dict(steps=64, warmup=2, spp=16, width=1920, height=1080, adaptive=0)
 
 # Algorithmic bytes per unit: per ray 112 B per 4-wide BVH node
 # fetched (four child boxes of 24 B + four 4-B child refs), 36 B per primitive
@@ -137,11 +151,13 @@ def _gather_check(r, dist, rank, world, mine):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=64)
-    p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--spp", type=int, default=16, help="samples per pixel per step (pass)")
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default 64; c5: 2)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2; c5: 1)")
+    p.add_argument("--spp", type=int, default=None, help="samples per pixel per step (pass; default 16, c5: 1)")
+    p.add_argument("--width", type=int, default=None, help="default 1920 (c5: 3840)")
+    p.add_argument("--height", type=int, default=None, help="default 1080 (c5: 2160)")
+    p.add_argument("--adaptive", type=int, default=None,
+                   help="Renderer.AdaptiveSamples (Renderer.cs:340-410; default 0, c5: 32 as Example.cs:355,412)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     p.add_argument("--tris", type=int, default=None, help="mesh triangles (default: 1,000,000 for c4, 69,451 for c3)")
     p.add_argument("--seed", type=int, default=1234)
@@ -157,7 +173,11 @@ def parse():
     p.add_argument("--shard", default=None, metavar="K/N",
                    help="render only rank K's tiles of an N-way split, in this one process (profiling the "
                         "per-rank workload of an N-GPU run on one GPU; value then counts this shard only)")
-    return p.parse_args()
+    a = p.parse_args()
+    for k, v in DEFAULTS.get(a.workload, DEFAULT).items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 def main():
@@ -185,8 +205,9 @@ def main():
     if a.workload == "c2":
         scene, camera, sampler = scenes.gopher3()
     else:
+        frame = scenes.mixed if a.workload == "c5" else scenes.bunny_frame
         if a.tris is None:
-            a.tris = 1_000_000 if a.workload == "c4" else 69_451
+            a.tris = 69_451 if a.workload == "c3" else 1_000_000
         if a.mesh_source == "obj":
             # Example.bunny loads its mesh with OBJ.Load (Example.cs:1088): the seeded mesh is written as
             # an OBJ file and read back through pt_obj_load (OBJ.cs's quirks), as SURVEY.md §8d specifies
@@ -204,9 +225,9 @@ def main():
             obj_info = {"obj_bytes": size, "obj_write_s": round(tw, 3), "obj_load_s": round(tl, 3),
                    "obj_triangles": len(mesh.v1)}
             raw = {k: getattr(mesh, k).copy() for k in ("v1", "v2", "v3", "n1", "n2", "n3", "t1", "t2", "t3")}
-            scene, camera, sampler = scenes.bunny_frame(a.tris, seed=a.seed, mesh=mesh)
+            scene, camera, sampler = frame(a.tris, seed=a.seed, mesh=mesh)
         else:
-            scene, camera, sampler = scenes.bunny_frame(a.tris, seed=a.seed)
+            scene, camera, sampler = frame(a.tris, seed=a.seed)
     scene.Compile()
     t_scene = time.perf_counter() - t_scene
     if obj_info is not None:   # the OBJ round trip is exact: the loaded Triangle[] is the generator's, bit for bit
@@ -218,6 +239,7 @@ def main():
     W, H = a.width, a.height
     r = Renderer.NewRenderer(scene, camera, sampler, W, H, True, device=local)
     r.SamplesPerPixel = a.spp
+    r.AdaptiveSamples = a.adaptive
     r.Seed = a.seed
     r.Engine = {"auto": 0, "mega": 1, "wave": 2}[a.engine]
     if a.shard:
@@ -244,9 +266,16 @@ def main():
     # closest-hit and shadow kernels the library runs on this scene: per-lane refill
     # (k_wf_*_lanes) above 64 triangle-BVH nodes (pt_wavefront.hip kLanesMinNodes); the bench scene's
     # analytic BVH (floor cube, two light spheres) is one node
+    # (SDF shapes, volumes or transformed shapes: the FULL instantiations, pt_wavefront.hip depth_loop)
+    fl = scene.Compile()
+    fullg = any(fl.counts_ext[1:4])
+    full = fullg or len(fl.texture_list) > 0 or fl.env_texture >= 0
     lanes = st.bvh_nodes - 1 > 64
-    trace_name = "k_wf_trace_lanes<false>" if lanes else "k_wf_trace<false, false>"
-    shadow_name = "k_wf_shadow_lanes<false>" if lanes else "k_wf_shadow<false, false>"
+    trace_name = ("k_wf_trace<false, true>" if fullg else "k_wf_trace_lanes<false>" if lanes
+                  else "k_wf_trace<false, false>")
+    shadow_name = ("k_wf_shadow<false, true>" if fullg else "k_wf_shadow_lanes<false>" if lanes
+                   else "k_wf_shadow<false, false>")
+    shade_name = "k_wf_shade<false, true, *>" if full else "k_wf_shade<false, false, *>"
 
     # Passes per call: a rank's 1/N share of the frame is batched N passes per call (the Buffer is
     # the one separate passes leave, bit for bit), so every launch sees a whole frame's worth of
@@ -352,10 +381,13 @@ def main():
         return
 
     value = total_rays / elapsed / 1e6
+    # camera samples traced per pixel per step: the pass' own, then AdaptiveSamples (Renderer.cs:355-372;
+    # its second loop only fills pixelVariances, which nothing reads, and is not traced: DESIGN.md §1a)
+    cam_spp = a.spp + a.adaptive
     # kernel names as rocprofv3 reports them (template arguments <COUNT, FULL>; the shade
     # class times both of its forms <COUNT, FULL, SCAN>, one of which returns at once; the
     # closest-hit class is k_wf_trace_lanes<COUNT> on triangle scenes)
-    names = ["k_wf_camera", trace_name, "k_wf_shade<false, false, *>", shadow_name,
+    names = ["k_wf_camera", trace_name, shade_name, shadow_name,
              "k_wf_finalize", "k_render_pass<false, false>", "k_wf_nee_accum", "-"]
     # the closest-hit kernel is the dominant one by design (on a multi-GPU shard the shadow
     # passes run beside it on a second stream, so their event spans overlap it)
@@ -398,18 +430,20 @@ def main():
         "dtype": "f32/f64",
         "data": ("synthetic (seeded displaced-sphere mesh" + (", written as OBJ and loaded through pt_obj_load"
                                                                if obj_info else "")
+                 + ("; seeded environment texture, SDF torus and 32x32x16 voxel Volume" if a.workload == "c5" else "")
                  + "; no model assets ship with the reference)") if a.workload != "c2"
         else "synthetic (analytic gopher3 scene)",
         "config": {
             "workload": WORKLOADS[a.workload],
             "width": W, "height": H, "spp_per_step": a.spp, "total_spp": a.spp * a.steps,
+            "adaptive_samples": a.adaptive,
             "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}" + (f" shard {a.shard}" if a.shard else "")
             + (f" (rehearsal: {world} ranks on {ndev.value} GPU(s))" if shared else "")
             + (f", gather {gather}" if gather else ""),
             "gather_check": gather_check,
             "passes_per_call": ppc,
-            "camera_samples_per_s": round(W * H * a.spp * a.steps / elapsed, 1),
-            "rays_per_camera_sample": round(total_rays / (W * H * a.spp * a.steps), 3),
+            "camera_samples_per_s": round(W * H * cam_spp * a.steps / elapsed, 1),
+            "rays_per_camera_sample": round(total_rays / (W * H * cam_spp * a.steps), 3),
             "shadow_ray_fraction": round(ctr.shadow_rays / max(ctr.rays, 1), 4),
             "lit_shadow_rays_per_step": int(ctr.lit_shadow_rays), "accum_runs_per_step": int(ctr.accum_runs),
             "engine": a.engine, "scene_build_s": round(t_scene, 3), "bvh_build_ms": round(build_ms, 1),
@@ -439,6 +473,26 @@ def main():
             "pass_achieved_gbs": round(bytes_all / max(ctr.rays, 1) * rays / (kernel_ms * 1e-3) / 1e9, 2),
         },
     }
+
+    if a.workload == "c5":
+        # C5: the marches (Volume.Intersect's fixed 1/512 steps, SDFShape's sphere tracing) are fp64
+        # scalar work: the pass' algorithmic flops (BVH nodes and primitive tests in fp32 as C2's,
+        # march steps in fp64) over the whole pass' kernel time, against the FP64 vector peak (the
+        # binding one for the steps that dominate), the dominant kernel and the step counts beside it
+        fl_ray = (F_NODE * ctr.nodes_visited + F_PRIM * ctr.prims_tested + F_SHADE * ctr.shading_fetches
+                  + F_VOX * ctr.volume_samples + F_SDF * ctr.sdf_evals) / max(ctr.rays, 1)
+        tflops = fl_ray * rays / (kernel_ms * 1e-3) / 1e12
+        out["roofline"] = {
+            "bound": "valu", "kernel": "whole pass", "achieved": round(tflops, 4), "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(tflops / FP64_PEAK_TFLOPS, 6), "traffic": None,
+            "flops_per_ray": round(fl_ray, 2),
+            "volume_samples_per_ray": round(ctr.volume_samples / max(ctr.rays, 1), 3),
+            "sdf_evals_per_ray": round(ctr.sdf_evals / max(ctr.rays, 1), 3),
+            "nodes_per_ray": round(ctr.nodes_visited / max(ctr.rays, 1), 3),
+            "dominant_kernel": names[dom], "dominant_kernel_ms_per_step": round(float(kms[dom]) / a.steps, 3),
+            "flop_model": f"{F_NODE}/BVH4 node, {F_PRIM}/primitive test, {F_SHADE}/shading fetch (fp32), "
+                          f"{F_VOX}/Volume.Sample, {F_SDF}/SDF evaluation (fp64)",
+        }
 
     if a.workload == "c2":
         # C2 is priced in flops against the FP32 vector peak (whole pass), with the

@@ -146,6 +146,7 @@ namespace PTSharpCore
         {
             public ulong rays, nodes_visited, prims_tested, shading_fetches, shadow_rays, shadow_nodes, shadow_prims;
             public ulong lit_shadow_rays, accum_runs;
+            public ulong volume_samples, sdf_evals;   // Volume.Intersect / SDFShape.Intersect march steps
         }
 
         [StructLayout(LayoutKind.Sequential)]

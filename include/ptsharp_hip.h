@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 5
+#define PT_ABI_VERSION 6
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -398,6 +398,8 @@ typedef struct pt_trace_counters {
     uint64_t shadow_prims;
     uint64_t lit_shadow_rays; /* shadow rays whose light was the nearest hit (terms added)   */
     uint64_t accum_runs;      /* their per-pixel runs after wave aggregation (atomic sets)  */
+    uint64_t volume_samples;  /* Volume.Sample calls of Volume.Intersect's march (Volume.cs:168-197) */
+    uint64_t sdf_evals;       /* SDF evaluations of SDFShape.Intersect's sphere tracing (SDF.cs:32-76) */
 } pt_trace_counters;
 int pt_render_pass_counted(void* ctx, const pt_camera* camera, const pt_sampler* sampler,
                            const pt_pass_params* pass, pt_trace_counters* out);

@@ -1267,6 +1267,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     plan.lanes_shadow_blocks = c->grids.lanes_shadow_blocks;
     plan.full_trace_blocks = c->grids.full_trace_blocks;
     plan.full_shadow_blocks = c->grids.full_shadow_blocks;
+    plan.full_lanes_trace_blocks = c->grids.full_lanes_trace_blocks;
+    plan.full_lanes_shadow_blocks = c->grids.full_lanes_shadow_blocks;
     const bool extra = pass->adaptive_samples > 0 || pass->firefly_samples > 0;
     const bool serial = (pass->flags & PT_PASS_SERIAL) != 0;   // Renderer.Render's extra phases (NumCPU == 1)
     // pt_pass_params.passes: K consecutive passes.  Plain RenderParallel passes run as one batch
@@ -1381,6 +1383,13 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     const bool timing = (pass->flags & PT_PASS_KERNEL_TIMING) != 0;
     c->timer.reset(c->stream);
     PT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));   // and the overflow flag
+    // a counted pass also counts the Volume / SDFShape march steps (counters 9, 10); the launches
+    // take the scene by value, so the pointer is cleared again whichever way this call returns
+    struct MarchScope {
+        pt::DevScene& S;
+        ~MarchScope() { S.march = nullptr; }
+    } march_scope{c->S};
+    c->S.march = counted ? c->d_counters + 9 : nullptr;
     PT_HIP(hipEventRecord(c->ev0, c->stream));
     if (engine == PT_ENGINE_WAVEFRONT) {
         pt::LaunchTimer* tm = timing ? &c->timer : nullptr;
@@ -1469,6 +1478,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         counted->shadow_prims = ctr[6];
         counted->lit_shadow_rays = ctr[7];
         counted->accum_runs = ctr[8];
+        counted->volume_samples = ctr[9];
+        counted->sdf_evals = ctr[10];
     }
     return PT_OK;
 }

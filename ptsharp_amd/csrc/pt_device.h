@@ -54,8 +54,14 @@ __device__ __noinline__ double inner_t(const DevScene& S, const float4* r, int32
         case KIND_SPHERE: return isect_sphere(v3{a.x, a.y, a.z}, rec_radius(r), o, d);
         case KIND_CUBE: return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
         case KIND_PLANE: return isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
-        case KIND_SDF: return sdf_t(S.sdf_prog, S.sdf_params, S.sdf_shapes[rec_ext(r)], o, d);
-        case KIND_VOLUME: return vol_t(S.volumes[rec_ext(r)], o, d);
+        case KIND_SDF:
+        case KIND_VOLUME: {   // the marches; a counted pass adds their steps (S.march)
+            uint32_t n = 0;
+            const double t = kind == KIND_SDF ? sdf_t(S.sdf_prog, S.sdf_params, S.sdf_shapes[rec_ext(r)], o, d, &n)
+                                              : vol_t(S.volumes[rec_ext(r)], o, d, &n);
+            if (S.march) atomicAdd(S.march + (kind == KIND_SDF ? 1 : 0), (unsigned long long)n);
+            return t;
+        }
     }
     return kHitInf;
 }

@@ -199,26 +199,32 @@ PT_HD double sdf_eval(const DevSdfIns* prog, const double* params, int begin, in
 }
 
 // SDFShape.Intersect (SDF.cs:32-76): sphere tracing within the bounding box.
-PT_HD double sdf_t(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 o, v3 d) {
+// `evals` (instrumentation, may be null): the SDF evaluations the march made.
+PT_HD double sdf_t(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 o, v3 d,
+                   uint32_t* evals = nullptr) {
     const double epsilon = (double)0.00001f, start = (double)0.0001f, jump_size = (double)0.001f;
     double t1, t2;
     box_span(sh.bmin, sh.bmax, o, d, t1, t2);
     if (t2 < t1 || t2 < 0) return kHitInf;
     double t = net_max(start, t1);
     bool jump = true;
+    uint32_t n = 0;
+    double r = kHitInf;
     for (int i = 0; i < 1000; i++) {
         double dist = sdf_eval(prog, params, sh.begin, sh.len, add(o, muls(d, t)));
+        n++;
         if (jump && dist < 0) {
             t -= jump_size;
             jump = false;
             continue;
         }
-        if (dist < epsilon) return t;
+        if (dist < epsilon) { r = t; break; }
         if (jump && dist < jump_size) dist = jump_size;
         t += dist;
-        if (t > t2) return kHitInf;
+        if (t > t2) break;
     }
-    return kHitInf;
+    if (evals) *evals = n;
+    return r;
 }
 // SDFShape.NormalAt (SDF.cs:83-92)
 PT_HD v3 sdf_normal(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 p) {
@@ -262,9 +268,44 @@ PT_HD double vol_sample(const DevVolume& v, double x, double y, double z) {
     const double c1 = c01 * (1 - y) + c11 * y;
     return c0 * (1 - z) + c1 * z;
 }
-// Volume.Sign (Volume.cs:114-131): its `i` is never incremented, so "below a window" is 1.
-PT_HD int vol_sign(const DevVolume& v, v3 a) {
-    const double s = vol_sample(v, a.x, a.y, a.z);
+// The eight corner values of the last cell Volume.Intersect's march sampled: its steps (1/512
+// of a unit) cross a cell (2/W of a unit, before the instance transform) tens of steps apart,
+// so the march re-reads the grid only when the cell changes.  The values and the arithmetic
+// after them are Volume.Sample's, bit for bit.
+struct VolCell {
+    int x0, y0, z0;
+    double c[8];   // v000 v001 v010 v011 v100 v101 v110 v111
+};
+PT_HD double vol_sample_cell(const DevVolume& v, double x, double y, double z, VolCell& k) {
+    (void)y;
+    z /= v.zscale;
+    x = ((x + 1) / 2) * (double)v.w;
+    y = ((z + 1) / 2) * (double)v.h;
+    z = ((z + 2) / 2) * (double)v.d;
+    const double lim = 2147483647.0;
+    if (!(fabs(x) < lim && fabs(y) < lim && fabs(z) < lim)) return 0;
+    const int x0 = (int)floor(x), y0 = (int)floor(y), z0 = (int)floor(z);
+    if (x0 != k.x0 || y0 != k.y0 || z0 != k.z0) {
+        const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
+        k.c[0] = vol_get(v, x0, y0, z0); k.c[1] = vol_get(v, x0, y0, z1); k.c[2] = vol_get(v, x0, y1, z0);
+        k.c[3] = vol_get(v, x0, y1, z1); k.c[4] = vol_get(v, x1, y0, z0); k.c[5] = vol_get(v, x1, y0, z1);
+        k.c[6] = vol_get(v, x1, y1, z0); k.c[7] = vol_get(v, x1, y1, z1);
+        k.x0 = x0; k.y0 = y0; k.z0 = z0;
+    }
+    x -= (double)x0;
+    y -= (double)y0;
+    z -= (double)z0;
+    const double c00 = k.c[0] * (1 - x) + k.c[4] * x;
+    const double c01 = k.c[1] * (1 - x) + k.c[5] * x;
+    const double c10 = k.c[2] * (1 - x) + k.c[6] * x;
+    const double c11 = k.c[3] * (1 - x) + k.c[7] * x;
+    const double c0 = c00 * (1 - y) + c10 * y;
+    const double c1 = c01 * (1 - y) + c11 * y;
+    return c0 * (1 - z) + c1 * z;
+}
+// Volume.Sign (Volume.cs:114-131) of a sample value: its `i` is never incremented, so
+// "below a window" is 1.
+PT_HD int vol_sign_of(const DevVolume& v, double s) {
     for (int i = 0; i < v.nwin; i++) {
         if (s < v.windows[i].lo) return 1;
         if (s > v.windows[i].hi) continue;
@@ -272,6 +313,7 @@ PT_HD int vol_sign(const DevVolume& v, v3 a) {
     }
     return v.nwin + 1;
 }
+PT_HD int vol_sign(const DevVolume& v, v3 a) { return vol_sign_of(v, vol_sample(v, a.x, a.y, a.z)); }
 // Volume.NormalAt (Volume.cs:138-145)
 PT_HD v3 vol_normal(const DevVolume& v, v3 p) {
     const double eps = (double)0.001f;
@@ -295,27 +337,40 @@ PT_HD int vol_material(const DevVolume& v, v3 p, int default_mat) {
 }
 // Volume.Intersect (Volume.cs:168-197).  The reference loop has no bound; 2^24 steps
 // stand in for it (a ray that needs more never finishes in the reference either).
-PT_HD double vol_t(const DevVolume& v, v3 o, v3 d) {
+// `samples` (instrumentation, may be null): the Volume.Sample calls the march made.
+PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr) {
     double tmin, tmax;
     box_span(v.bmin, v.bmax, o, d, tmin, tmax);
     double step = (double)(1.0f / 512.0f);
     const double start = net_max(step, tmin);
     int sign = -1;
     int iters = 0;
+    VolCell k;
+    k.x0 = k.y0 = k.z0 = -2147483647 - 1;   // no cell: floor() of an in-range coordinate is above it
+    uint32_t n = 0;
+    auto done = [&](double r) {
+        if (samples) *samples = n;
+        return r;
+    };
+    auto sign_at = [&](double t) {
+        n++;
+        const v3 a = add(o, muls(d, t));
+        return vol_sign_of(v, vol_sample_cell(v, a.x, a.y, a.z, k));
+    };
     for (double t = start; t <= tmax && iters < (1 << 24); t += step, iters++) {
-        const int sg = vol_sign(v, add(o, muls(d, t)));
+        const int sg = sign_at(t);
         if (sg == 0 || (sign >= 0 && sg != sign)) {
             t -= step;
             step /= 64;
             t += step;
             for (int i = 0; i < 64; i++) {
-                if (vol_sign(v, add(o, muls(d, t))) == 0) return t - step;
+                if (sign_at(t) == 0) return done(t - step);
                 t += step;
             }
         }
         sign = sg;
     }
-    return kHitInf;
+    return done(kHitInf);
 }
 
 }  // namespace pt

@@ -103,6 +103,9 @@ struct DevScene {
     // refill, every lane the same record (scalar loads), instead of an analytic-BVH phase
     int32_t ana_count;         // records in ana_recs
     int32_t ana_linear;        // 1: test ana_recs linearly in the refill kernels
+    // counted passes only (else null): [0] Volume.Sample calls and [1] SDF evaluations of the
+    // Volume / SDFShape intersect marches (DevBuffer::counters words 9 and 10)
+    unsigned long long* march;
 };
 
 struct DevCamera {
@@ -134,6 +137,7 @@ struct DevBuffer {
     int32_t* n;                // [P]    sample count   (Pixel.Samples)
     unsigned long long* counters;  // [0..2] closest-hit rays/nodes/prims, [3] shading fetches, [4..6] shadow
                                    // rays/nodes/prims, [7] lit shadow rays, [8] their accumulation runs,
+                                   // [9] volume samples, [10] SDF evaluations (DevScene::march),
                                    // [15] wavefront queue overflow flag
 };
 

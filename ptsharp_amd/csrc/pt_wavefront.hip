@@ -470,8 +470,17 @@ constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
 #ifndef PT_SHADOW_REFILL_IDLE
 #define PT_SHADOW_REFILL_IDLE 32   // shadow: 16 / 24 / 32 / 48 measured, 32 best
 #endif
-template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+// FULL: the same kernel over scenes with §8f row 4 shapes (SDF, Volume, TransformedShape) in the
+// analytic BVH; their intersects are calls (inner_t / xform_t), made by the lanes that reach them.
+#ifndef PT_FULL_LANES_WAVES
+#define PT_FULL_LANES_WAVES 4
+#endif
+#define PT_FULL_LANES_VGPRS ((512 / PT_FULL_LANES_WAVES) & ~7)
+#ifndef PT_FULL_LANES
+#define PT_FULL_LANES 0   // 1: row-4 scenes with a mesh take these (C5 634 vs 667 Mrays/s lockstep: DESIGN §8)
+#endif
+template <bool COUNT, bool FULL>
+__device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
 #if PT_COOP
     __shared__ float4 s_coop[kCoopRows];
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                         for (int p = 0; p < S.ana_count; p++) {
                             if (COUNT) ctr.prims++;
                             int32_t kind;
-                            const double t = prim_t<false, false>(S, S.ana_recs, (uint32_t)p, o, d, kind);
+                            const double t = prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind);
                             if (t < bt) { bt = t; bkind = kind; bidx = p; }
                         }
                     }
@@ -617,7 +626,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
             for (uint32_t k = 0; k < cntl; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
-                const double t = prim_t<false, false>(S, S.ana_recs, first + k, o, d, kind);
+                const double t = prim_t<false, FULL>(S, S.ana_recs, first + k, o, d, kind);
                 if (t < bt) {
                     bt = t; bkind = kind; bidx = (int32_t)(first + k);
                     tmax = tmax_bound(t);
@@ -648,8 +657,22 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
         }
     }
 }
+template <bool COUNT>
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+    trace_lanes<COUNT, false>(S, Q, qi, counters);
+}
+template <bool COUNT>
+__global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_FULL_LANES_VGPRS))) void k_wf_trace_lanes_full(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+    trace_lanes<COUNT, true>(S, Q, qi, counters);
+}
 
 // ---------------------------------------------------------------- shade / bounce
+#ifndef PT_NEE_VERTEX_MAJOR
+// 1: a vertex' shadow rays take consecutive slots (its children's light terms then sit in one
+// run, summed in registers by k_wf_nee_accum's wave aggregation); 0: child-major like the
+// extension rays (child c of every vertex of the block, then child c + 1)
+#define PT_NEE_VERTEX_MAJOR 0
+#endif
 #ifndef PT_SHADE_WAVES
 #define PT_SHADE_WAVES 3
 #endif
@@ -768,6 +791,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     // whole lines.  Which children exist is unchanged, so is every child's key.  With
     // more children per vertex than s_cc holds, each wave fills its own share that way.
     uint32_t ej = block_major ? blk_e : __shfl(ebase, 0, 64), nj = block_major ? blk_n : __shfl(nbase, 0, 64);
+    uint32_t nk = nbase;   // PT_NEE_VERTEX_MAJOR: this vertex' next shadow-ray slot
     for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
         const int mode = ma + c % nm;
         const uint64_t E = child_key(node, (uint32_t)c);
@@ -786,9 +810,10 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
                 te += ce; tn += cn;
             }
         }
-        const uint32_t my_n = nj + (pn + (uint32_t)__popcll(bn & below)) * rays_per_nee;
+        const uint32_t my_n = PT_NEE_VERTEX_MAJOR ? nk : nj + (pn + (uint32_t)__popcll(bn & below)) * rays_per_nee;
         const uint32_t my_e = ej + pe + (uint32_t)__popcll(be & below);
         nj += tn * rays_per_nee;
+        if (emit_nee) nk += rays_per_nee;
         ej += te;
         if (!live) continue;
         const double fp = mode == 0 ? 1.0 : (refl ? pv : 1 - pv);
@@ -1003,8 +1028,8 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // light's own t and the planes at refill, then one step loop over the analytic BVH and
 // the triangle BVH, any-hit (a primitive strictly nearer than the light ends the ray
 // unlit).  The outcome goes to n_lit; k_wf_nee_accum adds the lit rays' terms.
-template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+template <bool COUNT, bool FULL>
+__device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
 #if PT_COOP
     __shared__ float4 s_coop[kCoopRows];
@@ -1074,7 +1099,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                         run = S.tri_num_nodes > 0;
                         tri = true;
                     } else {
-                        tl = light_t<false>(S, L, o, d);
+                        tl = light_t<FULL>(S, L, o, d);
                         run = tl < kHitInf;
                         for (int p = 0; run && p < S.num_planes; p++) {
                             const float4 pa = S.planes[2 * p], pb = S.planes[2 * p + 1];
@@ -1084,7 +1109,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
                             for (int p = 0; p < S.ana_count; p++) {
                                 if (COUNT) ctr.prims++;
                                 int32_t kind;
-                                if (prim_t<false, false>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) run = false;
+                                if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) run = false;
                             }
                         tri = S.ana_linear || S.ana_num_nodes <= 0;
                     }
@@ -1207,7 +1232,7 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
             for (uint32_t k = 0; k < cntl; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
-                if (prim_t<false, false>(S, S.ana_recs, first + k, o, d, kind) < tl) { blocked = true; break; }
+                if (prim_t<false, FULL>(S, S.ana_recs, first + k, o, d, kind) < tl) { blocked = true; break; }
             }
         }
 #if PT_SHADOW_HELP
@@ -1263,6 +1288,14 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
         }
     }
 }
+template <bool COUNT>
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+    shadow_lanes<COUNT, false>(S, Q, qo, counters);
+}
+template <bool COUNT>
+__global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_FULL_LANES_VGPRS))) void k_wf_shadow_lanes_full(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+    shadow_lanes<COUNT, true>(S, Q, qo, counters);
+}
 
 // ---------------------------------------------------------------- direct-light terms
 // The light terms (throughput·weight·light colour·coverage, set up by k_wf_shade) of the
@@ -1273,9 +1306,15 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
 #ifndef PT_ACCUM_LDS
 #define PT_ACCUM_LDS 1   // k_wf_nee_accum sums a window's runs per pixel in LDS before the atomics
 #endif
-constexpr uint32_t kAccWin = 16;       // 256-slot rows per block window (one shade block's child-major region
+#ifndef PT_ACC_WIN
+#define PT_ACC_WIN 16
+#endif
+constexpr uint32_t kAccWin = PT_ACC_WIN;       // 256-slot rows per block window (one shade block's child-major region
                                        // of FirstHitSamples 16 children)
-constexpr uint32_t kAccTable = 512;    // LDS table entries
+#ifndef PT_ACC_TABLE
+#define PT_ACC_TABLE 512
+#endif
+constexpr uint32_t kAccTable = PT_ACC_TABLE;   // LDS table entries (a power of two)
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsigned long long* counters) {
     const Group G = xcd_group();
@@ -1462,12 +1501,15 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     // Per-lane refill traversal (k_wf_trace_lanes, k_wf_shadow_lanes) where rays are long
     // enough to pay for it: scenes with a triangle BVH of more than kLanesMinNodes nodes
     // (gopher3's five analytic shapes: trace 16.0 → 23.5 ms with refill).
-    const bool lanes = plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes;
+    const bool lanes = plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes && (PT_FULL_LANES || !fullg);
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
-        const unsigned tg = grid_for(n, kTB, fullg ? plan.full_trace_blocks : lanes ? plan.lanes_trace_blocks : plan.trace_blocks);
+        const unsigned tg = grid_for(n, kTB, fullg ? (lanes ? plan.full_lanes_trace_blocks : plan.full_trace_blocks)
+                                                  : lanes ? plan.lanes_trace_blocks : plan.trace_blocks);
         begin_k(1, stream);
-        if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        if (fullg && lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes_full<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (fullg && lanes) hipLaunchKernelGGL((k_wf_trace_lanes_full<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
 #ifndef PT_NO_TRACE_LANES
         else if (lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
@@ -1503,9 +1545,12 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         }
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
         const unsigned hg = grid_for(children * plan.lights_per_child, kTB,
-                                     fullg ? plan.full_shadow_blocks : lanes ? plan.lanes_shadow_blocks : plan.shadow_blocks);
+                                     fullg ? (lanes ? plan.full_lanes_shadow_blocks : plan.full_shadow_blocks)
+                                           : lanes ? plan.lanes_shadow_blocks : plan.shadow_blocks);
         begin_k(3, side);
-        if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        if (fullg && lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes_full<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (fullg && lanes) hipLaunchKernelGGL((k_wf_shadow_lanes_full<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
 #ifndef PT_NO_SHADOW_LANES
         else if (lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
@@ -1611,6 +1656,10 @@ hipError_t wavefront_grids(WfPlan& plan) {
     if (e == hipSuccess) plan.lanes_trace_blocks = resident(nb, kWfMaxBlocks);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow_lanes<false>, kTB, 0);
     if (e == hipSuccess) plan.lanes_shadow_blocks = resident(nb, kWfMaxBlocks);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace_lanes_full<false>, kTB, 0);
+    if (e == hipSuccess) plan.full_lanes_trace_blocks = resident(nb, kWfMaxBlocks);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow_lanes_full<false>, kTB, 0);
+    if (e == hipSuccess) plan.full_lanes_shadow_blocks = resident(nb, kWfMaxBlocks);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace<false, true>, kTB, 0);
     if (e == hipSuccess) plan.full_trace_blocks = resident(nb, kWfMaxBlocks);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false, true>, kTB, 0);

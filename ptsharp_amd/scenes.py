@@ -418,11 +418,11 @@ def instances(copies: int = 6, mesh_tris: int = 3000):
     return scene, camera, sampler
 
 
-def mixed(n_tris: int = 1_000_000, seed: int = 1234):
+def mixed(n_tris: int = 1_000_000, seed: int = 1234, mesh: Mesh = None):
     """BASELINE.json configs[4]'s kind of scene (C5): the C4 mesh frame plus an SDF shape, a
     voxel Volume (iso-windows) and an environment texture standing in for the HDRI (the
     reference's environment is an 8-bit ColorTexture lookup, Sampler.cs:177-189)."""
-    scene, camera, sampler = bunny_frame(n_tris, seed=seed)
+    scene, camera, sampler = bunny_frame(n_tris, seed=seed, mesh=mesh)
     scene.Texture = seeded_texture(512, 256, 21)
     scene.TextureAngle = Util.Radians(40)
     ring = TransformSDF.NewTransformSDF(TorusSDF.NewTorusSDF(F(0.45), F(0.12)),

@@ -50,3 +50,34 @@ def test_row4_adaptive(gpu):
     smp.MaxBounces = 2
     g, gr, o, orr = render_both(s, c, smp, 40, 30, spp=1, seed=33, engine=_abi.ENGINE_WAVEFRONT, adaptive=2)
     check(g, gr, o, orr)
+
+
+def test_march_counters(gpu):
+    """pt_render_pass_counted reports the Volume / SDFShape march steps (the C5 bench's flop
+    model): both present in the mixed scene, neither in a scene without those shapes, and a
+    counted pass leaves the same Buffer as an uncounted one."""
+    from ptsharp_amd import Renderer
+    s, c, smp = scenes.mixed(3000, seed=5)
+    smp.MaxBounces = 2
+    bufs = []
+    for counted in (False, True):
+        r = Renderer.NewRenderer(s, c, smp, 48, 36, True)
+        r.SamplesPerPixel = 2
+        r.Seed = 7
+        r.Engine = _abi.ENGINE_WAVEFRONT
+        if counted:
+            ctr = r.RenderCounted()
+        else:
+            r.RenderParallel()
+        b = r.ReadBuffer()
+        bufs.append((b.M.copy(), b.V.copy(), b.N.copy()))
+        r.close()
+    assert ctr.volume_samples > 0 and ctr.sdf_evals > 0
+    for x, y in zip(*bufs):
+        assert np.array_equal(x, y)
+    s2, c2, smp2 = scenes.gopher3()
+    r = Renderer.NewRenderer(s2, c2, smp2, 32, 24, True)
+    r.SamplesPerPixel = 1
+    ctr2 = r.RenderCounted()
+    r.close()
+    assert ctr2.rays > 0 and ctr2.volume_samples == 0 and ctr2.sdf_evals == 0
