@@ -32,6 +32,16 @@ struct Counters {
     uint32_t rays, nodes, prims, shades;
 };
 
+#ifndef PT_COOP_MARCH
+#define PT_COOP_MARCH 1   // Volume marches by the wave's active lanes together (coop_vol_t); 0: by the lane alone
+#endif
+#ifndef PT_COOP_SHADE
+#define PT_COOP_SHADE 1   // Hit.Info's march again (TransformedShape of a Volume) the same way
+#endif
+#ifndef PT_COOP_MIN_LANES
+#define PT_COOP_MIN_LANES 8   // fewer active lanes: each marches its own ray (vol_t, one grid read per cell)
+#endif
+
 __device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
 
 // Round a hit distance up so the fp32 cull never drops an equal-t candidate.
@@ -89,6 +99,13 @@ __device__ __forceinline__ double prim_t(const DevScene& S, const float4* __rest
     if (!FULL || kind == KIND_CUBE) return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
     if (kind == KIND_XFORM) return xform_t(S, S.xforms[rec_ext(r)], o, d);
     return inner_t(S, r, kind, o, d);
+}
+
+// Is this analytic record a Volume march (a Volume, or a TransformedShape of one)?
+__device__ __forceinline__ bool march_deferred(const DevScene& S, const float4* r) {
+    const int32_t kind = (int32_t)f2u(r[0].w);
+    if (kind == KIND_VOLUME) return true;
+    return kind == KIND_XFORM && S.xforms[rec_ext(r)].kind == KIND_VOLUME;
 }
 
 // Per-lane traversal stacks.  LdsStack: all kStackMax entries in LDS (column
@@ -218,10 +235,12 @@ __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, floa
 // the nearest descended and the others pushed far-to-near on the per-lane stack
 // (LdsStack / SpillStack).  The collapse bounds every path's pushes by kStackMax.
 // ANY: stop at the first primitive with t < best.t (shadow visibility).
+// pend (FULL, analytic BVH): the first Volume record reached is not marched here but left in
+// *pend for the wave's cooperative march after the traversal (march_pending).
 template <bool TRI, bool COUNT, bool ANY, bool FULL, class STK>
 __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __restrict__ nodes, int32_t num_nodes,
                                          const float4* __restrict__ recs, v3 o, v3 d, v3 invd, HitRec& best,
-                                         const STK& stack, Counters& ctr) {
+                                         const STK& stack, Counters& ctr, int32_t* pend = nullptr) {
     if (num_nodes <= 0) return false;
     uint32_t ref = 0;  // root: always an inner node
     int sp = 0;
@@ -252,6 +271,10 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
             for (uint32_t k = 0; k < cnt; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
+                if (FULL && PT_COOP_MARCH && pend && *pend < 0 && march_deferred(S, recs + 3 * (size_t)(first + k))) {
+                    *pend = (int32_t)(first + k);
+                    continue;
+                }
                 double t = prim_t<TRI, FULL>(S, recs, first + k, o, d, kind);
                 if (t < best.t) {
                     if (ANY) return true;
@@ -361,6 +384,135 @@ __device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 
     return (double)lengthf(sub(position, o));
 }
 
+// ---------------------------------------------------------------- cooperative Volume march
+// Volume.Intersect (Volume.cs:168-197) marches a ray in fixed 1/512 steps, hundreds per ray
+// that crosses the grid's box.  Marched by the lane that meets it (vol_t), the rest of the
+// wave waits that long with one lane active.  Here the active lanes march one ray together:
+// lane of rank k takes the k-th next sample position, the ballots find the first sample where
+// the reference's loop would act (a window, or a sign change), and the 64 fine steps of that
+// refinement are taken the same way.  Every position is the reference's own repeated fp64
+// addition (each lane repeats k additions of the step from the chunk's first t), and the
+// actions are the sequential loop's, so the t returned is vol_t's, bit for bit.
+__device__ __forceinline__ int nth_lane(uint64_t m, int r) {   // the lane of the r-th set bit of m
+    for (int k = 0; k < r; k++) m &= m - 1ull;
+    return __builtin_ctzll(m);
+}
+// Every active lane passes the same (v, o, d); returns vol_t(v, o, d) to all of them and, in
+// `samples`, the Volume.Sample calls vol_t makes (instrumentation).
+__device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& samples) {
+    const uint64_t act = __ballot(true);
+    const int lane = threadIdx.x & 63;
+    const uint64_t lower = act & ((1ull << lane) - 1ull);
+    const int rank = __popcll(lower), nact = __popcll(act);
+    const int prev_lane = lower ? 63 - __builtin_clzll(lower) : lane;
+    const int last_lane = 63 - __builtin_clzll(act);
+    double tmin, tmax;
+    box_span(v.bmin, v.bmax, o, d, tmin, tmax);
+    double step = (double)(1.0f / 512.0f);
+    double t = net_max(step, tmin);
+    int sign = -1, iters = 0;
+    samples = 0;
+    auto sign_at = [&](double tt) { return vol_sign(v, add(o, muls(d, tt))); };
+    for (;;) {   // wave-uniform: every branch below is on ballots
+        double tk = t;
+        for (int j = 0; j < rank; j++) tk += step;
+        const bool valid = tk <= tmax && iters + rank < (1 << 24);   // a prefix of the ranks (t grows)
+        const int sg = valid ? sign_at(tk) : 0;
+        const int sp = __shfl(sg, prev_lane, 64);
+        const int prev = rank == 0 ? sign : sp;
+        const uint64_t evb = __ballot(valid && (sg == 0 || (prev >= 0 && sg != prev)));
+        if (evb == 0ull) {
+            const uint64_t vb = __ballot(valid);
+            if (vb != act) {   // the loop's condition ended it first
+                samples += (uint32_t)__popcll(vb);
+                return kHitInf;
+            }
+            samples += (uint32_t)nact;
+            t = __shfl(tk, last_lane, 64) + step;
+            sign = __shfl(sg, last_lane, 64);
+            iters += nact;
+            continue;
+        }
+        const int ke = __builtin_ctzll(evb);
+        const int re = __popcll(act & ((1ull << ke) - 1ull));
+        samples += (uint32_t)(re + 1);
+        double tr = __shfl(tk, ke, 64);
+        const int sge = __shfl(sg, ke, 64);
+        tr -= step;   // the refinement (Volume.cs:183-191)
+        step /= 64;
+        tr += step;
+        for (int j0 = 0; j0 < 64; j0 += nact) {
+            double u = tr;
+            for (int j = 0; j < rank; j++) u += step;
+            const bool in = j0 + rank < 64;
+            const uint64_t zb = __ballot(in && sign_at(u) == 0);
+            if (zb) {
+                const int kz = __builtin_ctzll(zb);
+                samples += (uint32_t)(__popcll(act & ((1ull << kz) - 1ull)) + 1);
+                return __shfl(u, kz, 64) - step;
+            }
+            const int cnt = min(nact, 64 - j0);
+            samples += (uint32_t)cnt;
+            tr = __shfl(u, cnt == nact ? last_lane : nth_lane(act, cnt - 1), 64) + step;
+        }
+        t = tr + step;   // the outer loop's t += step, with the refined step
+        sign = sge;
+        iters += re + 1;
+    }
+}
+// Intersect of analytic record p (march_deferred) by the active lanes together: prim_t's t.
+__device__ inline double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind) {
+    const float4* r = S.ana_recs + 3 * (size_t)p;
+    kind = (int32_t)f2u(r[0].w);
+    uint32_t n = 0;
+    double t;
+    if (kind == KIND_VOLUME) {
+        t = coop_vol_t(S.volumes[rec_ext(r)], o, d, n);
+    } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
+        const DevXform& X = S.xforms[rec_ext(r)];
+        const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
+        t = coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n);
+        if (t < kHitInf) {
+            const v3 position = mat_position(X.m, add(so, muls(sd, t)));
+            t = (double)lengthf(sub(position, o));
+        }
+    }
+    if (S.march && (threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) atomicAdd(S.march, (unsigned long long)n);
+    return t;
+}
+// The lanes' pending Volume records (traverse's pend), one ray at a time by all active lanes.
+// Closest hit: the march's t replaces the best when nearer, and on a tie with a triangle (the
+// analytic BVH is traversed before the triangles, which replace only a strictly farther best);
+// any-hit (ANY): *blocked when nearer than the light.
+template <bool ANY>
+__device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked = nullptr) {
+    const int lane = threadIdx.x & 63;
+    auto merge = [&](double t, int32_t kind, int32_t p) {
+        if (ANY) {
+            if (t < best.t) *blocked = true;
+        } else if (t < best.t || (t == best.t && best.kind == KIND_TRI)) {
+            best.t = t; best.kind = kind; best.idx = p;
+        }
+    };
+    if (__popcll(__ballot(true)) < PT_COOP_MIN_LANES) {   // too few lanes to share a march: each its own
+        if (pend >= 0) {
+            int32_t kind;
+            const double t = prim_t<false, true>(S, S.ana_recs, (uint32_t)pend, o, d, kind);
+            merge(t, kind, pend);
+        }
+        return;
+    }
+    for (uint64_t todo = __ballot(pend >= 0); todo; todo &= todo - 1ull) {   // wave-uniform
+        const int src = __builtin_ctzll(todo);
+        const int32_t p = __shfl(pend, src, 64);
+        const v3 so{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
+        const v3 sd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+        int32_t kind;
+        const double t = coop_record_t(S, p, so, sd, kind);
+        if (lane == src) merge(t, kind, p);
+    }
+}
+
 // Scene.Intersect (Scene.cs:75-79): closest hit over planes, analytic BVH, triangle BVH.
 template <bool COUNT, bool FULL, class STK>
 __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK& stack, Counters& ctr) {
@@ -372,6 +524,7 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         if (t < best.t) { best.t = t; best.kind = KIND_PLANE; best.idx = i; }
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    int32_t pend = -1;   // FULL: a Volume left for the cooperative march
     if (S.ana_linear) {   // a few analytic shapes, one by one (as the refill kernels test them; pt_scene.h)
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
@@ -380,9 +533,11 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
             if (t < best.t) { best.t = t; best.kind = kind; best.idx = p; }
         }
     } else {
-        traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr);
+        traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
+                                            FULL ? &pend : nullptr);
     }
     traverse_tri<COUNT, false>(S, o, d, invd, best, stack, ctr);
+    if (FULL && PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
     return best;
 }
 
@@ -420,6 +575,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    int32_t pend = -1;   // FULL: a Volume left for the cooperative march
     if (S.ana_linear) {
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
@@ -427,10 +583,15 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
             if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return false;
         }
     } else if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack,
-                                                 ctr)) {
+                                                 ctr, FULL ? &pend : nullptr)) {
         return false;
     }
     if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return false;
+    if (FULL && PT_COOP_MARCH) {   // the lanes still unblocked march their pending Volume together
+        bool blocked = false;
+        march_pending<true>(S, o, d, pend, best, &blocked);
+        if (blocked) return false;
+    }
     return true;
 }
 
@@ -657,7 +818,24 @@ __device__ __noinline__ void ext_hit_info(const DevScene& S, const HitRec& h, v3
             surface_at<true>(T, S.mats[s.mat], KIND_TRI, ih.idx, sp, s.col, s.gloss);
         } else {
             const float4* ir = S.ext_recs + 3 * (size_t)X.rec;
-            const double t = inner_t(S, ir, X.kind, so, sd);
+            double t;
+            if (PT_COOP_MARCH && PT_COOP_SHADE && __popcll(__ballot(true)) >= PT_COOP_MIN_LANES) {   // the inner Volume's march
+                                                                                  // again, by this branch's lanes together
+                const bool vol = X.kind == KIND_VOLUME;
+                t = vol ? kHitInf : inner_t(S, ir, X.kind, so, sd);
+                const int lane = threadIdx.x & 63;
+                for (uint64_t todo = __ballot(vol); todo; todo &= todo - 1ull) {
+                    const int src = __builtin_ctzll(todo);
+                    const int32_t vi = __shfl(rec_ext(ir), src, 64);
+                    const v3 o2{__shfl(so.x, src, 64), __shfl(so.y, src, 64), __shfl(so.z, src, 64)};
+                    const v3 d2{__shfl(sd.x, src, 64), __shfl(sd.y, src, 64), __shfl(sd.z, src, 64)};
+                    uint32_t n;
+                    const double tv = coop_vol_t(S.volumes[vi], o2, d2, n);
+                    if (lane == src) t = tv;
+                }
+            } else {
+                t = inner_t(S, ir, X.kind, so, sd);
+            }
             sp = add(so, muls(sd, t));
             sn = inner_normal(S, ir, X.kind, sp);
             s.mat = inner_material(S, ir, X.kind, sp);

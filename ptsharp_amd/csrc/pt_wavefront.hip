@@ -1607,6 +1607,11 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     return hipGetLastError();
 }
 
+#ifndef PT_EXTRA_CHUNK
+// camera samples per chunk of the extra phases (0: the pass' chunk); their per-sample accumulators
+// (48 B each) are the light terms' atomic targets
+#define PT_EXTRA_CHUNK 0
+#endif
 hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                            const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
                            LaunchTimer* timer, int firefly, int32_t K, uint32_t sample_base, uint64_t entries,
@@ -1616,7 +1621,9 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
     auto end_k = [&](int cls) { if (timer) timer->end(cls, stream); };
     WfQueues Qx = Q;
     Qx.acc = Q.acc_s;  // per-sample accumulators
-    uint64_t per_chunk = plan.chunk / (uint64_t)K;  // entries per chunk (whole pixels)
+    uint64_t chunk = plan.chunk;
+    if (PT_EXTRA_CHUNK > 0 && chunk > (uint64_t)PT_EXTRA_CHUNK) chunk = (uint64_t)PT_EXTRA_CHUNK;
+    uint64_t per_chunk = chunk / (uint64_t)K;  // entries per chunk (whole pixels)
     if (per_chunk < 1) per_chunk = 1;
     for (uint64_t e0 = 0; e0 < entries; e0 += per_chunk) {
         const uint64_t ne = (entries - e0) < per_chunk ? (entries - e0) : per_chunk;
