@@ -269,7 +269,7 @@ def main():
     # (SDF shapes, volumes or transformed shapes: the FULL instantiations, pt_wavefront.hip depth_loop)
     fl = scene.Compile()
     fullg = any(fl.counts_ext[1:4])
-    full = fullg or len(fl.texture_list) > 0 or fl.env_texture >= 0
+    full = fullg or len(fl.texture_list) > 0 or fl.env_texture > 0   # (1-based texture slots, 0 = none)
     lanes = st.bvh_nodes - 1 > 64
     trace_name = ("k_wf_trace<false, true>" if fullg else "k_wf_trace_lanes<false>" if lanes
                   else "k_wf_trace<false, false>")

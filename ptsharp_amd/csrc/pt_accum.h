@@ -29,11 +29,17 @@ constexpr double kFixLoScale = 4294967296.0;             // 2^32
 constexpr double kFixBig = 524288.0;                     // |x| ≥ 2^19: side sum
 constexpr double kFixWave = 8192.0;                      // |x| < 2^13: |V| < 2^57, 64 of them sum without overflow
 constexpr double kFixMagicLo = 4503599627370496.0;       // 2^52: round(y), y ∈ [0, 2^32], is the low mantissa of y + 2^52
-constexpr int kFixWords = 6;                             // {low r, g, b, high r, g, b}
+#ifndef PT_FIX_SPLIT
+#define PT_FIX_SPLIT 1   // 0: each accumulator's high words next to its low words ({lo r, g, b, hi r, g, b}, 48 B)
+#endif
+constexpr int kFixWords = PT_FIX_SPLIT ? 3 : 6;          // words per accumulator in w (hi: the same stride)
 
-// Accumulators of n pixels (or samples): w [n][6] 64-bit words, big [n][3] fp64.
+// Accumulators of n pixels (or samples): the low words w [n][3], the high words hi [n][3] (touched
+// only by a carry out of the low word, so the atomics' working set is w alone: 24 B per pixel or
+// sample), big [n][3] fp64.
 struct FixAcc {
     unsigned long long* w;
+    unsigned long long* hi;
     double* big;
 };
 
@@ -83,23 +89,22 @@ __device__ __forceinline__ void fixreg_add3(FixReg& a, double r, double g, doubl
 }
 __device__ __forceinline__ double fixreg_value(const FixReg& a, int k) { return fix_value(a.hi[k], a.lo[k]) + a.big[k]; }
 
-// v (a fixed-point sum, as a signed 64-bit value) into channel k of a pixel's words: one
+// v (a fixed-point sum, as a signed 64-bit value) into channel k of accumulator i: one
 // returning atomic on the low word; the high word gets the carry (and v's sign extension).
-__device__ __forceinline__ void fix_atomic(unsigned long long* w, int k, long long v) {
-    const unsigned long long old = atomicAdd(w + k, (unsigned long long)v);
+__device__ __forceinline__ void fix_atomic(const FixAcc& A, size_t i, int k, long long v) {
+    const unsigned long long old = atomicAdd(A.w + kFixWords * i + k, (unsigned long long)v);
     const unsigned long long now = old + (unsigned long long)v;
     const long long dh = (v < 0 ? -1 : 0) + (now < old ? 1 : 0);
-    if (dh) atomicAdd(w + 3 + k, (unsigned long long)dh);
+    if (dh) atomicAdd(A.hi + kFixWords * i + k, (unsigned long long)dh);
 }
 
 // One lane's term into accumulator i.
 __device__ __forceinline__ void fix_add_lane(const FixAcc& A, size_t i, double r, double g, double b) {
-    unsigned long long* w = A.w + kFixWords * i;
     const double x[3] = {r, g, b};
     for (int k = 0; k < 3; k++) {
         if (x[k] == 0.0) continue;
         if (!fix_ok(x[k])) { atomicAdd(A.big + 3 * i + k, x[k]); continue; }
-        fix_atomic(w, k, to_fix(x[k]));
+        fix_atomic(A, i, k, to_fix(x[k]));
     }
 }
 
@@ -154,7 +159,7 @@ __device__ __forceinline__ uint32_t fix_add_wave(const FixAcc& A, uint32_t idx, 
         for (int k = 0; k < 3; k++)
             if (x[k] != 0.0 && !(fabs(x[k]) < lim)) {
                 if (!fix_ok(x[k])) atomicAdd(A.big + 3 * (size_t)idx + k, x[k]);
-                else fix_atomic(A.w + kFixWords * (size_t)idx, k, to_fix(x[k]));
+                else fix_atomic(A, idx, k, to_fix(x[k]));
             }
     }
     // Runs are taken over the lanes that add: a lane without a term does not split its
@@ -181,9 +186,8 @@ __device__ __forceinline__ uint32_t fix_add_wave(const FixAcc& A, uint32_t idx, 
         }
     }
     if (head && (v[0] | v[1] | v[2]) && !(T && lds_fix_add(*T, idx, v))) {
-        unsigned long long* w = A.w + kFixWords * (size_t)idx;
         for (int k = 0; k < 3; k++)
-            if (v[k]) fix_atomic(w, k, v[k]);
+            if (v[k]) fix_atomic(A, idx, k, v[k]);
     }
     return (uint32_t)__popcll(heads);
 }
@@ -191,10 +195,11 @@ __device__ __forceinline__ uint32_t fix_add_wave(const FixAcc& A, uint32_t idx, 
 // Value of accumulator i (then cleared for the next pass).
 __device__ __forceinline__ void fix_take(const FixAcc& A, size_t i, double out[3]) {
     unsigned long long* w = A.w + kFixWords * i;
+    unsigned long long* h = A.hi + kFixWords * i;
     double* bg = A.big + 3 * i;
     for (int k = 0; k < 3; k++) {
-        out[k] = fix_value((long long)w[3 + k], w[k]) + bg[k];
-        w[k] = 0ull; w[3 + k] = 0ull; bg[k] = 0.0;
+        out[k] = fix_value((long long)h[k], w[k]) + bg[k];
+        w[k] = 0ull; h[k] = 0ull; bg[k] = 0.0;
     }
 }
 

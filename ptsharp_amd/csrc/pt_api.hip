@@ -226,7 +226,10 @@ void free_wavefront(Ctx* c) {
     c->d_plist2 = nullptr;
     c->d_fcount = nullptr;
     c->d_snap = nullptr;
-    if (c->acc_s.w) { (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.big); }
+    if (c->acc_s.w) {
+        (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.big);
+        if (PT_FIX_SPLIT) (void)hipFree(c->acc_s.hi);
+    }
     c->acc_s = pt::FixAcc{};
     c->acc_s_cap = 0;
 }
@@ -273,8 +276,14 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     // per-pixel accumulators of one pass, or of each pass of a batch (pt_pass_params.passes)
     size_t P = (size_t)c->width * (size_t)c->height * (size_t)acc_passes;
     if ((rc = wf_alloc(c, &Q.acc.w, P * pt::kFixWords))) return rc;
+    if (PT_FIX_SPLIT) {
+        if ((rc = wf_alloc(c, &Q.acc.hi, P * pt::kFixWords))) return rc;
+    } else {
+        Q.acc.hi = Q.acc.w + 3;
+    }
     if ((rc = wf_alloc(c, &Q.acc.big, P * 3))) return rc;
     PT_HIP(hipMemsetAsync(Q.acc.w, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
+    if (PT_FIX_SPLIT) PT_HIP(hipMemsetAsync(Q.acc.hi, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
     PT_HIP(hipMemsetAsync(Q.acc.big, 0, P * 3 * sizeof(double), c->stream));
     PT_HIP(hipMemsetAsync(Q.counts, 0, pt::kCountWords * sizeof(uint32_t), c->stream));
     Q.cap = cap;
@@ -300,17 +309,25 @@ int ensure_extra(Ctx* c, uint64_t chunk) {
         if ((rc = wf_alloc(c, &c->d_fcount, 2))) return rc;
         if ((rc = wf_alloc(c, &c->d_snap, P * 3))) return rc;
     }
-    if (c->acc_s.w) { (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.big); c->acc_s = pt::FixAcc{}; c->acc_s_cap = 0; }
+    if (c->acc_s.w) {
+        (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.big);
+        if (PT_FIX_SPLIT) (void)hipFree(c->acc_s.hi);
+        c->acc_s = pt::FixAcc{}; c->acc_s_cap = 0;
+    }
     c->Q.acc_s = pt::FixAcc{};
     if (hipMalloc(&c->acc_s.w, chunk * pt::kFixWords * sizeof(unsigned long long)) != hipSuccess)
         return fail(PT_ERR_OUT_OF_MEMORY, "hipMalloc per-sample accumulators");
-    if (hipMalloc(&c->acc_s.big, chunk * 3 * sizeof(double)) != hipSuccess) {
+    if (!PT_FIX_SPLIT) c->acc_s.hi = c->acc_s.w + 3;
+    if ((PT_FIX_SPLIT && hipMalloc(&c->acc_s.hi, chunk * pt::kFixWords * sizeof(unsigned long long)) != hipSuccess) ||
+        hipMalloc(&c->acc_s.big, chunk * 3 * sizeof(double)) != hipSuccess) {
         (void)hipFree(c->acc_s.w);
+        if (PT_FIX_SPLIT && c->acc_s.hi) (void)hipFree(c->acc_s.hi);
         c->acc_s = pt::FixAcc{};
         return fail(PT_ERR_OUT_OF_MEMORY, "hipMalloc per-sample accumulators");
     }
     c->acc_s_cap = chunk;
     PT_HIP(hipMemsetAsync(c->acc_s.w, 0, chunk * pt::kFixWords * sizeof(unsigned long long), c->stream));
+    if (PT_FIX_SPLIT) PT_HIP(hipMemsetAsync(c->acc_s.hi, 0, chunk * pt::kFixWords * sizeof(unsigned long long), c->stream));
     PT_HIP(hipMemsetAsync(c->acc_s.big, 0, chunk * 3 * sizeof(double), c->stream));
     c->Q.acc_s = c->acc_s;
     return PT_OK;

@@ -36,7 +36,7 @@ struct Counters {
 #define PT_COOP_MARCH 1   // Volume marches by the wave's active lanes together (coop_vol_t); 0: by the lane alone
 #endif
 #ifndef PT_COOP_SHADE
-#define PT_COOP_SHADE 1   // Hit.Info's march again (TransformedShape of a Volume) the same way
+#define PT_COOP_SHADE 0   // 1: Hit.Info's march again (TransformedShape of a Volume) the same way: C5 855 -> 826
 #endif
 #ifndef PT_COOP_MIN_LANES
 #define PT_COOP_MIN_LANES 8   // fewer active lanes: each marches its own ray (vol_t, one grid read per cell)

@@ -1358,10 +1358,9 @@ __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsign
         for (uint32_t e = threadIdx.x; e < kAccTable; e += 256u) {
             const uint32_t k = s_key[e];
             if (k == kLdsFree) continue;
-            unsigned long long* w = Q.acc.w + kFixWords * (size_t)k;
             for (int c = 0; c < 3; c++) {
                 const long long v = (long long)s_sum[3 * e + c];
-                if (v) fix_atomic(w, c, v);
+                if (v) fix_atomic(Q.acc, k, c, v);
                 s_sum[3 * e + c] = 0ull;
             }
             s_key[e] = kLdsFree;
