@@ -17,6 +17,7 @@ struct HitRec {
     double t;
     int32_t kind;   // KIND_* of the primitive hit; -1 = miss
     int32_t idx;    // record position: tri_recs / ana_recs / planes
+    double tx = 0;  // KIND_XFORM (FULL): the inner shape's object-space t, so Hit.Info need not intersect again
 };
 
 // A whole traversal stack in a private array (scratch): the nested traversal of an instanced mesh.
@@ -34,9 +35,6 @@ struct Counters {
 
 #ifndef PT_COOP_MARCH
 #define PT_COOP_MARCH 1   // Volume marches by the wave's active lanes together (coop_vol_t); 0: by the lane alone
-#endif
-#ifndef PT_COOP_SHADE
-#define PT_COOP_SHADE 0   // 1: Hit.Info's march again (TransformedShape of a Volume) the same way: C5 855 -> 826
 #endif
 #ifndef PT_COOP_MIN_LANES
 #define PT_COOP_MIN_LANES 8   // fewer active lanes: each marches its own ray (vol_t, one grid read per cell)
@@ -80,13 +78,14 @@ __device__ __noinline__ HitRec blas_hit(const DevScene& S, int b, v3 o, v3 d);  
 
 // TransformedShape.Intersect (TransformedShape.cs:43-73) up to hit.T: the inner hit mapped
 // back to world space, T = |position - origin| (fp32 Length).
-__device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 o, v3 d);
+__device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 o, v3 d, double* tobj = nullptr);
 
 // Intersect one record; returns t (kHitInf = miss) and the primitive kind.  FULL adds
 // the §8f row 4 kinds of the analytic BVH (SDF, volume, transformed shape).
+// tx (FULL, may be null): a TransformedShape's inner object-space t (HitRec::tx).
 template <bool TRI, bool FULL = false>
 __device__ __forceinline__ double prim_t(const DevScene& S, const float4* __restrict__ recs, uint32_t pos, v3 o, v3 d,
-                                         int32_t& kind) {
+                                         int32_t& kind, double* tx = nullptr) {
     const float4* r = recs + 3 * (size_t)pos;
     if (TRI) {
         float4 a = r[0], b = r[1], c = r[2];
@@ -97,7 +96,7 @@ __device__ __forceinline__ double prim_t(const DevScene& S, const float4* __rest
     kind = (int32_t)f2u(a.w);
     if (kind == KIND_SPHERE) return isect_sphere(v3{a.x, a.y, a.z}, rec_radius(r), o, d);
     if (!FULL || kind == KIND_CUBE) return isect_cube(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
-    if (kind == KIND_XFORM) return xform_t(S, S.xforms[rec_ext(r)], o, d);
+    if (kind == KIND_XFORM) return xform_t(S, S.xforms[rec_ext(r)], o, d, tx);
     return inner_t(S, r, kind, o, d);
 }
 
@@ -275,10 +274,12 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
                     *pend = (int32_t)(first + k);
                     continue;
                 }
-                double t = prim_t<TRI, FULL>(S, recs, first + k, o, d, kind);
+                double tx = 0;
+                double t = prim_t<TRI, FULL>(S, recs, first + k, o, d, kind, FULL ? &tx : nullptr);
                 if (t < best.t) {
                     if (ANY) return true;
                     best.t = t; best.kind = kind; best.idx = (int32_t)(first + k);
+                    if (FULL) best.tx = tx;
                     tmax = tmax_bound(t);
                 }
             }
@@ -374,12 +375,13 @@ __device__ __noinline__ HitRec blas_hit(const DevScene& S, int b, v3 o, v3 d) {
     return best;
 }
 
-__device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 o, v3 d) {
+__device__ __noinline__ double xform_t(const DevScene& S, const DevXform& X, v3 o, v3 d, double* tobj) {
     const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);   // Matrix.Inverse().MulRay
     double t;
     if (X.kind == KIND_MESH) t = blas_hit(S, X.rec, so, sd).t;
     else t = inner_t(S, S.ext_recs + 3 * (size_t)X.rec, X.kind, so, sd);
     if (!(t < kHitInf)) return kHitInf;
+    if (tobj) *tobj = t;
     const v3 position = mat_position(X.m, add(so, muls(sd, t)));
     return (double)lengthf(sub(position, o));
 }
@@ -461,17 +463,19 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     }
 }
 // Intersect of analytic record p (march_deferred) by the active lanes together: prim_t's t.
-__device__ inline double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind) {
+__device__ inline double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj) {
     const float4* r = S.ana_recs + 3 * (size_t)p;
     kind = (int32_t)f2u(r[0].w);
     uint32_t n = 0;
     double t;
     if (kind == KIND_VOLUME) {
         t = coop_vol_t(S.volumes[rec_ext(r)], o, d, n);
+        tobj = t;
     } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
         const DevXform& X = S.xforms[rec_ext(r)];
         const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
         t = coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n);
+        tobj = t;
         if (t < kHitInf) {
             const v3 position = mat_position(X.m, add(so, muls(sd, t)));
             t = (double)lengthf(sub(position, o));
@@ -487,18 +491,19 @@ __device__ inline double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d,
 template <bool ANY>
 __device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked = nullptr) {
     const int lane = threadIdx.x & 63;
-    auto merge = [&](double t, int32_t kind, int32_t p) {
+    auto merge = [&](double t, int32_t kind, int32_t p, double tx) {
         if (ANY) {
             if (t < best.t) *blocked = true;
         } else if (t < best.t || (t == best.t && best.kind == KIND_TRI)) {
-            best.t = t; best.kind = kind; best.idx = p;
+            best.t = t; best.kind = kind; best.idx = p; best.tx = tx;
         }
     };
     if (__popcll(__ballot(true)) < PT_COOP_MIN_LANES) {   // too few lanes to share a march: each its own
         if (pend >= 0) {
             int32_t kind;
-            const double t = prim_t<false, true>(S, S.ana_recs, (uint32_t)pend, o, d, kind);
-            merge(t, kind, pend);
+            double tx = 0;
+            const double t = prim_t<false, true>(S, S.ana_recs, (uint32_t)pend, o, d, kind, &tx);
+            merge(t, kind, pend, tx);
         }
         return;
     }
@@ -508,8 +513,9 @@ __device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend
         const v3 so{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
         const v3 sd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
         int32_t kind;
-        const double t = coop_record_t(S, p, so, sd, kind);
-        if (lane == src) merge(t, kind, p);
+        double tx = 0;
+        const double t = coop_record_t(S, p, so, sd, kind, tx);
+        if (lane == src) merge(t, kind, p, tx);
     }
 }
 
@@ -529,8 +535,9 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
             int32_t kind;
-            const double t = prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind);
-            if (t < best.t) { best.t = t; best.kind = kind; best.idx = p; }
+            double tx = 0;
+            const double t = prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind, FULL ? &tx : nullptr);
+            if (t < best.t) { best.t = t; best.kind = kind; best.idx = p; if (FULL) best.tx = tx; }
         }
     } else {
         traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
@@ -818,24 +825,9 @@ __device__ __noinline__ void ext_hit_info(const DevScene& S, const HitRec& h, v3
             surface_at<true>(T, S.mats[s.mat], KIND_TRI, ih.idx, sp, s.col, s.gloss);
         } else {
             const float4* ir = S.ext_recs + 3 * (size_t)X.rec;
-            double t;
-            if (PT_COOP_MARCH && PT_COOP_SHADE && __popcll(__ballot(true)) >= PT_COOP_MIN_LANES) {   // the inner Volume's march
-                                                                                  // again, by this branch's lanes together
-                const bool vol = X.kind == KIND_VOLUME;
-                t = vol ? kHitInf : inner_t(S, ir, X.kind, so, sd);
-                const int lane = threadIdx.x & 63;
-                for (uint64_t todo = __ballot(vol); todo; todo &= todo - 1ull) {
-                    const int src = __builtin_ctzll(todo);
-                    const int32_t vi = __shfl(rec_ext(ir), src, 64);
-                    const v3 o2{__shfl(so.x, src, 64), __shfl(so.y, src, 64), __shfl(so.z, src, 64)};
-                    const v3 d2{__shfl(sd.x, src, 64), __shfl(sd.y, src, 64), __shfl(sd.z, src, 64)};
-                    uint32_t n;
-                    const double tv = coop_vol_t(S.volumes[vi], o2, d2, n);
-                    if (lane == src) t = tv;
-                }
-            } else {
-                t = inner_t(S, ir, X.kind, so, sd);
-            }
+            // the inner intersect's t as the closest-hit query found it (HitRec::tx), not a second
+            // intersect here (for a Volume, a whole march per hit)
+            const double t = h.tx;
             sp = add(so, muls(sd, t));
             sn = inner_normal(S, ir, X.kind, sp);
             s.mat = inner_material(S, ir, X.kind, sp);

@@ -345,7 +345,8 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
             float4 a = nt_load(&Q.q_o[qi][i]);
             HitRec h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
             kept += (h.kind >= 0 || !env_black) ? 1u : 0u;
-            unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
+            // a TransformedShape hit keeps its inner object-space t, what Hit.Info needs (HitRec::tx)
+            unsigned long long tb = (unsigned long long)__double_as_longlong(FULL && h.kind == KIND_XFORM ? h.tx : h.t);
             hit_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
         }
     }
@@ -506,11 +507,11 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     uint32_t i = 0, ref = 0;   // i: the ray's slot; bit 31 set = the ray misses the triangle BVH's root box
     int sp = 0;
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
-    double bt = kHitInf;
+    double bt = kHitInf, btx = 0.0;   // btx (FULL): HitRec::tx of the best
     int32_t bkind = -1, bidx = -1;
     float tmax = 0.f;
     auto finish = [&]() {
-        unsigned long long tb = (unsigned long long)__double_as_longlong(bt);
+        unsigned long long tb = (unsigned long long)__double_as_longlong(FULL && bkind == KIND_XFORM ? btx : bt);
         hit_store(&Q.hits[i & 0x7FFFFFFFu], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
         kept += (bkind >= 0 || !env_black) ? 1u : 0u;
         has = false;
@@ -555,8 +556,9 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                         for (int p = 0; p < S.ana_count; p++) {
                             if (COUNT) ctr.prims++;
                             int32_t kind;
-                            const double t = prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind);
-                            if (t < bt) { bt = t; bkind = kind; bidx = p; }
+                            double tx = 0;
+                            const double t = prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind, FULL ? &tx : nullptr);
+                            if (t < bt) { bt = t; bkind = kind; bidx = p; if (FULL) btx = tx; }
                         }
                     }
                     tmax = tmax_bound(bt);
@@ -626,9 +628,11 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
             for (uint32_t k = 0; k < cntl; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
-                const double t = prim_t<false, FULL>(S, S.ana_recs, first + k, o, d, kind);
+                double tx = 0;
+                const double t = prim_t<false, FULL>(S, S.ana_recs, first + k, o, d, kind, FULL ? &tx : nullptr);
                 if (t < bt) {
                     bt = t; bkind = kind; bidx = (int32_t)(first + k);
+                    if (FULL) btx = tx;
                     tmax = tmax_bound(t);
                 }
             }
@@ -717,6 +721,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     h.t = __longlong_as_double((long long)(((unsigned long long)hr.y << 32) | hr.x));
     h.kind = (int32_t)hr.z;
     h.idx = (int32_t)hr.w;
+    h.tx = h.t;   // a TransformedShape hit's record holds its inner object-space t (k_wf_trace)
     const double thr[3] = {rt.x, rt.y, __longlong_as_double((long long)rk.y)};
     const v3 o{ro.x, ro.y, ro.z}, d{rd.x, rd.y, rd.z};
     Shade sh{};
