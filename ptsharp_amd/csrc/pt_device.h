@@ -399,9 +399,28 @@ __device__ __forceinline__ int nth_lane(uint64_t m, int r) {   // the lane of th
     for (int k = 0; k < r; k++) m &= m - 1ull;
     return __builtin_ctzll(m);
 }
+// t plus k steps, k = 0..63, as k repeated fp64 additions of `step` give it (a power of two: the
+// march's 1/512, divided by 64 at each refinement).  When t's ulp divides the step and t + 63
+// steps stays in t's binade, every partial sum is exact, so one addition of k·step (exact) gives
+// the same bits; otherwise the k additions are made.
+__device__ __forceinline__ double march_pos(double t, double step, int k, bool exact) {
+    if (exact) return t + (double)k * step;
+    double u = t;
+    for (int j = 0; j < k; j++) u += step;
+    return u;
+}
+__device__ __forceinline__ bool march_exact(double t, double step) {   // t > 0
+    int e;
+    (void)frexp(t, &e);   // t in [2^(e-1), 2^e), ulp 2^(e-53)
+    return ldexp(1.0, e - 53) <= step && t + 63.0 * step < ldexp(1.0, e);
+}
 // Every active lane passes the same (v, o, d); returns vol_t(v, o, d) to all of them and, in
 // `samples`, the Volume.Sample calls vol_t makes (instrumentation).
 __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& samples) {
+#ifdef PT_PROBE_NO_VOL   // timing probe only (wrong images): Volumes never hit
+    samples = 0;
+    return kHitInf;
+#endif
     const uint64_t act = __ballot(true);
     const int lane = threadIdx.x & 63;
     const uint64_t lower = act & ((1ull << lane) - 1ull);
@@ -416,8 +435,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     samples = 0;
     auto sign_at = [&](double tt) { return vol_sign(v, add(o, muls(d, tt))); };
     for (;;) {   // wave-uniform: every branch below is on ballots
-        double tk = t;
-        for (int j = 0; j < rank; j++) tk += step;
+        const double tk = march_pos(t, step, rank, march_exact(t, step));
         const bool valid = tk <= tmax && iters + rank < (1 << 24);   // a prefix of the ranks (t grows)
         const int sg = valid ? sign_at(tk) : 0;
         const int sp = __shfl(sg, prev_lane, 64);
@@ -444,8 +462,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
         step /= 64;
         tr += step;
         for (int j0 = 0; j0 < 64; j0 += nact) {
-            double u = tr;
-            for (int j = 0; j < rank; j++) u += step;
+            const double u = march_pos(tr, step, rank, march_exact(tr, step));
             const bool in = j0 + rank < 64;
             const uint64_t zb = __ballot(in && sign_at(u) == 0);
             if (zb) {
@@ -463,7 +480,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     }
 }
 // Intersect of analytic record p (march_deferred) by the active lanes together: prim_t's t.
-__device__ inline double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj) {
+__device__ __noinline__ double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj) {
     const float4* r = S.ana_recs + 3 * (size_t)p;
     kind = (int32_t)f2u(r[0].w);
     uint32_t n = 0;

@@ -203,6 +203,9 @@ PT_HD double sdf_eval(const DevSdfIns* prog, const double* params, int begin, in
 PT_HD double sdf_t(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 o, v3 d,
                    uint32_t* evals = nullptr) {
     const double epsilon = (double)0.00001f, start = (double)0.0001f, jump_size = (double)0.001f;
+#ifdef PT_PROBE_NO_SDF   // timing probe only (wrong images): SDF shapes never hit
+    if (epsilon > 0) return kHitInf;
+#endif
     double t1, t2;
     box_span(sh.bmin, sh.bmax, o, d, t1, t2);
     if (t2 < t1 || t2 < 0) return kHitInf;
@@ -339,6 +342,9 @@ PT_HD int vol_material(const DevVolume& v, v3 p, int default_mat) {
 // stand in for it (a ray that needs more never finishes in the reference either).
 // `samples` (instrumentation, may be null): the Volume.Sample calls the march made.
 PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr) {
+#ifdef PT_PROBE_NO_VOL   // timing probe only (wrong images): Volumes never hit
+    if (samples) return kHitInf;
+#endif
     double tmin, tmax;
     box_span(v.bmin, v.bmax, o, d, tmin, tmax);
     double step = (double)(1.0f / 512.0f);

@@ -477,6 +477,9 @@ constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
 #define PT_FULL_LANES_WAVES 4
 #endif
 #define PT_FULL_LANES_VGPRS ((512 / PT_FULL_LANES_WAVES) & ~7)
+#ifndef PT_FULL_LANES_SHADOW
+#define PT_FULL_LANES_SHADOW PT_FULL_LANES   // the shadow side of PT_FULL_LANES
+#endif
 #ifndef PT_FULL_LANES
 #define PT_FULL_LANES 0   // 1: row-4 scenes with a mesh take these (C5 634 vs 667 Mrays/s lockstep: DESIGN §8)
 #endif
@@ -504,6 +507,8 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     uint32_t kept = 0;
     const float inf = __int_as_float(0x7f800000);
     bool has = false, tri = false, more = true;
+    int32_t pend = -1;    // FULL: a Volume record left for the wave's cooperative march (march_pending)
+    bool mwait = false;   // FULL: this lane's traversal is done, its pending Volume not yet marched
     uint32_t i = 0, ref = 0;   // i: the ray's slot; bit 31 set = the ray misses the triangle BVH's root box
     int sp = 0;
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
@@ -517,6 +522,26 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
         has = false;
     };
     for (;;) {
+        if constexpr (FULL && PT_COOP_MARCH) {   // wave-uniform: every lane is here
+            const uint64_t mq = __ballot(mwait);
+            for (uint64_t todo = mq; todo; todo &= todo - 1ull) {   // each waiting ray, marched by the whole wave
+                const int src = __builtin_ctzll(todo);
+                const int32_t p = __shfl(pend, src, 64);
+                const v3 so{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
+                const v3 sd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+                int32_t kind;
+                double tx = 0;
+                const double t = coop_record_t(S, p, so, sd, kind, tx);
+                if (lane == (uint32_t)src && (t < bt || (t == bt && bkind == KIND_TRI))) {
+                    bt = t; bkind = kind; bidx = p; btx = tx;
+                }
+            }
+            if (mwait) {
+                mwait = false;
+                pend = -1;
+                finish();
+            }
+        }
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (more && (nidle >= PT_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
@@ -567,7 +592,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                     // tested at the refill's bound (planes only), kept as a bit of i: no register for it
                     if (!tri_reach(S, o, invd, tmax)) i |= 0x80000000u;
                     tri = S.ana_linear || S.ana_num_nodes <= 0;
-                    if (tri && (i >> 31)) finish();
+                    if (tri && (i >> 31)) finish();   // (FULL scenes traverse the analytic BVH first: tri false)
                 }
             }
         }
@@ -576,11 +601,11 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
         const bool leaf = (ref & 0x80000000u) != 0;
         float4 q0, q1, q2, q3, q4, q5, q6;   // the step's line
 #if PT_COOP
-        coop_line(S.lines, step_line(S, has, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
-                  q3, q4, q5, q6);
-        if (!has) continue;
+        coop_line(S.lines, step_line(S, has && !(FULL && mwait), tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7),
+                  lane, q0, q1, q2, q3, q4, q5, q6);
+        if (!has || (FULL && mwait)) continue;
 #else
-        if (!has) continue;
+        if (!has || (FULL && mwait)) continue;
         {   // one 128-B line, seven 16-B pieces, by a 32-bit offset into the one allocation of all
             // traversal lines (no per-BVH 64-bit base: the step loop then holds its state without
             // spilling).  An analytic leaf reads its records in prim_t; its line is not used.
@@ -628,6 +653,10 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
             for (uint32_t k = 0; k < cntl; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
+                if (FULL && PT_COOP_MARCH && pend < 0 && march_deferred(S, S.ana_recs + 3 * (size_t)(first + k))) {
+                    pend = (int32_t)(first + k);
+                    continue;
+                }
                 double tx = 0;
                 const double t = prim_t<false, FULL>(S, S.ana_recs, first + k, o, d, kind, FULL ? &tx : nullptr);
                 if (t < bt) {
@@ -644,6 +673,8 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
             } else if (!tri && !(i >> 31)) {
                 tri = true;
                 ref = 0;
+            } else if (FULL && pend >= 0) {
+                mwait = true;   // the wave marches it at the top of the loop
             } else {
                 finish();
             }
@@ -1506,6 +1537,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     // enough to pay for it: scenes with a triangle BVH of more than kLanesMinNodes nodes
     // (gopher3's five analytic shapes: trace 16.0 → 23.5 ms with refill).
     const bool lanes = plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes && (PT_FULL_LANES || !fullg);
+    const bool lanes_sh = plan.lanes >= 0 ? plan.lanes == 1
+                                          : S.tri_num_nodes > kLanesMinNodes && (PT_FULL_LANES_SHADOW || !fullg);
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
         const unsigned tg = grid_for(n, kTB, fullg ? (lanes ? plan.full_lanes_trace_blocks : plan.full_trace_blocks)
@@ -1549,16 +1582,16 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         }
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
         const unsigned hg = grid_for(children * plan.lights_per_child, kTB,
-                                     fullg ? (lanes ? plan.full_lanes_shadow_blocks : plan.full_shadow_blocks)
-                                           : lanes ? plan.lanes_shadow_blocks : plan.shadow_blocks);
+                                     fullg ? (lanes_sh ? plan.full_lanes_shadow_blocks : plan.full_shadow_blocks)
+                                           : lanes_sh ? plan.lanes_shadow_blocks : plan.shadow_blocks);
         begin_k(3, side);
-        if (fullg && lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes_full<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-        else if (fullg && lanes) hipLaunchKernelGGL((k_wf_shadow_lanes_full<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        if (fullg && lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes_full<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (fullg && lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes_full<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
 #ifndef PT_NO_SHADOW_LANES
-        else if (lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-        else if (lanes) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
 #endif
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
