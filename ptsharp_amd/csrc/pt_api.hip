@@ -856,6 +856,16 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
                     (size_t)d->volumes[i].w * d->volumes[i].h * d->volumes[i].d * sizeof(double));
     // host views (Scene.Add's MaterialAt(new Vector()) for light registration)
     auto host_volume = [&](int i) { return dev_volume(d->volumes[i], vox.data() + vol_off[(size_t)i], windows.data() + win_off[(size_t)i]); };
+    // uniform-cell tables of the march skip (pt_ext.h vol_build_runs), one per volume
+    std::vector<int8_t> vol_runs;
+    std::vector<size_t> runs_off;
+    std::vector<int32_t> zero_sign((size_t)std::max(d->num_volumes, 0));
+    for (int i = 0; i < d->num_volumes; i++) {
+        const pt_volume& v = d->volumes[i];
+        runs_off.push_back(vol_runs.size());
+        vol_runs.resize(vol_runs.size() + (size_t)(v.w + 1) * (v.h + 1) * (v.d + 1));
+        pt::vol_build_runs(host_volume(i), vol_runs.data() + runs_off.back(), zero_sign[(size_t)i]);
+    }
     const pt::v3 origin = pt::zero3();
     // IShape.BoundingBox of a shape that can be analytic or inner (exact, as the reference computes it)
     auto shape_box = [&](int k, int j) -> HostBox {
@@ -1185,9 +1195,14 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     const pt::DevWindow* d_win = nullptr;
     rc = upload(c, vox, &d_vox); if (rc) return rc;
     rc = upload(c, windows, &d_win); if (rc) return rc;
+    const int8_t* d_runs = nullptr;
+    rc = upload(c, vol_runs, &d_runs); if (rc) return rc;
     std::vector<pt::DevVolume> vols;
-    for (int i = 0; i < d->num_volumes; i++)
+    for (int i = 0; i < d->num_volumes; i++) {
         vols.push_back(dev_volume(d->volumes[i], d_vox + vol_off[(size_t)i], d_win ? d_win + win_off[(size_t)i] : nullptr));
+        vols.back().runs = d_runs ? d_runs + runs_off[(size_t)i] : nullptr;
+        vols.back().zero_sign = zero_sign[(size_t)i];
+    }
     rc = upload(c, vols, &S.volumes); if (rc) return rc;
     rc = upload(c, xforms, &S.xforms); if (rc) return rc;
     rc = upload(c, ext_recs, &S.ext_recs); if (rc) return rc;

@@ -435,6 +435,20 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     samples = 0;
     auto sign_at = [&](double tt) { return vol_sign(v, add(o, muls(d, tt))); };
     for (;;) {   // wave-uniform: every branch below is on ballots
+        if (PT_VOL_SKIP && v.runs) {   // pass a run of positions that cannot act (pt_ext.h vol_run)
+            const int s = sign < 0 ? vol_key_sign(v, vol_key(v, o, d, t)) : sign;
+            if (s > 0) {
+                bool all;
+                const long long kk = vol_skip(v, o, d, t, step, s, tmax, iters, all);   // the same on every lane
+                samples += (uint32_t)kk;
+                if (all) return kHitInf;
+                if (kk) {
+                    sign = s;
+                    t = t_after(t, step, kk);
+                    iters += (int)kk;
+                }
+            }
+        }
         const double tk = march_pos(t, step, rank, march_exact(t, step));
         const bool valid = tk <= tmax && iters + rank < (1 << 24);   // a prefix of the ranks (t grows)
         const int sg = valid ? sign_at(tk) : 0;

@@ -54,6 +54,11 @@ struct DevVolume {
     int32_t w, h, d, nwin;
     double zscale;
     float bmin[3], bmax[3];
+    // Uniform cells (vol_build_runs): per cell (x0, y0, z0) of Sample's lattice, indices -1..w-1
+    // etc., the Sign every sample inside it has (1 or nwin + 1), or 0 when it cannot be vouched
+    // for; null: no skipping.  zero_sign: the Sign of a cell with every corner outside the grid.
+    const int8_t* runs;
+    int32_t zero_sign, _pad;
 };
 struct DevBlas {          // object-space BVH4 of a mesh instanced by TransformedShape
     int32_t node_off;     // first node in blas_nodes
@@ -338,6 +343,191 @@ PT_HD int vol_material(const DevVolume& v, v3 p, int default_mat) {
     }
     return bm;
 }
+// ---------------------------------------------------------------- Volume march skipping
+#ifndef PT_VOL_SKIP
+#define PT_VOL_SKIP 1   // 0: march every position (the reference loop as written)
+#endif
+// Volume.Intersect acts at a march position only when its Sign is 0 or differs from the last
+// one.  Sample is a convex combination of its cell's eight corners, so a cell whose corner range
+// lies inside one Sign band (with a margin far above the interpolation's rounding) gives every
+// position in it that band's Sign.  A run of positions whose cells all carry the running Sign
+// is therefore passed without any action, and the march can move past it at once: the run's
+// end is found from the exact positions (the reference's own repeated additions, t_after, and
+// fp32 Ray.Position), so the t returned is the loop's, bit for bit.  In the reference's own
+// volume scene (Example.volume) Sample's y-from-z slip puts most of the box beyond the grid's
+// last slice, where every sample is exactly 0.
+//
+// The band of a value: 2i for "below window i's lo" (i = nwin: above every window), 2i + 1 for
+// "inside window i" (Sign 0); bands 2i all have Sign 1 except 2·nwin (Sign nwin + 1).
+PT_HD int vol_band(const DevVolume& v, double s) {
+    for (int i = 0; i < v.nwin; i++) {
+        if (s < v.windows[i].lo) return 2 * i;
+        if (s <= v.windows[i].hi) return 2 * i + 1;
+    }
+    return 2 * v.nwin;
+}
+// Host: fill out[(x0+1) + (y0+1)(w+1) + (z0+1)(w+1)(h+1)] for cells x0 in -1..w-1, y0 in -1..h-1,
+// z0 in -1..d-1 (a cell outside that range has every corner outside the grid: zero_sign).
+inline void vol_build_runs(const DevVolume& v, int8_t* out, int32_t& zero_sign) {
+    const int sx = v.w + 1, sy = v.h + 1, sz = v.d + 1;
+    auto sign_of_band = [&](int b) { return (b & 1) ? 0 : (b == 2 * v.nwin ? v.nwin + 1 : 1); };
+    zero_sign = sign_of_band(vol_band(v, 0.0));
+    for (int z0 = -1; z0 < v.d; z0++)
+        for (int y0 = -1; y0 < v.h; y0++)
+            for (int x0 = -1; x0 < v.w; x0++) {
+                double mn = 0, mx = 0;
+                bool first = true;
+                for (int c = 0; c < 8; c++) {
+                    const double g = vol_get(v, x0 + (c >> 2 & 1), y0 + (c >> 1 & 1), z0 + (c & 1));
+                    if (first || g < mn) mn = g;
+                    if (first || g > mx) mx = g;
+                    first = false;
+                }
+                const double margin = 1e-9 * (1.0 + fabs(mn) + fabs(mx));
+                const int b0 = vol_band(v, mn - margin), b1 = vol_band(v, mx + margin);
+                const int sg = (b0 == b1 && mn == mn && mx == mx) ? sign_of_band(b0) : 0;
+                out[(x0 + 1) + (size_t)(y0 + 1) * sx + (size_t)(z0 + 1) * sx * sy] = (int8_t)sg;
+                (void)sz;
+            }
+}
+// t after k more additions of step (a power of two) made one at a time, as Volume.Intersect's
+// `t += step`: inside one binade, with t's ulp dividing step, every partial sum is exact, so k·step
+// is added at once; the addition that crosses into the next binade rounds, and is made alone.
+PT_HD double t_after(double t, double step, long long k) {
+    while (k > 0) {
+        int e;
+        (void)frexp(t, &e);   // t in [2^(e-1), 2^e), t > 0
+        if (ldexp(1.0, e - 53) > step) {   // every addition rounds (t >= 2^44 at 1/512): one by one
+            for (; k > 0; k--) t += step;
+            break;
+        }
+        const double lim = ldexp(1.0, e);
+        const long long room = (long long)ceil((lim - t) / step) - 1;   // additions that stay below lim
+        if (room >= k) return t + (double)k * step;
+        t = t + (double)room * step;
+        t += step;   // into the next binade: rounded, as the reference's
+        k -= room + 1;
+    }
+    return t;
+}
+// The cell of march position t, with each index clamped to the band -2..dim (a clamped index is
+// a cell outside the grid); clamping keeps every index monotone along the ray.
+struct VolKey {
+    int x, y, z;
+};
+PT_HD VolKey vol_key(const DevVolume& v, v3 o, v3 d, double t) {
+    const v3 a = add(o, muls(d, t));   // Ray.Position, as vol_t's positions
+    double x = a.x, z = a.z;
+    z /= v.zscale;
+    x = ((x + 1) / 2) * (double)v.w;
+    const double y = ((z + 1) / 2) * (double)v.h;
+    z = ((z + 2) / 2) * (double)v.d;
+    auto cl = [](double c, int n) {   // floor, clamped to -2..n (non-finite: outside)
+        if (!(c > -2.0)) return -2;
+        if (!(c < (double)n)) return n;
+        return (int)floor(c);
+    };
+    return VolKey{cl(x, v.w), cl(y, v.h), cl(z, v.d)};
+}
+PT_HD int vol_key_sign(const DevVolume& v, VolKey k) {
+    if (k.x < -1 || k.y < -1 || k.z < -1 || k.x >= v.w || k.y >= v.h || k.z >= v.d) return v.zero_sign;
+    return v.runs[(k.x + 1) + (size_t)(k.y + 1) * (v.w + 1) + (size_t)(k.z + 1) * (v.w + 1) * (v.h + 1)];
+}
+// Positions k = 0, 1, ... from t (t_after(t, step, k)); kmax: the positions the loop still takes.
+// Returns how many leading positions lie in cells of Sign `sign` (> 0): kmax when all of them do.
+PT_HD long long vol_run(const DevVolume& v, v3 o, v3 d, double t, double step, int sign, long long kmax) {
+    if (!v.runs || sign <= 0 || kmax <= 0) return 0;
+    VolKey c = vol_key(v, o, d, t);
+    if (vol_key_sign(v, c) != sign) return 0;
+    // index directions along the ray (x from d.x; y and z from d.z / zscale)
+    const int dx = d.x > 0 ? 1 : (d.x < 0 ? -1 : 0);
+    const int sdz = d.z > 0 ? 1 : (d.z < 0 ? -1 : 0);
+    const int dz = v.zscale > 0 ? sdz : -sdz;
+    long long k0 = 0;
+    for (int guard = 0; guard < 4096; guard++) {
+        // outside the grid for good: every later cell is a zero cell
+        const bool gone = (c.x == v.w && dx >= 0) || (c.x == -2 && dx <= 0) || (c.y == v.h && dz >= 0) ||
+                          (c.y == -2 && dz <= 0) || (c.z == v.d && dz >= 0) || (c.z == -2 && dz <= 0);
+        if (gone) return kmax;
+        auto same = [&](long long k) {
+            const VolKey q = vol_key(v, o, d, t_after(t, step, k));
+            return q.x == c.x && q.y == c.y && q.z == c.z;
+        };
+        // estimate: the nearest lattice plane ahead on each axis, from the fp64 line
+        double tc = 1e300;
+        const double t0 = t_after(t, step, k0);
+        auto plane = [&](double p0, double dp, double target) {   // the lattice plane ahead on one axis
+            if (dp != 0) {
+                const double tt = (target - p0) / dp;
+                if (tt > t0 && tt < tc) tc = tt;
+            }
+        };
+        if (dx != 0) plane(o.x, d.x, 2.0 * (c.x + (dx > 0 ? 1 : 0)) / v.w - 1.0);
+        if (dz != 0) {
+            plane(o.z, d.z, v.zscale * (2.0 * (c.y + (dz > 0 ? 1 : 0)) / v.h - 1.0));
+            plane(o.z, d.z, v.zscale * (2.0 * (c.z + (dz > 0 ? 1 : 0)) / v.d - 2.0));
+        }
+        long long g = k0 + 1;
+        if (tc < 1e300) {
+            const double kk = floor((tc - t0) / step);
+            if (kk > 1 && kk < 1e15) g = k0 + (long long)kk;
+        }
+        if (g > kmax) g = kmax;
+        // the first k > k0 with another cell (or kmax): same() is true on [k0, first) and false after
+        long long lo = k0, hi;
+        if (g == kmax || !same(g)) {
+            hi = g;
+            for (long long s = 1; hi - lo > 1;) {   // gallop down from the estimate
+                const long long m = hi - s > lo ? hi - s : lo + 1;
+                if (same(m)) { lo = m; break; }
+                hi = m;
+                s *= 2;
+            }
+        } else {
+            lo = g;
+            for (long long s = 1;; s *= 2) {   // gallop up
+                const long long m = lo + s < kmax ? lo + s : kmax;
+                if (m == kmax || !same(m)) { hi = m; break; }
+                lo = m;
+            }
+        }
+        while (hi - lo > 1) {
+            const long long m = lo + (hi - lo) / 2;
+            if (same(m)) lo = m;
+            else hi = m;
+        }
+        if (hi >= kmax) return kmax;
+        c = vol_key(v, o, d, t_after(t, step, hi));
+        if (vol_key_sign(v, c) != sign) return hi;
+        k0 = hi;
+    }
+    return k0;   // (never: a ray crosses at most w + h + d + 6 planes)
+}
+// The positions the loop still takes from t: t_after(t, step, k) <= tmax and iters + k < 2^24.
+PT_HD long long vol_positions_left(double t, double step, double tmax, int iters) {
+    const long long cap = (1ll << 24) - iters;
+    if (cap <= 0 || !(t <= tmax)) return 0;
+    double est = floor((tmax - t) / step) + 1;
+    long long k = est < (double)cap ? (long long)est : cap;
+    if (k < 1) k = 1;
+    while (k > 1 && !(t_after(t, step, k - 1) <= tmax)) k--;   // the estimate is exact or one high
+    while (k < cap && t_after(t, step, k) <= tmax) k++;
+    return k;
+}
+
+// The positions from t the march can pass without acting (vol_run), given the running Sign, the
+// loop bound and the iterations so far; `all` is set when that is every position the loop has left
+// (the loop then ends with no hit).
+PT_HD long long vol_skip(const DevVolume& v, v3 o, v3 d, double t, double step, int sign, double tmax, int iters,
+                         bool& all) {
+    all = false;
+    if (!v.runs || sign <= 0 || vol_key_sign(v, vol_key(v, o, d, t)) != sign) return 0;
+    const long long left = vol_positions_left(t, step, tmax, iters);
+    const long long k = vol_run(v, o, d, t, step, sign, left);
+    all = k >= left;
+    return k;
+}
+
 // Volume.Intersect (Volume.cs:168-197).  The reference loop has no bound; 2^24 steps
 // stand in for it (a ray that needs more never finishes in the reference either).
 // `samples` (instrumentation, may be null): the Volume.Sample calls the march made.
@@ -364,6 +554,24 @@ PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr) 
         return vol_sign_of(v, vol_sample_cell(v, a.x, a.y, a.z, k));
     };
     for (double t = start; t <= tmax && iters < (1 << 24); t += step, iters++) {
+        if (PT_VOL_SKIP && v.runs) {
+            // the first position (its cell's Sign), or the last position's cell carries the running
+            // Sign: pass the run of positions that cannot act
+            int s = sign;
+            if (s < 0) s = vol_key_sign(v, vol_key(v, o, d, t));
+            else if (vol_key_sign(v, VolKey{k.x0, k.y0, k.z0}) != s) s = 0;
+            if (s > 0) {
+                bool all;
+                const long long kk = vol_skip(v, o, d, t, step, s, tmax, iters, all);
+                n += (uint32_t)kk;   // counted: the reference samples them
+                if (all) return done(kHitInf);
+                if (kk) {
+                    sign = s;
+                    t = t_after(t, step, kk);
+                    iters += (int)kk;
+                }
+            }
+        }
         const int sg = sign_at(t);
         if (sg == 0 || (sign >= 0 && sg != sign)) {
             t -= step;

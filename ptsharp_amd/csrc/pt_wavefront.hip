@@ -458,6 +458,31 @@ __device__ __forceinline__ bool tri_reach(const DevScene& S, v3 o, v3 invd, floa
 #ifndef PT_REFILL_IDLE
 #define PT_REFILL_IDLE 40   // closest hit: 8 / 16 / 24 / 32 / 40 / 48 measured on C4, 40 best
 #endif
+// Leaf turns (PT_LEAF_VOTE = T > 0).  A wave whose lanes sit partly at inner nodes and partly
+// at leaves runs both the node test and the leaf's triangle loop every step, and the triangle
+// loop (up to 3 Moeller-Trumbore tests with their fp64 tail) costs more VALU than the node
+// test.  With leaf turns the wave votes: a step is a leaf step only once T of its active lanes
+// wait at a leaf (or no active lane is at an inner node); otherwise it is a node step and the
+// leaf lanes keep their leaf for a later step.  Every ray still takes its own steps in its own
+// order, so hits are unchanged.  Wave-uniform call.
+#ifndef PT_LEAF_VOTE
+#define PT_LEAF_VOTE 0
+#endif
+__device__ __forceinline__ bool leaf_turn(bool act, bool leaf) {
+    const uint64_t am = __ballot(act), lm = __ballot(act && leaf);
+    const bool leaf_step = lm == am || (uint32_t)__popcll(lm) >= (uint32_t)PT_LEAF_VOTE;
+    return leaf == leaf_step;
+}
+// Prefetch (PT_PREFETCH): a node step that pushes a second child also reads one word of that
+// child's line, so the line is on its way to the L2 when the lane pops it (after the nearest
+// child's subtree).  An empty asm after the next step's loads keeps the word alive.
+#ifndef PT_PREFETCH
+#define PT_PREFETCH 0
+#endif
+__device__ __forceinline__ uint32_t line_of(const DevScene& S, bool tri, uint32_t ref) {
+    const bool leaf = (ref & 0x80000000u) != 0;
+    return tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu) : (leaf ? 0u : ref);
+}
 #ifndef PT_LANES_MIN_NODES
 #define PT_LANES_MIN_NODES 64
 #endif
@@ -507,6 +532,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     uint32_t kept = 0;
     const float inf = __int_as_float(0x7f800000);
     bool has = false, tri = false, more = true;
+    uint32_t pf_val = 0;   // PT_PREFETCH: the word read ahead (kept alive until the next step)
     int32_t pend = -1;    // FULL: a Volume record left for the wave's cooperative march (march_pending)
     bool mwait = false;   // FULL: this lane's traversal is done, its pending Volume not yet marched
     uint32_t i = 0, ref = 0;   // i: the ray's slot; bit 31 set = the ray misses the triangle BVH's root box
@@ -605,6 +631,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                   lane, q0, q1, q2, q3, q4, q5, q6);
         if (!has || (FULL && mwait)) continue;
 #else
+        if (PT_LEAF_VOTE && !leaf_turn(has && !(FULL && mwait), leaf)) continue;
         if (!has || (FULL && mwait)) continue;
         {   // one 128-B line, seven 16-B pieces, by a 32-bit offset into the one allocation of all
             // traversal lines (no per-BVH 64-bit base: the step loop then holds its state without
@@ -618,6 +645,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
         }
 #endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
+        if (PT_PREFETCH) asm volatile("" ::"v"(pf_val));
         bool pop = true;
         if (!leaf) {
             if (COUNT) ctr.nodes++;
@@ -633,6 +661,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                 push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
                 ref = v0;
                 pop = false;
+                if (PT_PREFETCH && k1 != inf) pf_val = __float_as_uint(S.lines[8u * line_of(S, tri, v1)].x);
             }
         } else if (tri) {
             const uint32_t cntl = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q0.x);
@@ -1085,6 +1114,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
     double tl = kHitInf;
     float tmax = 0.f;
+    uint32_t pf_val = 0;   // PT_PREFETCH: the word read ahead (kept alive until the next step)
     bool waiting = false;   // a root whose traversal is done, waiting for its tail helpers
 #if PT_SHADOW_HELP
     // The tail (queue drained): idle lanes take stack entries of busy lanes' rays and traverse
@@ -1224,6 +1254,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                   q3, q4, q5, q6);
         if (!has || waiting) continue;
 #else
+        if (PT_LEAF_VOTE && !leaf_turn(has && !waiting, leaf)) continue;
         if (!has || waiting) continue;
         {   // one 128-B line, seven 16-B pieces, by a 32-bit offset into the one allocation of all
             // traversal lines (no per-BVH 64-bit base: the step loop then holds its state without
@@ -1237,6 +1268,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
         }
 #endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
+        if (PT_PREFETCH) asm volatile("" ::"v"(pf_val));
         bool pop = true, blocked = false;
         if (!leaf) {
             if (COUNT) ctr.nodes++;
@@ -1252,6 +1284,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                 push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
                 ref = v0;
                 pop = false;
+                if (PT_PREFETCH && k1 != inf) pf_val = __float_as_uint(S.lines[8u * line_of(S, tri, v1)].x);
             }
         } else if (tri) {
             const uint32_t cntl = ((ref >> 29) & 3u) + 1u;

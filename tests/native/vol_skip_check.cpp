@@ -1,0 +1,137 @@
+// Host check of the Volume march skip (ptsharp_amd/csrc/pt_ext.h vol_run / vol_skip / t_after):
+// vol_t, which passes runs of uniform cells at once, against the reference loop of
+// Volume.Intersect (Volume.cs:168-197) restated here position by position, on seeded volumes
+// (smooth blobs with noise and exact-zero regions, the reference's narrow windows, Sample's
+// y-from-z slip) and seeded rays, bit for bit; and t_after against k repeated additions.
+// usage: vol_skip_check [rays per volume]   (exit status 1 on any difference)
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <chrono>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../../ptsharp_amd/csrc/pt_ext.h"
+
+using namespace pt;
+
+// Volume.Intersect as written: every position sampled
+static double naive_t(const DevVolume& v, v3 o, v3 d) {
+    double tmin, tmax;
+    box_span(v.bmin, v.bmax, o, d, tmin, tmax);
+    double step = (double)(1.0f / 512.0f);
+    const double start = net_max(step, tmin);
+    int sign = -1, iters = 0;
+    auto sg_at = [&](double t) { return vol_sign_of(v, vol_sample(v, (double)add(o, muls(d, t)).x, 0, (double)add(o, muls(d, t)).z)); };
+    for (double t = start; t <= tmax && iters < (1 << 24); t += step, iters++) {
+        const int s = sg_at(t);
+        if (s == 0 || (sign >= 0 && s != sign)) {
+            t -= step;
+            step /= 64;
+            t += step;
+            for (int i = 0; i < 64; i++) {
+                if (sg_at(t) == 0) return t - step;
+                t += step;
+            }
+        }
+        sign = s;
+    }
+    return kHitInf;
+}
+
+int main(int argc, char** argv) {
+    const int rays = argc > 1 ? atoi(argv[1]) : 20000;
+    std::mt19937_64 rng(12345);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    std::normal_distribution<double> N(0.0, 1.0);
+    long long bad = 0, total = 0, hits = 0;
+    double t_skip = 0, t_naive = 0;
+    // t_after against repeated addition, across binade crossings
+    for (int i = 0; i < 200000; i++) {
+        const double step = (i & 1) ? (double)(1.0f / 512.0f) : (double)(1.0f / 512.0f) / 64;
+        double t = std::ldexp(U(rng), (int)(U(rng) * 8) - 3) + step;
+        const long long k = (long long)(U(rng) * 3000);
+        double r = t;
+        for (long long j = 0; j < k; j++) r += step;
+        if (t_after(t, step, k) != r) {
+            if (bad < 5) printf("t_after(%.17g, %g, %lld) = %.17g, repeated %.17g\n", t, step, k, t_after(t, step, k), r);
+            bad++;
+        }
+    }
+    printf("t_after: 200000 cases, %lld differences\n", bad);
+    const int dims[][3] = {{32, 32, 16}, {16, 16, 8}, {48, 48, 24}, {7, 5, 3}};
+    const double zscales[] = {3.4 / 0.9765625, 1.0, 0.37};
+    int vi = 0;
+    for (const auto& dm : dims)
+        for (double zs : zscales) {
+            const int w = dm[0], h = dm[1], dd = dm[2];
+            std::vector<double> data((size_t)w * h * dd);
+            for (int z = 0; z < dd; z++)
+                for (int y = 0; y < h; y++)
+                    for (int x = 0; x < w; x++) {   // volume_slices-like: blob + noise, clipped, 8-bit
+                        const double X = 2.0 * x / (w - 1) - 1, Y = 2.0 * y / (h - 1) - 1, Z = 2.0 * z / (dd - 1) - 1;
+                        const double r2 = X * X + 1.3 * Y * Y + 0.8 * Z * Z;
+                        double f = 0.75 * std::exp(-1.5 * r2) + 0.08 * N(rng);
+                        if ((vi & 1) && X > 0.3) f = 0;   // exact-zero slab
+                        f = std::fmin(std::fmax(std::round(f * 255), 0.0), 255.0) / 255;
+                        data[(size_t)x + (size_t)y * w + (size_t)z * w * h] = f;
+                    }
+            std::vector<DevWindow> win;
+            for (int i = 0; i < 5; i++) {
+                const double lo = (double)(0.2f + 0.1f * (float)i);
+                win.push_back(DevWindow{lo, (double)((float)lo + 0.01f), i, 0});
+            }
+            DevVolume v{};
+            v.data = data.data();
+            v.windows = win.data();
+            v.w = w; v.h = h; v.d = dd; v.nwin = (int)win.size();
+            v.zscale = zs;
+            const float bmn[3] = {-1, -1, -0.2f}, bmx[3] = {1, 1, 1};
+            for (int k = 0; k < 3; k++) { v.bmin[k] = bmn[k]; v.bmax[k] = bmx[k]; }
+            std::vector<int8_t> runs((size_t)(w + 1) * (h + 1) * (dd + 1));
+            vol_build_runs(v, runs.data(), v.zero_sign);
+            v.runs = runs.data();
+            long long uni = 0;
+            for (int8_t r : runs) uni += r != 0;
+            long long vbad = 0;
+            for (int i = 0; i < rays; i++) {
+                v3 o, dir;
+                const int kind = i % 5;
+                o = v3{(float)(U(rng) * 4 - 2), (float)(U(rng) * 4 - 2), (float)(U(rng) * 3 - 1.2)};
+                v3 aim{(float)(U(rng) * 2 - 1), (float)(U(rng) * 2 - 1), (float)(U(rng) * 1.2 - 0.2)};
+                dir = normalize(sub(aim, o));
+                if (kind == 1) dir = normalize(v3{dir.x, dir.y, 0.0f});    // d.z = 0
+                if (kind == 2) dir = normalize(v3{0.0f, dir.y, dir.z});    // d.x = 0
+                if (kind == 3) o = aim;                                   // origin inside the box
+                if (kind == 4) {   // grazing: nearly parallel to the x planes, origin on a lattice plane
+                    dir = normalize(v3{(float)(1e-6 * (U(rng) - 0.5)), dir.y, dir.z});
+                    if (i & 8) o.x = (float)(2.0 * (int)(U(rng) * w) / w - 1.0);
+                }
+                if (!(dir.x == dir.x)) continue;
+                uint32_t n = 0;
+                const auto c0 = std::chrono::steady_clock::now();
+                const double a = vol_t(v, o, dir, &n);
+                const auto c1 = std::chrono::steady_clock::now();
+                const double b = naive_t(v, o, dir);
+                const auto c2 = std::chrono::steady_clock::now();
+                t_skip += std::chrono::duration<double>(c1 - c0).count();
+                t_naive += std::chrono::duration<double>(c2 - c1).count();
+                total++;
+                hits += b < kHitInf;
+                if (a != b && !(a != a && b != b)) {
+                    if (vbad < 5)
+                        printf("vol %d ray %d: skip %.17g naive %.17g  o=(%a,%a,%a) d=(%a,%a,%a)\n", vi, i, a, b, o.x, o.y, o.z,
+                               dir.x, dir.y, dir.z);
+                    vbad++;
+                }
+            }
+            printf("volume %dx%dx%d zscale %.4g: %lld of %zu cells uniform, zero sign %d, %d rays, %lld differences\n", w, h,
+                   dd, zs, uni, runs.size(), v.zero_sign, rays, vbad);
+            bad += vbad;
+            vi++;
+        }
+    printf("%lld rays, %lld hits, %lld differences; vol_t %.3f s, the loop as written %.3f s\n", total, hits, bad, t_skip,
+           t_naive);
+    return bad ? 1 : 0;
+}

@@ -1,0 +1,20 @@
+"""The Volume march skip (ptsharp_amd/csrc/pt_ext.h vol_run / vol_skip / t_after), host build:
+vol_t, which passes runs of uniform cells at once, equals Volume.Intersect's loop as written
+(Volume.cs:168-197, restated position by position in tests/native/vol_skip_check.cpp) bit for bit
+on seeded volumes and rays, including grazing rays and rays along lattice planes; t_after equals
+k repeated fp64 additions across binade crossings."""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(ROOT, "tests", "native")
+
+
+def test_vol_skip_bit_identical():
+    subprocess.run(["make", "-s", "-C", NATIVE, "vol_skip_check"], check=True)
+    r = subprocess.run([os.path.join(NATIVE, "_build", "vol_skip_check"), "4000"], capture_output=True, text=True,
+                       timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "t_after: 200000 cases, 0 differences" in r.stdout
+    assert " 0 differences;" in r.stdout.splitlines()[-1]
