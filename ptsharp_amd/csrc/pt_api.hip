@@ -1220,6 +1220,9 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     // C4's floor cube and two light spheres: a linear test of 3 records at refill costs less than a BVH
     // node step (seven loads through the texture path) and leaf record loads per ray
     S.ana_linear = (na > 0 && na <= (size_t)PT_ANA_LINEAR && !S.full_geom) ? 1 : 0;
+    S.lights_lean = 1;
+    for (const pt::DevLight& L : lights)
+        if (!L.phantom && (L.kind == pt::KIND_SDF || L.kind == pt::KIND_VOLUME || L.kind == pt::KIND_XFORM)) S.lights_lean = 0;
     S.num_planes = (int32_t)plane_scene.size();
     S.num_lights = (int32_t)lights.size();
     for (int k = 0; k < 3; k++) S.env[k] = d->env_color[k];

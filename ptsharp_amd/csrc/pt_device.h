@@ -436,18 +436,10 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     auto sign_at = [&](double tt) { return vol_sign(v, add(o, muls(d, tt))); };
     for (;;) {   // wave-uniform: every branch below is on ballots
         if (PT_VOL_SKIP && v.runs) {   // pass a run of positions that cannot act (pt_ext.h vol_run)
-            const int s = sign < 0 ? vol_key_sign(v, vol_key(v, o, d, t)) : sign;
-            if (s > 0) {
-                bool all;
-                const long long kk = vol_skip(v, o, d, t, step, s, tmax, iters, all);   // the same on every lane
-                samples += (uint32_t)kk;
-                if (all) return kHitInf;
-                if (kk) {
-                    sign = s;
-                    t = t_after(t, step, kk);
-                    iters += (int)kk;
-                }
-            }
+            const VolSkip r = vol_skip(v, o, d, t, step, sign, tmax, iters);   // the same on every lane
+            samples += r.k;
+            if (r.all) return kHitInf;
+            t = r.t; sign = r.sign; iters = r.iters;
         }
         const double tk = march_pos(t, step, rank, march_exact(t, step));
         const bool valid = tk <= tmax && iters + rank < (1 << 24);   // a prefix of the ranks (t grows)
@@ -631,6 +623,64 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         if (blocked) return false;
     }
     return true;
+}
+
+// Split traversal (scenes with §8f row 4 shapes and a large triangle BVH, pt_wavefront.hip
+// "split"): the lean refill kernels take the planes and the triangle BVH, then the FULL kernel
+// takes the analytic BVH of the same ray, starting from that hit.  Scene.Intersect visits planes,
+// the analytic BVH, then the triangles, each replacing the best only when strictly nearer, so an
+// analytic hit beats a triangle at an equal t and loses to a plane at an equal t: with a triangle
+// best its t is raised by one ulp for the analytic pass (no double lies between), and restored
+// when no analytic hit took it.  The triangles the refill kernel found without the analytic
+// hit's tighter bound are the same: a bound only prunes, it never reorders the visits.
+template <bool COUNT, class STK>
+__device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const STK& stack, Counters& ctr, HitRec& best) {
+    const double t_in = best.t;
+    const bool tri_best = best.kind == KIND_TRI;
+    if (tri_best) best.t = nextafter(best.t, (double)INFINITY);
+    v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    int32_t pend = -1;
+    if (S.ana_linear) {
+        for (int p = 0; p < S.ana_count; p++) {
+            if (COUNT) ctr.prims++;
+            int32_t kind;
+            double tx = 0;
+            const double t = prim_t<false, true>(S, S.ana_recs, (uint32_t)p, o, d, kind, &tx);
+            if (t < best.t) { best.t = t; best.kind = kind; best.idx = p; best.tx = tx; }
+        }
+    } else {
+        traverse<false, COUNT, false, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr, &pend);
+    }
+    if (PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
+    if (best.kind == KIND_TRI && tri_best) best.t = t_in;
+}
+// The analytic half of a split shadow query (light_visible's analytic part): is any analytic
+// primitive strictly nearer than the light?  The refill kernel already cleared the planes and
+// the triangles.
+template <bool COUNT, class STK>
+__device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L, v3 o, v3 d, const STK& stack,
+                                            Counters& ctr) {
+    const double tl = light_t<true>(S, L, o, d);
+    if (!(tl < kHitInf)) return true;   // (the refill kernel found it lit, so tl is finite)
+    HitRec best{tl, -1, -1};
+    v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    int32_t pend = -1;
+    if (S.ana_linear) {
+        for (int p = 0; p < S.ana_count; p++) {
+            if (COUNT) ctr.prims++;
+            int32_t kind;
+            if (prim_t<false, true>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return true;
+        }
+    } else if (traverse<false, COUNT, true, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
+                                                   &pend)) {
+        return true;
+    }
+    if (PT_COOP_MARCH) {
+        bool blocked = false;
+        march_pending<true>(S, o, d, pend, best, &blocked);
+        if (blocked) return true;
+    }
+    return false;
 }
 
 // ---------------------------------------------------------------- textures (§8f row 3)

@@ -345,7 +345,7 @@ PT_HD int vol_material(const DevVolume& v, v3 p, int default_mat) {
 }
 // ---------------------------------------------------------------- Volume march skipping
 #ifndef PT_VOL_SKIP
-#define PT_VOL_SKIP 1   // 0: march every position (the reference loop as written)
+#define PT_VOL_SKIP 0   // 1: the cooperative march passes runs of uniform cells (measured slower on C5)
 #endif
 // Volume.Intersect acts at a march position only when its Sign is 0 or differs from the last
 // one.  Sample is a convex combination of its cell's eight corners, so a cell whose corner range
@@ -515,23 +515,42 @@ PT_HD long long vol_positions_left(double t, double step, double tmax, int iters
     return k;
 }
 
-// The positions from t the march can pass without acting (vol_run), given the running Sign, the
-// loop bound and the iterations so far; `all` is set when that is every position the loop has left
-// (the loop then ends with no hit).
-PT_HD long long vol_skip(const DevVolume& v, v3 o, v3 d, double t, double step, int sign, double tmax, int iters,
-                         bool& all) {
-    all = false;
-    if (!v.runs || sign <= 0 || vol_key_sign(v, vol_key(v, o, d, t)) != sign) return 0;
+// The positions from t the march can pass without acting (vol_run), given the running Sign (-1
+// before the first position: then the first cell's), the loop bound and the iterations so far.
+// Returned: the positions passed (k), the march's t, Sign and iterations after them, and `all`
+// when that is every position the loop has left (the loop then ends with no hit).  Taken by the
+// cooperative march only (coop_vol_t, inside the non-inlined coop_record_t): inlined into the
+// FULL traversal kernels' own march, or made a call, it cost their step loops spills.
+#define PT_HD_CALL PT_HD
+struct VolSkip {
+    double t;
+    uint32_t k;
+    int32_t sign, iters, all;
+};
+PT_HD_CALL VolSkip vol_skip(const DevVolume& v, v3 o, v3 d, double t, double step, int sign, double tmax, int iters) {
+    VolSkip r{t, 0u, sign, iters, 0};
+    if (!v.runs) return r;
+    const int s = vol_key_sign(v, vol_key(v, o, d, t));
+    if (s <= 0 || (sign >= 0 && s != sign)) return r;
     const long long left = vol_positions_left(t, step, tmax, iters);
-    const long long k = vol_run(v, o, d, t, step, sign, left);
-    all = k >= left;
-    return k;
+    const long long k = vol_run(v, o, d, t, step, s, left);
+    r.all = k >= left;
+    if (k > 0) {
+        r.k = (uint32_t)k;
+        r.sign = s;
+        r.t = t_after(t, step, k);
+        r.iters = iters + (int)k;
+    }
+    return r;
 }
 
 // Volume.Intersect (Volume.cs:168-197).  The reference loop has no bound; 2^24 steps
 // stand in for it (a ray that needs more never finishes in the reference either).
 // `samples` (instrumentation, may be null): the Volume.Sample calls the march made.
-PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr) {
+// skip: pass runs of uniform cells (vol_skip); the traversal kernels' per-lane march leaves it
+// off (its registers would cost their step loops), the cooperative march (coop_vol_t) and the
+// host paths take it.
+PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr, bool skip = false) {
 #ifdef PT_PROBE_NO_VOL   // timing probe only (wrong images): Volumes never hit
     if (samples) return kHitInf;
 #endif
@@ -554,23 +573,13 @@ PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr) 
         return vol_sign_of(v, vol_sample_cell(v, a.x, a.y, a.z, k));
     };
     for (double t = start; t <= tmax && iters < (1 << 24); t += step, iters++) {
-        if (PT_VOL_SKIP && v.runs) {
-            // the first position (its cell's Sign), or the last position's cell carries the running
-            // Sign: pass the run of positions that cannot act
-            int s = sign;
-            if (s < 0) s = vol_key_sign(v, vol_key(v, o, d, t));
-            else if (vol_key_sign(v, VolKey{k.x0, k.y0, k.z0}) != s) s = 0;
-            if (s > 0) {
-                bool all;
-                const long long kk = vol_skip(v, o, d, t, step, s, tmax, iters, all);
-                n += (uint32_t)kk;   // counted: the reference samples them
-                if (all) return done(kHitInf);
-                if (kk) {
-                    sign = s;
-                    t = t_after(t, step, kk);
-                    iters += (int)kk;
-                }
-            }
+        if (skip && v.runs && (sign < 0 || vol_key_sign(v, VolKey{k.x0, k.y0, k.z0}) == sign)) {
+            // the first position, or the last position's cell carries the running Sign: pass the
+            // run of positions that cannot act
+            const VolSkip r = vol_skip(v, o, d, t, step, sign, tmax, iters);
+            n += r.k;   // counted: the reference samples them
+            if (r.all) return done(kHitInf);
+            t = r.t; sign = r.sign; iters = r.iters;
         }
         const int sg = sign_at(t);
         if (sg == 0 || (sign >= 0 && sg != sign)) {

@@ -55,14 +55,15 @@ struct WfQueues {
 constexpr int kCountStride = PT_COUNT_STRIDE;
 static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
 constexpr int kFetchSlot = 2 * kParts;
-constexpr int kKeptSlot = 6 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
-constexpr int kEndSlot = 6 * kParts + 2;
+constexpr int kKeptSlot = 9 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
+constexpr int kEndSlot = 9 * kParts + 2;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kCountWords = count_word(kEndSlot);
 constexpr int kChunkResetWords = kCountWords;   // every slot is zeroed per chunk
 constexpr int kOverflowCounter = 15;            // DevBuffer::counters word of WfQueues::overflow
-// work-fetch cursor of kernel k (0 trace, 1 shade, 2 + q shadow rays of set q) in partition g
+// work-fetch cursor of kernel k (0 trace, 1 shade, 2 + q shadow rays of set q, 4 the analytic phase
+// of a split closest hit, 5 + q that of split shadow rays of set q; pt_wavefront.hip "split") in partition g
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
 

@@ -310,18 +310,20 @@ __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQ
 #ifndef PT_TRACE_WAVES
 #define PT_TRACE_WAVES 7
 #endif
-template <bool COUNT, bool FULL>
+// SPLIT (FULL only): the analytic half of a split closest hit (pt_device.h trace_ana): the refill
+// kernel left the planes' and triangles' hit in Q.hits; this pass adds the analytic BVH's.
+template <bool COUNT, bool FULL, bool SPLIT = false>
 __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) void k_wf_trace(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
-    if (blockIdx.x == 0 && threadIdx.x < kParts) {
+    if (!SPLIT && blockIdx.x == 0 && threadIdx.x < kParts) {
         *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
         Q.counts[fetch_word(1, threadIdx.x)] = 0u;               // k_wf_shade's fetch cursors
     }
     const Group G = xcd_group();
     const uint32_t cnt = *ray_count(Q, qi, G.g);
     const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
-    uint32_t* cursor = Q.counts + fetch_word(0, G.g);
+    uint32_t* cursor = Q.counts + fetch_word(SPLIT ? 4 : 0, G.g);
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
     const bool env_black = (!FULL_SHADE_ENV(S)) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
@@ -343,7 +345,17 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
                 continue;
             }
             float4 a = nt_load(&Q.q_o[qi][i]);
-            HitRec h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+            HitRec h;
+            if constexpr (SPLIT) {
+                const uint4 r = Q.hits[i];   // the planes' and triangles' hit (k_wf_trace_lanes, split)
+                h.t = __longlong_as_double((long long)(((unsigned long long)r.y << 32) | r.x));
+                h.kind = (int32_t)r.z;
+                h.idx = (int32_t)r.w;
+                h.tx = h.t;
+                trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h);
+            } else {
+                h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+            }
             kept += (h.kind >= 0 || !env_black) ? 1u : 0u;
             // a TransformedShape hit keeps its inner object-space t, what Hit.Info needs (HitRec::tx)
             unsigned long long tb = (unsigned long long)__double_as_longlong(FULL && h.kind == KIND_XFORM ? h.tx : h.t);
@@ -483,6 +495,9 @@ __device__ __forceinline__ uint32_t line_of(const DevScene& S, bool tri, uint32_
     const bool leaf = (ref & 0x80000000u) != 0;
     return tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu) : (leaf ? 0u : ref);
 }
+#ifndef PT_SPLIT
+#define PT_SPLIT 1   // row-4 scenes with a triangle BVH: split traversal (depth_loop)
+#endif
 #ifndef PT_LANES_MIN_NODES
 #define PT_LANES_MIN_NODES 64
 #endif
@@ -508,8 +523,11 @@ constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
 #ifndef PT_FULL_LANES
 #define PT_FULL_LANES 0   // 1: row-4 scenes with a mesh take these (C5 634 vs 667 Mrays/s lockstep: DESIGN §8)
 #endif
+// split: the planes and the triangle BVH only (the refill half of a split closest hit; the FULL
+// k_wf_trace<.., SPLIT> pass adds the analytic BVH and counts the kept rays).
 template <bool COUNT, bool FULL>
-__device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q, int qi, unsigned long long* counters) {
+__device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q, int qi, unsigned long long* counters,
+                                            int split) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
 #if PT_COOP
     __shared__ float4 s_coop[kCoopRows];
@@ -544,7 +562,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     auto finish = [&]() {
         unsigned long long tb = (unsigned long long)__double_as_longlong(FULL && bkind == KIND_XFORM ? btx : bt);
         hit_store(&Q.hits[i & 0x7FFFFFFFu], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
-        kept += (bkind >= 0 || !env_black) ? 1u : 0u;
+        if (!split) kept += (bkind >= 0 || !env_black) ? 1u : 0u;
         has = false;
     };
     for (;;) {
@@ -617,7 +635,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                     ref = 0;
                     // tested at the refill's bound (planes only), kept as a bit of i: no register for it
                     if (!tri_reach(S, o, invd, tmax)) i |= 0x80000000u;
-                    tri = S.ana_linear || S.ana_num_nodes <= 0;
+                    tri = split || S.ana_linear || S.ana_num_nodes <= 0;
                     if (tri && (i >> 31)) finish();   // (FULL scenes traverse the analytic BVH first: tri false)
                 }
             }
@@ -722,12 +740,12 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     }
 }
 template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
-    trace_lanes<COUNT, false>(S, Q, qi, counters);
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters, int split) {
+    trace_lanes<COUNT, false>(S, Q, qi, counters, split);
 }
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_FULL_LANES_VGPRS))) void k_wf_trace_lanes_full(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
-    trace_lanes<COUNT, true>(S, Q, qi, counters);
+    trace_lanes<COUNT, true>(S, Q, qi, counters, 0);
 }
 
 // ---------------------------------------------------------------- shade / bounce
@@ -952,6 +970,8 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         Q.counts[fetch_word(2 + (1 - qi), threadIdx.x)] = 0u;   // the fetch cursors of the shadow rays it writes
         Q.counts[fetch_word(0, threadIdx.x)] = 0u;              // the next k_wf_trace's (it may run beside k_wf_shadow)
+        Q.counts[fetch_word(4, threadIdx.x)] = 0u;              // its analytic half's (split)
+        Q.counts[fetch_word(5 + (1 - qi), threadIdx.x)] = 0u;   // the split shadow rays' analytic half
         if (threadIdx.x == 0) Q.counts[kept_word(1 - qi)] = 0u;   // the next k_wf_trace's kept count
     }
     const Group G = xcd_group();
@@ -1049,14 +1069,15 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
 #endif
 // One thread per shadow ray that k_wf_shade set up (light, direction, the colour the
 // light adds if it is the nearest hit): the visibility query of Sampler.cs:261-265.
-template <bool COUNT, bool FULL>
+// SPLIT (FULL only): the analytic half of split shadow rays: the rays the refill kernel left lit.
+template <bool COUNT, bool FULL, bool SPLIT = false>
 __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
     const uint32_t cnt = *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
-    uint32_t* cursor = Q.counts + fetch_word(2 + qo, G.g);
+    uint32_t* cursor = Q.counts + fetch_word(SPLIT ? 5 + qo : 2 + qo, G.g);
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
     for (;;) {  // kFetchBatches × 64 rays per claim, 64 at a time (see k_wf_trace)
@@ -1067,10 +1088,14 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
         for (uint32_t k0 = kc; k0 < kc + 64u * kFetchBatches && k0 < n; k0 += 64u) {
             const uint32_t i = base + k0 + lane;
             if (k0 + lane >= n) continue;
+            if (SPLIT && Q.n_lit[qo][i] == 0) continue;   // blocked (or dead) in the refill half
             bool lit = false;
             const float4 b = nt_load(&Q.n_n[qo][i]);
             const uint32_t li = __float_as_uint(b.w);
-            if (li != kDead) {
+            if (SPLIT) {
+                const float4 a = nt_load(&Q.n_o[qo][i]);
+                if (!ana_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) continue;
+            } else if (li != kDead) {
                 const float4 a = nt_load(&Q.n_o[qo][i]);
                 const DevLight L = S.lights[li];
                 lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
@@ -1093,8 +1118,11 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // light's own t and the planes at refill, then one step loop over the analytic BVH and
 // the triangle BVH, any-hit (a primitive strictly nearer than the light ends the ray
 // unlit).  The outcome goes to n_lit; k_wf_nee_accum adds the lit rays' terms.
+// split: the planes and the triangle BVH only; the FULL k_wf_shadow<.., SPLIT> pass then tests the
+// analytic BVH of the rays left lit.
 template <bool COUNT, bool FULL>
-__device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters) {
+__device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters,
+                                             int split) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
 #if PT_COOP
     __shared__ float4 s_coop[kCoopRows];
@@ -1177,7 +1205,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                                 int32_t kind;
                                 if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) run = false;
                             }
-                        tri = S.ana_linear || S.ana_num_nodes <= 0;
+                        tri = split || S.ana_linear || S.ana_num_nodes <= 0;
                     }
                     tmax = tmax_bound(tl);
                     sp = 0;
@@ -1358,12 +1386,12 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     }
 }
 template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
-    shadow_lanes<COUNT, false>(S, Q, qo, counters);
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters, int split) {
+    shadow_lanes<COUNT, false>(S, Q, qo, counters, split);
 }
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_FULL_LANES_VGPRS))) void k_wf_shadow_lanes_full(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
-    shadow_lanes<COUNT, true>(S, Q, qo, counters);
+    shadow_lanes<COUNT, true>(S, Q, qo, counters, 0);
 }
 
 // ---------------------------------------------------------------- direct-light terms
@@ -1572,18 +1600,36 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
     const bool lanes = plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes && (PT_FULL_LANES || !fullg);
     const bool lanes_sh = plan.lanes >= 0 ? plan.lanes == 1
                                           : S.tri_num_nodes > kLanesMinNodes && (PT_FULL_LANES_SHADOW || !fullg);
+    // Split traversal (row-4 scenes with a triangle BVH): the lean refill kernels take the planes and
+    // the triangles at their occupancy, then the FULL lockstep kernels add the analytic BVH (where
+    // the §8f row-4 shapes live) from that result (pt_device.h trace_ana / ana_blocked).  Shadow rays
+    // split only when every light's own t is a lean intersect (spheres, cubes, planes).
+    const bool split = PT_SPLIT && plan.lanes < 0 && fullg && !PT_FULL_LANES && S.tri_num_nodes > kLanesMinNodes;
+    const bool split_sh = split && !PT_FULL_LANES_SHADOW && S.lights_lean;
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
+        begin_k(1, stream);
+        if (split) {
+            const unsigned tl = grid_for(n, kTB, plan.lanes_trace_blocks), ta = grid_for(n, kTB, plan.full_trace_blocks);
+            if (count) {
+                hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters, 1);
+                hipLaunchKernelGGL((k_wf_trace<true, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+            } else {
+                hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters, 1);
+                hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+            }
+            end_k(1, stream);
+            return;
+        }
         const unsigned tg = grid_for(n, kTB, fullg ? (lanes ? plan.full_lanes_trace_blocks : plan.full_trace_blocks)
                                                   : lanes ? plan.lanes_trace_blocks : plan.trace_blocks);
-        begin_k(1, stream);
         if (fullg && lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes_full<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (fullg && lanes) hipLaunchKernelGGL((k_wf_trace_lanes_full<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
 #ifndef PT_NO_TRACE_LANES
-        else if (lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-        else if (lanes) hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters, 0);
+        else if (lanes) hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters, 0);
 #endif
         else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
@@ -1618,13 +1664,23 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
                                      fullg ? (lanes_sh ? plan.full_lanes_shadow_blocks : plan.full_shadow_blocks)
                                            : lanes_sh ? plan.lanes_shadow_blocks : plan.shadow_blocks);
         begin_k(3, side);
-        if (fullg && lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes_full<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        if (split_sh) {
+            const unsigned hl = grid_for(children * plan.lights_per_child, kTB, plan.lanes_shadow_blocks);
+            const unsigned ha = grid_for(children * plan.lights_per_child, kTB, plan.full_shadow_blocks);
+            if (count) {
+                hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters, 1);
+                hipLaunchKernelGGL((k_wf_shadow<true, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+            } else {
+                hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters, 1);
+                hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+            }
+        } else if (fullg && lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes_full<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg && lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes_full<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
 #ifndef PT_NO_SHADOW_LANES
-        else if (lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-        else if (lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters, 0);
+        else if (lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters, 0);
 #endif
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);

@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
                 if (!(dir.x == dir.x)) continue;
                 uint32_t n = 0;
                 const auto c0 = std::chrono::steady_clock::now();
-                const double a = vol_t(v, o, dir, &n);
+                const double a = vol_t(v, o, dir, &n, PT_VOL_SKIP != 0);
                 const auto c1 = std::chrono::steady_clock::now();
                 const double b = naive_t(v, o, dir);
                 const auto c2 = std::chrono::steady_clock::now();
