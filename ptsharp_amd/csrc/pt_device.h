@@ -414,6 +414,32 @@ __device__ __forceinline__ bool march_exact(double t, double step) {   // t > 0
     (void)frexp(t, &e);   // t in [2^(e-1), 2^e), ulp 2^(e-53)
     return ldexp(1.0, e - 53) <= step && t + 63.0 * step < ldexp(1.0, e);
 }
+// The Sign of march position t: a uniform cell's (pt_ext.h vol_build_runs: every sample in it has
+// that Sign) without the eight corner loads and the interpolation, else Volume.Sign of the sample.
+__device__ __forceinline__ int vol_sign_fast(const DevVolume& v, v3 o, v3 d, double t) {
+    if (PT_VOL_TABLE && v.runs) {
+        const int s = vol_key_sign(v, vol_key(v, o, d, t));
+        if (s > 0) return s;
+    }
+    return vol_sign(v, add(o, muls(d, t)));
+}
+// Every cell of the index box spanned by cells a and b (at most one step apart per axis) has
+// Sign `sign`: then every position between a position in a and a later one in b lies in such a
+// cell (each index is monotone along the ray, so the cells between lie in that box).
+__device__ __forceinline__ bool vol_box_sign(const DevVolume& v, VolKey a, VolKey b, int sign) {
+    const int x0 = min(a.x, b.x), y0 = min(a.y, b.y), z0 = min(a.z, b.z);
+    const int nx = max(a.x, b.x) - x0, ny = max(a.y, b.y) - y0, nz = max(a.z, b.z) - z0;
+    if (nx > 1 || ny > 1 || nz > 1) return false;
+    for (int c = 0; c < 8; c++) {
+        const int dx = c & 1, dy = (c >> 1) & 1, dz = c >> 2;
+        if (dx > nx || dy > ny || dz > nz) continue;
+        if (vol_key_sign(v, VolKey{x0 + dx, y0 + dy, z0 + dz}) != sign) return false;
+    }
+    return true;
+}
+#ifndef PT_VOL_STRIDE
+#define PT_VOL_STRIDE 16   // the strided pass's positions per lane (0: off)
+#endif
 // Every active lane passes the same (v, o, d); returns vol_t(v, o, d) to all of them and, in
 // `samples`, the Volume.Sample calls vol_t makes (instrumentation).
 __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& samples) {
@@ -433,13 +459,37 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     double t = net_max(step, tmin);
     int sign = -1, iters = 0;
     samples = 0;
-    auto sign_at = [&](double tt) { return vol_sign(v, add(o, muls(d, tt))); };
+    auto sign_at = [&](double tt) { return vol_sign_fast(v, o, d, tt); };
     for (;;) {   // wave-uniform: every branch below is on ballots
         if (PT_VOL_SKIP && v.runs) {   // pass a run of positions that cannot act (pt_ext.h vol_run)
             const VolSkip r = vol_skip(v, o, d, t, step, sign, tmax, iters);   // the same on every lane
             samples += r.k;
             if (r.all) return kHitInf;
             t = r.t; sign = r.sign; iters = r.iters;
+        }
+        // Strided pass over runs of uniform cells: lane of rank r looks at position (r + 1)·S from
+        // t; when the cells of consecutive looked-at positions (and of position 0) span only cells
+        // of the running Sign, no position up to there can act, and the march moves past them,
+        // 64·S positions per round.  The positions are the reference's repeated additions (t_after).
+        while (PT_VOL_STRIDE > 0 && v.runs) {   // wave-uniform
+            const VolKey k0 = vol_key(v, o, d, t);
+            const int s0 = vol_key_sign(v, k0);
+            if (s0 <= 0 || (sign >= 0 && s0 != sign)) break;
+            const int off = (rank + 1) * PT_VOL_STRIDE;
+            const double tr = t_after(t, step, off);
+            const bool valid = tr <= tmax && iters + off < (1 << 24);
+            const VolKey kr = vol_key(v, o, d, tr);
+            VolKey kp{__shfl(kr.x, prev_lane, 64), __shfl(kr.y, prev_lane, 64), __shfl(kr.z, prev_lane, 64)};
+            if (rank == 0) kp = k0;
+            const uint64_t unsafe = __ballot(!(valid && vol_box_sign(v, kp, kr, s0)));
+            const int f = unsafe ? __popcll(act & ((1ull << __builtin_ctzll(unsafe)) - 1ull)) : nact;   // safe ranks
+            if (f == 0) break;
+            const int k = f * PT_VOL_STRIDE + 1;   // positions 0 .. f·S: all of Sign s0
+            samples += (uint32_t)k;   // counted: the reference samples them
+            t = t_after(t, step, k);
+            iters += k;
+            sign = s0;
+            if (f < nact) break;
         }
         const double tk = march_pos(t, step, rank, march_exact(t, step));
         const bool valid = tk <= tmax && iters + rank < (1 << 24);   // a prefix of the ranks (t grows)

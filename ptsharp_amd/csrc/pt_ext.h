@@ -344,6 +344,9 @@ PT_HD int vol_material(const DevVolume& v, v3 p, int default_mat) {
     return bm;
 }
 // ---------------------------------------------------------------- Volume march skipping
+#ifndef PT_VOL_TABLE
+#define PT_VOL_TABLE 1   // the cooperative march reads a uniform cell's Sign from its table entry
+#endif
 #ifndef PT_VOL_SKIP
 #define PT_VOL_SKIP 0   // 1: the cooperative march passes runs of uniform cells (measured slower on C5)
 #endif

@@ -4,6 +4,7 @@
 // (smooth blobs with noise and exact-zero regions, the reference's narrow windows, Sample's
 // y-from-z slip) and seeded rays, bit for bit; and t_after against k repeated additions.
 // usage: vol_skip_check [rays per volume]   (exit status 1 on any difference)
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -40,12 +41,95 @@ static double naive_t(const DevVolume& v, v3 o, v3 d) {
     return kHitInf;
 }
 
+// pt_device.h coop_vol_t with its strided pass over uniform runs (PT_VOL_STRIDE) and the table
+// Sign (vol_sign_fast), its 64 lanes as loops: lane r of a round takes the r-th position.
+static int sign_fast(const DevVolume& v, v3 o, v3 d, double t) {
+    const int s = vol_key_sign(v, vol_key(v, o, d, t));
+    if (s > 0) return s;
+    return vol_sign(v, add(o, muls(d, t)));
+}
+static bool box_sign(const DevVolume& v, VolKey a, VolKey b, int sign) {
+    const int x0 = std::min(a.x, b.x), y0 = std::min(a.y, b.y), z0 = std::min(a.z, b.z);
+    const int nx = std::max(a.x, b.x) - x0, ny = std::max(a.y, b.y) - y0, nz = std::max(a.z, b.z) - z0;
+    if (nx > 1 || ny > 1 || nz > 1) return false;
+    for (int c = 0; c < 8; c++) {
+        const int dx = c & 1, dy = (c >> 1) & 1, dz = c >> 2;
+        if (dx > nx || dy > ny || dz > nz) continue;
+        if (vol_key_sign(v, VolKey{x0 + dx, y0 + dy, z0 + dz}) != sign) return false;
+    }
+    return true;
+}
+static double coop_emul(const DevVolume& v, v3 o, v3 d, int S) {
+    const int nact = 64;
+    double tmin, tmax;
+    box_span(v.bmin, v.bmax, o, d, tmin, tmax);
+    double step = (double)(1.0f / 512.0f);
+    double t = net_max(step, tmin);
+    int sign = -1, iters = 0;
+    for (;;) {
+        while (S > 0) {
+            const VolKey k0 = vol_key(v, o, d, t);
+            const int s0 = vol_key_sign(v, k0);
+            if (s0 <= 0 || (sign >= 0 && s0 != sign)) break;
+            int f = nact;
+            VolKey kp = k0;
+            for (int r = 0; r < nact; r++) {
+                const int off = (r + 1) * S;
+                const double tr = t_after(t, step, off);
+                const bool valid = tr <= tmax && iters + off < (1 << 24);
+                const VolKey kr = vol_key(v, o, d, tr);
+                if (!(valid && box_sign(v, kp, kr, s0))) { f = r; break; }
+                kp = kr;
+            }
+            if (f == 0) break;
+            const int k = f * S + 1;
+            t = t_after(t, step, k);
+            iters += k;
+            sign = s0;
+            if (f < nact) break;
+        }
+        double tk[64];
+        int sg[64];
+        bool valid[64];
+        for (int r = 0; r < nact; r++) {
+            tk[r] = t_after(t, step, r);
+            valid[r] = tk[r] <= tmax && iters + r < (1 << 24);
+            sg[r] = valid[r] ? sign_fast(v, o, d, tk[r]) : 0;
+        }
+        int ke = -1;
+        for (int r = 0; r < nact && ke < 0; r++) {
+            const int prev = r == 0 ? sign : sg[r - 1];
+            if (valid[r] && (sg[r] == 0 || (prev >= 0 && sg[r] != prev))) ke = r;
+        }
+        if (ke < 0) {
+            for (int r = 0; r < nact; r++)
+                if (!valid[r]) return kHitInf;
+            t = tk[nact - 1] + step;
+            sign = sg[nact - 1];
+            iters += nact;
+            continue;
+        }
+        double tr = tk[ke];
+        const int sge = sg[ke];
+        tr -= step;
+        step /= 64;
+        tr += step;
+        for (int j = 0; j < 64; j++) {
+            if (sign_fast(v, o, d, tr) == 0) return tr - step;
+            tr += step;
+        }
+        t = tr + step;   // the outer loop's t += step, with the refined step
+        sign = sge;
+        iters += ke + 1;
+    }
+}
+
 int main(int argc, char** argv) {
     const int rays = argc > 1 ? atoi(argv[1]) : 20000;
     std::mt19937_64 rng(12345);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     std::normal_distribution<double> N(0.0, 1.0);
-    long long bad = 0, total = 0, hits = 0;
+    long long bad = 0, total = 0, hits = 0, cbad = 0;
     double t_skip = 0, t_naive = 0;
     // t_after against repeated addition, across binade crossings
     for (int i = 0; i < 200000; i++) {
@@ -117,6 +201,13 @@ int main(int argc, char** argv) {
                 const auto c2 = std::chrono::steady_clock::now();
                 t_skip += std::chrono::duration<double>(c1 - c0).count();
                 t_naive += std::chrono::duration<double>(c2 - c1).count();
+                for (int S : {8, 16, 32}) {
+                    const double c = coop_emul(v, o, dir, S);
+                    if (c != b && !(c != c && b != b)) {
+                        if (cbad < 5) printf("vol %d ray %d stride %d: coop %.17g naive %.17g\n", vi, i, S, c, b);
+                        cbad++;
+                    }
+                }
                 total++;
                 hits += b < kHitInf;
                 if (a != b && !(a != a && b != b)) {
@@ -131,6 +222,8 @@ int main(int argc, char** argv) {
             bad += vbad;
             vi++;
         }
+    printf("cooperative march with the strided pass (strides 8, 16, 32), emulated: %lld differences\n", cbad);
+    bad += cbad;
     printf("%lld rays, %lld hits, %lld differences; vol_t %.3f s, the loop as written %.3f s\n", total, hits, bad, t_skip,
            t_naive);
     return bad ? 1 : 0;
