@@ -228,6 +228,32 @@ __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, floa
     if (v3r == kEmpty4) k3 = inf;
 }
 
+// SDF records (an SDFShape, or a TransformedShape of one): their sphere tracing runs up to 1000
+// dependent steps.  Taken where a lane's traversal meets the leaf, the lanes that meet it at
+// different steps run the tracing one after the other; deferred (PT_DEFER_SDF: the first SDF
+// record a ray reaches is left in pend_sdf and traced after the traversal, sdf_pending) every
+// such lane of the wave traces at once.  Merged as the deferred Volume march is (march_pending).
+#ifndef PT_DEFER_SDF
+#define PT_DEFER_SDF 0
+#endif
+__device__ __forceinline__ bool sdf_deferred(const DevScene& S, const float4* r) {
+    const int32_t kind = (int32_t)f2u(r[0].w);
+    if (kind == KIND_SDF) return true;
+    return kind == KIND_XFORM && S.xforms[rec_ext(r)].kind == KIND_SDF;
+}
+template <bool ANY>
+__device__ __forceinline__ void sdf_pending(const DevScene& S, v3 o, v3 d, int32_t p, HitRec& best, bool* blocked = nullptr) {
+    if (p < 0) return;
+    int32_t kind;
+    double tx = 0;
+    const double t = prim_t<false, true>(S, S.ana_recs, (uint32_t)p, o, d, kind, &tx);
+    if (ANY) {
+        if (t < best.t) *blocked = true;
+    } else if (t < best.t || (t == best.t && best.kind == KIND_TRI)) {
+        best.t = t; best.kind = kind; best.idx = p; best.tx = tx;
+    }
+}
+
 // Stack-based BVH4 traversal (node layout: pt_bvh.h, collapse_bvh4).  A node is
 // one 128-byte line fetched with seven independent 16-byte loads; the four
 // child slabs are tested, hits sorted nearest-first with a 5-comparator network,
@@ -239,7 +265,8 @@ __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, floa
 template <bool TRI, bool COUNT, bool ANY, bool FULL, class STK>
 __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __restrict__ nodes, int32_t num_nodes,
                                          const float4* __restrict__ recs, v3 o, v3 d, v3 invd, HitRec& best,
-                                         const STK& stack, Counters& ctr, int32_t* pend = nullptr) {
+                                         const STK& stack, Counters& ctr, int32_t* pend = nullptr,
+                                         int32_t* pend_sdf = nullptr) {
     if (num_nodes <= 0) return false;
     uint32_t ref = 0;  // root: always an inner node
     int sp = 0;
@@ -272,6 +299,10 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
                 int32_t kind;
                 if (FULL && PT_COOP_MARCH && pend && *pend < 0 && march_deferred(S, recs + 3 * (size_t)(first + k))) {
                     *pend = (int32_t)(first + k);
+                    continue;
+                }
+                if (FULL && PT_DEFER_SDF && pend_sdf && *pend_sdf < 0 && sdf_deferred(S, recs + 3 * (size_t)(first + k))) {
+                    *pend_sdf = (int32_t)(first + k);
                     continue;
                 }
                 double tx = 0;
@@ -603,7 +634,7 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         if (t < best.t) { best.t = t; best.kind = KIND_PLANE; best.idx = i; }
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    int32_t pend = -1;   // FULL: a Volume left for the cooperative march
+    int32_t pend = -1, pend_sdf = -1;   // FULL: a Volume left for the cooperative march, an SDF for sdf_pending
     if (S.ana_linear) {   // a few analytic shapes, one by one (as the refill kernels test them; pt_scene.h)
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
@@ -614,10 +645,11 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         }
     } else {
         traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
-                                            FULL ? &pend : nullptr);
+                                            FULL ? &pend : nullptr, FULL ? &pend_sdf : nullptr);
     }
     traverse_tri<COUNT, false>(S, o, d, invd, best, stack, ctr);
     if (FULL && PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
+    if (FULL) sdf_pending<false>(S, o, d, pend_sdf, best);
     return best;
 }
 
@@ -655,7 +687,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    int32_t pend = -1;   // FULL: a Volume left for the cooperative march
+    int32_t pend = -1, pend_sdf = -1;   // FULL: a Volume left for the cooperative march, an SDF for sdf_pending
     if (S.ana_linear) {
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
@@ -663,13 +695,18 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
             if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return false;
         }
     } else if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack,
-                                                 ctr, FULL ? &pend : nullptr)) {
+                                                 ctr, FULL ? &pend : nullptr, FULL ? &pend_sdf : nullptr)) {
         return false;
     }
     if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return false;
     if (FULL && PT_COOP_MARCH) {   // the lanes still unblocked march their pending Volume together
         bool blocked = false;
         march_pending<true>(S, o, d, pend, best, &blocked);
+        if (blocked) return false;
+    }
+    if (FULL) {
+        bool blocked = false;
+        sdf_pending<true>(S, o, d, pend_sdf, best, &blocked);
         if (blocked) return false;
     }
     return true;
@@ -689,7 +726,7 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
     const bool tri_best = best.kind == KIND_TRI;
     if (tri_best) best.t = nextafter(best.t, (double)INFINITY);
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    int32_t pend = -1;
+    int32_t pend = -1, pend_sdf = -1;
     if (S.ana_linear) {
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
@@ -699,9 +736,11 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
             if (t < best.t) { best.t = t; best.kind = kind; best.idx = p; best.tx = tx; }
         }
     } else {
-        traverse<false, COUNT, false, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr, &pend);
+        traverse<false, COUNT, false, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr, &pend,
+                                            &pend_sdf);
     }
     if (PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
+    sdf_pending<false>(S, o, d, pend_sdf, best);
     if (best.kind == KIND_TRI && tri_best) best.t = t_in;
 }
 // The analytic half of a split shadow query (light_visible's analytic part): is any analytic
@@ -714,7 +753,7 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
     if (!(tl < kHitInf)) return true;   // (the refill kernel found it lit, so tl is finite)
     HitRec best{tl, -1, -1};
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    int32_t pend = -1;
+    int32_t pend = -1, pend_sdf = -1;
     if (S.ana_linear) {
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
@@ -722,7 +761,7 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
             if (prim_t<false, true>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return true;
         }
     } else if (traverse<false, COUNT, true, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
-                                                   &pend)) {
+                                                   &pend, &pend_sdf)) {
         return true;
     }
     if (PT_COOP_MARCH) {
@@ -730,7 +769,9 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
         march_pending<true>(S, o, d, pend, best, &blocked);
         if (blocked) return true;
     }
-    return false;
+    bool blocked = false;
+    sdf_pending<true>(S, o, d, pend_sdf, best, &blocked);
+    return blocked;
 }
 
 // ---------------------------------------------------------------- textures (§8f row 3)
