@@ -525,9 +525,9 @@ constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
 #endif
 // split: the planes and the triangle BVH only (the refill half of a split closest hit; the FULL
 // k_wf_trace<.., SPLIT> pass adds the analytic BVH and counts the kept rays).
-template <bool COUNT, bool FULL>
-__device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q, int qi, unsigned long long* counters,
-                                            int split) {
+template <bool COUNT, bool FULL, bool SPLIT = false>
+__device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q, int qi, unsigned long long* counters) {
+    constexpr bool split = SPLIT;   // a template flag: the unsplit kernel keeps its registers
     __shared__ uint32_t s_stack[kLdsStack * kTB];
 #if PT_COOP
     __shared__ float4 s_coop[kCoopRows];
@@ -739,13 +739,13 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
         }
     }
 }
-template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters, int split) {
-    trace_lanes<COUNT, false>(S, Q, qi, counters, split);
+template <bool COUNT, bool SPLIT = false>
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+    trace_lanes<COUNT, false, SPLIT>(S, Q, qi, counters);
 }
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_FULL_LANES_VGPRS))) void k_wf_trace_lanes_full(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
-    trace_lanes<COUNT, true>(S, Q, qi, counters, 0);
+    trace_lanes<COUNT, true>(S, Q, qi, counters);
 }
 
 // ---------------------------------------------------------------- shade / bounce
@@ -1120,9 +1120,9 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // unlit).  The outcome goes to n_lit; k_wf_nee_accum adds the lit rays' terms.
 // split: the planes and the triangle BVH only; the FULL k_wf_shadow<.., SPLIT> pass then tests the
 // analytic BVH of the rays left lit.
-template <bool COUNT, bool FULL>
-__device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters,
-                                             int split) {
+template <bool COUNT, bool FULL, bool SPLIT = false>
+__device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters) {
+    constexpr bool split = SPLIT;
     __shared__ uint32_t s_stack[kLdsStack * kTB];
 #if PT_COOP
     __shared__ float4 s_coop[kCoopRows];
@@ -1385,13 +1385,13 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
         }
     }
 }
-template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters, int split) {
-    shadow_lanes<COUNT, false>(S, Q, qo, counters, split);
+template <bool COUNT, bool SPLIT = false>
+__global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+    shadow_lanes<COUNT, false, SPLIT>(S, Q, qo, counters);
 }
 template <bool COUNT>
 __global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_FULL_LANES_VGPRS))) void k_wf_shadow_lanes_full(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
-    shadow_lanes<COUNT, true>(S, Q, qo, counters, 0);
+    shadow_lanes<COUNT, true>(S, Q, qo, counters);
 }
 
 // ---------------------------------------------------------------- direct-light terms
@@ -1612,10 +1612,10 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         if (split) {
             const unsigned tl = grid_for(n, kTB, plan.lanes_trace_blocks), ta = grid_for(n, kTB, plan.full_trace_blocks);
             if (count) {
-                hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters, 1);
+                hipLaunchKernelGGL((k_wf_trace_lanes<true, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<true, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             } else {
-                hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters, 1);
+                hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
             end_k(1, stream);
@@ -1628,8 +1628,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         else if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
 #ifndef PT_NO_TRACE_LANES
-        else if (lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters, 0);
-        else if (lanes) hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters, 0);
+        else if (lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (lanes) hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
 #endif
         else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
@@ -1668,10 +1668,10 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
             const unsigned hl = grid_for(children * plan.lights_per_child, kTB, plan.lanes_shadow_blocks);
             const unsigned ha = grid_for(children * plan.lights_per_child, kTB, plan.full_shadow_blocks);
             if (count) {
-                hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters, 1);
+                hipLaunchKernelGGL((k_wf_shadow_lanes<true, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<true, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             } else {
-                hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters, 1);
+                hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
         } else if (fullg && lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes_full<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
@@ -1679,8 +1679,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
 #ifndef PT_NO_SHADOW_LANES
-        else if (lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters, 0);
-        else if (lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters, 0);
+        else if (lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
 #endif
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
