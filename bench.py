@@ -271,9 +271,11 @@ def main():
     fullg = any(fl.counts_ext[1:4])
     full = fullg or len(fl.texture_list) > 0 or fl.env_texture > 0   # (1-based texture slots, 0 = none)
     lanes = st.bvh_nodes - 1 > 64
-    trace_name = ("k_wf_trace<false, true>" if fullg else "k_wf_trace_lanes<false>" if lanes
+    # (row-4 scenes with a mesh split each traversal: the lean refill kernel <false, true>, then the FULL
+    # kernel <false, true, true>; the class below times both)
+    trace_name = ("k_wf_trace<false, true>" if fullg else "k_wf_trace_lanes<false, false>" if lanes
                   else "k_wf_trace<false, false>")
-    shadow_name = ("k_wf_shadow<false, true>" if fullg else "k_wf_shadow_lanes<false>" if lanes
+    shadow_name = ("k_wf_shadow<false, true>" if fullg else "k_wf_shadow_lanes<false, false>" if lanes
                    else "k_wf_shadow<false, false>")
     shade_name = "k_wf_shade<false, true, *>" if full else "k_wf_shade<false, false, *>"
 

@@ -9,8 +9,8 @@ import csv
 import glob
 import sys
 
-KERNELS = ("k_wf_trace_lanes<false>", "k_wf_trace<false, false>", "k_wf_shade<false, false, false>", "k_wf_shade<false, false, true>",
-           "k_wf_shadow_lanes<false>", "k_wf_shadow<false, false>")
+KERNELS = ("k_wf_trace_lanes<false, false>", "k_wf_trace<false, false>", "k_wf_shade<false, false, false>", "k_wf_shade<false, false, true>",
+           "k_wf_shadow_lanes<false, false>", "k_wf_shadow<false, false>")
 
 
 def load(d, p):

@@ -8,7 +8,7 @@ import json
 import sys
 
 d = sys.argv[1]
-K = "k_wf_trace_lanes<false>"
+K = "k_wf_trace_lanes<false, false>"
 
 
 def total(p, counter):
