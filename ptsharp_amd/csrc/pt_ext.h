@@ -372,25 +372,25 @@ PT_HD int vol_band(const DevVolume& v, double s) {
 // Host: fill out[(x0+1) + (y0+1)(w+1) + (z0+1)(w+1)(h+1)] for cells x0 in -1..w-1, y0 in -1..h-1,
 // z0 in -1..d-1 (a cell outside that range has every corner outside the grid: zero_sign).
 inline void vol_build_runs(const DevVolume& v, int8_t* out, int32_t& zero_sign) {
-    const int sx = v.w + 1, sy = v.h + 1, sz = v.d + 1;
+    const int sx = v.w + 1, sy = v.h + 1;
     auto sign_of_band = [&](int b) { return (b & 1) ? 0 : (b == 2 * v.nwin ? v.nwin + 1 : 1); };
     zero_sign = sign_of_band(vol_band(v, 0.0));
     for (int z0 = -1; z0 < v.d; z0++)
         for (int y0 = -1; y0 < v.h; y0++)
             for (int x0 = -1; x0 < v.w; x0++) {
                 double mn = 0, mx = 0;
-                bool first = true;
+                bool first = true, finite = true;   // a NaN / infinite corner can interpolate to NaN (Sign 0)
                 for (int c = 0; c < 8; c++) {
                     const double g = vol_get(v, x0 + (c >> 2 & 1), y0 + (c >> 1 & 1), z0 + (c & 1));
+                    finite = finite && isfinite(g);
                     if (first || g < mn) mn = g;
                     if (first || g > mx) mx = g;
                     first = false;
                 }
                 const double margin = 1e-9 * (1.0 + fabs(mn) + fabs(mx));
                 const int b0 = vol_band(v, mn - margin), b1 = vol_band(v, mx + margin);
-                const int sg = (b0 == b1 && mn == mn && mx == mx) ? sign_of_band(b0) : 0;
+                const int sg = (finite && b0 == b1) ? sign_of_band(b0) : 0;
                 out[(x0 + 1) + (size_t)(y0 + 1) * sx + (size_t)(z0 + 1) * sx * sy] = (int8_t)sg;
-                (void)sz;
             }
 }
 // t after k more additions of step (a power of two) made one at a time, as Volume.Intersect's
