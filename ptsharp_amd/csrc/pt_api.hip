@@ -187,8 +187,8 @@ struct Ctx {
 // samples whose widest depth fits the queues; every chunk pays the fill and drain of
 // 16 persistent launches, so fewer, larger chunks are faster (C4, 16 spp per pass: 8
 // chunks of 32M-entry queues 2574 Mrays/s, 2 chunks 2809, one chunk 2853).  The bound is
-// the largest power of two whose queues (274 B per entry: two extension queues of
-// o, d, throughput r g, key + throughput b + hits + two shadow sets) fit a quarter of the device's memory
+// the largest power of two whose queues (290 B per entry: two extension queues of
+// o, d, throughput r g, key + throughput b + hits + the SDF queue + two shadow sets) fit a quarter of the device's memory
 // and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
 // MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
@@ -196,7 +196,7 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #define PT_SIDE_MAX_RAYS (64ull << 20)
 #endif
 constexpr double kSideStreamMaxRays = (double)PT_SIDE_MAX_RAYS;   // a chunk's widest depth, extension rays
-constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 2 * (64 + 1);
+constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 16 + 2 * (64 + 1);   // (+ the SDF queue)
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
 uint32_t wf_max_cap(Ctx* c) {
@@ -260,6 +260,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
         if ((rc = wf_alloc(c, &Q.q_k[q], cap))) return rc;
     }
     if ((rc = wf_alloc(c, &Q.hits, cap))) return rc;
+    if ((rc = wf_alloc(c, &Q.sdfq, cap))) return rc;
     for (int q = 0; q < 2; q++) {   // shadow-ray sets by depth parity
         if ((rc = wf_alloc(c, &Q.n_o[q], scap))) return rc;
         if ((rc = wf_alloc(c, &Q.n_n[q], scap))) return rc;
@@ -1220,6 +1221,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     // C4's floor cube and two light spheres: a linear test of 3 records at refill costs less than a BVH
     // node step (seven loads through the texture path) and leaf record loads per ray
     S.ana_linear = (na > 0 && na <= (size_t)PT_ANA_LINEAR && !S.full_geom) ? 1 : 0;
+    S.num_sdf = d->num_sdf_shapes;
     S.lights_lean = 1;
     for (const pt::DevLight& L : lights)
         if (!L.phantom && (L.kind == pt::KIND_SDF || L.kind == pt::KIND_VOLUME || L.kind == pt::KIND_XFORM)) S.lights_lean = 0;

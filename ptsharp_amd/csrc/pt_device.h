@@ -236,6 +236,11 @@ __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, floa
 #ifndef PT_DEFER_SDF
 #define PT_DEFER_SDF 0
 #endif
+// PT_SDF_QUEUE: the analytic half of a split closest hit (k_wf_trace<.., SPLIT>) leaves the first SDF
+// record of a ray in a compact queue instead, and k_wf_sdf_hits traces the queue with every lane busy.
+#ifndef PT_SDF_QUEUE
+#define PT_SDF_QUEUE 0
+#endif
 __device__ __forceinline__ bool sdf_deferred(const DevScene& S, const float4* r) {
     const int32_t kind = (int32_t)f2u(r[0].w);
     if (kind == KIND_SDF) return true;
@@ -301,7 +306,8 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
                     *pend = (int32_t)(first + k);
                     continue;
                 }
-                if (FULL && PT_DEFER_SDF && pend_sdf && *pend_sdf < 0 && sdf_deferred(S, recs + 3 * (size_t)(first + k))) {
+                if (FULL && (PT_DEFER_SDF || PT_SDF_QUEUE) && pend_sdf && *pend_sdf < 0 &&
+                    sdf_deferred(S, recs + 3 * (size_t)(first + k))) {
                     *pend_sdf = (int32_t)(first + k);
                     continue;
                 }
@@ -645,7 +651,7 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         }
     } else {
         traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
-                                            FULL ? &pend : nullptr, FULL ? &pend_sdf : nullptr);
+                                            FULL ? &pend : nullptr, FULL && PT_DEFER_SDF ? &pend_sdf : nullptr);
     }
     traverse_tri<COUNT, false>(S, o, d, invd, best, stack, ctr);
     if (FULL && PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
@@ -695,7 +701,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
             if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return false;
         }
     } else if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack,
-                                                 ctr, FULL ? &pend : nullptr, FULL ? &pend_sdf : nullptr)) {
+                                                 ctr, FULL ? &pend : nullptr, FULL && PT_DEFER_SDF ? &pend_sdf : nullptr)) {
         return false;
     }
     if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return false;
@@ -720,8 +726,10 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
 // best its t is raised by one ulp for the analytic pass (no double lies between), and restored
 // when no analytic hit took it.  The triangles the refill kernel found without the analytic
 // hit's tighter bound are the same: a bound only prunes, it never reorders the visits.
+// sdf_out (PT_SDF_QUEUE): the SDF record left for k_wf_sdf_hits (-1: none), not merged here.
 template <bool COUNT, class STK>
-__device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const STK& stack, Counters& ctr, HitRec& best) {
+__device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const STK& stack, Counters& ctr, HitRec& best,
+                                          int32_t* sdf_out = nullptr) {
     const double t_in = best.t;
     const bool tri_best = best.kind == KIND_TRI;
     if (tri_best) best.t = nextafter(best.t, (double)INFINITY);
@@ -737,10 +745,11 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
         }
     } else {
         traverse<false, COUNT, false, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr, &pend,
-                                            &pend_sdf);
+                                            PT_DEFER_SDF || sdf_out ? &pend_sdf : nullptr);
     }
     if (PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
-    sdf_pending<false>(S, o, d, pend_sdf, best);
+    if (sdf_out) *sdf_out = pend_sdf;
+    else sdf_pending<false>(S, o, d, pend_sdf, best);
     if (best.kind == KIND_TRI && tri_best) best.t = t_in;
 }
 // The analytic half of a split shadow query (light_visible's analytic part): is any analytic
@@ -761,7 +770,7 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
             if (prim_t<false, true>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return true;
         }
     } else if (traverse<false, COUNT, true, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
-                                                   &pend, &pend_sdf)) {
+                                                   &pend, PT_DEFER_SDF ? &pend_sdf : nullptr)) {
         return true;
     }
     if (PT_COOP_MARCH) {

@@ -104,6 +104,7 @@ struct DevScene {
     int32_t ana_count;         // records in ana_recs
     int32_t ana_linear;        // 1: test ana_recs linearly in the refill kernels
     int32_t lights_lean;       // 1: every light's own t is a lean intersect (no SDF / Volume light): split shadow rays
+    int32_t num_sdf;           // SDFShapes (the split closest hit queues their records: k_wf_sdf_hits)
     // counted passes only (else null): [0] Volume.Sample calls and [1] SDF evaluations of the
     // Volume / SDFShape intersect marches (DevBuffer::counters words 9 and 10)
     unsigned long long* march;

@@ -22,6 +22,7 @@ struct WfQueues {
     double2* q_t[2];     // {throughput.r, throughput.g} (fp64, as the reference's Colour)
     ulonglong2* q_k[2];  // {RNG node key of the vertex the ray leads to, throughput.b (fp64 bits)}
     uint4* hits;         // {t (fp64 bits), kind, record}
+    uint4* sdfq;         // split closest hit, PT_SDF_QUEUE: {slot, SDF record, best world t (fp64 bits)} (k_wf_sdf_hits)
     // Shadow rays (a diffuse child's sampleLights, set up by k_wf_shade), two sets by depth
     // parity (set q holds the shadow rays counted in pair word q), so the shadow pass and the
     // light-term accumulation of depth d can run beside the closest-hit and shade passes of d + 1.
@@ -56,7 +57,8 @@ constexpr int kCountStride = PT_COUNT_STRIDE;
 static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
 constexpr int kFetchSlot = 2 * kParts;
 constexpr int kKeptSlot = 9 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
-constexpr int kEndSlot = 9 * kParts + 2;
+constexpr int kSdfSlot = 9 * kParts + 2;   // entries of Q.sdfq (PT_SDF_QUEUE)
+constexpr int kEndSlot = 9 * kParts + 3;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kCountWords = count_word(kEndSlot);
@@ -66,6 +68,7 @@ constexpr int kOverflowCounter = 15;            // DevBuffer::counters word of W
 // of a split closest hit, 5 + q that of split shadow rays of set q; pt_wavefront.hip "split") in partition g
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
+constexpr int kSdfWord = count_word(kSdfSlot);
 
 #ifndef PT_LDS_STACK
 #define PT_LDS_STACK 16

@@ -352,7 +352,21 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
                 h.kind = (int32_t)r.z;
                 h.idx = (int32_t)r.w;
                 h.tx = h.t;
-                trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h);
+                int32_t sdf = -1;
+                trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h, PT_SDF_QUEUE ? &sdf : nullptr);
+                if (PT_SDF_QUEUE) {   // k_wf_sdf_hits traces it, every lane busy (the active lanes append here)
+                    const uint64_t m = __ballot(sdf >= 0);
+                    if (m) {
+                        const int lead = __builtin_ctzll(m);
+                        uint32_t at = 0;
+                        if ((int)lane == lead) at = atomicAdd(Q.counts + kSdfWord, (uint32_t)__popcll(m));
+                        at = (uint32_t)__shfl((int)at, lead, 64) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                        if (sdf >= 0 && at < Q.cap) {
+                            const unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
+                            Q.sdfq[at] = make_uint4(i, (uint32_t)sdf, (uint32_t)tb, (uint32_t)(tb >> 32));
+                        }
+                    }
+                }
             } else {
                 h = trace<COUNT, FULL>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
             }
@@ -385,6 +399,34 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 // atomic per refill).  A new ray's head work is two queue loads and the planes (none in
 // C4), so a refill holds the busy lanes for one load round trip.  Same visit order,
 // same arithmetic as trace(): bit-identical hits.
+// The SDF records the analytic half of a split closest hit queued (PT_SDF_QUEUE): one lane per
+// entry, so SDFShape's sphere tracing (up to 1000 dependent steps) runs with every lane busy
+// instead of with the few lanes of a wave whose rays reach the shape.  Merged into the hit record
+// as the traversal would have: nearer wins, and an equal t beats a triangle (the analytic BVH
+// precedes the triangles in Scene.Intersect).  One entry per ray: no two lanes write one record.
+__global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevScene S, WfQueues Q, int qi) {
+    const uint32_t n = min(Q.counts[kSdfWord], Q.cap);
+    const bool env_black = S.env_tex < 0 && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
+    uint32_t gained = 0;   // misses that became hits: rays with work for k_wf_shade (kept_word)
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint4 e = Q.sdfq[k];
+        const uint32_t i = e.x;
+        const double bt = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
+        const float4 a = nt_load(&Q.q_o[qi][i]), b = nt_load(&Q.q_d[qi][i]);
+        int32_t kind;
+        double tx = 0;
+        const double t = prim_t<false, true>(S, S.ana_recs, e.y, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, kind, &tx);
+        const int32_t hk = (int32_t)Q.hits[i].z;
+        if (t < bt || (t == bt && hk == KIND_TRI)) {
+            const unsigned long long tb = (unsigned long long)__double_as_longlong(kind == KIND_XFORM ? tx : t);
+            hit_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)kind, e.y));
+            gained += (hk < 0 && env_black) ? 1u : 0u;
+        }
+    }
+    gained = wave_sum(gained);
+    if ((threadIdx.x & 63) == 0 && gained) atomicAdd(Q.counts + kept_word(qi), gained);
+}
+
 #ifndef PT_COOP
 #define PT_COOP 0            // 1: the per-lane refill kernels fetch lines cooperatively (measured slower)
 #endif
@@ -971,6 +1013,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         Q.counts[fetch_word(2 + (1 - qi), threadIdx.x)] = 0u;   // the fetch cursors of the shadow rays it writes
         Q.counts[fetch_word(0, threadIdx.x)] = 0u;              // the next k_wf_trace's (it may run beside k_wf_shadow)
         Q.counts[fetch_word(4, threadIdx.x)] = 0u;              // its analytic half's (split)
+        if (threadIdx.x == 0) Q.counts[kSdfWord] = 0u;          // and that half's SDF queue
         Q.counts[fetch_word(5 + (1 - qi), threadIdx.x)] = 0u;   // the split shadow rays' analytic half
         if (threadIdx.x == 0) Q.counts[kept_word(1 - qi)] = 0u;   // the next k_wf_trace's kept count
     }
@@ -1618,6 +1661,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
+            if (PT_SDF_QUEUE && S.num_sdf > 0)
+                hipLaunchKernelGGL(k_wf_sdf_hits, dim3(grid_for(n, 256, 8192)), dim3(256), 0, stream, S, Q, qi);
             end_k(1, stream);
             return;
         }
