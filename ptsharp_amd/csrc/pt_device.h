@@ -239,7 +239,7 @@ __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, floa
 // PT_SDF_QUEUE: the analytic half of a split closest hit (k_wf_trace<.., SPLIT>) leaves the first SDF
 // record of a ray in a compact queue instead, and k_wf_sdf_hits traces the queue with every lane busy.
 #ifndef PT_SDF_QUEUE
-#define PT_SDF_QUEUE 0
+#define PT_SDF_QUEUE 1
 #endif
 __device__ __forceinline__ bool sdf_deferred(const DevScene& S, const float4* r) {
     const int32_t kind = (int32_t)f2u(r[0].w);
