@@ -755,9 +755,10 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
 // The analytic half of a split shadow query (light_visible's analytic part): is any analytic
 // primitive strictly nearer than the light?  The refill kernel already cleared the planes and
 // the triangles.
+// sdf_out (PT_SDF_QUEUE): the SDF record left for k_wf_sdf_shadow (-1: none), with the light's t.
 template <bool COUNT, class STK>
 __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L, v3 o, v3 d, const STK& stack,
-                                            Counters& ctr) {
+                                            Counters& ctr, int32_t* sdf_out = nullptr, double* tl_out = nullptr) {
     const double tl = light_t<true>(S, L, o, d);
     if (!(tl < kHitInf)) return true;   // (the refill kernel found it lit, so tl is finite)
     HitRec best{tl, -1, -1};
@@ -770,13 +771,18 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
             if (prim_t<false, true>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return true;
         }
     } else if (traverse<false, COUNT, true, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
-                                                   &pend, PT_DEFER_SDF ? &pend_sdf : nullptr)) {
+                                                   &pend, PT_DEFER_SDF || sdf_out ? &pend_sdf : nullptr)) {
         return true;
     }
     if (PT_COOP_MARCH) {
         bool blocked = false;
         march_pending<true>(S, o, d, pend, best, &blocked);
         if (blocked) return true;
+    }
+    if (sdf_out) {   // left for k_wf_sdf_shadow
+        *sdf_out = pend_sdf;
+        *tl_out = tl;
+        return false;
     }
     bool blocked = false;
     sdf_pending<true>(S, o, d, pend_sdf, best, &blocked);

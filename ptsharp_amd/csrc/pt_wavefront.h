@@ -23,6 +23,7 @@ struct WfQueues {
     ulonglong2* q_k[2];  // {RNG node key of the vertex the ray leads to, throughput.b (fp64 bits)}
     uint4* hits;         // {t (fp64 bits), kind, record}
     uint4* sdfq;         // split closest hit, PT_SDF_QUEUE: {slot, SDF record, best world t (fp64 bits)} (k_wf_sdf_hits)
+    uint4* sdfq_sh;      // split shadow rays, PT_SDF_QUEUE: {slot, SDF record, the light's t (fp64 bits)} (k_wf_sdf_shadow)
     // Shadow rays (a diffuse child's sampleLights, set up by k_wf_shade), two sets by depth
     // parity (set q holds the shadow rays counted in pair word q), so the shadow pass and the
     // light-term accumulation of depth d can run beside the closest-hit and shade passes of d + 1.
@@ -58,7 +59,8 @@ static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
 constexpr int kFetchSlot = 2 * kParts;
 constexpr int kKeptSlot = 9 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
 constexpr int kSdfSlot = 9 * kParts + 2;   // entries of Q.sdfq (PT_SDF_QUEUE)
-constexpr int kEndSlot = 9 * kParts + 3;
+constexpr int kSdfShSlot = 9 * kParts + 3;   // entries of Q.sdfq_sh
+constexpr int kEndSlot = 9 * kParts + 4;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kCountWords = count_word(kEndSlot);
@@ -69,6 +71,7 @@ constexpr int kOverflowCounter = 15;            // DevBuffer::counters word of W
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
 constexpr int kSdfWord = count_word(kSdfSlot);
+constexpr int kSdfShWord = count_word(kSdfShSlot);
 
 #ifndef PT_LDS_STACK
 #define PT_LDS_STACK 16

@@ -427,6 +427,19 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevSce
     if ((threadIdx.x & 63) == 0 && gained) atomicAdd(Q.counts + kept_word(qi), gained);
 }
 
+// The SDF records the analytic half of split shadow rays queued (PT_SDF_QUEUE_SHADOW): one lane per
+// entry; a ray whose SDF is strictly nearer than its light is blocked.
+__global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_shadow(DevScene S, WfQueues Q, int qo) {
+    const uint32_t n = min(Q.counts[kSdfShWord], Q.s_cap);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint4 e = Q.sdfq_sh[k];
+        const double tl = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
+        const float4 a = nt_load(&Q.n_o[qo][e.x]), b = nt_load(&Q.n_n[qo][e.x]);
+        int32_t kind;
+        if (prim_t<false, true>(S, S.ana_recs, e.y, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, kind) < tl) Q.n_lit[qo][e.x] = 0;
+    }
+}
+
 #ifndef PT_COOP
 #define PT_COOP 0            // 1: the per-lane refill kernels fetch lines cooperatively (measured slower)
 #endif
@@ -537,6 +550,9 @@ __device__ __forceinline__ uint32_t line_of(const DevScene& S, bool tri, uint32_
     const bool leaf = (ref & 0x80000000u) != 0;
     return tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu) : (leaf ? 0u : ref);
 }
+#ifndef PT_SDF_QUEUE_SHADOW
+#define PT_SDF_QUEUE_SHADOW 0   // split shadow rays queue their SDF records too (k_wf_sdf_shadow)
+#endif
 #ifndef PT_SPLIT
 #define PT_SPLIT 1   // row-4 scenes with a triangle BVH: split traversal (depth_loop)
 #endif
@@ -1137,7 +1153,24 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
             const uint32_t li = __float_as_uint(b.w);
             if (SPLIT) {
                 const float4 a = nt_load(&Q.n_o[qo][i]);
-                if (!ana_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr)) continue;
+                int32_t sdf = -1;
+                double tl = 0;
+                const bool blocked = ana_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr,
+                                                        PT_SDF_QUEUE_SHADOW ? &sdf : nullptr, &tl);
+                if (PT_SDF_QUEUE_SHADOW) {   // k_wf_sdf_shadow tests it, every lane busy
+                    const uint64_t m = __ballot(!blocked && sdf >= 0);
+                    if (m) {
+                        const int lead = __builtin_ctzll(m);
+                        uint32_t at = 0;
+                        if ((int)lane == lead) at = atomicAdd(Q.counts + kSdfShWord, (uint32_t)__popcll(m));
+                        at = (uint32_t)__shfl((int)at, lead, 64) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                        if (!blocked && sdf >= 0 && at < Q.s_cap) {
+                            const unsigned long long tb = (unsigned long long)__double_as_longlong(tl);
+                            Q.sdfq_sh[at] = make_uint4(i, (uint32_t)sdf, (uint32_t)tb, (uint32_t)(tb >> 32));
+                        }
+                    }
+                }
+                if (!blocked) continue;
             } else if (li != kDead) {
                 const float4 a = nt_load(&Q.n_o[qo][i]);
                 const DevLight L = S.lights[li];
@@ -1712,6 +1745,8 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         if (split_sh) {
             const unsigned hl = grid_for(children * plan.lights_per_child, kTB, plan.lanes_shadow_blocks);
             const unsigned ha = grid_for(children * plan.lights_per_child, kTB, plan.full_shadow_blocks);
+            const bool sq = PT_SDF_QUEUE_SHADOW && S.num_sdf > 0;
+            if (sq) (void)hipMemsetAsync(Q.counts + kSdfShWord, 0, sizeof(uint32_t), side);
             if (count) {
                 hipLaunchKernelGGL((k_wf_shadow_lanes<true, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<true, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
@@ -1719,6 +1754,9 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
                 hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
+            if (sq)
+                hipLaunchKernelGGL(k_wf_sdf_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256), 0,
+                                   side, S, Q, 1 - qi);
         } else if (fullg && lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes_full<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg && lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes_full<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
