@@ -551,7 +551,7 @@ __device__ __forceinline__ uint32_t line_of(const DevScene& S, bool tri, uint32_
     return tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu) : (leaf ? 0u : ref);
 }
 #ifndef PT_SDF_QUEUE_SHADOW
-#define PT_SDF_QUEUE_SHADOW 0   // split shadow rays queue their SDF records too (k_wf_sdf_shadow)
+#define PT_SDF_QUEUE_SHADOW 1   // split shadow rays queue their SDF records too (k_wf_sdf_shadow)
 #endif
 #ifndef PT_SPLIT
 #define PT_SPLIT 1   // row-4 scenes with a triangle BVH: split traversal (depth_loop)
