@@ -187,8 +187,8 @@ struct Ctx {
 // samples whose widest depth fits the queues; every chunk pays the fill and drain of
 // 16 persistent launches, so fewer, larger chunks are faster (C4, 16 spp per pass: 8
 // chunks of 32M-entry queues 2574 Mrays/s, 2 chunks 2809, one chunk 2853).  The bound is
-// the largest power of two whose queues (306 B per entry: two extension queues of
-// o, d, throughput r g, key + throughput b + hits + the SDF queues + two shadow sets) fit a quarter of the device's memory
+// the largest power of two whose queues (274 B per entry: two extension queues of
+// o, d, throughput r g, key + throughput b + hits + two shadow sets) fit a quarter of the device's memory
 // and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
 // MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
@@ -196,7 +196,9 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #define PT_SIDE_MAX_RAYS (64ull << 20)
 #endif
 constexpr double kSideStreamMaxRays = (double)PT_SIDE_MAX_RAYS;   // a chunk's widest depth, extension rays
-constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 16 + 2 * (64 + 1) + 16;   // (+ the SDF queues)
+// (a scene with SDF shapes adds its two SDF queues, 32 B per entry, outside this budget: counted in,
+// they halved C4's queues from 2^28 to 2^27 entries and split its pass in two chunks, -3 %)
+constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 2 * (64 + 1);
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
 uint32_t wf_max_cap(Ctx* c) {
@@ -246,7 +248,9 @@ int wf_alloc(Ctx* c, T** out, size_t n) {
 }
 
 int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
-    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes) return PT_OK;
+    const bool want_sdf = c->S.num_sdf > 0;   // the split traversal's SDF queues (pt_wavefront.hip k_wf_sdf_*)
+    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes && (!want_sdf || c->Q.sdfq))
+        return PT_OK;
     cap = std::max(cap, c->wf_cap);
     scap = std::max(scap, c->wf_scap);
     acc_passes = std::max(acc_passes, c->acc_passes);
@@ -260,14 +264,14 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
         if ((rc = wf_alloc(c, &Q.q_k[q], cap))) return rc;
     }
     if ((rc = wf_alloc(c, &Q.hits, cap))) return rc;
-    if ((rc = wf_alloc(c, &Q.sdfq, cap))) return rc;
+    if (want_sdf && (rc = wf_alloc(c, &Q.sdfq, cap))) return rc;
     for (int q = 0; q < 2; q++) {   // shadow-ray sets by depth parity
         if ((rc = wf_alloc(c, &Q.n_o[q], scap))) return rc;
         if ((rc = wf_alloc(c, &Q.n_n[q], scap))) return rc;
         if ((rc = wf_alloc(c, &Q.n_w[q], 2 * (size_t)scap))) return rc;
         if ((rc = wf_alloc(c, &Q.n_lit[q], scap))) return rc;
     }
-    if ((rc = wf_alloc(c, &Q.sdfq_sh, scap))) return rc;   // one shadow pass at a time uses it
+    if (want_sdf && (rc = wf_alloc(c, &Q.sdfq_sh, scap))) return rc;   // one shadow pass at a time uses it
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
     Q.overflow = c->d_counters + pt::kOverflowCounter;
     // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
