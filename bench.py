@@ -6,10 +6,15 @@ Workload (BASELINE.json configs[3], the north-star target): a seeded
 1,000,000-triangle mesh in Example.bunny's scene (floor cube, two light spheres,
 NewSampler(4,4), SpecularModeFirst), 1920x1080.  One step = one
 Renderer.RenderParallel pass at --spp samples per pixel; K steps accumulate
-K·spp samples per pixel (default 64 × 16 = 1024 spp).  N > 1: one process per
-GPU (torchrun), the image's 32x32 tiles are dealt round-robin to ranks, the
-scene is replicated, and the Welford Buffer is gathered onto rank 0 over RCCL
-at the end of the timed region (strong scaling: the image is fixed).
+K·spp samples per pixel (default 64 × 16 = 1024 spp).  N > 1: the image's 32x32
+tiles are dealt round-robin to ranks, the scene is replicated, and the Welford
+Buffer is gathered onto rank 0 over RCCL at the end of the timed region (strong
+scaling: the image is fixed).  Two launch forms: under torch.distributed.run
+(WORLD_SIZE set) one process per GPU joined by pt_comm_init; without a launcher,
+`--gpus N` makes this one process drive devices 0..N-1 — N contexts joined by
+pt_comm_init_all, one host thread per device, pt_comm_gather_all — the form the
+.NET host's HipRendererGroup uses (Renderer.cs:257-333 spreads one frame over the
+whole machine from one process).
 
 Rank 0 prints one JSON line (driver contract), with `roofline` for the closest-hit
 kernel and `cpu_baseline` (the oracle port timed on this host).
@@ -148,9 +153,27 @@ def _gather_check(r, dist, rank, world, mine):
             "what": "rank 0's Buffer after the gather vs each rank's own pt_read_tiles, {M, V, N}"}
 
 
-def parse():
+def _group_gather_check(rs, W, H, tiles_for_rank):
+    """The one-process form's check: context 0's Buffer after pt_comm_gather_all against every other
+    context's own pt_read_tiles of its tile list, bit for bit."""
+    bad, checked = 0, 0
+    for k, x in enumerate(rs):
+        ids = tiles_for_rank(W, H, k, len(rs))
+        if not len(ids):
+            continue
+        got = rs[0].ReadTiles(ids)
+        mine = x.ReadTiles(ids)
+        bad += sum(int(not np.array_equal(g, m)) for g, m in zip(got, mine))
+        checked += len(ids)
+    return {"tiles": checked, "bit_exact": bad == 0,
+            "what": "context 0's Buffer after pt_comm_gather_all vs each context's own pt_read_tiles, {M, V, N}"}
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="GPUs of this node; under torch.distributed.run (WORLD_SIZE set) one per process, "
+                        "otherwise this one process drives devices 0..N-1 (pt_comm_init_all, one host thread each)")
     p.add_argument("--steps", type=int, default=None, help="timed steps (default 64; c5: 2)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2; c5: 1)")
     p.add_argument("--spp", type=int, default=None, help="samples per pixel per step (pass; default 16, c5: 1)")
@@ -173,20 +196,64 @@ def parse():
     p.add_argument("--shard", default=None, metavar="K/N",
                    help="render only rank K's tiles of an N-way split, in this one process (profiling the "
                         "per-rank workload of an N-GPU run on one GPU; value then counts this shard only)")
-    a = p.parse_args()
+    p.add_argument("--group", action="store_true",
+                   help="the one-process multi-GPU form even at --gpus 1 (a one-context pt_comm_init_all group)")
+    a = p.parse_args(argv)
     for k, v in DEFAULTS.get(a.workload, DEFAULT).items():
         if getattr(a, k) is None:
             setattr(a, k, v)
+    if a.gpus < 1:
+        p.error("--gpus must be >= 1")
     return a
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def resolve_world(gpus, env, group_flag=False):
+    """How this process takes part in an N-GPU run.  Returns (mode, world, rank, local_rank):
+    'dist'  — launched by torch.distributed.run (WORLD_SIZE in env): one rank per process, --gpus is
+              the launcher's business (the env wins);
+    'group' — no launcher and --gpus N > 1 (or --group): this process creates N contexts on devices
+              0..N-1, joins them with pt_comm_init_all and drives each from its own host thread
+              (Renderer.cs:257-333's whole-machine parallelism; HipRendererGroup's form);
+    'single' — one GPU, one context."""
+    if env.get("WORLD_SIZE") is not None:
+        world = int(env["WORLD_SIZE"])
+        return ("dist" if world > 1 else "single"), world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+    if gpus > 1 or group_flag:
+        return "group", int(gpus), 0, 0
+    return "single", 1, 0, 0
+
+
+def _each(rs, fn):
+    """fn(i, rs[i]) for every local context, concurrently (one host thread per device: the library's
+    calls release the GIL, and every entry point sets its context's device), results in order."""
+    if len(rs) == 1:
+        return [fn(0, rs[0])]
+    import threading
+    out, errs = [None] * len(rs), []
+
+    def run(i):
+        try:
+            out[i] = fn(i, rs[i])
+        except BaseException as e:   # re-raised on the calling thread
+            errs.append((i, e))
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(len(rs))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        i, e = sorted(errs, key=lambda x: x[0])[0]
+        raise RuntimeError(f"device {i}: {e}") from e
+    return out
+
+
+def main(argv=None):
+    a = parse(argv)
+    mode, world, rank, local = resolve_world(a.gpus, os.environ, a.group)
+    if mode == "dist" and a.gpus not in (1, world):
+        print(f"--gpus {a.gpus} ignored: WORLD_SIZE={world} (one rank per process)", file=sys.stderr, flush=True)
     dist = None
-    if world > 1:
+    if mode == "dist":
         import torch.distributed as dist  # control plane only (barrier, id broadcast, max/sum)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -197,7 +264,11 @@ def main():
     # RCCL cannot put two ranks on one GPU, so the tiles are gathered over gloo there, and said so.
     ndev = C.c_int32(0)
     _abi.load_library().pt_device_count(C.byref(ndev))
-    shared = world > 1 and ndev.value < world and not os.environ.get("PT_BENCH_FORCE_RCCL")
+    if mode == "group" and ndev.value < world:
+        print(f"bench.py --gpus {world}: this process sees {ndev.value} HIP device(s); the one-process form "
+              f"needs one device per GPU requested", file=sys.stderr, flush=True)
+        sys.exit(2)
+    shared = mode == "dist" and ndev.value < world and not os.environ.get("PT_BENCH_FORCE_RCCL")
     rccl_ok = False
     local = local % max(ndev.value, 1)
     t_scene = time.perf_counter()
@@ -237,30 +308,40 @@ def main():
         del gen, raw
 
     W, H = a.width, a.height
-    r = Renderer.NewRenderer(scene, camera, sampler, W, H, True, device=local)
-    r.SamplesPerPixel = a.spp
-    r.AdaptiveSamples = a.adaptive
-    r.Seed = a.seed
-    r.Engine = {"auto": 0, "mega": 1, "wave": 2}[a.engine]
-    if a.shard:
-        k, nsh = (int(x) for x in a.shard.split("/"))
-        r.Tiles = tiles_for_rank(W, H, k, nsh)
-    if world > 1:
-        r.Tiles = tiles_for_rank(W, H, rank, world)
-        if not shared:
-            obj = [Renderer.CommUniqueId() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            ok = 1
-            try:
-                r.CommInit(world, rank, obj[0])
-            except Exception as e:
-                print(f"pt_comm_init failed ({e}); the tiles will be gathered over gloo", file=sys.stderr, flush=True)
-                ok = 0
-            import torch
-            t_ok = torch.tensor([ok], dtype=torch.int32)
-            dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
-            rccl_ok = bool(t_ok[0])
-    r._ensure_scene()
+    # the contexts this process drives: one (single / dist), or one per device (group), local index 0 = rank 0
+    ranks = list(range(world)) if mode == "group" else [rank]
+    devices = list(range(world)) if mode == "group" else [local]
+    rs = []
+    for rk, dev in zip(ranks, devices):
+        r = Renderer.NewRenderer(scene, camera, sampler, W, H, True, device=dev)
+        r.SamplesPerPixel = a.spp
+        r.AdaptiveSamples = a.adaptive
+        r.Seed = a.seed
+        r.Engine = {"auto": 0, "mega": 1, "wave": 2}[a.engine]
+        if a.shard:
+            k, nsh = (int(x) for x in a.shard.split("/"))
+            r.Tiles = tiles_for_rank(W, H, k, nsh)
+        if world > 1:
+            r.Tiles = tiles_for_rank(W, H, rk, world)
+        rs.append(r)
+    r = rs[0]
+    if mode == "group":
+        Renderer.CommInitAll(rs)   # pt_comm_init_all: ncclCommInitAll over devices 0..N-1, one call
+        rccl_ok = True
+    elif mode == "dist" and not shared:
+        obj = [Renderer.CommUniqueId() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ok = 1
+        try:
+            r.CommInit(world, rank, obj[0])
+        except Exception as e:
+            print(f"pt_comm_init failed ({e}); the tiles will be gathered over gloo", file=sys.stderr, flush=True)
+            ok = 0
+        import torch
+        t_ok = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
+        rccl_ok = bool(t_ok[0])
+    _each(rs, lambda i, x: x._ensure_scene())   # every device builds and uploads its replica
     st = r.Stats()
     build_ms, bvh_bytes = st.build_ms, st.bvh_bytes
     # closest-hit and shadow kernels the library runs on this scene: per-lane refill
@@ -285,20 +366,27 @@ def main():
     shares = world if world > 1 else (int(a.shard.split("/")[1]) if a.shard else 1)
     ppc = a.passes_per_call or max(1, min(shares, 8))
 
-    def passes(k):   # k passes, ppc per call
-        done = 0
+    def run_passes(x, k, timed=False):   # k passes on context x, ppc per call; per-call stats when timed
+        done, rays_k, kms_k, kl_k, kern = 0, 0, np.zeros(_abi.K_SLOTS), np.zeros(_abi.K_SLOTS, np.int64), 0.0
         while done < k:
             m = min(ppc, k - done)
             if m == 1:
-                r.RenderParallel()
+                x.RenderParallel()
             else:
-                r.RenderPasses(m)
+                x.RenderPasses(m)
             done += m
-            yield m
+            if timed:
+                s = x.Stats()
+                rays_k += s.rays
+                kern += s.last_pass_ms
+                kms_k += np.array(s.kernel_ms[:])
+                kl_k += np.array(s.kernel_launches[:])
+        return rays_k, kern, kms_k, kl_k
 
-    for _ in passes(max(a.warmup, ppc if a.warmup else 0)):   # warm-up includes one full batch (its accumulators)
-        pass
-    # one instrumented (untimed) pass: traversal counters → algorithmic bytes per ray, per kernel
+    # warm-up includes one full batch (its accumulators)
+    _each(rs, lambda i, x: run_passes(x, max(a.warmup, ppc if a.warmup else 0)))
+    # one instrumented (untimed) pass on rank 0's context: traversal counters → algorithmic bytes per
+    # ray, per kernel (every rank's share is the same mix of rays)
     ctr = r.RenderCounted()
     ext_rays = ctr.rays - ctr.shadow_rays
     ext_nodes = ctr.nodes_visited - ctr.shadow_nodes
@@ -306,32 +394,32 @@ def main():
     bytes_ext = B_NODE * ext_nodes + B_PRIM * ext_prims + B_RAY * ext_rays
     bytes_sh = B_NODE * ctr.shadow_nodes + B_PRIM * ctr.shadow_prims + B_RAY * ctr.shadow_rays
     bytes_all = bytes_ext + bytes_sh + B_SHADE * ctr.shading_fetches
-    r.ResetBuffer()
+    _each(rs, lambda i, x: x.ResetBuffer())
 
+    def timing_on(i, x):
+        x.Flags = _abi.PASS_KERNEL_TIMING
+        x.Synchronize()
     # ---------------- timed region (per-kernel hipEvent timing on the library's stream)
-    r.Flags = _abi.PASS_KERNEL_TIMING
+    _each(rs, timing_on)
     if dist:
         dist.barrier()
-    r.Synchronize()
     t0 = time.perf_counter()
-    rays = 0
-    kernel_ms = 0.0
-    kms = np.zeros(_abi.K_SLOTS)
-    klaunch = np.zeros(_abi.K_SLOTS, np.int64)
-    for _ in passes(a.steps):
-        s = r.Stats()
-        rays += s.rays
-        kernel_ms += s.last_pass_ms
-        kms += np.array(s.kernel_ms[:])
-        klaunch += np.array(s.kernel_launches[:])
+    per = _each(rs, lambda i, x: run_passes(x, a.steps, timed=True))
+    rays_local = [p[0] for p in per]
+    rays, kernel_ms, kms, klaunch = per[0]   # rank 0's kernels for the roofline
     gather = None
     if shared:   # no RCCL between ranks on one device: the same tile protocol over gloo
         _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
         gather = "gloo (rehearsal)"
-    elif world > 1 and not rccl_ok:
+    elif mode == "dist" and not rccl_ok:
         _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
         gather = "gloo (RCCL init failed)"
-    elif world > 1:
+    elif mode == "group":
+        dog = _watchdog(GATHER_WATCHDOG_S, "pt_comm_gather_all")
+        Renderer.GatherAll(rs, 0)   # pt_comm_gather_all: every context's sends / receives in one RCCL group
+        dog.cancel()
+        gather = "rccl (one process, pt_comm_gather_all)"
+    elif mode == "dist":
         # A failure inside the RCCL group on one rank would leave its peers blocked in the group:
         # the watchdog ends this process (non-zero) instead of letting the job hang.  A failure
         # every rank sees alike (the MIN below) falls back to the same protocol over gloo.
@@ -351,7 +439,7 @@ def main():
             _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
             gather = "gloo (RCCL gather failed)"
         dog.cancel()
-    r.Synchronize()
+    _each(rs, lambda i, x: x.Synchronize())
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
@@ -365,15 +453,17 @@ def main():
         dist.all_reduce(rr, op=dist.ReduceOp.SUM)
         total_rays = int(rr[0])
     else:
-        total_rays = rays
+        total_rays = int(sum(rays_local))   # group: every device's rays, one clock around all of them
 
     gather_check = None
-    if world > 1:
+    if mode == "dist":
         # after the timed region: rank 0's gathered Buffer must hold every rank's tiles as that rank
         # rendered them (each rank's pt_read_tiles of its own list, sent over gloo), bit for bit
         dog = _watchdog(GATHER_WATCHDOG_S, "gather check")
         gather_check = _gather_check(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
         dog.cancel()
+    elif mode == "group":
+        gather_check = _group_gather_check(rs, W, H, tiles_for_rank)
 
     if rank != 0:
         r.close()
@@ -381,6 +471,8 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
+    for x in rs[1:]:
+        x.close()
 
     value = total_rays / elapsed / 1e6
     # camera samples traced per pixel per step: the pass' own, then AdaptiveSamples (Renderer.cs:355-372;
@@ -423,6 +515,8 @@ def main():
         "value": round(value, 3),
         "unit": "Msamples/s",
         "n_gpus": world,
+        "launch": {"single": "one process", "dist": "torch.distributed.run, one process per GPU",
+                   "group": "one process, one host thread per GPU (pt_comm_init_all)"}[mode],
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 3),

@@ -154,7 +154,8 @@ struct Ctx {
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
-    bool gathered = false;          // other ranks' tiles are in the Buffer (a gather, pt_write_buffer, pt_write_tiles) until the next pass
+    bool gathered = false;          // other ranks' tiles are in the Buffer (a gather, pt_write_tiles) until the next pass
+    bool loaded = false;            // pt_write_buffer put a whole checkpoint in (foreign pixels once the context has a communicator)
     uint8_t* d_own = nullptr;       // [tiles] 1 = a tile of this context's last tile list
     int32_t pass_tiles = 0;         // tiles of the last pass (0: the whole image); their ids are in d_tiles
     // tile-compacted gather workspace (allocated by the first gather): ids, M, V, N of up to
@@ -1244,6 +1245,19 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     return PT_OK;
 }
 
+// Passes one batch may hold: its accumulator sets (pt::kFixWords 64-bit words + 3 fp64 side sums per
+// pixel and pass) within an eighth of the device's memory.  PT_BATCH_MAX_PASSES (environment, tests)
+// lowers it.
+static int32_t batch_passes_max(Ctx* c) {
+    const size_t per_pass = (size_t)c->width * (size_t)c->height *
+                            ((PT_FIX_SPLIT ? 2 : 1) * pt::kFixWords * sizeof(unsigned long long) + 3 * sizeof(double));
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0) total_b = (size_t)8 << 30;
+    int64_t k = (int64_t)std::max<size_t>(1, (total_b / 8) / std::max<size_t>(per_pass, 1));
+    if (const char* env = std::getenv("PT_BATCH_MAX_PASSES")) k = std::min<int64_t>(k, std::max(1LL, std::atoll(env)));
+    return (int32_t)std::min<int64_t>(k, INT32_MAX);
+}
+
 static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* sampler, const pt_pass_params* pass,
                             pt_trace_counters* counted) {
     if (!c || !camera || !sampler || !pass) return fail(PT_ERR_INVALID_ARG, "NULL argument");
@@ -1320,7 +1334,11 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     if (batch > 1 && counted) return fail(PT_ERR_INVALID_ARG, "counted passes run one at a time (passes = 1)");
     const bool batchable = batch > 1 && !extra && !serial && !pass->stratified && pass->engine != PT_ENGINE_MEGAKERNEL &&
                            (uint64_t)P.acc_stride * (uint64_t)batch <= 0xFFFFFFFFull;
-    if (batchable) P.passes = batch;
+    // A batch keeps one set of per-pixel accumulators per pass (72 B per pixel): the sets of one launch
+    // sequence stay within an eighth of the device's memory; a larger K runs as consecutive sub-batches,
+    // each bit-identical to its passes run one by one (4K at K = 500 would ask for ~300 GB).
+    const int32_t sub = batchable ? std::min(batch, batch_passes_max(c)) : 1;
+    if (batchable && sub == batch) P.passes = batch;
     const uint64_t cam_samples = (uint64_t)num_tiles * 1024u * (uint64_t)(pass->stratified ? 1 : pass->spp) *
                                  (uint64_t)P.passes;
     double growth = 1.0;   // queue growth beyond depth 1 (SpecularModeAll doubles every depth)
@@ -1353,14 +1371,15 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         return fail(PT_ERR_UNSUPPORTED, "wavefront queues cannot hold one camera sample of this sampler (use the megakernel)");
     if (engine != PT_ENGINE_WAVEFRONT && engine != PT_ENGINE_MEGAKERNEL) return fail(PT_ERR_INVALID_ARG, "bad engine");
     if (batch > 1 && !(P.passes > 1 && engine == PT_ENGINE_WAVEFRONT)) {
-        // not one batch: the K passes one after another, the stats summed
+        // not one batch: the K passes one after another (or sub-batches of `sub` passes), the stats summed
+        const int32_t step = (sub > 1 && engine == PT_ENGINE_WAVEFRONT) ? sub : 1;
         pt_pass_params one = *pass;
-        one.passes = 1;
         pt_stats sum = c->stats;
         uint64_t rays = 0, shadow = 0;
         double ms = 0.0;
-        for (int32_t k = 0; k < batch; k++) {
+        for (int32_t k = 0; k < batch; k += step) {
             one.pass_index = pass->pass_index + (uint32_t)k;
+            one.passes = std::min(step, batch - k);
             if (int rc = render_pass_impl(c, camera, sampler, &one, nullptr)) return rc;
             rays += c->stats.rays;
             shadow += c->stats.shadow_rays;
@@ -1408,8 +1427,9 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         if (extra && (rc = ensure_extra(c, chunk))) return rc;
     }
     c->last_engine = engine;
-    if (c->gathered) {
+    if (c->gathered || (c->loaded && c->comm)) {
         c->gathered = false;
+        c->loaded = false;
         if (pass->num_tiles > 0) {
             const int ntiles = tiles_x * tiles_y;
             std::vector<uint8_t> own((size_t)ntiles, 0);
@@ -1565,10 +1585,12 @@ int pt_write_buffer(void* ctx, const double* m, const double* v, const int32_t* 
     if (v) PT_HIP(hipMemcpyAsync(c->d_v, v, P * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
     if (n) PT_HIP(hipMemcpyAsync(c->d_n, n, P * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
-    // The loaded Buffer may hold other ranks' pixels (every rank loads the whole checkpoint): the
-    // next tile-subset pass clears them first, as after a gather, so a firefly snapshot's
-    // all-reduce and a later gather see each pixel on its owner only.
-    c->gathered = true;
+    // The loaded Buffer may hold other ranks' pixels (every rank loads the whole checkpoint): on a
+    // context that is part of a communicator the next tile-subset pass clears them first, as after a
+    // gather, so a firefly snapshot's all-reduce and a later gather see each pixel on its owner only.
+    // A lone context keeps them (a host resuming a frame and then rendering it tile subset by tile
+    // subset keeps every restored pixel).
+    c->loaded = true;
     return PT_OK;
 }
 

@@ -9,6 +9,7 @@
 #include <thread>
 
 namespace pt {
+int g_bvh_bins = 32;
 namespace {
 
 struct Aabb {
@@ -25,7 +26,7 @@ struct Aabb {
     }
 };
 
-constexpr int kBins = 32;
+constexpr int kMaxBins = 256;
 constexpr int64_t kParallelCutoff = 16384;
 
 struct Builder {
@@ -100,7 +101,8 @@ struct Builder {
             float best_cost = INFINITY; int best_axis = -1, best_split = -1;
             for (int ax = 0; ax < 3; ax++) {
                 if (ext[ax] <= 0.f) continue;
-                Aabb bb[kBins]; int cnt[kBins] = {0};
+                const int kBins = std::min(std::max(g_bvh_bins, 2), kMaxBins);
+                Aabb bb[kMaxBins]; int cnt[kMaxBins] = {0};
                 for (int b = 0; b < kBins; b++) bb[b].reset();
                 float scale = (float)kBins / ext[ax];
                 for (int64_t i = begin; i < end; i++) {
@@ -110,7 +112,7 @@ struct Builder {
                     cnt[b]++;
                     bb[b].grow(prim_box(p));
                 }
-                float rarea[kBins]; int rcnt[kBins];
+                float rarea[kMaxBins]; int rcnt[kMaxBins];
                 Aabb acc; acc.reset(); int c = 0;
                 for (int b = kBins - 1; b > 0; b--) { acc.grow(bb[b]); c += cnt[b]; rarea[b] = acc.area(); rcnt[b] = c; }
                 acc.reset(); c = 0;
@@ -130,6 +132,7 @@ struct Builder {
                     return cent[(size_t)a * 3 + axis] < cent[(size_t)b * 3 + axis];
                 });
             } else {
+                const int kBins = std::min(std::max(g_bvh_bins, 2), kMaxBins);
                 float scale = (float)kBins / ext[best_axis];
                 float lo = cb.lo[best_axis];
                 auto it = std::partition(idx.begin() + begin, idx.begin() + end, [&](uint32_t p) {
@@ -253,7 +256,157 @@ struct Collapser {
     }
 };
 
+// SAH-optimal 4-wide collapse (the dynamic program of Ylitie, Karras and Laine 2017, "Efficient
+// incoherent ray traversal on GPUs through compressed wide BVHs", §4.1, for 4 slots).  cost(n, i) is
+// the least expected cost of BVH2 subtree n when it may take up to i child slots of the wide node
+// above it: one slot holds it as a leaf chunk (at most kChunkTris triangles, contiguous in `order`,
+// so any BVH2 subtree that small can become one) or as an inner node of its own; more slots let its
+// children (or their children) be lifted into the parent.  A step (an inner node or a leaf chunk:
+// one 128-B line) costs c_step, a triangle test c_tri, each weighted by its box's surface area.
+struct SahCollapser {
+    const std::vector<BvhNode>& n2;
+    Bvh4Result& out;
+    double c_step, c_tri;
+    int max_leaf;
+    std::vector<double> cost;      // [node][4]: cost(n, i + 1)
+    std::vector<int8_t> choice;    // [node][4]: 0 = one slot (leaf or inner), -1 = as with one slot fewer, k > 0: k slots to the left child
+    std::vector<uint8_t> as_leaf;  // one slot: a leaf chunk rather than an inner node
+    std::vector<uint32_t> prims, first;
+
+    bool is_leaf(uint32_t i) const { return n2[i].b != 0; }
+    double area(uint32_t i) const {
+        const BvhNode& n = n2[i];
+        double dx = (double)n.bmax[0] - n.bmin[0], dy = (double)n.bmax[1] - n.bmin[1], dz = (double)n.bmax[2] - n.bmin[2];
+        if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+        return dx * dy + dy * dz + dz * dx;
+    }
+    void solve(uint32_t n) {
+        double* C = &cost[(size_t)n * 4];
+        int8_t* ch = &choice[(size_t)n * 4];
+        const double a = area(n);
+        if (is_leaf(n)) {
+            prims[n] = n2[n].b;
+            first[n] = n2[n].a;
+            for (int i = 0; i < 4; i++) { C[i] = a * (c_step + c_tri * (double)prims[n]); ch[i] = 0; }
+            as_leaf[n] = 1;
+            return;
+        }
+        const uint32_t l = n2[n].a, r = l + 1;
+        solve(l);
+        solve(r);
+        prims[n] = prims[l] + prims[r];
+        first[n] = first[l];
+        const double* CL = &cost[(size_t)l * 4];
+        const double* CR = &cost[(size_t)r * 4];
+        auto dist = [&](int j, int& kbest) {   // j slots between the two children
+            double best = INFINITY;
+            kbest = -1;
+            for (int k = 1; k < j; k++) {
+                const double c = CL[k - 1] + CR[j - k - 1];
+                if (c < best) { best = c; kbest = k; }
+            }
+            return best;
+        };
+        int k4;
+        const double inner = a * c_step + dist(4, k4);
+        const double leaf = (int)prims[n] <= max_leaf ? a * (c_step + c_tri * (double)prims[n]) : INFINITY;
+        as_leaf[n] = leaf <= inner;
+        C[0] = std::min(leaf, inner);
+        ch[0] = 0;
+        for (int i = 2; i <= 4; i++) {
+            int k;
+            const double d = dist(i, k);
+            if (d < C[i - 2]) { C[i - 1] = d; ch[i - 1] = (int8_t)k; }
+            else { C[i - 1] = C[i - 2]; ch[i - 1] = -1; }
+        }
+    }
+    // the BVH2 nodes that fill the slots of subtree n given i slots
+    void slots(uint32_t n, int i, std::vector<uint32_t>& outs) const {
+        const int8_t c = choice[(size_t)n * 4 + (size_t)(i - 1)];
+        if (c == 0) { outs.push_back(n); return; }
+        if (c < 0) { slots(n, i - 1, outs); return; }
+        slots(n2[n].a, c, outs);
+        slots(n2[n].a + 1, i - c, outs);
+    }
+    uint32_t alloc() {
+        out.words.resize(out.words.size() + kNode4Words, 0u);
+        return (uint32_t)(out.nodes() - 1);
+    }
+    // wide node `at` for BVH2 inner node n (its 4 slots), A entries pushed by the ancestors
+    void emit(uint32_t at, uint32_t n, int A, int depth) {
+        out.depth = std::max(out.depth, depth);
+        std::vector<uint32_t> C;
+        slots(n2[n].a, choice_split(n), C);
+        slots(n2[n].a + 1, 4 - choice_split(n), C);
+        const int pushed = A + (int)C.size() - 1;
+        out.stack_need = std::max(out.stack_need, pushed);
+        out.children += (int64_t)C.size();
+        uint32_t refs[4] = {kEmpty4, kEmpty4, kEmpty4, kEmpty4};
+        std::vector<std::pair<uint32_t, uint32_t>> inner;
+        for (size_t k = 0; k < C.size(); k++) {
+            const uint32_t c = C[k];
+            if (as_leaf[c]) {
+                refs[k] = 0x80000000u | ((prims[c] - 1u) << 29) | (first[c] & 0x1FFFFFFFu);
+            } else {
+                const uint32_t node4 = alloc();
+                inner.emplace_back(c, node4);
+                refs[k] = node4;
+            }
+        }
+        uint32_t* w = &out.words[(size_t)at * kNode4Words];
+        for (size_t k = 0; k < 4; k++) {
+            float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
+            if (k < C.size())
+                for (int ax = 0; ax < 3; ax++) { lo[ax] = n2[C[k]].bmin[ax]; hi[ax] = n2[C[k]].bmax[ax]; }
+            for (int ax = 0; ax < 3; ax++) {
+                std::memcpy(&w[8 * ax + k], &lo[ax], 4);
+                std::memcpy(&w[8 * ax + 4 + k], &hi[ax], 4);
+            }
+            w[24 + k] = refs[k];
+        }
+        for (auto& pr : inner) emit(pr.second, pr.first, pushed, depth + 1);
+    }
+    int choice_split(uint32_t n) const {   // the left child's share of an inner node's 4 slots
+        const double* CL = &cost[(size_t)n2[n].a * 4];
+        const double* CR = &cost[(size_t)(n2[n].a + 1) * 4];
+        int kbest = 1;
+        double best = INFINITY;
+        for (int k = 1; k < 4; k++) {
+            const double c = CL[k - 1] + CR[4 - k - 1];
+            if (c < best) { best = c; kbest = k; }
+        }
+        return kbest;
+    }
+};
+
 }  // namespace
+
+void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out, double c_step, double c_tri, int max_leaf) {
+    out.words.clear();
+    out.stack_need = 0;
+    out.depth = 0;
+    out.children = 0;
+    if (bvh2.nodes.empty()) return;
+    const size_t nn = bvh2.nodes.size();
+    SahCollapser c{bvh2.nodes, out, c_step, c_tri, max_leaf, std::vector<double>(nn * 4, 0.0),
+                   std::vector<int8_t>(nn * 4, 0), std::vector<uint8_t>(nn, 0), std::vector<uint32_t>(nn, 0),
+                   std::vector<uint32_t>(nn, 0)};
+    c.solve(0);
+    const uint32_t root = c.alloc();
+    if (c.is_leaf(0)) {   // a lone leaf: the root node holds it in slot 0
+        uint32_t* w = &out.words[0];
+        for (int k = 0; k < 4; k++) w[24 + k] = kEmpty4;
+        for (int ax = 0; ax < 3; ax++) {
+            std::memcpy(&w[8 * ax], &bvh2.nodes[0].bmin[ax], 4);
+            std::memcpy(&w[8 * ax + 4], &bvh2.nodes[0].bmax[ax], 4);
+        }
+        w[24] = 0x80000000u | ((bvh2.nodes[0].b - 1u) << 29) | (bvh2.nodes[0].a & 0x1FFFFFFFu);
+        out.children = 1;
+        return;
+    }
+    c.emit(root, 0, 0, 0);
+    if (out.stack_need > stack_budget) collapse_bvh4(bvh2, stack_budget, out);   // the greedy form keeps the bound
+}
 
 void collapse_bvh4(const BvhResult& bvh2, int stack_budget, Bvh4Result& out) {
     out.words.clear();

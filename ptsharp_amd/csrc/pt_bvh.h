@@ -24,6 +24,7 @@ constexpr int kMaxDepth = 32;     // BVH2 depth bound
 constexpr int kStackMax = PT_STACK_MAX;
 static_assert(kStackMax >= kMaxDepth, "the collapse needs at least the BVH2 depth");
 constexpr int kMaxLeafSize = 4;
+extern int g_bvh_bins;   // SAH bins per axis of build_bvh (tools/bvh_quality.cpp varies it)
 
 // 32-byte node; nodes[0] is the root, nodes[1] is padding, every child pair
 // (left = 2k, right = 2k+1) starts on a 64-byte boundary.
@@ -73,5 +74,12 @@ struct Bvh4Result {
 // limited on the tallest paths to keep every root-to-leaf path's pushes within
 // `stack_budget` (the LDS stack depth) — the guarantee the BVH2 had by depth.
 void collapse_bvh4(const BvhResult& bvh2, int stack_budget, Bvh4Result& out);
+
+// The SAH-optimal collapse (pt_bvh.cpp SahCollapser): children chosen by a dynamic program over the
+// BVH2 that minimises the expected traversal cost, c_step per step (inner node or leaf chunk) and
+// c_tri per triangle test, weighted by surface area; BVH2 subtrees of at most max_leaf triangles may
+// merge into one leaf chunk.  Falls back to collapse_bvh4 if a path would exceed stack_budget.
+void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out, double c_step = 1.0,
+                       double c_tri = 0.5, int max_leaf = 3);
 
 }  // namespace pt

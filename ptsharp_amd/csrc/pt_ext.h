@@ -390,7 +390,8 @@ inline void vol_build_runs(const DevVolume& v, int8_t* out, int32_t& zero_sign) 
                 const double margin = 1e-9 * (1.0 + fabs(mn) + fabs(mx));
                 const int b0 = vol_band(v, mn - margin), b1 = vol_band(v, mx + margin);
                 const int sg = (finite && b0 == b1) ? sign_of_band(b0) : 0;
-                out[(x0 + 1) + (size_t)(y0 + 1) * sx + (size_t)(z0 + 1) * sx * sy] = (int8_t)sg;
+                // a Sign past int8 (above every window of 127 or more) is stored as 0: "no shortcut"
+                out[(x0 + 1) + (size_t)(y0 + 1) * sx + (size_t)(z0 + 1) * sx * sy] = (int8_t)(sg > 127 ? 0 : sg);
             }
 }
 // t after k more additions of step (a power of two) made one at a time, as Volume.Intersect's

@@ -364,6 +364,8 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
                         if (sdf >= 0 && at < Q.cap) {
                             const unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
                             Q.sdfq[at] = make_uint4(i, (uint32_t)sdf, (uint32_t)tb, (uint32_t)(tb >> 32));
+                        } else if (sdf >= 0) {
+                            *Q.overflow = 1ull;   // a dropped entry would lose the SDF hit: the pass reports it
                         }
                     }
                 }
@@ -1167,6 +1169,8 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
                         if (!blocked && sdf >= 0 && at < Q.s_cap) {
                             const unsigned long long tb = (unsigned long long)__double_as_longlong(tl);
                             Q.sdfq_sh[at] = make_uint4(i, (uint32_t)sdf, (uint32_t)tb, (uint32_t)(tb >> 32));
+                        } else if (!blocked && sdf >= 0) {
+                            *Q.overflow = 1ull;
                         }
                     }
                 }
@@ -1664,7 +1668,7 @@ static unsigned grid_for(uint64_t items, unsigned block, unsigned cap_blocks) {
 }
 
 // Trace / shade / shadow for every depth of one chunk whose camera rays are queued.
-static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer& B, const WfQueues& Q,
+static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer& B, const WfQueues& Q,
                        const WfPlan& plan, bool count, hipStream_t stream, LaunchTimer* timer, uint64_t bound) {
     auto begin_k = [&](int cls, hipStream_t s) { if (timer) timer->begin(cls, s); };
     auto end_k = [&](int cls, hipStream_t s) { if (timer) timer->end(cls, s); };
@@ -1746,7 +1750,10 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
             const unsigned hl = grid_for(children * plan.lights_per_child, kTB, plan.lanes_shadow_blocks);
             const unsigned ha = grid_for(children * plan.lights_per_child, kTB, plan.full_shadow_blocks);
             const bool sq = PT_SDF_QUEUE_SHADOW && S.num_sdf > 0;
-            if (sq) (void)hipMemsetAsync(Q.counts + kSdfShWord, 0, sizeof(uint32_t), side);
+            if (sq) {
+                const hipError_t e = hipMemsetAsync(Q.counts + kSdfShWord, 0, sizeof(uint32_t), side);
+                if (e != hipSuccess) return e;
+            }
             if (count) {
                 hipLaunchKernelGGL((k_wf_shadow_lanes<true, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<true, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
@@ -1786,6 +1793,7 @@ static void depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer
         (void)hipStreamWaitEvent(stream, plan.ev_side[0], 0);
         (void)hipStreamWaitEvent(stream, plan.ev_side[1], 0);
     }
+    return hipSuccess;
 }
 
 hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
@@ -1807,7 +1815,7 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
             hipLaunchKernelGGL(k_wf_camera, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Q, begin,
                                cnt, spp_launch, r);
             end_k(0);
-            depth_loop(S, smp, B, Q, plan, count, stream, timer, cnt);
+            if ((e = depth_loop(S, smp, B, Q, plan, count, stream, timer, cnt)) != hipSuccess) return e;
         }
         begin_k(4);
         hipLaunchKernelGGL(k_wf_finalize, dim3(grid_for(pix_slots, 256, 4096)), dim3(256), 0, stream, P, B, Q, spp_d);
@@ -1843,7 +1851,7 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
         hipLaunchKernelGGL(k_wf_camera_extra, dim3(grid_for(cnt, 256, 4096)), dim3(256), 0, stream, cam, P, Qx,
                            e0 * (uint64_t)K, cnt, K, sample_base, plist, firefly == EXTRA_ADD_SCALED ? 1 : 0);
         end_k(0);
-        depth_loop(S, smp, B, Qx, plan, count, stream, timer, cnt);
+        if ((e = depth_loop(S, smp, B, Qx, plan, count, stream, timer, cnt)) != hipSuccess) return e;
         begin_k(4);
         hipLaunchKernelGGL(k_wf_finalize_extra, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, stream, P, B, Q.acc_s,
                            e0, (uint32_t)ne, K, plist, firefly == EXTRA_FIREFLY_STOP ? 1 : 0, snap, next_list,

@@ -154,3 +154,94 @@ def test_resume_then_firefly_pass_clears_foreign_pixels(gpu):
     assert (out[1].N[~own] == 0).all(), "foreign pixels survived the resume"
     assert (out[0].N[own] > 3).any(), "no firefly samples: the test exercises nothing"
     same_buffer(out[1], out[0])
+
+
+def test_contexts_driven_from_threads_equal_full_frame(gpu):
+    """bench.py's one-process form drives each context from its own host thread (bench._each).  Two
+    contexts on device 0 render the two halves of an interleaved tile split concurrently, in pass
+    batches of 2; context 0 takes context 1's tiles (pt_read_tiles → pt_write_tiles, the host form of
+    the gather) and must hold the single-context full-frame render, bit for bit."""
+    import bench
+    w, h = 160, 96
+    s, c, smp = _scene()
+    rs = []
+    try:
+        for k in range(2):
+            r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+            r.SamplesPerPixel, r.Seed, r.Engine = 2, 61, _abi.ENGINE_WAVEFRONT
+            r.Tiles = tiles_for_rank(w, h, k, 2)
+            rs.append(r)
+        bench._each(rs, lambda i, x: x.RenderPasses(2))
+        bench._each(rs, lambda i, x: x.Synchronize())
+        t1 = tiles_for_rank(w, h, 1, 2)
+        rs[0].WriteTiles(t1, *rs[1].ReadTiles(t1))
+        b = rs[0].ReadBuffer()
+        got = _Buf(b.M.copy(), b.V.copy(), b.N.copy())
+    finally:
+        for r in rs:
+            r.close()
+    same_buffer(got, _Buf(*_render(w, h, 2)))
+
+
+def test_bench_group_form_one_gpu(gpu, tmp_path):
+    """`bench.py --group --gpus 1`: the one-process multi-GPU form (pt_comm_init_all, one host thread per
+    device, pt_comm_gather_all inside the timed region) on this box's one GPU; the JSON line reports it,
+    and the gathered Buffer passes the bit check."""
+    import json
+
+    import bench
+    out = tmp_path / "b.json"
+    bench.main(["--group", "--gpus", "1", "--steps", "2", "--warmup", "1", "--spp", "2", "--cpu-seconds", "0",
+                "--no-parity", "--width", "256", "--height", "128", "--tris", "20000", "--mesh-source", "generator",
+                "--json-out", str(out)])
+    j = json.loads(out.read_text())
+    assert j["n_gpus"] == 1 and j["launch"].startswith("one process, one host thread")
+    assert j["config"]["gather_check"]["bit_exact"] is True
+    assert "pt_comm_gather_all" in j["config"]["parallelism"]
+    assert j["value"] > 0
+
+
+def test_group_pass_equals_plain_pass(gpu):
+    """The group form's render (pt_comm_init_all over one context, passes issued from a worker thread,
+    pt_comm_gather_all) leaves the Buffer a plain context leaves, bit for bit."""
+    import bench
+    w, h = 128, 96
+    s, c, smp = _scene()
+    r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+    try:
+        r.SamplesPerPixel, r.Seed, r.Engine = 2, 61, _abi.ENGINE_WAVEFRONT
+        Renderer.CommInitAll([r])
+        bench._each([r, r], lambda i, x: None)   # (the helper's threaded branch, no work)
+        import threading
+        t = threading.Thread(target=lambda: (r.RenderParallel(), r.RenderParallel()))
+        t.start()
+        t.join()
+        Renderer.GatherAll([r], 0)
+        b = r.ReadBuffer()
+        got = _Buf(b.M.copy(), b.V.copy(), b.N.copy())
+    finally:
+        r.close()
+    same_buffer(got, _Buf(*_render(w, h, 2)))
+
+
+def test_single_context_resume_keeps_restored_pixels(gpu):
+    """A lone context (no communicator) that loads a checkpoint and then renders tile subsets one after
+    another keeps every restored pixel outside the current subset (pt_write_buffer used to
+    mark the whole checkpoint foreign, and the first subset pass cleared the rest of the frame)."""
+    w, h = 96, 64
+    m, v, n = _render(w, h, 2)
+    s, c, smp = _scene()
+    r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+    try:
+        r.SamplesPerPixel, r.Seed, r.Engine = 2, 61, _abi.ENGINE_WAVEFRONT
+        r.LoadBuffer(_Buf(m, v, n), passes_done=2)
+        for k in range(2):          # pass 3 over the frame's two tile halves, one subset after the other
+            r.Tiles = tiles_for_rank(w, h, k, 2)
+            r.RenderParallel()
+            r._pass -= 1            # both halves are pass 3 of the frame
+        r._pass += 1
+        b = r.ReadBuffer()
+        got = _Buf(b.M.copy(), b.V.copy(), b.N.copy())
+    finally:
+        r.close()
+    same_buffer(got, _Buf(*_render(w, h, 3)))

@@ -361,6 +361,17 @@ def test_pass_batch_many_chunks(gpu, monkeypatch):
     _batched_vs_separate(s, c, smp, 320, 180, 4, 6)
 
 
+def test_pass_batch_split_by_memory_budget(gpu, monkeypatch):
+    """A batch whose accumulator sets exceed the memory budget runs as consecutive sub-batches (here
+    forced to 2 passes per launch sequence: 7 = 2 + 2 + 2 + 1), still the separate passes' bits and the
+    ray count summed over all 7 (a large K used to ask for K full-frame accumulator sets)."""
+    monkeypatch.setenv("PT_BATCH_MAX_PASSES", "2")
+    s, c, smp = scenes.bunny_frame(4000, seed=9)
+    smp.MaxBounces = 2
+    n = _batched_vs_separate(s, c, smp, 96, 64, 2, 7)
+    assert (n == 8).all()
+
+
 @pytest.mark.parametrize("case", ["megakernel", "stratified", "adaptive", "firefly"])
 def test_pass_batch_fallbacks(gpu, case):
     """Passes that cannot share one batch (megakernel engine, stratified, adaptive / firefly phases)

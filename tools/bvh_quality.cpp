@@ -1,0 +1,263 @@
+// bvh_quality — host-side measure of triangle-BVH4 quality on the C4 frame's ray mix.
+//
+// The closest-hit and shadow kernels are bound by their traversal steps (a step = one 128-B line:
+// an inner BVH4 node or a leaf chunk), so a tree is judged by the steps an actual ray mix takes
+// through it.  This tool builds the BVH the library builds (pt_bvh.cpp: binned-SAH BVH2, leaves of
+// <= 3 triangles, 4-wide collapse within the 32-entry stack) in its variants, then traces on the CPU:
+//   depth 0  camera rays of a strided pixel grid (Camera.CastRay without the jitter),
+//   depth 1+ cosine bounces from every hit (mesh triangles, or the floor y = 0), no origin offset,
+//            as the reference's Ray.Bounce starts at the hit point,
+//   shadow   from every hit to the two light spheres' centres (any-hit),
+// and reports steps, node steps, leaf steps and triangle tests per ray, by depth, plus the tree's
+// SAH cost.  Input: tools/dump_c4_mesh.py's file (triangles after FitInside, camera basis).
+//   usage: bvh_quality MESH.bin [stride] [variant ...]   variant: greedy | sah
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../ptsharp_amd/csrc/pt_bvh.h"
+#include "../ptsharp_amd/csrc/pt_math.h"
+
+using namespace pt;
+
+struct Mesh {
+    int n = 0;
+    std::vector<float> v1, v2, v3;
+    float cam_p[3], cam_u[3], cam_v[3], cam_w[3], cam_m;
+};
+
+static bool load(const char* path, Mesh& m) {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return false;
+    int32_t n = 0;
+    bool ok = std::fread(&n, 4, 1, f) == 1;
+    m.n = n;
+    m.v1.resize((size_t)n * 3); m.v2.resize((size_t)n * 3); m.v3.resize((size_t)n * 3);
+    ok = ok && std::fread(m.v1.data(), 4, (size_t)n * 3, f) == (size_t)n * 3;
+    ok = ok && std::fread(m.v2.data(), 4, (size_t)n * 3, f) == (size_t)n * 3;
+    ok = ok && std::fread(m.v3.data(), 4, (size_t)n * 3, f) == (size_t)n * 3;
+    ok = ok && std::fread(m.cam_p, 4, 3, f) == 3 && std::fread(m.cam_u, 4, 3, f) == 3 && std::fread(m.cam_v, 4, 3, f) == 3 &&
+         std::fread(m.cam_w, 4, 3, f) == 3 && std::fread(&m.cam_m, 4, 1, f) == 1;
+    std::fclose(f);
+    return ok;
+}
+
+struct Tree {
+    std::vector<uint32_t> words;   // BVH4 nodes, pt_bvh.h layout
+    std::vector<uint32_t> order;   // leaf position -> triangle
+    int stack_need = 0;
+    size_t nodes = 0, leaves = 0;
+    double fill = 0;
+};
+
+struct Count {
+    double rays = 0, nodes = 0, leaves = 0, tris = 0;
+    void add(const Count& o) { rays += o.rays; nodes += o.nodes; leaves += o.leaves; tris += o.tris; }
+};
+
+struct Tracer {
+    const Mesh& m;
+    const Tree& T;
+    v3 tv1(uint32_t p) const { uint32_t s = T.order[p]; return v3{m.v1[3 * s], m.v1[3 * s + 1], m.v1[3 * s + 2]}; }
+    v3 tv2(uint32_t p) const { uint32_t s = T.order[p]; return v3{m.v2[3 * s], m.v2[3 * s + 1], m.v2[3 * s + 2]}; }
+    v3 tv3(uint32_t p) const { uint32_t s = T.order[p]; return v3{m.v3[3 * s], m.v3[3 * s + 1], m.v3[3 * s + 2]}; }
+
+    // closest hit (any = false) or any hit before tlim (any = true); ordered BVH4 traversal, near child first
+    double trace(v3 o, v3 d, bool any, double tlim, Count& c, int32_t& prim) const {
+        c.rays++;
+        const v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        double best = any ? tlim : kHitInf;
+        prim = -1;
+        float tmax = (float)best;
+        uint32_t stack[64];
+        int sp = 0;
+        uint32_t ref = 0;
+        for (;;) {
+            if (!(ref & 0x80000000u)) {
+                c.nodes++;
+                const float* w = reinterpret_cast<const float*>(&T.words[(size_t)ref * kNode4Words]);
+                const uint32_t* refs = &T.words[(size_t)ref * kNode4Words + 24];
+                float key[4];
+                uint32_t ch[4];
+                int nh = 0;
+                for (int k = 0; k < 4; k++) {
+                    if (refs[k] == kEmpty4) continue;
+                    const float tx0 = (w[k] - o.x) * invd.x, tx1 = (w[4 + k] - o.x) * invd.x;
+                    const float ty0 = (w[8 + k] - o.y) * invd.y, ty1 = (w[12 + k] - o.y) * invd.y;
+                    const float tz0 = (w[16 + k] - o.z) * invd.z, tz1 = (w[20 + k] - o.z) * invd.z;
+                    const float tn = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmax(std::fmin(tz0, tz1), 0.f));
+                    const float tf = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmin(std::fmax(tz0, tz1), tmax));
+                    if (tn <= tf) { key[nh] = tn; ch[nh] = refs[k]; nh++; }
+                }
+                for (int a = 1; a < nh; a++)   // sort by entry distance
+                    for (int b = a; b > 0 && key[b] < key[b - 1]; b--) { std::swap(key[b], key[b - 1]); std::swap(ch[b], ch[b - 1]); }
+                if (nh > 0) {
+                    for (int k = nh - 1; k >= 1; k--) stack[sp++] = ch[k];
+                    ref = ch[0];
+                    continue;
+                }
+            } else {
+                c.leaves++;
+                const uint32_t first = ref & 0x1FFFFFFFu, cnt = ((ref >> 29) & 3u) + 1u;
+                for (uint32_t k = 0; k < cnt; k++) {
+                    c.tris++;
+                    const v3 a = tv1(first + k);
+                    const double t = isect_tri(a, sub(tv2(first + k), a), sub(tv3(first + k), a), o, d);
+                    if (t < best) {
+                        best = t;
+                        prim = (int32_t)(first + k);
+                        tmax = (float)t * 1.0000002f;
+                        if (any) return best;
+                    }
+                }
+            }
+            if (sp == 0) break;
+            ref = stack[--sp];
+        }
+        return best;
+    }
+};
+
+static double tree_sah(const Tree& T, double c_tri) {
+    // expected steps per ray through the root box: Σ P(node)·1 + Σ P(leaf)·(1 + n·c_tri), P = area ratio
+    auto area = [](const float* lo, const float* hi) {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return (double)(dx * dy + dy * dz + dz * dx);
+    };
+    const float* w0 = reinterpret_cast<const float*>(T.words.data());
+    float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < 4; k++) {
+        if (T.words[24 + k] == kEmpty4) continue;
+        for (int ax = 0; ax < 3; ax++) { rlo[ax] = std::fmin(rlo[ax], w0[8 * ax + k]); rhi[ax] = std::fmax(rhi[ax], w0[8 * ax + 4 + k]); }
+    }
+    const double ar = area(rlo, rhi);
+    double cost = 1.0;   // the root step
+    for (size_t n = 0; n < T.nodes; n++) {
+        const float* w = reinterpret_cast<const float*>(&T.words[n * kNode4Words]);
+        const uint32_t* refs = &T.words[n * kNode4Words + 24];
+        for (int k = 0; k < 4; k++) {
+            if (refs[k] == kEmpty4) continue;
+            float lo[3] = {w[k], w[8 + k], w[16 + k]}, hi[3] = {w[4 + k], w[12 + k], w[20 + k]};
+            const double p = area(lo, hi) / ar;
+            cost += (refs[k] & 0x80000000u) ? p * (1.0 + c_tri * (double)(((refs[k] >> 29) & 3u) + 1u)) : p;
+        }
+    }
+    return cost;
+}
+
+static void build(const Mesh& m, const std::string& variant, Tree& T, double& build_s) {
+    const size_t n = (size_t)m.n;
+    std::vector<float> lo(n * 3), hi(n * 3);
+    for (size_t i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++) {
+            const float a = m.v1[3 * i + k], b = m.v2[3 * i + k], c = m.v3[3 * i + k];
+            float l = std::fmin(std::fmin(a, b), c), h = std::fmax(std::fmax(a, b), c);
+            const float e = std::fmax(std::fabs(l), std::fabs(h)) * 2.0e-6f + 1e-30f;   // pt_api.hip pad_box
+            lo[3 * i + k] = l - e; hi[3 * i + k] = h + e;
+        }
+    const auto t0 = std::chrono::steady_clock::now();
+    BvhResult b2;
+    build_bvh(lo.data(), hi.data(), (int64_t)n, 0, b2, 3, false);
+    Bvh4Result b4;
+    if (variant == "sah") collapse_bvh4_sah(b2, kStackMax, b4);
+    else if (variant == "sah_nb") collapse_bvh4_sah(b2, 1000, b4);
+    else if (variant == "greedy_nb") collapse_bvh4(b2, 1000, b4);
+    else collapse_bvh4(b2, kStackMax, b4);
+    build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    T.words = b4.words;
+    T.order = b2.order;
+    T.stack_need = b4.stack_need;
+    T.nodes = b4.nodes();
+    T.fill = (double)b4.children / (4.0 * (double)T.nodes);
+    T.leaves = 0;
+    for (size_t i = 0; i < T.nodes; i++)
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r = T.words[i * kNode4Words + 24 + k];
+            if (r != kEmpty4 && (r & 0x80000000u)) T.leaves++;
+        }
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) { std::fprintf(stderr, "usage: %s MESH.bin [stride] [variant ...]\n", argv[0]); return 2; }
+    Mesh m;
+    if (!load(argv[1], m)) { std::fprintf(stderr, "cannot read %s\n", argv[1]); return 2; }
+    const int stride = argc > 2 ? std::atoi(argv[2]) : 16;
+    std::vector<std::string> variants;
+    for (int i = 3; i < argc; i++) variants.push_back(argv[i]);
+    if (variants.empty()) variants = {"greedy", "sah"};
+    if (const char* b = std::getenv("BINS")) g_bvh_bins = std::atoi(b);
+    const int W = 1920, H = 1080, kDepth = 4;
+    const v3 lights[2] = {v3{0.f, 5.f, 0.f}, v3{4.f, 5.f, 4.f}};
+    for (const auto& var : variants) {
+        Tree T;
+        double bs = 0;
+        build(m, var, T, bs);
+        Tracer tr{m, T};
+        Count cd[kDepth + 1], csh;
+        std::mt19937_64 rng(12345);
+        std::uniform_real_distribution<double> U(0.0, 1.0);
+        const v3 cp{m.cam_p[0], m.cam_p[1], m.cam_p[2]}, cu{m.cam_u[0], m.cam_u[1], m.cam_u[2]};
+        const v3 cv{m.cam_v[0], m.cam_v[1], m.cam_v[2]}, cw{m.cam_w[0], m.cam_w[1], m.cam_w[2]};
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int y = stride / 2; y < H; y += stride)
+            for (int x = stride / 2; x < W; x += stride) {
+                const double aspect = W / (double)H;
+                const double px = ((x + 0.5 - 0.5) / (W - 1.0)) * 2 - 1, py = ((y + 0.5 - 0.5) / (H - 1.0)) * 2 - 1;
+                v3 d = normalize(add(add(muls(cu, -px * aspect), muls(cv, -py)), muls(cw, m.cam_m)));
+                v3 o = cp;
+                for (int depth = 0; depth <= kDepth; depth++) {
+                    int32_t prim;
+                    double t = tr.trace(o, d, false, 0, cd[depth], prim);
+                    v3 nrm;
+                    if (d.y < 0) {   // the floor (the cube's top face, y = 0), tested beside the BVH as the kernels do
+                        const double tf = -(double)o.y / (double)d.y;
+                        if (tf > kEps && tf < t) { t = tf; prim = -2; }
+                    }
+                    if (prim == -1) break;
+                    const v3 p = add(o, muls(d, t));
+                    if (prim == -2) nrm = v3{0.f, 1.f, 0.f};
+                    else {
+                        const v3 a = tr.tv1((uint32_t)prim);
+                        nrm = normalize(cross(sub(tr.tv2((uint32_t)prim), a), sub(tr.tv3((uint32_t)prim), a)));
+                        if (dotf(nrm, d) > 0) nrm = neg(nrm);
+                    }
+                    for (const v3& L : lights) {   // shadow rays (hard, to the centre), any-hit before the light
+                        const v3 ld = normalize(sub(L, p));
+                        const double tl = (double)lengthf(sub(L, p)) - 1.0;
+                        int32_t sprim;
+                        tr.trace(p, ld, true, tl, csh, sprim);
+                    }
+                    // cosine bounce
+                    const double r1 = U(rng) * 2 * kPi, r2 = U(rng), r2s = std::sqrt(r2);
+                    const v3 ax = std::fabs(nrm.x) > 0.1f ? v3{0.f, 1.f, 0.f} : v3{1.f, 0.f, 0.f};
+                    const v3 u = normalize(cross(ax, nrm)), vv = cross(nrm, u);
+                    d = normalize(add(add(muls(u, std::cos(r1) * r2s), muls(vv, std::sin(r1) * r2s)), muls(nrm, std::sqrt(1 - r2))));
+                    o = p;
+                }
+            }
+        const double ts = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        Count all;
+        for (auto& c : cd) all.add(c);
+        std::printf("variant %-8s nodes %zu leaves %zu fill %.3f stack %d build %.2fs sah(ctri=0.5) %.3f trace %.1fs\n", var.c_str(),
+                    T.nodes, T.leaves, T.fill, T.stack_need, bs, tree_sah(T, 0.5), ts);
+        auto row = [](const char* name, const Count& c) {
+            if (c.rays == 0) return;
+            std::printf("  %-9s rays %9.0f  steps/ray %6.3f  nodes/ray %6.3f  leaves/ray %6.3f  tris/ray %6.3f\n", name, c.rays,
+                        (c.nodes + c.leaves) / c.rays, c.nodes / c.rays, c.leaves / c.rays, c.tris / c.rays);
+        };
+        row("closest", all);
+        for (int k = 0; k <= kDepth; k++) {
+            char nm[16];
+            std::snprintf(nm, sizeof nm, "depth %d", k);
+            row(nm, cd[k]);
+        }
+        row("shadow", csh);
+        std::fflush(stdout);
+    }
+    return 0;
+}
