@@ -391,9 +391,19 @@ inline void pad_box(float* lo, float* hi) {
 
 // BVH2 → 4-wide nodes (pt_bvh.h collapse_bvh4) as device float4 rows.  The
 // collapse keeps every path's pushes within the kStackMax-entry traversal stack.
-int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_nodes) {
+#ifndef PT_BVH_SAH
+#define PT_BVH_SAH 0   // 1: the SAH-optimal collapse (pt_bvh.h collapse_bvh4_sah) for the triangle BVH
+#endif
+#ifndef PT_BVH_CTRI
+#define PT_BVH_CTRI 0.5   // its triangle-test cost in traversal steps
+#endif
+#ifndef PT_BVH_BINS
+#define PT_BVH_BINS 32   // SAH bins per axis of the BVH2 build
+#endif
+int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_nodes, bool sah = false) {
     pt::Bvh4Result r;
-    pt::collapse_bvh4(b, pt::kStackMax, r);
+    if (sah) pt::collapse_bvh4_sah(b, pt::kStackMax, r, 1.0, PT_BVH_CTRI, 3);
+    else pt::collapse_bvh4(b, pt::kStackMax, r);
     if (r.stack_need > pt::kStackMax) return fail(PT_ERR_UNSUPPORTED, "BVH4 traversal stack bound exceeded");
     out.resize(r.words.size() / 4);
     std::memcpy(out.data(), r.words.data(), r.words.size() * sizeof(uint32_t));
@@ -1022,7 +1032,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         pad_box(&bmin[3 * i], &bmax[3 * i]);
     }
     pt::BvhResult tb;
-    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb, 3, PT_BVH_FILL_LEAVES != 0);   // leaves fit one chunk
+    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb, 3, PT_BVH_FILL_LEAVES != 0, PT_BVH_BINS);   // leaves fit one chunk
     std::vector<float4> tri_recs(nt * 3), tri_shade(nt * 3);
     const bool want_uv = d->num_textures > 0 && nt > 0;   // texture coordinates only matter with textures
     std::vector<float4> tri_uv(want_uv ? nt * 2 : 0);
@@ -1048,7 +1058,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     }
     std::vector<float4> tri_nodes;
     int32_t tri_num_nodes = 0;
-    if ((rc = pack_nodes(tb, tri_nodes, tri_num_nodes))) return rc;
+    if ((rc = pack_nodes(tb, tri_nodes, tri_num_nodes, PT_BVH_SAH != 0))) return rc;
     std::vector<float4> tri_chunks;
     if ((rc = make_leaf_chunks(tri_nodes, tri_recs, tri_chunks))) return rc;
     float tri_box[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};

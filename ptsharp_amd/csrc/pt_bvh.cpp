@@ -9,7 +9,6 @@
 #include <thread>
 
 namespace pt {
-int g_bvh_bins = 32;
 namespace {
 
 struct Aabb {
@@ -42,10 +41,11 @@ struct Builder {
     int max_threads;
     int max_leaf;
     bool fill_leaves;
+    int bins;
 
-    Builder(const float* a, const float* b, int64_t n, std::vector<BvhNode>& out, int threads, int leaf, bool fill)
+    Builder(const float* a, const float* b, int64_t n, std::vector<BvhNode>& out, int threads, int leaf, bool fill, int nbins)
         : pmin(a), pmax(b), cent((size_t)n * 3), idx((size_t)n), nodes(out), max_threads(threads), max_leaf(leaf),
-          fill_leaves(fill) {
+          fill_leaves(fill), bins(std::min(std::max(nbins, 2), kMaxBins)) {
         for (int64_t i = 0; i < n; i++) {
             idx[(size_t)i] = (uint32_t)i;
             for (int k = 0; k < 3; k++) cent[(size_t)i * 3 + k] = 0.5f * (pmin[i * 3 + k] + pmax[i * 3 + k]);
@@ -101,7 +101,7 @@ struct Builder {
             float best_cost = INFINITY; int best_axis = -1, best_split = -1;
             for (int ax = 0; ax < 3; ax++) {
                 if (ext[ax] <= 0.f) continue;
-                const int kBins = std::min(std::max(g_bvh_bins, 2), kMaxBins);
+                const int kBins = bins;
                 Aabb bb[kMaxBins]; int cnt[kMaxBins] = {0};
                 for (int b = 0; b < kBins; b++) bb[b].reset();
                 float scale = (float)kBins / ext[ax];
@@ -132,7 +132,7 @@ struct Builder {
                     return cent[(size_t)a * 3 + axis] < cent[(size_t)b * 3 + axis];
                 });
             } else {
-                const int kBins = std::min(std::max(g_bvh_bins, 2), kMaxBins);
+                const int kBins = bins;
                 float scale = (float)kBins / ext[best_axis];
                 float lo = cb.lo[best_axis];
                 auto it = std::partition(idx.begin() + begin, idx.begin() + end, [&](uint32_t p) {
@@ -163,7 +163,7 @@ struct Builder {
 }  // namespace
 
 void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out, int max_leaf,
-               bool fill_leaves) {
+               bool fill_leaves, int bins) {
     out.nodes.clear();
     out.order.clear();
     out.max_depth = 0;
@@ -171,7 +171,7 @@ void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int thre
     if (n <= 0) return;
     if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
     out.nodes.assign((size_t)(2 * n + 2), BvhNode{});
-    Builder b(prim_min, prim_max, n, out.nodes, threads, std::min(std::max(max_leaf, 1), kMaxLeafSize), fill_leaves);
+    Builder b(prim_min, prim_max, n, out.nodes, threads, std::min(std::max(max_leaf, 1), kMaxLeafSize), fill_leaves, bins);
     b.build(0, 0, n, 0);
     out.nodes.resize(b.next_pair.load());
     // padding node 1: an empty leaf
@@ -268,6 +268,8 @@ struct SahCollapser {
     Bvh4Result& out;
     double c_step, c_tri;
     int max_leaf;
+    Collapser* greedy;             // budget-keeping fallback for subtrees on the tallest paths (heights filled)
+    int budget;
     std::vector<double> cost;      // [node][4]: cost(n, i + 1)
     std::vector<int8_t> choice;    // [node][4]: 0 = one slot (leaf or inner), -1 = as with one slot fewer, k > 0: k slots to the left child
     std::vector<uint8_t> as_leaf;  // one slot: a leaf chunk rather than an inner node
@@ -339,6 +341,16 @@ struct SahCollapser {
         slots(n2[n].a, choice_split(n), C);
         slots(n2[n].a + 1, 4 - choice_split(n), C);
         const int pushed = A + (int)C.size() - 1;
+        // The stack bound: below a child c the greedy collapse can always finish within
+        // pushed + height(c) entries (its BVH2 pushes); where the DP's choice would leave a path
+        // without that room, this subtree is collapsed greedily instead (it keeps the bound by
+        // construction, as long as A + height(n) <= budget, which holds from the root down).
+        int maxh = 0;
+        for (uint32_t c : C) maxh = std::max(maxh, as_leaf[c] ? 0 : greedy->height[c]);
+        if (pushed + maxh > budget) {
+            greedy->emit(at, {n2[n].a, n2[n].a + 1}, A, depth);
+            return;
+        }
         out.stack_need = std::max(out.stack_need, pushed);
         out.children += (int64_t)C.size();
         uint32_t refs[4] = {kEmpty4, kEmpty4, kEmpty4, kEmpty4};
@@ -388,7 +400,9 @@ void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out,
     out.children = 0;
     if (bvh2.nodes.empty()) return;
     const size_t nn = bvh2.nodes.size();
-    SahCollapser c{bvh2.nodes, out, c_step, c_tri, max_leaf, std::vector<double>(nn * 4, 0.0),
+    Collapser g{bvh2.nodes, out, stack_budget, std::vector<int>(nn, 0)};
+    g.fill_height(0);
+    SahCollapser c{bvh2.nodes, out, c_step, c_tri, max_leaf, &g, stack_budget, std::vector<double>(nn * 4, 0.0),
                    std::vector<int8_t>(nn * 4, 0), std::vector<uint8_t>(nn, 0), std::vector<uint32_t>(nn, 0),
                    std::vector<uint32_t>(nn, 0)};
     c.solve(0);
@@ -405,7 +419,6 @@ void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out,
         return;
     }
     c.emit(root, 0, 0, 0);
-    if (out.stack_need > stack_budget) collapse_bvh4(bvh2, stack_budget, out);   // the greedy form keeps the bound
 }
 
 void collapse_bvh4(const BvhResult& bvh2, int stack_budget, Bvh4Result& out) {

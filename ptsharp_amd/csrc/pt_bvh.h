@@ -24,7 +24,6 @@ constexpr int kMaxDepth = 32;     // BVH2 depth bound
 constexpr int kStackMax = PT_STACK_MAX;
 static_assert(kStackMax >= kMaxDepth, "the collapse needs at least the BVH2 depth");
 constexpr int kMaxLeafSize = 4;
-extern int g_bvh_bins;   // SAH bins per axis of build_bvh (tools/bvh_quality.cpp varies it)
 
 // 32-byte node; nodes[0] is the root, nodes[1] is padding, every child pair
 // (left = 2k, right = 2k+1) starts on a 64-byte boundary.
@@ -49,8 +48,9 @@ struct BvhResult {
 // are 128-B chunks that one traversal step reads whole (7 loads for 1, 2 or 3 triangles), so a
 // leaf of three costs about what a leaf of one does, and SAH's per-primitive cost (which splits
 // most 3-triangle nodes) only adds steps.
+// bins: SAH bins per axis (2..256).
 void build_bvh(const float* prim_min, const float* prim_max, int64_t n, int threads, BvhResult& out,
-               int max_leaf = kMaxLeafSize, bool fill_leaves = false);
+               int max_leaf = kMaxLeafSize, bool fill_leaves = false, int bins = 32);
 
 // 4-wide BVH collapsed from the BVH2: one 128-byte node (one cache line) per
 // step of the traversal instead of a 64-byte child pair, so a ray makes about
@@ -78,7 +78,8 @@ void collapse_bvh4(const BvhResult& bvh2, int stack_budget, Bvh4Result& out);
 // The SAH-optimal collapse (pt_bvh.cpp SahCollapser): children chosen by a dynamic program over the
 // BVH2 that minimises the expected traversal cost, c_step per step (inner node or leaf chunk) and
 // c_tri per triangle test, weighted by surface area; BVH2 subtrees of at most max_leaf triangles may
-// merge into one leaf chunk.  Falls back to collapse_bvh4 if a path would exceed stack_budget.
+// merge into one leaf chunk.  Subtrees whose DP choice would break stack_budget on some path are
+// collapsed greedily (collapse_bvh4), so the bound holds.
 void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out, double c_step = 1.0,
                        double c_tri = 0.5, int max_leaf = 3);
 

@@ -502,6 +502,55 @@ __device__ __forceinline__ void coop_line(const float4* __restrict__ lines, uint
     }
 }
 
+// Cooperative line fetch without LDS (PT_COOP == 2).  The wave's lanes form 8 groups of 8: group
+// q = lane & 7, member m = lane >> 3 (lanes q, q + 8, ..., q + 56).  Load k (k = 0..7): member m < 7
+// loads piece m of the line of member k of its group, so each load instruction touches at most 8
+// distinct lines (one per group) instead of up to 64, and the texture-address path charges per
+// distinct line.  Lane (m, q) then holds piece m of its group's 8 lines; an 8x8 transpose of 16-B
+// elements across the members gives lane (k, q) the pieces of its own line: three butterfly stages
+// over member bits 4 / 2 / 1 = lane bits 32 / 16 / 8, done with gfx950's v_permlane32_swap and
+// v_permlane16_swap (one instruction per dword pair, no selects) and a DPP row_ror:8 exchange.
+// Wave-uniform call; `line` = kNoLine for a lane with nothing to fetch.
+__device__ __forceinline__ void swap32(float& a, float& b) {   // a's upper 32 lanes <-> b's lower 32 lanes
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap16(float& a, float& b) {   // a's odd rows of 16 <-> b's even rows
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap8(float& a, float& b, bool top) {   // a's lanes 8-15 <-> b's lanes 0-7 of each row
+    const float u = __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(a), 0x128, 0xf, 0xf, false));
+    const float v = __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(b), 0x128, 0xf, 0xf, false));
+    b = top ? u : b;
+    a = top ? a : v;
+}
+__device__ __forceinline__ void swap32(float4& a, float4& b) { swap32(a.x, b.x); swap32(a.y, b.y); swap32(a.z, b.z); swap32(a.w, b.w); }
+__device__ __forceinline__ void swap16(float4& a, float4& b) { swap16(a.x, b.x); swap16(a.y, b.y); swap16(a.z, b.z); swap16(a.w, b.w); }
+__device__ __forceinline__ void swap8(float4& a, float4& b, bool top) {
+    swap8(a.x, b.x, top); swap8(a.y, b.y, top); swap8(a.z, b.z, top); swap8(a.w, b.w, top);
+}
+__device__ __forceinline__ void coop_line_x(const float4* __restrict__ lines, uint32_t line, uint32_t lane, float4& q0,
+                                            float4& q1, float4& q2, float4& q3, float4& q4, float4& q5, float4& q6) {
+    const uint32_t m = lane >> 3, q = lane & 7u;
+    float4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {   // member m loads piece m of member k's line
+        const uint32_t src = (uint32_t)__shfl((int)line, 8 * k + (int)q, 64);
+        x[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (src != kNoLine && m < 7u) x[k] = lines[8 * (size_t)src + m];
+    }
+    // x[k] of lane (m, q) = element (m, k); transposed: x[j] of lane (k, q) = piece j of member k's line
+#pragma unroll
+    for (int k = 0; k < 4; k++) swap32(x[k], x[k | 4]);
+    swap16(x[0], x[2]); swap16(x[1], x[3]); swap16(x[4], x[6]); swap16(x[5], x[7]);
+    const bool top = (lane & 8u) == 0u;
+    swap8(x[0], x[1], top); swap8(x[2], x[3], top); swap8(x[4], x[5], top); swap8(x[6], x[7], top);
+    q0 = x[0]; q1 = x[1]; q2 = x[2]; q3 = x[3]; q4 = x[4]; q5 = x[5]; q6 = x[6];
+}
+
 // The line a traversal lane reads at its next step (coop_line's index; the arrays are one
 // allocation, pt_scene.h `lines`); an analytic leaf reads its records instead.
 __device__ __forceinline__ uint32_t step_line(const DevScene& S, bool has, bool tri, uint32_t ref) {
@@ -589,7 +638,7 @@ template <bool COUNT, bool FULL, bool SPLIT = false>
 __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q, int qi, unsigned long long* counters) {
     constexpr bool split = SPLIT;   // a template flag: the unsplit kernel keeps its registers
     __shared__ uint32_t s_stack[kLdsStack * kTB];
-#if PT_COOP
+#if PT_COOP == 1
     __shared__ float4 s_coop[kCoopRows];
 #endif
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
@@ -704,9 +753,12 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
         // one step: inner node or leaf of the current BVH (one 128-B line)
         const bool leaf = (ref & 0x80000000u) != 0;
         float4 q0, q1, q2, q3, q4, q5, q6;   // the step's line
-#if PT_COOP
+#if PT_COOP == 1
         coop_line(S.lines, step_line(S, has && !(FULL && mwait), tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7),
                   lane, q0, q1, q2, q3, q4, q5, q6);
+        if (!has || (FULL && mwait)) continue;
+#elif PT_COOP == 2
+        coop_line_x(S.lines, step_line(S, has && !(FULL && mwait), tri, ref), lane, q0, q1, q2, q3, q4, q5, q6);
         if (!has || (FULL && mwait)) continue;
 #else
         if (PT_LEAF_VOTE && !leaf_turn(has && !(FULL && mwait), leaf)) continue;
@@ -1204,7 +1256,7 @@ template <bool COUNT, bool FULL, bool SPLIT = false>
 __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters) {
     constexpr bool split = SPLIT;
     __shared__ uint32_t s_stack[kLdsStack * kTB];
-#if PT_COOP
+#if PT_COOP == 1
     __shared__ float4 s_coop[kCoopRows];
 #endif
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
@@ -1357,9 +1409,12 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
         // one step: inner node or leaf of the current BVH (one 128-B line)
         const bool leaf = (ref & 0x80000000u) != 0;
         float4 q0, q1, q2, q3, q4, q5, q6;   // the step's line
-#if PT_COOP
+#if PT_COOP == 1
         coop_line(S.lines, step_line(S, has && !waiting, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
                   q3, q4, q5, q6);
+        if (!has || waiting) continue;
+#elif PT_COOP == 2
+        coop_line_x(S.lines, step_line(S, has && !waiting, tri, ref), lane, q0, q1, q2, q3, q4, q5, q6);
         if (!has || waiting) continue;
 #else
         if (PT_LEAF_VOTE && !leaf_turn(has && !waiting, leaf)) continue;

@@ -56,8 +56,8 @@ struct Tree {
 };
 
 struct Count {
-    double rays = 0, nodes = 0, leaves = 0, tris = 0;
-    void add(const Count& o) { rays += o.rays; nodes += o.nodes; leaves += o.leaves; tris += o.tris; }
+    double rays = 0, nodes = 0, leaves = 0, tris = 0, inside = 0;   // inside: steps whose box holds the origin
+    void add(const Count& o) { rays += o.rays; nodes += o.nodes; leaves += o.leaves; tris += o.tris; inside += o.inside; }
 };
 
 struct Tracer {
@@ -92,7 +92,12 @@ struct Tracer {
                     const float tz0 = (w[16 + k] - o.z) * invd.z, tz1 = (w[20 + k] - o.z) * invd.z;
                     const float tn = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmax(std::fmin(tz0, tz1), 0.f));
                     const float tf = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmin(std::fmax(tz0, tz1), tmax));
-                    if (tn <= tf) { key[nh] = tn; ch[nh] = refs[k]; nh++; }
+                    if (tn <= tf) {
+                        key[nh] = tn; ch[nh] = refs[k]; nh++;
+                        if (o.x >= w[k] && o.x <= w[4 + k] && o.y >= w[8 + k] && o.y <= w[12 + k] && o.z >= w[16 + k] &&
+                            o.z <= w[20 + k])
+                            c.inside++;
+                    }
                 }
                 for (int a = 1; a < nh; a++)   // sort by entry distance
                     for (int b = a; b > 0 && key[b] < key[b - 1]; b--) { std::swap(key[b], key[b - 1]); std::swap(ch[b], ch[b - 1]); }
@@ -162,7 +167,7 @@ static void build(const Mesh& m, const std::string& variant, Tree& T, double& bu
         }
     const auto t0 = std::chrono::steady_clock::now();
     BvhResult b2;
-    build_bvh(lo.data(), hi.data(), (int64_t)n, 0, b2, 3, false);
+    build_bvh(lo.data(), hi.data(), (int64_t)n, 0, b2, 3, false, std::getenv("BINS") ? std::atoi(std::getenv("BINS")) : 32);
     Bvh4Result b4;
     if (variant == "sah") collapse_bvh4_sah(b2, kStackMax, b4);
     else if (variant == "sah_nb") collapse_bvh4_sah(b2, 1000, b4);
@@ -190,7 +195,6 @@ int main(int argc, char** argv) {
     std::vector<std::string> variants;
     for (int i = 3; i < argc; i++) variants.push_back(argv[i]);
     if (variants.empty()) variants = {"greedy", "sah"};
-    if (const char* b = std::getenv("BINS")) g_bvh_bins = std::atoi(b);
     const int W = 1920, H = 1080, kDepth = 4;
     const v3 lights[2] = {v3{0.f, 5.f, 0.f}, v3{4.f, 5.f, 4.f}};
     for (const auto& var : variants) {
@@ -247,8 +251,9 @@ int main(int argc, char** argv) {
                     T.nodes, T.leaves, T.fill, T.stack_need, bs, tree_sah(T, 0.5), ts);
         auto row = [](const char* name, const Count& c) {
             if (c.rays == 0) return;
-            std::printf("  %-9s rays %9.0f  steps/ray %6.3f  nodes/ray %6.3f  leaves/ray %6.3f  tris/ray %6.3f\n", name, c.rays,
-                        (c.nodes + c.leaves) / c.rays, c.nodes / c.rays, c.leaves / c.rays, c.tris / c.rays);
+            std::printf("  %-9s rays %9.0f  steps/ray %6.3f  nodes/ray %6.3f  leaves/ray %6.3f  tris/ray %6.3f  origin-box steps/ray %6.3f\n",
+                        name, c.rays, (c.nodes + c.leaves) / c.rays, c.nodes / c.rays, c.leaves / c.rays, c.tris / c.rays,
+                        c.inside / c.rays);
         };
         row("closest", all);
         for (int k = 0; k <= kDepth; k++) {

@@ -1,22 +1,23 @@
-# A/B of compile-time variants: the GPU tests on the first variant, then a short bench per variant
-# (and tools/bench_scenes.py on SCENES, bench.py --shard SHARD, if set).  usage: VARIANTS="base:|w6:-DPT_RAYS_WAVES=6" bash tools/gpu_ab.sh
+# A/B of compile-time variants on one box.  Per variant: rebuild, a parity subset (PARITY tests, the
+# refill-kernel and C4-tile checks by default), then the C4 bench (STEPS steps), and optionally the C2
+# bench (C2=1), the 1/8 share (SHARD=1) and the C5 bench (C5=1).  Stops at the first failure.
+# usage: VARIANTS="base:|coop:-DPT_COOP=2" bash tools/gpu_ab.sh TAG
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/ab
+D=gpurun_out/${1:-ab}; mkdir -p $D
 IFS='|' read -ra VS <<< "${VARIANTS:-base:}"
-first=1
+PARITY=${PARITY:-tests/test_00_gpu_baseline.py::test_c4_mesh1m_tiles tests/test_gpu_parity.py::test_refill_kernels_match_lockstep tests/test_gpu_parity.py::test_side_stream_deep_bvh_spill}
 for V in "${VS[@]}"; do
   NAME=${V%%:*}; FLAGS=${V#*:}
-  make -s -C ptsharp_amd/csrc clean >/dev/null && make -s -j16 -C ptsharp_amd/csrc EXTRA="$FLAGS" > gpurun_out/ab/build_$NAME.log 2>&1 || exit 1
-  if [ $first = 1 ] || [ -n "$TESTS_ALL" ]; then
-    timeout -k 10 900 python -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/ab/tests_$NAME.log 2>&1 || exit 1
-    first=0
+  echo "== $NAME ($FLAGS)" >> $D/progress.log
+  make -s -C ptsharp_amd/csrc clean >/dev/null && make -s -j16 -C ptsharp_amd/csrc EXTRA="$FLAGS" > $D/build_$NAME.log 2>&1 || exit 1
+  if [ "$PARITY" != "none" ]; then
+    timeout -k 10 600 python -u -m pytest $PARITY -x -q -m gpu --timeout 240 --timeout-method thread > $D/tests_$NAME.log 2>&1 || exit 1
   fi
-  timeout -k 10 300 python bench.py --steps ${STEPS:-8} --warmup 1 --spp ${SPP:-16} --cpu-seconds 0 --no-parity --json-out gpurun_out/ab/$NAME.json > gpurun_out/ab/$NAME.log 2>&1 || exit 1
-  if [ -n "$SHARD" ]; then
-    timeout -k 10 300 python bench.py --steps 32 --warmup 2 --cpu-seconds 0 --no-parity --shard $SHARD --json-out gpurun_out/ab/shard_$NAME.json > gpurun_out/ab/shard_$NAME.log 2>&1 || exit 1
-  fi
-  if [ -n "$SCENES" ]; then
-    timeout -k 10 300 python tools/bench_scenes.py $SCENES > gpurun_out/ab/scenes_$NAME.jsonl 2> gpurun_out/ab/scenes_$NAME.log || exit 1
-  fi
+  timeout -k 10 300 python -u bench.py --steps ${STEPS:-16} --warmup 2 --cpu-seconds 0 --no-parity --json-out $D/c4_$NAME.json > $D/c4_$NAME.log 2>&1 || exit 1
+  [ -n "$C2" ] && { timeout -k 10 300 python -u bench.py --workload c2 --steps 6 --warmup 1 --cpu-seconds 0 --no-parity --json-out $D/c2_$NAME.json > $D/c2_$NAME.log 2>&1 || exit 1; }
+  [ -n "$SHARD" ] && { timeout -k 10 300 python -u bench.py --shard 0/8 --steps 32 --warmup 2 --cpu-seconds 0 --no-parity --json-out $D/shard8_$NAME.json > $D/shard8_$NAME.log 2>&1 || exit 1; }
+  [ -n "$C5" ] && { timeout -k 10 400 python -u bench.py --workload c5 --steps 1 --warmup 1 --cpu-seconds 0 --no-parity --json-out $D/c5_$NAME.json > $D/c5_$NAME.log 2>&1 || exit 1; }
 done
+make -s -C ptsharp_amd/csrc clean >/dev/null && make -s -j16 -C ptsharp_amd/csrc > $D/build_final.log 2>&1
+exit 0
