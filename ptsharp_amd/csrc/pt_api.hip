@@ -250,7 +250,9 @@ int wf_alloc(Ctx* c, T** out, size_t n) {
 
 int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     const bool want_sdf = c->S.num_sdf > 0;   // the split traversal's SDF queues (pt_wavefront.hip k_wf_sdf_*)
-    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes && (!want_sdf || c->Q.sdfq))
+    const bool want_heavy = c->S.route != 0;  // the routed split's queues of rays that reach a row-4 shape's box
+    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes && (!want_sdf || c->Q.sdfq) &&
+        (!want_heavy || c->Q.hq))
         return PT_OK;
     cap = std::max(cap, c->wf_cap);
     scap = std::max(scap, c->wf_scap);
@@ -273,6 +275,8 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
         if ((rc = wf_alloc(c, &Q.n_lit[q], scap))) return rc;
     }
     if (want_sdf && (rc = wf_alloc(c, &Q.sdfq_sh, scap))) return rc;   // one shadow pass at a time uses it
+    if (want_heavy && (rc = wf_alloc(c, &Q.hq, cap))) return rc;
+    if (want_heavy && (rc = wf_alloc(c, &Q.hq_sh, scap))) return rc;   // one shadow pass at a time uses it
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
     Q.overflow = c->d_counters + pt::kOverflowCounter;
     // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
@@ -387,6 +391,12 @@ inline void pad_box(float* lo, float* hi) {
 // (pt_scene.h ana_linear); 0: always through the analytic BVH.
 #ifndef PT_ANA_LINEAR
 #define PT_ANA_LINEAR 8
+#endif
+#ifndef PT_SHADE_ROUTE
+#define PT_SHADE_ROUTE 1   // the routed shade (pt_scene.h shade_route); 0: every vertex of a FULL scene through the FULL shade
+#endif
+#ifndef PT_ROUTE
+#define PT_ROUTE 1   // the routed split traversal (pt_scene.h route); 0: every ray through the FULL analytic half
 #endif
 
 // BVH2 → 4-wide nodes (pt_bvh.h collapse_bvh4) as device float4 rows.  The
@@ -1112,6 +1122,16 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         make_rec(k, j, shape_mat_any(k, j, origin), &ana_recs[3 * i]);
         if (ana_pos[(size_t)k][(size_t)j] < 0) ana_pos[(size_t)k][(size_t)j] = (int32_t)i;
     }
+    // the row-4 records (SDF shapes, volumes, transformed shapes) with their BVH boxes, in record order:
+    // what the routed split's refill kernels test against a ray's segment (pt_scene.h route)
+    std::vector<float4> heavy;
+    for (size_t i = 0; i < na; i++) {
+        const size_t src = ab.order[i];
+        const int k = ana_kind[src];
+        if (k != PT_SHAPE_SDF && k != PT_SHAPE_VOLUME && k != PT_SHAPE_TRANSFORMED) continue;
+        heavy.push_back(f4(amin[3 * src], amin[3 * src + 1], amin[3 * src + 2], u2f((uint32_t)i)));
+        heavy.push_back(f4(amax[3 * src], amax[3 * src + 1], amax[3 * src + 2], 0.f));
+    }
     std::vector<float4> ana_nodes;
     int32_t ana_num_nodes = 0;
     if ((rc = pack_nodes(ab, ana_nodes, ana_num_nodes))) return rc;
@@ -1241,6 +1261,15 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     S.lights_lean = 1;
     for (const pt::DevLight& L : lights)
         if (!L.phantom && (L.kind == pt::KIND_SDF || L.kind == pt::KIND_VOLUME || L.kind == pt::KIND_XFORM)) S.lights_lean = 0;
+    // Routed split (C5's kind of scene: the 1M-triangle mesh, a floor cube, light spheres, one SDF shape and
+    // one transformed Volume): only the rays whose segment reaches a row-4 box take the FULL kernels
+    S.route = (PT_ROUTE && S.full_geom && S.lights_lean && na <= (size_t)PT_ANA_LINEAR && !heavy.empty() &&
+               tri_num_nodes > 64) ? 1 : 0;
+    S.heavy_count = (int32_t)(heavy.size() / 2);
+    bool mat_tex = false;
+    for (const auto& m : mats) mat_tex = mat_tex || m.tex >= 0 || m.ntex >= 0 || m.btex >= 0 || m.gtex >= 0;
+    S.shade_route = (PT_SHADE_ROUTE && S.full && !mat_tex) ? 1 : 0;
+    rc = upload(c, heavy, &S.heavy); if (rc) return rc;
     S.num_planes = (int32_t)plane_scene.size();
     S.num_lights = (int32_t)lights.size();
     for (int k = 0; k < 3; k++) S.env[k] = d->env_color[k];

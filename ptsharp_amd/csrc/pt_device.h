@@ -789,6 +789,83 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
     return blocked;
 }
 
+// ---- Routed split (DevScene::route).  The refill kernels test the lean analytic records (spheres,
+// cubes) themselves; a ray whose segment [0, best] reaches the BVH box of a row-4 ("heavy") record is
+// the only kind that goes on to the FULL kernels, which test just those records.  The boxes are the
+// ones the analytic BVH holds (widened by the march pads, so every reference hit lies inside), and a
+// record the BVH would reach lies inside every box on its path: testing its own box prunes exactly
+// the records that cannot give a nearer hit, as the split's bound does.
+__device__ __forceinline__ bool heavy_reach(const DevScene& S, v3 o, v3 invd, float tmax) {
+    for (int h = 0; h < S.heavy_count; h++) {
+        const float4 lo = S.heavy[2 * h], hi = S.heavy[2 * h + 1];
+        if (slab1(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, o, invd, tmax) != __int_as_float(0x7f800000)) return true;
+    }
+    return false;
+}
+// trace_ana over the heavy records only (the refill kernel took the planes, the lean analytic records
+// and the triangles): the same merge rules, the same deferred Volume march and SDF queue.
+template <bool COUNT>
+__device__ __forceinline__ void trace_heavy(const DevScene& S, v3 o, v3 d, Counters& ctr, HitRec& best,
+                                            int32_t* sdf_out) {
+    const double t_in = best.t;
+    const bool tri_best = best.kind == KIND_TRI;
+    if (tri_best) best.t = nextafter(best.t, (double)INFINITY);
+    const v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    int32_t pend = -1, pend_sdf = -1;
+    for (int h = 0; h < S.heavy_count; h++) {
+        const float4 lo = S.heavy[2 * h], hi = S.heavy[2 * h + 1];
+        if (slab1(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, o, invd, tmax_bound(best.t)) == __int_as_float(0x7f800000)) continue;
+        const uint32_t p = f2u(lo.w);
+        if (COUNT) ctr.prims++;
+        const float4* r = S.ana_recs + 3 * (size_t)p;
+        if (PT_COOP_MARCH && pend < 0 && march_deferred(S, r)) { pend = (int32_t)p; continue; }
+        if (sdf_out && pend_sdf < 0 && sdf_deferred(S, r)) { pend_sdf = (int32_t)p; continue; }
+        int32_t kind;
+        double tx = 0;
+        const double t = prim_t<false, true>(S, S.ana_recs, p, o, d, kind, &tx);
+        if (t < best.t) { best.t = t; best.kind = kind; best.idx = (int32_t)p; best.tx = tx; }
+    }
+    if (PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
+    if (sdf_out) *sdf_out = pend_sdf;
+    else sdf_pending<false>(S, o, d, pend_sdf, best);
+    if (best.kind == KIND_TRI && tri_best) best.t = t_in;
+}
+// ana_blocked over the heavy records only.
+template <bool COUNT>
+__device__ __forceinline__ bool heavy_blocked(const DevScene& S, const DevLight& L, v3 o, v3 d, Counters& ctr,
+                                              int32_t* sdf_out, double* tl_out) {
+    const double tl = light_t<true>(S, L, o, d);
+    if (!(tl < kHitInf)) return true;
+    HitRec best{tl, -1, -1};
+    const v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    const float tmax = tmax_bound(tl);
+    int32_t pend = -1, pend_sdf = -1;
+    for (int h = 0; h < S.heavy_count; h++) {
+        const float4 lo = S.heavy[2 * h], hi = S.heavy[2 * h + 1];
+        if (slab1(lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, o, invd, tmax) == __int_as_float(0x7f800000)) continue;
+        const uint32_t p = f2u(lo.w);
+        if (COUNT) ctr.prims++;
+        const float4* r = S.ana_recs + 3 * (size_t)p;
+        if (PT_COOP_MARCH && pend < 0 && march_deferred(S, r)) { pend = (int32_t)p; continue; }
+        if (sdf_out && pend_sdf < 0 && sdf_deferred(S, r)) { pend_sdf = (int32_t)p; continue; }
+        int32_t kind;
+        if (prim_t<false, true>(S, S.ana_recs, p, o, d, kind) < tl) return true;
+    }
+    if (PT_COOP_MARCH) {
+        bool blocked = false;
+        march_pending<true>(S, o, d, pend, best, &blocked);
+        if (blocked) return true;
+    }
+    if (sdf_out) {
+        *sdf_out = pend_sdf;
+        *tl_out = tl;
+        return false;
+    }
+    bool blocked = false;
+    sdf_pending<true>(S, o, d, pend_sdf, best, &blocked);
+    return blocked;
+}
+
 // ---------------------------------------------------------------- textures (§8f row 3)
 // Util.Modf / ColorTexture.Fract (Util.cs:108-113, Texture.cs:218-222): fractional part, sign kept.
 __device__ __forceinline__ double fract_d(double x) { return x - trunc(x); }

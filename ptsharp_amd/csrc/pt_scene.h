@@ -105,6 +105,16 @@ struct DevScene {
     int32_t ana_linear;        // 1: test ana_recs linearly in the refill kernels
     int32_t lights_lean;       // 1: every light's own t is a lean intersect (no SDF / Volume light): split shadow rays
     int32_t num_sdf;           // SDFShapes (the split closest hit queues their records: k_wf_sdf_hits)
+    // Routed split traversal (a scene with §8f row-4 shapes, at most 8 analytic records, lean lights and a
+    // large triangle BVH): the refill kernels test the lean analytic records (spheres, cubes) linearly and
+    // the row-4 ("heavy") records' boxes; only rays whose segment reaches such a box take the FULL half
+    int32_t route;
+    // Routed shade (a FULL scene whose materials carry no textures: only the environment texture or the
+    // row-4 shapes make it FULL): vertices hitting spheres, cubes, planes and triangles go to the lean
+    // shade kernel, the rest (row-4 hits, environment-texture misses) to the FULL one
+    int32_t shade_route;
+    int32_t heavy_count;
+    const float4* heavy;       // 2 float4 per heavy record: {box lo.xyz, record index (bits)} {box hi.xyz, 0}
     // counted passes only (else null): [0] Volume.Sample calls and [1] SDF evaluations of the
     // Volume / SDFShape intersect marches (DevBuffer::counters words 9 and 10)
     unsigned long long* march;

@@ -24,6 +24,10 @@ struct WfQueues {
     uint4* hits;         // {t (fp64 bits), kind, record}
     uint4* sdfq;         // split closest hit, PT_SDF_QUEUE: {slot, SDF record, best world t (fp64 bits)} (k_wf_sdf_hits)
     uint4* sdfq_sh;      // split shadow rays, PT_SDF_QUEUE: {slot, SDF record, the light's t (fp64 bits)} (k_wf_sdf_shadow)
+    // Routed split (DevScene::route): the slots of the rays whose segment reaches a §8f row-4 shape's box,
+    // per partition (pcap / spcap entries each): only these go through the FULL analytic half
+    uint32_t* hq;        // closest-hit rays (k_wf_trace_lanes → k_wf_trace<.., SPLIT>)
+    uint32_t* hq_sh;     // shadow rays (k_wf_shadow_lanes → k_wf_shadow<.., SPLIT>; one shadow pass at a time)
     // Shadow rays (a diffuse child's sampleLights, set up by k_wf_shade), two sets by depth
     // parity (set q holds the shadow rays counted in pair word q), so the shadow pass and the
     // light-term accumulation of depth d can run beside the closest-hit and shade passes of d + 1.
@@ -56,22 +60,27 @@ struct WfQueues {
 #endif
 constexpr int kCountStride = PT_COUNT_STRIDE;
 static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
-constexpr int kFetchSlot = 2 * kParts;
-constexpr int kKeptSlot = 9 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
-constexpr int kSdfSlot = 9 * kParts + 2;   // entries of Q.sdfq (PT_SDF_QUEUE)
-constexpr int kSdfShSlot = 9 * kParts + 3;   // entries of Q.sdfq_sh
-constexpr int kEndSlot = 9 * kParts + 4;
+constexpr int kFetchSlot = 2 * kParts;   // 8 cursors (k = 0..7) per partition
+constexpr int kKeptSlot = 10 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
+constexpr int kSdfSlot = 10 * kParts + 2;   // entries of Q.sdfq (PT_SDF_QUEUE)
+constexpr int kSdfShSlot = 10 * kParts + 3;   // entries of Q.sdfq_sh
+constexpr int kHeavySlot = 10 * kParts + 4;     // kParts slots: entries of Q.hq per partition
+constexpr int kHeavyShSlot = 11 * kParts + 4;  // kParts slots: entries of Q.hq_sh per partition
+constexpr int kEndSlot = 12 * kParts + 4;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kCountWords = count_word(kEndSlot);
 constexpr int kChunkResetWords = kCountWords;   // every slot is zeroed per chunk
 constexpr int kOverflowCounter = 15;            // DevBuffer::counters word of WfQueues::overflow
 // work-fetch cursor of kernel k (0 trace, 1 shade, 2 + q shadow rays of set q, 4 the analytic phase
-// of a split closest hit, 5 + q that of split shadow rays of set q; pt_wavefront.hip "split") in partition g
+// of a split closest hit, 5 + q that of split shadow rays of set q; pt_wavefront.hip "split"; 7 the FULL
+// shade of a routed shade, DevScene::shade_route) in partition g
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
 constexpr int kSdfWord = count_word(kSdfSlot);
 constexpr int kSdfShWord = count_word(kSdfShSlot);
+constexpr int heavy_word(int g) { return count_word(kHeavySlot + g); }
+constexpr int heavy_sh_word(int g) { return count_word(kHeavyShSlot + g); }
 
 #ifndef PT_LDS_STACK
 #define PT_LDS_STACK 16

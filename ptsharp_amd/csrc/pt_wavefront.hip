@@ -319,9 +319,11 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
     if (!SPLIT && blockIdx.x == 0 && threadIdx.x < kParts) {
         *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
         Q.counts[fetch_word(1, threadIdx.x)] = 0u;               // k_wf_shade's fetch cursors
+        Q.counts[fetch_word(7, threadIdx.x)] = 0u;               // (the FULL one's of a routed shade)
     }
     const Group G = xcd_group();
-    const uint32_t cnt = *ray_count(Q, qi, G.g);
+    const bool route = SPLIT && S.route;   // the heavy queue's rays only (the refill half finished the others)
+    const uint32_t cnt = route ? Q.counts[heavy_word((int)G.g)] : *ray_count(Q, qi, G.g);
     const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
     uint32_t* cursor = Q.counts + fetch_word(SPLIT ? 4 : 0, G.g);
     const uint32_t lane = threadIdx.x & 63;
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
         if (kc >= n) break;
         for (uint32_t k0 = kc; k0 < kc + 64u * kFetchBatches && k0 < n; k0 += 64u) {
             if (k0 + lane >= n) continue;
-            const uint32_t i = base + k0 + lane;
+            const uint32_t i = route ? Q.hq[base + k0 + lane] : base + k0 + lane;
             float4 b = nt_load(&Q.q_d[qi][i]);
             if (__float_as_uint(b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
                 hit_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
@@ -353,7 +355,8 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
                 h.idx = (int32_t)r.w;
                 h.tx = h.t;
                 int32_t sdf = -1;
-                trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h, PT_SDF_QUEUE ? &sdf : nullptr);
+                if (route) trace_heavy<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, ctr, h, PT_SDF_QUEUE ? &sdf : nullptr);
+                else trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h, PT_SDF_QUEUE ? &sdf : nullptr);
                 if (PT_SDF_QUEUE) {   // k_wf_sdf_hits traces it, every lane busy (the active lanes append here)
                     const uint64_t m = __ballot(sdf >= 0);
                     if (m) {
@@ -645,6 +648,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
         Q.counts[fetch_word(1, threadIdx.x)] = 0u;               // k_wf_shade's fetch cursors
+        Q.counts[fetch_word(7, threadIdx.x)] = 0u;               // (the FULL one's of a routed shade)
     }
     const Group G = xcd_group();
     // claims start in the XCD's own partition; with PT_STEAL a wave whose partition is drained
@@ -668,13 +672,30 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     double bt = kHitInf, btx = 0.0;   // btx (FULL): HitRec::tx of the best
     int32_t bkind = -1, bidx = -1;
     float tmax = 0.f;
+    const bool route = split && S.route;   // routed split: only rays that reach a heavy box go on (hq)
+    bool hpend = false;                       // this lane's finished ray goes to the heavy queue (at the loop top)
     auto finish = [&]() {
         unsigned long long tb = (unsigned long long)__double_as_longlong(FULL && bkind == KIND_XFORM ? btx : bt);
         hit_store(&Q.hits[i & 0x7FFFFFFFu], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
-        if (!split) kept += (bkind >= 0 || !env_black) ? 1u : 0u;
+        if (route) hpend = heavy_reach(S, o, invd, tmax_bound(bt));
+        if (!split || (route && !hpend)) kept += (bkind >= 0 || !env_black) ? 1u : 0u;
         has = false;
     };
     for (;;) {
+        if (route) {   // wave-uniform: the finished rays that reach a heavy box, appended with one atomic per wave
+            const uint64_t hm = __ballot(hpend);
+            if (hm) {
+                const int lead = __builtin_ctzll(hm);
+                uint32_t at = 0;
+                if ((int)lane == lead) at = atomicAdd(Q.counts + heavy_word((int)part), (uint32_t)__popcll(hm));
+                at = (uint32_t)__shfl((int)at, lead, 64) + (uint32_t)__popcll(hm & below);
+                if (hpend) {
+                    if (at < Q.pcap) Q.hq[part * Q.pcap + at] = i & 0x7FFFFFFFu;
+                    else *Q.overflow = 1ull;
+                    hpend = false;
+                }
+            }
+        }
         if constexpr (FULL && PT_COOP_MARCH) {   // wave-uniform: every lane is here
             const uint64_t mq = __ballot(mwait);
             for (uint64_t todo = mq; todo; todo &= todo - 1ull) {   // each waiting ray, marched by the whole wave
@@ -730,8 +751,9 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                         const double t = isect_plane(v3{pa.x, pa.y, pa.z}, v3{pb.x, pb.y, pb.z}, o, d);
                         if (t < bt) { bt = t; bkind = KIND_PLANE; bidx = p; }
                     }
-                    if (S.ana_linear) {   // a few analytic shapes: every lane the same record (one line per load)
+                    if (S.ana_linear || route) {   // a few analytic shapes: every lane the same record (one line per load)
                         for (int p = 0; p < S.ana_count; p++) {
+                            if (route && f2u(S.ana_recs[3 * p].w) > (uint32_t)KIND_CUBE) continue;   // heavy: its box at finish
                             if (COUNT) ctr.prims++;
                             int32_t kind;
                             double tx = 0;
@@ -1075,7 +1097,10 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     // beat the direct form down to ~92 % kept in the lean kernels (C4 +1.6 %, C2 +9.8 %); the
     // FULL kernels keep the round-1 rule (SCAN below half kept; forcing it cost them 8-10 %).
     const unsigned long long kept = Q.counts[kept_word(qi)];
-    const bool scan = form ? form == 2
+    // routed shade: the lean and the FULL kernel each list their own vertices (SCAN only)
+    const bool routed = S.shade_route != 0;
+    const bool scan = routed ? true
+                    : form ? form == 2
                            : (FULL || !PT_SCAN_MOST) ? 2ull * kept < (unsigned long long)queued
                                                      : 32ull * kept < 31ull * (unsigned long long)queued;
     if (scan != SCAN) return;
@@ -1102,6 +1127,10 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         }
     } else {
         const bool env_black = (!FULL || S.env_tex < 0) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
+        // routed: the lean kernel takes the hits on spheres, cubes, planes and triangles, and the misses unless the
+        // environment is textured; the FULL kernel takes the rest
+        const bool env_lean = S.env_tex < 0;
+        uint32_t* const shade_cursor = Q.counts + fetch_word(routed && FULL ? 7 : 1, G.g);
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
         const uint64_t below = (1ull << lane) - 1ull;
         __shared__ uint32_t s_wcnt[kShadeScan * 4];
@@ -1115,7 +1144,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         // fewer than PT_SCAN_CLAIMS claims (small chunks: one rank's share of a multi-GPU frame)
         const uint32_t rows = max(1u, min((uint32_t)kShadeScan, n / (G.nb * 256u * (uint32_t)PT_SCAN_CLAIMS)));
         for (;;) {
-            if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u * rows);
+            if (threadIdx.x == 0) s_k0 = atomicAdd(shade_cursor, 256u * rows);
             __syncthreads();
             const uint32_t k0 = s_k0;  // thread 0 rewrites it only after the barriers below
             const bool last = k0 >= n;   // block-uniform: nothing claimed, shade what is held over
@@ -1129,7 +1158,9 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                     hv[j] = make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u);
                     if ((uint32_t)j < rows && sl < n) hv[j] = nt_load(&Q.hits[base + sl]);
                     const int32_t kind = (int32_t)hv[j].z;
-                    keep |= (kind != kDeadKind && (kind >= 0 || !env_black)) ? 1u << j : 0u;
+                    bool k = kind != kDeadKind && (kind >= 0 || !env_black);
+                    if (routed) k = k && ((kind >= 0 ? kind <= KIND_TRI : env_lean) != FULL);
+                    keep |= k ? 1u << j : 0u;
                 }
                 uint64_t bal[kShadeScan];
 #pragma unroll
@@ -1188,7 +1219,8 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
-    const uint32_t cnt = *nee_count(Q, qo, G.g);
+    const bool route = SPLIT && S.route;   // the heavy queue's rays only (the refill half decided the others)
+    const uint32_t cnt = route ? Q.counts[heavy_sh_word((int)G.g)] : *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
     uint32_t* cursor = Q.counts + fetch_word(SPLIT ? 5 + qo : 2 + qo, G.g);
     const uint32_t lane = threadIdx.x & 63;
@@ -1199,8 +1231,8 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
         kc = __shfl(kc, 0, 64);
         if (kc >= n) break;
         for (uint32_t k0 = kc; k0 < kc + 64u * kFetchBatches && k0 < n; k0 += 64u) {
-            const uint32_t i = base + k0 + lane;
             if (k0 + lane >= n) continue;
+            const uint32_t i = route ? Q.hq_sh[base + k0 + lane] : base + k0 + lane;
             if (SPLIT && Q.n_lit[qo][i] == 0) continue;   // blocked (or dead) in the refill half
             bool lit = false;
             const float4 b = nt_load(&Q.n_n[qo][i]);
@@ -1209,8 +1241,11 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
                 const float4 a = nt_load(&Q.n_o[qo][i]);
                 int32_t sdf = -1;
                 double tl = 0;
-                const bool blocked = ana_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr,
-                                                        PT_SDF_QUEUE_SHADOW ? &sdf : nullptr, &tl);
+                const bool blocked =
+                    route ? heavy_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, ctr,
+                                                 PT_SDF_QUEUE_SHADOW ? &sdf : nullptr, &tl)
+                          : ana_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr,
+                                               PT_SDF_QUEUE_SHADOW ? &sdf : nullptr, &tl);
                 if (PT_SDF_QUEUE_SHADOW) {   // k_wf_sdf_shadow tests it, every lane busy
                     const uint64_t m = __ballot(!blocked && sdf >= 0);
                     if (m) {
@@ -1276,6 +1311,14 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     float tmax = 0.f;
     uint32_t pf_val = 0;   // PT_PREFETCH: the word read ahead (kept alive until the next step)
     bool waiting = false;   // a root whose traversal is done, waiting for its tail helpers
+    const bool route = split && S.route;   // routed split: lit rays that reach a heavy box go on (hq_sh)
+    bool hpend = false;
+    // a root ray found nothing nearer than its light: lit (a phantom light never is); under the routed
+    // split, provisionally when the ray reaches a heavy box (the FULL half decides: k_wf_shadow<.., SPLIT>)
+    auto report_lit = [&]() {
+        Q.n_lit[qo][i] = phantom ? 0 : 1;
+        if (route && !phantom) hpend = heavy_reach(S, o, invd, tmax);
+    };
 #if PT_SHADOW_HELP
     // The tail (queue drained): idle lanes take stack entries of busy lanes' rays and traverse
     // those subtrees (any-hit: the ray is blocked iff some subtree holds a blocker, in any order).
@@ -1288,6 +1331,20 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     const uint32_t wbase = threadIdx.x & ~63u;
 #endif
     for (;;) {
+        if (route) {   // wave-uniform: the provisionally lit rays that reach a heavy box, one atomic per wave
+            const uint64_t hm = __ballot(hpend);
+            if (hm) {
+                const int lead = __builtin_ctzll(hm);
+                uint32_t at = 0;
+                if ((int)lane == lead) at = atomicAdd(Q.counts + heavy_sh_word((int)part), (uint32_t)__popcll(hm));
+                at = (uint32_t)__shfl((int)at, lead, 64) + (uint32_t)__popcll(hm & below);
+                if (hpend) {
+                    if (at < Q.spcap) Q.hq_sh[part * Q.spcap + at] = i;
+                    else *Q.overflow = 1ull;
+                    hpend = false;
+                }
+            }
+        }
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (more && (nidle >= PT_SHADOW_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
@@ -1331,8 +1388,9 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                             const float4 pa = S.planes[2 * p], pb = S.planes[2 * p + 1];
                             if (isect_plane(v3{pa.x, pa.y, pa.z}, v3{pb.x, pb.y, pb.z}, o, d) < tl) run = false;
                         }
-                        if (S.ana_linear)   // the light itself gives t == tl, never nearer
+                        if (S.ana_linear || route)   // the light itself gives t == tl, never nearer
                             for (int p = 0; p < S.ana_count; p++) {
+                                if (route && f2u(S.ana_recs[3 * p].w) > (uint32_t)KIND_CUBE) continue;   // heavy: its box at the end
                                 if (COUNT) ctr.prims++;
                                 int32_t kind;
                                 if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) run = false;
@@ -1344,7 +1402,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                     ref = 0;
                     if (run && tri && !tri_reach(S, o, invd, tmax)) {   // nothing of the mesh before the light
                         run = false;
-                        Q.n_lit[qo][i] = phantom ? 0 : 1;
+                        report_lit();
                     } else if (!run) {
                         Q.n_lit[qo][i] = 0;
                     }
@@ -1364,7 +1422,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                     if (!helper) Q.n_lit[qo][i] = 0;
                     has = false;
                 } else if (waiting && st == 0u) {   // the root's own traversal and every helper done
-                    Q.n_lit[qo][i] = phantom ? 0 : 1;
+                    report_lit();
                     has = false;
                 }
             }
@@ -1487,7 +1545,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                 ref = 0;
             } else if (s_help[root] == 0u) {   // no primitive nearer than the light: lit (a phantom light never is)
                 has = false;
-                Q.n_lit[qo][i] = phantom ? 0 : 1;
+                report_lit();
             } else {
                 waiting = true;   // the tail block above decides once the helpers are done
             }
@@ -1505,7 +1563,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                 ref = 0;
             } else {   // no primitive nearer than the light: lit (a phantom light never is)
                 has = false;
-                Q.n_lit[qo][i] = phantom ? 0 : 1;
+                report_lit();
             }
         }
 #endif
@@ -1744,6 +1802,8 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
         begin_k(1, stream);
+        if (split && S.route)   // the routed split's heavy queue counts, before the refill half appends
+            (void)hipMemsetAsync(Q.counts + heavy_word(0), 0, sizeof(uint32_t) * count_word(kParts), stream);
         if (split) {
             const unsigned tl = grid_for(n, kTB, plan.lanes_trace_blocks), ta = grid_for(n, kTB, plan.full_trace_blocks);
             if (count) {
@@ -1777,8 +1837,17 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     for (int depth = 0; depth <= smp.mb; depth++) {
         const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
         begin_k(2, stream);
-        // both forms (the one the kept count selects runs, the other returns at once)
-        if (count && full) {
+        // both forms (the one the kept count selects runs, the other returns at once); a routed shade runs
+        // the lean and the FULL SCAN kernels, each on its own vertices
+        if (full && S.shade_route) {
+            if (count) {
+                hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            } else {
+                hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            }
+        } else if (count && full) {
             hipLaunchKernelGGL((k_wf_shade<true, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
             hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
         } else if (count) {
@@ -1807,6 +1876,10 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
             const bool sq = PT_SDF_QUEUE_SHADOW && S.num_sdf > 0;
             if (sq) {
                 const hipError_t e = hipMemsetAsync(Q.counts + kSdfShWord, 0, sizeof(uint32_t), side);
+                if (e != hipSuccess) return e;
+            }
+            if (S.route) {   // the routed split's heavy shadow queue counts
+                const hipError_t e = hipMemsetAsync(Q.counts + heavy_sh_word(0), 0, sizeof(uint32_t) * count_word(kParts), side);
                 if (e != hipSuccess) return e;
             }
             if (count) {

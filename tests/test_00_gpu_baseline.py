@@ -65,3 +65,26 @@ def test_c5_mixed_4k_tiles_adaptive(gpu):
                                 engine=_abi.ENGINE_WAVEFRONT, adaptive=2)
     assert (g.N > 0).sum() == len(tiles) * 1024 and (g.N[g.N > 0] == 2 * (1 + 2)).all()
     check(g, gr, o, orr)
+
+
+def test_c2_gopher3_1080p_tiles(gpu):
+    """C2 at its own frame: gopher3 with NewSampler(16,16) at 1920x1080 (no triangle BVH, the lockstep
+    kernels), on one 512th of the frame's tiles (4 tiles), 1 pass of 2 spp."""
+    s, c, smp = scenes.gopher3()
+    tiles = tiles_for_rank(1920, 1080, 7, 512)
+    g, gr, o, orr = render_both(s, c, smp, 1920, 1080, spp=2, passes=1, seed=22, tiles=tiles,
+                                engine=_abi.ENGINE_WAVEFRONT)
+    assert (g.N > 0).sum() == len(tiles) * 1024
+    check(g, gr, o, orr)
+
+
+def test_c5_mixed_4k_tiles_adaptive32(gpu):
+    """C5 as the bench runs it: the mixed scene at 3840x2160, RenderParallel with AdaptiveSamples 32
+    (Example.cs:355,412): 1 + 32 camera samples per pixel, each adaptive one its own AddSample; on two
+    of the 4K frame's tiles (every 4096th), 1 pass."""
+    s, c, smp = scenes.mixed(1_000_000)
+    tiles = tiles_for_rank(3840, 2160, 1, 4096)
+    g, gr, o, orr = render_both(s, c, smp, 3840, 2160, spp=1, passes=1, seed=4097, tiles=tiles,
+                                engine=_abi.ENGINE_WAVEFRONT, adaptive=32)
+    assert (g.N[g.N > 0] == 33).all() and (g.N > 0).sum() == len(tiles) * 1024
+    check(g, gr, o, orr)
