@@ -860,6 +860,13 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         sdfc.node(d->sdf_shapes[i].root);
         o.len = (int32_t)sdfc.prog.size() - o.begin;
         o.mat = d->sdf_shapes[i].material;
+        int leaves = 0, folds = 0;   // a chain: one leaf, no fold (pt_ext.h sdf_eval_chain)
+        for (int k = o.begin; k < o.begin + o.len; k++) {
+            const int op = sdfc.prog[(size_t)k].op;
+            if (op <= pt::SDF_LEAF_TORUS) leaves++;
+            if (op == pt::SDF_UNION || op == pt::SDF_DIFFERENCE || op == pt::SDF_INTERSECTION || op == pt::SDF_CONST0) folds++;
+        }
+        o.chain = (leaves == 1 && folds == 0) ? 1 : 0;
         sdf_boxes[i] = sdf_box(d, d->sdf_shapes[i].root);   // SDFShape.BoundingBox (SDF.cs:100-103)
         o.bmin[0] = sdf_boxes[i].mn.x; o.bmin[1] = sdf_boxes[i].mn.y; o.bmin[2] = sdf_boxes[i].mn.z;
         o.bmax[0] = sdf_boxes[i].mx.x; o.bmax[1] = sdf_boxes[i].mx.y; o.bmax[2] = sdf_boxes[i].mx.z;

@@ -246,6 +246,30 @@ __device__ __forceinline__ bool sdf_deferred(const DevScene& S, const float4* r)
     if (kind == KIND_SDF) return true;
     return kind == KIND_XFORM && S.xforms[rec_ext(r)].kind == KIND_SDF;
 }
+// Intersect of an SDF record (an SDFShape, or a TransformedShape of one): prim_t's t for the SDF
+// queues (k_wf_sdf_hits / k_wf_sdf_shadow) without prim_t's other kinds (their calls and stacks).
+__device__ __forceinline__ double sdf_record_t(const DevScene& S, uint32_t p, v3 o, v3 d, int32_t& kind, double& tx) {
+    const float4* r = S.ana_recs + 3 * (size_t)p;
+    kind = (int32_t)f2u(r[0].w);
+    uint32_t n = 0;
+    double t;
+    if (kind == KIND_SDF) {
+        t = sdf_t(S.sdf_prog, S.sdf_params, S.sdf_shapes[rec_ext(r)], o, d, &n);
+    } else {   // TransformedShape.Intersect (TransformedShape.cs:43-73) of an SDFShape, as xform_t
+        const DevXform& X = S.xforms[rec_ext(r)];
+        const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
+        t = sdf_t(S.sdf_prog, S.sdf_params, S.sdf_shapes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, &n);
+        if (t < kHitInf) {
+            tx = t;
+            const v3 position = mat_position(X.m, add(so, muls(sd, t)));
+            t = (double)lengthf(sub(position, o));
+        } else {
+            t = kHitInf;
+        }
+    }
+    if (S.march) atomicAdd(S.march + 1, (unsigned long long)n);
+    return t;
+}
 template <bool ANY>
 __device__ __forceinline__ void sdf_pending(const DevScene& S, v3 o, v3 d, int32_t p, HitRec& best, bool* blocked = nullptr) {
     if (p < 0) return;

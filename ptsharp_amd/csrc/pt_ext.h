@@ -41,7 +41,8 @@ struct DevSdfIns {
 };
 struct DevSdfShape {
     int32_t begin, len;   // program range
-    int32_t mat, _pad;
+    int32_t mat;
+    int32_t chain;        // 1: one leaf under point ops and value scalings only (no fold): sdf_eval_chain
     float bmin[3], bmax[3];   // SDFShape.BoundingBox (SDF.BoundingBox of the root)
 };
 struct DevWindow {
@@ -203,6 +204,39 @@ PT_HD double sdf_eval(const DevSdfIns* prog, const double* params, int begin, in
     return vals[0];
 }
 
+// SDF.Evaluate of a chain program (DevSdfShape::chain: Transform / Scale / Repeat nodes above one
+// leaf, no Union / Difference / Intersection): after the leaf only value scalings and point pops
+// follow, so no saved point is read again and the one value needs no stack.  The same operations as
+// sdf_eval in the same order, with the point and the value in registers (sdf_eval's stacks, indexed
+// at run time, live in scratch memory).
+PT_HD double sdf_eval_chain(const DevSdfIns* prog, const double* params, int begin, int len, v3 p) {
+    v3 q = p;
+    double v = 0.0;
+    for (int i = begin; i < begin + len; i++) {
+        const DevSdfIns I = prog[i];
+        const double* P = params + I.param;
+        switch (I.op) {
+            case SDF_PUSH_TRANSFORM: q = mat_position(P, q); break;
+            case SDF_PUSH_SCALE: q = mk((double)q.x / P[0], (double)q.y / P[0], (double)q.z / P[0]); break;
+            case SDF_PUSH_REPEAT: {
+                v3 st = mk(P[0], P[1], P[2]);
+                v3 m = mk((double)q.x - (double)st.x * floor((double)q.x / (double)st.x),
+                          (double)q.y - (double)st.y * floor((double)q.y / (double)st.y),
+                          (double)q.z - (double)st.z * floor((double)q.z / (double)st.z));
+                q = sub(m, mk((double)st.x / 2, (double)st.y / 2, (double)st.z / 2));
+                break;
+            }
+            case SDF_POP_POINT: break;
+            case SDF_MUL: v = v * P[0]; break;
+            default: v = sdf_leaf(I.op, P, q); break;
+        }
+    }
+    return v;
+}
+PT_HD double sdf_value(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 p) {
+    return sh.chain ? sdf_eval_chain(prog, params, sh.begin, sh.len, p) : sdf_eval(prog, params, sh.begin, sh.len, p);
+}
+
 // SDFShape.Intersect (SDF.cs:32-76): sphere tracing within the bounding box.
 // `evals` (instrumentation, may be null): the SDF evaluations the march made.
 PT_HD double sdf_t(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 o, v3 d,
@@ -219,7 +253,7 @@ PT_HD double sdf_t(const DevSdfIns* prog, const double* params, const DevSdfShap
     uint32_t n = 0;
     double r = kHitInf;
     for (int i = 0; i < 1000; i++) {
-        double dist = sdf_eval(prog, params, sh.begin, sh.len, add(o, muls(d, t)));
+        double dist = sdf_value(prog, params, sh, add(o, muls(d, t)));
         n++;
         if (jump && dist < 0) {
             t -= jump_size;
@@ -238,10 +272,9 @@ PT_HD double sdf_t(const DevSdfIns* prog, const double* params, const DevSdfShap
 PT_HD v3 sdf_normal(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 p) {
     const double e = 0.0001;
     const double x = p.x, y = p.y, z = p.z;
-    const int b = sh.begin, n = sh.len;
-    double nx = sdf_eval(prog, params, b, n, mk(x - e, y, z)) - sdf_eval(prog, params, b, n, mk(x + e, y, z));
-    double ny = sdf_eval(prog, params, b, n, mk(x, y - e, z)) - sdf_eval(prog, params, b, n, mk(x, y + e, z));
-    double nz = sdf_eval(prog, params, b, n, mk(x, y, z - e)) - sdf_eval(prog, params, b, n, mk(x, y, z + e));
+    double nx = sdf_value(prog, params, sh, mk(x - e, y, z)) - sdf_value(prog, params, sh, mk(x + e, y, z));
+    double ny = sdf_value(prog, params, sh, mk(x, y - e, z)) - sdf_value(prog, params, sh, mk(x, y + e, z));
+    double nz = sdf_value(prog, params, sh, mk(x, y, z - e)) - sdf_value(prog, params, sh, mk(x, y, z + e));
     return normalize(mk(nx, ny, nz));
 }
 

@@ -420,7 +420,7 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevSce
         const float4 a = nt_load(&Q.q_o[qi][i]), b = nt_load(&Q.q_d[qi][i]);
         int32_t kind;
         double tx = 0;
-        const double t = prim_t<false, true>(S, S.ana_recs, e.y, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, kind, &tx);
+        const double t = sdf_record_t(S, e.y, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, kind, tx);
         const int32_t hk = (int32_t)Q.hits[i].z;
         if (t < bt || (t == bt && hk == KIND_TRI)) {
             const unsigned long long tb = (unsigned long long)__double_as_longlong(kind == KIND_XFORM ? tx : t);
@@ -441,7 +441,8 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_shadow(DevS
         const double tl = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
         const float4 a = nt_load(&Q.n_o[qo][e.x]), b = nt_load(&Q.n_n[qo][e.x]);
         int32_t kind;
-        if (prim_t<false, true>(S, S.ana_recs, e.y, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, kind) < tl) Q.n_lit[qo][e.x] = 0;
+        double tx = 0;
+        if (sdf_record_t(S, e.y, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, kind, tx) < tl) Q.n_lit[qo][e.x] = 0;
     }
 }
 
