@@ -29,10 +29,7 @@ constexpr double kFixLoScale = 4294967296.0;             // 2^32
 constexpr double kFixBig = 524288.0;                     // |x| ≥ 2^19: side sum
 constexpr double kFixWave = 8192.0;                      // |x| < 2^13: |V| < 2^57, 64 of them sum without overflow
 constexpr double kFixMagicLo = 4503599627370496.0;       // 2^52: round(y), y ∈ [0, 2^32], is the low mantissa of y + 2^52
-#ifndef PT_FIX_SPLIT
-#define PT_FIX_SPLIT 1   // 0: each accumulator's high words next to its low words ({lo r, g, b, hi r, g, b}, 48 B)
-#endif
-constexpr int kFixWords = PT_FIX_SPLIT ? 3 : 6;          // words per accumulator in w (hi: the same stride)
+constexpr int kFixWords = 3;                             // words per accumulator in w (hi: its own array, the same stride)
 
 // Accumulators of n pixels (or samples): the low words w [n][3], the high words hi [n][3] (touched
 // only by a carry out of the low word, so the atomics' working set is w alone: 24 B per pixel or

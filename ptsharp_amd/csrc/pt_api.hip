@@ -193,10 +193,7 @@ struct Ctx {
 // and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
 // MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
-#ifndef PT_SIDE_MAX_RAYS
-#define PT_SIDE_MAX_RAYS (64ull << 20)
-#endif
-constexpr double kSideStreamMaxRays = (double)PT_SIDE_MAX_RAYS;   // a chunk's widest depth, extension rays
+constexpr double kSideStreamMaxRays = (double)(64ull << 20);   // a chunk's widest depth, extension rays
 // (a scene with SDF shapes adds its two SDF queues, 32 B per entry, outside this budget: counted in,
 // they halved C4's queues from 2^28 to 2^27 entries and split its pass in two chunks, -3 %)
 constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 2 * (64 + 1);
@@ -229,10 +226,7 @@ void free_wavefront(Ctx* c) {
     c->d_plist2 = nullptr;
     c->d_fcount = nullptr;
     c->d_snap = nullptr;
-    if (c->acc_s.w) {
-        (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.big);
-        if (PT_FIX_SPLIT) (void)hipFree(c->acc_s.hi);
-    }
+    if (c->acc_s.w) { (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.hi); (void)hipFree(c->acc_s.big); }
     c->acc_s = pt::FixAcc{};
     c->acc_s_cap = 0;
 }
@@ -287,14 +281,10 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     // per-pixel accumulators of one pass, or of each pass of a batch (pt_pass_params.passes)
     size_t P = (size_t)c->width * (size_t)c->height * (size_t)acc_passes;
     if ((rc = wf_alloc(c, &Q.acc.w, P * pt::kFixWords))) return rc;
-    if (PT_FIX_SPLIT) {
-        if ((rc = wf_alloc(c, &Q.acc.hi, P * pt::kFixWords))) return rc;
-    } else {
-        Q.acc.hi = Q.acc.w + 3;
-    }
+    if ((rc = wf_alloc(c, &Q.acc.hi, P * pt::kFixWords))) return rc;
     if ((rc = wf_alloc(c, &Q.acc.big, P * 3))) return rc;
     PT_HIP(hipMemsetAsync(Q.acc.w, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
-    if (PT_FIX_SPLIT) PT_HIP(hipMemsetAsync(Q.acc.hi, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
+    PT_HIP(hipMemsetAsync(Q.acc.hi, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
     PT_HIP(hipMemsetAsync(Q.acc.big, 0, P * 3 * sizeof(double), c->stream));
     PT_HIP(hipMemsetAsync(Q.counts, 0, pt::kCountWords * sizeof(uint32_t), c->stream));
     Q.cap = cap;
@@ -321,24 +311,22 @@ int ensure_extra(Ctx* c, uint64_t chunk) {
         if ((rc = wf_alloc(c, &c->d_snap, P * 3))) return rc;
     }
     if (c->acc_s.w) {
-        (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.big);
-        if (PT_FIX_SPLIT) (void)hipFree(c->acc_s.hi);
+        (void)hipFree(c->acc_s.w); (void)hipFree(c->acc_s.hi); (void)hipFree(c->acc_s.big);
         c->acc_s = pt::FixAcc{}; c->acc_s_cap = 0;
     }
     c->Q.acc_s = pt::FixAcc{};
     if (hipMalloc(&c->acc_s.w, chunk * pt::kFixWords * sizeof(unsigned long long)) != hipSuccess)
         return fail(PT_ERR_OUT_OF_MEMORY, "hipMalloc per-sample accumulators");
-    if (!PT_FIX_SPLIT) c->acc_s.hi = c->acc_s.w + 3;
-    if ((PT_FIX_SPLIT && hipMalloc(&c->acc_s.hi, chunk * pt::kFixWords * sizeof(unsigned long long)) != hipSuccess) ||
+    if (hipMalloc(&c->acc_s.hi, chunk * pt::kFixWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->acc_s.big, chunk * 3 * sizeof(double)) != hipSuccess) {
         (void)hipFree(c->acc_s.w);
-        if (PT_FIX_SPLIT && c->acc_s.hi) (void)hipFree(c->acc_s.hi);
+        if (c->acc_s.hi) (void)hipFree(c->acc_s.hi);
         c->acc_s = pt::FixAcc{};
         return fail(PT_ERR_OUT_OF_MEMORY, "hipMalloc per-sample accumulators");
     }
     c->acc_s_cap = chunk;
     PT_HIP(hipMemsetAsync(c->acc_s.w, 0, chunk * pt::kFixWords * sizeof(unsigned long long), c->stream));
-    if (PT_FIX_SPLIT) PT_HIP(hipMemsetAsync(c->acc_s.hi, 0, chunk * pt::kFixWords * sizeof(unsigned long long), c->stream));
+    PT_HIP(hipMemsetAsync(c->acc_s.hi, 0, chunk * pt::kFixWords * sizeof(unsigned long long), c->stream));
     PT_HIP(hipMemsetAsync(c->acc_s.big, 0, chunk * 3 * sizeof(double), c->stream));
     c->Q.acc_s = c->acc_s;
     return PT_OK;
@@ -379,14 +367,6 @@ inline void pad_box(float* lo, float* hi) {
     }
 }
 
-// Triangle BVH leaves: 1 makes every node of at most 3 triangles one leaf chunk (pt_bvh.h
-// build_bvh fill_leaves).  Measured slower on C4 (5915 → 5839 Mrays/s: nodes per ray 9.98 → 9.87,
-// triangle tests 2.96 → 3.23, closest hit 47.85 → 48.60 ms per pass; profiles/r03g_ab_leaves.txt):
-// the extra tests cost more than the saved steps, so SAH's own leaf decision stays (0).
-#ifndef PT_BVH_FILL_LEAVES
-#define PT_BVH_FILL_LEAVES 0
-#endif
-
 // Analytic shapes tested linearly by the refill traversal kernels when there are at most this many
 // (pt_scene.h ana_linear); 0: always through the analytic BVH.
 #ifndef PT_ANA_LINEAR
@@ -401,86 +381,21 @@ inline void pad_box(float* lo, float* hi) {
 
 // BVH2 → 4-wide nodes (pt_bvh.h collapse_bvh4) as device float4 rows.  The
 // collapse keeps every path's pushes within the kStackMax-entry traversal stack.
-#ifndef PT_BVH_SAH
-#define PT_BVH_SAH 0   // 1: the SAH-optimal collapse (pt_bvh.h collapse_bvh4_sah) for the triangle BVH
-#endif
-#ifndef PT_BVH_CTRI
-#define PT_BVH_CTRI 0.5   // its triangle-test cost in traversal steps
-#endif
-#ifndef PT_BVH_BINS
-#define PT_BVH_BINS 32   // SAH bins per axis of the BVH2 build
-#endif
+// The triangle BVH: a binned-SAH BVH2 with kTriBins bins per axis and leaves of at most 3 triangles
+// (one leaf chunk), collapsed to 4-wide nodes by the SAH-optimal dynamic program (pt_bvh.h
+// collapse_bvh4_sah, a triangle test priced at kTriCost traversal steps).  Against 32 bins and the
+// greedy collapse: C4 nodes per closest-hit ray 8.51 → 8.27, 6025 → 6065 Mrays/s (profiles/r04ab1_*).
+// Making SAH's leaf decision always take a full chunk (3 triangles) measured slower.
+constexpr int kTriBins = 128;
+constexpr double kTriCost = 0.5;
 int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_nodes, bool sah = false) {
     pt::Bvh4Result r;
-    if (sah) pt::collapse_bvh4_sah(b, pt::kStackMax, r, 1.0, PT_BVH_CTRI, 3);
+    if (sah) pt::collapse_bvh4_sah(b, pt::kStackMax, r, 1.0, kTriCost, 3);
     else pt::collapse_bvh4(b, pt::kStackMax, r);
     if (r.stack_need > pt::kStackMax) return fail(PT_ERR_UNSUPPORTED, "BVH4 traversal stack bound exceeded");
     out.resize(r.words.size() / 4);
     std::memcpy(out.data(), r.words.data(), r.words.size() * sizeof(uint32_t));
     num_nodes = (int32_t)r.nodes();
-    return PT_OK;
-}
-
-// ---- PT_NODE16 node lines (pt_device.h node4_test): child bounds as binary16 offsets from the node's
-// origin (the per-axis minimum of its children's lower bounds), rounded outward under the kernels' own
-// fp32 arithmetic `origin + (float)half`, so each decoded child box still contains its subtree.
-float half_to_float(uint16_t h) {
-    const uint32_t e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
-    float v = e == 0 ? std::ldexp((float)m, -24) : e == 31 ? (m ? NAN : INFINITY) : std::ldexp((float)(m | 0x400u), (int)e - 25);
-    return (h & 0x8000u) ? -v : v;
-}
-// the largest non-negative half h (finite) with fl32(origin + h) <= bound
-uint16_t half_lo(float origin, float bound) {
-    uint32_t lo = 0, hi = 0x7BFFu;   // fl(origin + 0) = origin <= bound
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) / 2;
-        if ((float)(origin + half_to_float((uint16_t)mid)) <= bound) lo = mid; else hi = mid - 1;
-    }
-    return (uint16_t)lo;
-}
-// the smallest non-negative half h with fl32(origin + h) >= bound (+inf if no finite half reaches it)
-uint16_t half_hi(float origin, float bound) {
-    if (!((float)(origin + half_to_float(0x7BFFu)) >= bound)) return 0x7C00u;
-    uint32_t lo = 0, hi = 0x7BFFu;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) / 2;
-        if ((float)(origin + half_to_float((uint16_t)mid)) >= bound) hi = mid; else lo = mid + 1;
-    }
-    return (uint16_t)lo;
-}
-// Old layout (pt_bvh.h: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4]) → PT_NODE16 layout, in place.
-int encode_nodes16(std::vector<float4>& nodes) {
-    if (!PT_NODE16) return PT_OK;
-    const size_t nn = nodes.size() / 8;
-    for (size_t n = 0; n < nn; n++) {
-        float* w = reinterpret_cast<float*>(&nodes[8 * n]);
-        uint32_t refs[4];
-        std::memcpy(refs, w + 24, sizeof refs);
-        float org[3];
-        for (int ax = 0; ax < 3; ax++) {
-            org[ax] = INFINITY;
-            for (int k = 0; k < 4; k++)
-                if (refs[k] != pt::kEmpty4) org[ax] = std::min(org[ax], w[8 * ax + k]);
-            if (!std::isfinite(org[ax]))
-                return fail(PT_ERR_UNSUPPORTED, "BVH node with a non-finite bound (binary16 node encoding)");
-        }
-        uint32_t out[32] = {0u};
-        std::memcpy(&out[0], org, sizeof org);
-        out[3] = refs[0]; out[4] = refs[1]; out[5] = refs[2]; out[6] = refs[3];
-        for (int ax = 0; ax < 3; ax++) {
-            uint16_t hl[4] = {0, 0, 0, 0}, hh[4] = {0, 0, 0, 0};
-            for (int k = 0; k < 4; k++) {
-                if (refs[k] == pt::kEmpty4) continue;
-                hl[k] = half_lo(org[ax], w[8 * ax + k]);
-                hh[k] = half_hi(org[ax], w[8 * ax + 4 + k]);
-            }
-            out[8 + 4 * ax + 0] = (uint32_t)hl[0] | ((uint32_t)hl[1] << 16);
-            out[8 + 4 * ax + 1] = (uint32_t)hl[2] | ((uint32_t)hl[3] << 16);
-            out[8 + 4 * ax + 2] = (uint32_t)hh[0] | ((uint32_t)hh[1] << 16);
-            out[8 + 4 * ax + 3] = (uint32_t)hh[2] | ((uint32_t)hh[3] << 16);
-        }
-        std::memcpy(w, out, sizeof out);
-    }
     return PT_OK;
 }
 
@@ -984,7 +899,6 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         std::vector<float4> nodes;
         int32_t nn = 0;
         if ((rc = pack_nodes(bb, nodes, nn))) return rc;
-        if ((rc = encode_nodes16(nodes))) return rc;
         pt::DevBlas B{(int32_t)(blas_nodes.size() / 8), nn, (int32_t)(blas_recs.size() / 3), 0};
         blas_nodes.insert(blas_nodes.end(), nodes.begin(), nodes.end());
         for (int t = 0; t < n; t++) {
@@ -1049,7 +963,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         pad_box(&bmin[3 * i], &bmax[3 * i]);
     }
     pt::BvhResult tb;
-    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb, 3, PT_BVH_FILL_LEAVES != 0, PT_BVH_BINS);   // leaves fit one chunk
+    pt::build_bvh(bmin.data(), bmax.data(), (int64_t)nt, 0, tb, 3, false, kTriBins);   // leaves fit one chunk
     std::vector<float4> tri_recs(nt * 3), tri_shade(nt * 3);
     const bool want_uv = d->num_textures > 0 && nt > 0;   // texture coordinates only matter with textures
     std::vector<float4> tri_uv(want_uv ? nt * 2 : 0);
@@ -1075,7 +989,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     }
     std::vector<float4> tri_nodes;
     int32_t tri_num_nodes = 0;
-    if ((rc = pack_nodes(tb, tri_nodes, tri_num_nodes, PT_BVH_SAH != 0))) return rc;
+    if ((rc = pack_nodes(tb, tri_nodes, tri_num_nodes, true))) return rc;
     std::vector<float4> tri_chunks;
     if ((rc = make_leaf_chunks(tri_nodes, tri_recs, tri_chunks))) return rc;
     float tri_box[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1091,7 +1005,6 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
             }
         }
     }
-    if ((rc = encode_nodes16(tri_nodes))) return rc;
 
     // --- analytic BVH (spheres, cubes, SDF shapes, volumes, transformed shapes)
     const size_t na = ana_kind.size();
@@ -1142,7 +1055,6 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     std::vector<float4> ana_nodes;
     int32_t ana_num_nodes = 0;
     if ((rc = pack_nodes(ab, ana_nodes, ana_num_nodes))) return rc;
-    if ((rc = encode_nodes16(ana_nodes))) return rc;
 
     // --- planes
     std::vector<float4> planes(plane_scene.size() * 2);
@@ -1275,7 +1187,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     S.heavy_count = (int32_t)(heavy.size() / 2);
     bool mat_tex = false;
     for (const auto& m : mats) mat_tex = mat_tex || m.tex >= 0 || m.ntex >= 0 || m.btex >= 0 || m.gtex >= 0;
-    S.shade_route = (PT_SHADE_ROUTE && S.full && !mat_tex) ? 1 : 0;
+    S.shade_route = (PT_SHADE_ROUTE && S.full && !mat_tex && S.lights_lean) ? 1 : 0;   // (a Volume light's colour is FULL work)
     rc = upload(c, heavy, &S.heavy); if (rc) return rc;
     S.num_planes = (int32_t)plane_scene.size();
     S.num_lights = (int32_t)lights.size();
@@ -1296,7 +1208,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
 // lowers it.
 static int32_t batch_passes_max(Ctx* c) {
     const size_t per_pass = (size_t)c->width * (size_t)c->height *
-                            ((PT_FIX_SPLIT ? 2 : 1) * pt::kFixWords * sizeof(unsigned long long) + 3 * sizeof(double));
+                            (2 * pt::kFixWords * sizeof(unsigned long long) + 3 * sizeof(double));
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0) total_b = (size_t)8 << 30;
     int64_t k = (int64_t)std::max<size_t>(1, (total_b / 8) / std::max<size_t>(per_pass, 1));
@@ -1369,8 +1281,6 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     plan.lanes_shadow_blocks = c->grids.lanes_shadow_blocks;
     plan.full_trace_blocks = c->grids.full_trace_blocks;
     plan.full_shadow_blocks = c->grids.full_shadow_blocks;
-    plan.full_lanes_trace_blocks = c->grids.full_lanes_trace_blocks;
-    plan.full_lanes_shadow_blocks = c->grids.full_lanes_shadow_blocks;
     const bool extra = pass->adaptive_samples > 0 || pass->firefly_samples > 0;
     const bool serial = (pass->flags & PT_PASS_SERIAL) != 0;   // Renderer.Render's extra phases (NumCPU == 1)
     // pt_pass_params.passes: K consecutive passes.  Plain RenderParallel passes run as one batch

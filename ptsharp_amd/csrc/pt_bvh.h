@@ -18,10 +18,7 @@ constexpr int kMaxDepth = 32;     // BVH2 depth bound
 // within it (the traversal kernels hold the first kLdsStack in LDS and the rest in a
 // per-thread global column; the megakernel all in LDS).  A larger budget lets the collapse
 // fill more nodes to four children (fewer, wider steps per ray).
-#ifndef PT_STACK_MAX
-#define PT_STACK_MAX 32
-#endif
-constexpr int kStackMax = PT_STACK_MAX;
+constexpr int kStackMax = 32;   // (48 or 64 measured: the BVH 1 % smaller, no faster)
 static_assert(kStackMax >= kMaxDepth, "the collapse needs at least the BVH2 depth");
 constexpr int kMaxLeafSize = 4;
 

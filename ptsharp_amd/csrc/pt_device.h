@@ -33,12 +33,9 @@ struct Counters {
     uint32_t rays, nodes, prims, shades;
 };
 
-#ifndef PT_COOP_MARCH
-#define PT_COOP_MARCH 1   // Volume marches by the wave's active lanes together (coop_vol_t); 0: by the lane alone
-#endif
-#ifndef PT_COOP_MIN_LANES
-#define PT_COOP_MIN_LANES 8   // fewer active lanes: each marches its own ray (vol_t, one grid read per cell)
-#endif
+// Volume marches by the wave's active lanes together (coop_vol_t); with fewer than this many active
+// lanes each marches its own ray (vol_t, one grid read per cell)
+constexpr int kCoopMinLanes = 8;
 
 __device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
 
@@ -180,48 +177,18 @@ __device__ __forceinline__ void cswap(float& ka, uint32_t& va, float& kb, uint32
     va = v;
 }
 
-// The four child slabs of a BVH4 node line (pt_bvh.h; PT_NODE16: pt_api.hip encode_nodes16) →
-// entry distances k0..k3 (+inf = miss or empty slot) and child refs v0..v3.
-//   PT_NODE16 = 0: 7 pieces, lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] refs[4] (round 2).
-//   PT_NODE16 = 1: 5 pieces, {origin.xyz, ref0} {ref1, ref2, ref3, -} and the child bounds as
-//   binary16 offsets from the origin, x / y / z rows of {lo c0|c1, lo c2|c3, hi c0|c1, hi c2|c3};
-//   bound = origin + offset in fp32, rounded outward on the host under this same arithmetic, so
-//   every child box contains its subtree (a step reads 80 B of its line instead of 112 B).
-//   Measured slower (C4 6124 → 5825 Mrays/s, closest hit 46.1 → 49.9 ms per pass; the decode's
-//   24 conversions and adds per node cost more than the two loads it saves;
-//   profiles/r03n_ab_node16.txt), so the default stays 0.
-#ifndef PT_NODE16
-#define PT_NODE16 0
-#endif
-constexpr int kNodePieces = PT_NODE16 ? 5 : 7;
-__device__ __forceinline__ float h16lo(float w) {
-    return (float)__builtin_bit_cast(_Float16, (unsigned short)(__float_as_uint(w) & 0xFFFFu));
-}
-__device__ __forceinline__ float h16hi(float w) {
-    return (float)__builtin_bit_cast(_Float16, (unsigned short)(__float_as_uint(w) >> 16));
-}
+// The four child slabs of a BVH4 node line (pt_bvh.h: seven pieces, lo.x[4] hi.x[4] lo.y[4] hi.y[4]
+// lo.z[4] hi.z[4] refs[4]) → entry distances k0..k3 (+inf = miss or empty slot) and child refs v0..v3.
+// Compressed lines (8-bit and binary16 child bounds) measured slower: the decode costs more than the
+// loads it saves.
 __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, float4 q3, float4 q4, float4 q5, float4 q6,
                                            v3 o, v3 invd, float tmax, float& k0, float& k1, float& k2, float& k3,
                                            uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& v3r) {
-#if PT_NODE16
-    (void)q5; (void)q6;
-    const float ox = q0.x, oy = q0.y, oz = q0.z;
-    k0 = slab1(ox + h16lo(q2.x), ox + h16lo(q2.z), oy + h16lo(q3.x), oy + h16lo(q3.z), oz + h16lo(q4.x), oz + h16lo(q4.z),
-               o, invd, tmax);
-    k1 = slab1(ox + h16hi(q2.x), ox + h16hi(q2.z), oy + h16hi(q3.x), oy + h16hi(q3.z), oz + h16hi(q4.x), oz + h16hi(q4.z),
-               o, invd, tmax);
-    k2 = slab1(ox + h16lo(q2.y), ox + h16lo(q2.w), oy + h16lo(q3.y), oy + h16lo(q3.w), oz + h16lo(q4.y), oz + h16lo(q4.w),
-               o, invd, tmax);
-    k3 = slab1(ox + h16hi(q2.y), ox + h16hi(q2.w), oy + h16hi(q3.y), oy + h16hi(q3.w), oz + h16hi(q4.y), oz + h16hi(q4.w),
-               o, invd, tmax);
-    v0 = __float_as_uint(q0.w); v1 = __float_as_uint(q1.x); v2 = __float_as_uint(q1.y); v3r = __float_as_uint(q1.z);
-#else
     k0 = slab1(q0.x, q1.x, q2.x, q3.x, q4.x, q5.x, o, invd, tmax);
     k1 = slab1(q0.y, q1.y, q2.y, q3.y, q4.y, q5.y, o, invd, tmax);
     k2 = slab1(q0.z, q1.z, q2.z, q3.z, q4.z, q5.z, o, invd, tmax);
     k3 = slab1(q0.w, q1.w, q2.w, q3.w, q4.w, q5.w, o, invd, tmax);
     v0 = __float_as_uint(q6.x); v1 = __float_as_uint(q6.y); v2 = __float_as_uint(q6.z); v3r = __float_as_uint(q6.w);
-#endif
     const float inf = __int_as_float(0x7f800000);
     if (v1 == kEmpty4) k1 = inf;  // slot 0 is never empty
     if (v2 == kEmpty4) k2 = inf;
@@ -229,18 +196,11 @@ __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, floa
 }
 
 // SDF records (an SDFShape, or a TransformedShape of one): their sphere tracing runs up to 1000
-// dependent steps.  Taken where a lane's traversal meets the leaf, the lanes that meet it at
-// different steps run the tracing one after the other; deferred (PT_DEFER_SDF: the first SDF
-// record a ray reaches is left in pend_sdf and traced after the traversal, sdf_pending) every
-// such lane of the wave traces at once.  Merged as the deferred Volume march is (march_pending).
-#ifndef PT_DEFER_SDF
-#define PT_DEFER_SDF 0
-#endif
-// PT_SDF_QUEUE: the analytic half of a split closest hit (k_wf_trace<.., SPLIT>) leaves the first SDF
-// record of a ray in a compact queue instead, and k_wf_sdf_hits traces the queue with every lane busy.
-#ifndef PT_SDF_QUEUE
-#define PT_SDF_QUEUE 1
-#endif
+// dependent steps, taken by the lane whose traversal meets the leaf.  The analytic half of a split
+// closest hit (k_wf_trace<.., SPLIT>) and of split shadow rays leaves the first SDF record of a ray in a
+// compact queue instead (pend_sdf → sdf_out), and k_wf_sdf_hits / k_wf_sdf_shadow trace the queue
+// with every lane busy (deferring it to the end of the traversal, every such lane of the wave at
+// once, measured slower: DESIGN.md §9c).
 __device__ __forceinline__ bool sdf_deferred(const DevScene& S, const float4* r) {
     const int32_t kind = (int32_t)f2u(r[0].w);
     if (kind == KIND_SDF) return true;
@@ -303,9 +263,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
     for (;;) {
         if (!(ref & 0x80000000u)) {
             const float4* c = nodes + 8 * (size_t)ref;
-            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4];
-            const float4 q5 = kNodePieces > 5 ? c[5] : z4, q6 = kNodePieces > 6 ? c[6] : z4;
+            const float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6];
             if (COUNT) ctr.nodes++;
             const float inf = __int_as_float(0x7f800000);
             float k0, k1, k2, k3;
@@ -326,11 +284,11 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
             for (uint32_t k = 0; k < cnt; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
-                if (FULL && PT_COOP_MARCH && pend && *pend < 0 && march_deferred(S, recs + 3 * (size_t)(first + k))) {
+                if (FULL && pend && *pend < 0 && march_deferred(S, recs + 3 * (size_t)(first + k))) {
                     *pend = (int32_t)(first + k);
                     continue;
                 }
-                if (FULL && (PT_DEFER_SDF || PT_SDF_QUEUE) && pend_sdf && *pend_sdf < 0 &&
+                if (FULL && pend_sdf && *pend_sdf < 0 &&
                     sdf_deferred(S, recs + 3 * (size_t)(first + k))) {
                     *pend_sdf = (int32_t)(first + k);
                     continue;
@@ -478,7 +436,7 @@ __device__ __forceinline__ bool march_exact(double t, double step) {   // t > 0
 // The Sign of march position t: a uniform cell's (pt_ext.h vol_build_runs: every sample in it has
 // that Sign) without the eight corner loads and the interpolation, else Volume.Sign of the sample.
 __device__ __forceinline__ int vol_sign_fast(const DevVolume& v, v3 o, v3 d, double t) {
-    if (PT_VOL_TABLE && v.runs) {
+    if (v.runs) {
         const int s = vol_key_sign(v, vol_key(v, o, d, t));
         if (s > 0) return s;
     }
@@ -498,16 +456,10 @@ __device__ __forceinline__ bool vol_box_sign(const DevVolume& v, VolKey a, VolKe
     }
     return true;
 }
-#ifndef PT_VOL_STRIDE
-#define PT_VOL_STRIDE 16   // the strided pass's positions per lane (0: off)
-#endif
+constexpr int kVolStride = 16;   // the strided pass's positions per lane (8 / 32 measured: no better)
 // Every active lane passes the same (v, o, d); returns vol_t(v, o, d) to all of them and, in
 // `samples`, the Volume.Sample calls vol_t makes (instrumentation).
 __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& samples) {
-#ifdef PT_PROBE_NO_VOL   // timing probe only (wrong images): Volumes never hit
-    samples = 0;
-    return kHitInf;
-#endif
     const uint64_t act = __ballot(true);
     const int lane = threadIdx.x & 63;
     const uint64_t lower = act & ((1ull << lane) - 1ull);
@@ -522,21 +474,15 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     samples = 0;
     auto sign_at = [&](double tt) { return vol_sign_fast(v, o, d, tt); };
     for (;;) {   // wave-uniform: every branch below is on ballots
-        if (PT_VOL_SKIP && v.runs) {   // pass a run of positions that cannot act (pt_ext.h vol_run)
-            const VolSkip r = vol_skip(v, o, d, t, step, sign, tmax, iters);   // the same on every lane
-            samples += r.k;
-            if (r.all) return kHitInf;
-            t = r.t; sign = r.sign; iters = r.iters;
-        }
         // Strided pass over runs of uniform cells: lane of rank r looks at position (r + 1)·S from
         // t; when the cells of consecutive looked-at positions (and of position 0) span only cells
         // of the running Sign, no position up to there can act, and the march moves past them,
         // 64·S positions per round.  The positions are the reference's repeated additions (t_after).
-        while (PT_VOL_STRIDE > 0 && v.runs) {   // wave-uniform
+        while (v.runs) {   // wave-uniform
             const VolKey k0 = vol_key(v, o, d, t);
             const int s0 = vol_key_sign(v, k0);
             if (s0 <= 0 || (sign >= 0 && s0 != sign)) break;
-            const int off = (rank + 1) * PT_VOL_STRIDE;
+            const int off = (rank + 1) * kVolStride;
             const double tr = t_after(t, step, off);
             const bool valid = tr <= tmax && iters + off < (1 << 24);
             const VolKey kr = vol_key(v, o, d, tr);
@@ -545,7 +491,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
             const uint64_t unsafe = __ballot(!(valid && vol_box_sign(v, kp, kr, s0)));
             const int f = unsafe ? __popcll(act & ((1ull << __builtin_ctzll(unsafe)) - 1ull)) : nact;   // safe ranks
             if (f == 0) break;
-            const int k = f * PT_VOL_STRIDE + 1;   // positions 0 .. f·S: all of Sign s0
+            const int k = f * kVolStride + 1;   // positions 0 .. f·S: all of Sign s0
             samples += (uint32_t)k;   // counted: the reference samples them
             t = t_after(t, step, k);
             iters += k;
@@ -632,7 +578,7 @@ __device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend
             best.t = t; best.kind = kind; best.idx = p; best.tx = tx;
         }
     };
-    if (__popcll(__ballot(true)) < PT_COOP_MIN_LANES) {   // too few lanes to share a march: each its own
+    if (__popcll(__ballot(true)) < kCoopMinLanes) {   // too few lanes to share a march: each its own
         if (pend >= 0) {
             int32_t kind;
             double tx = 0;
@@ -664,7 +610,7 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         if (t < best.t) { best.t = t; best.kind = KIND_PLANE; best.idx = i; }
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    int32_t pend = -1, pend_sdf = -1;   // FULL: a Volume left for the cooperative march, an SDF for sdf_pending
+    int32_t pend = -1;   // FULL: a Volume left for the cooperative march
     if (S.ana_linear) {   // a few analytic shapes, one by one (as the refill kernels test them; pt_scene.h)
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
@@ -675,11 +621,10 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
         }
     } else {
         traverse<false, COUNT, false, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
-                                            FULL ? &pend : nullptr, FULL && PT_DEFER_SDF ? &pend_sdf : nullptr);
+                                            FULL ? &pend : nullptr);
     }
     traverse_tri<COUNT, false>(S, o, d, invd, best, stack, ctr);
-    if (FULL && PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
-    if (FULL) sdf_pending<false>(S, o, d, pend_sdf, best);
+    if (FULL) march_pending<false>(S, o, d, pend, best);
     return best;
 }
 
@@ -717,7 +662,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
     }
     v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    int32_t pend = -1, pend_sdf = -1;   // FULL: a Volume left for the cooperative march, an SDF for sdf_pending
+    int32_t pend = -1;   // FULL: a Volume left for the cooperative march
     if (S.ana_linear) {
         for (int p = 0; p < S.ana_count; p++) {
             if (COUNT) ctr.prims++;
@@ -725,18 +670,13 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
             if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return false;
         }
     } else if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack,
-                                                 ctr, FULL ? &pend : nullptr, FULL && PT_DEFER_SDF ? &pend_sdf : nullptr)) {
+                                                 ctr, FULL ? &pend : nullptr)) {
         return false;
     }
     if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return false;
-    if (FULL && PT_COOP_MARCH) {   // the lanes still unblocked march their pending Volume together
+    if (FULL) {   // the lanes still unblocked march their pending Volume together
         bool blocked = false;
         march_pending<true>(S, o, d, pend, best, &blocked);
-        if (blocked) return false;
-    }
-    if (FULL) {
-        bool blocked = false;
-        sdf_pending<true>(S, o, d, pend_sdf, best, &blocked);
         if (blocked) return false;
     }
     return true;
@@ -750,7 +690,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
 // best its t is raised by one ulp for the analytic pass (no double lies between), and restored
 // when no analytic hit took it.  The triangles the refill kernel found without the analytic
 // hit's tighter bound are the same: a bound only prunes, it never reorders the visits.
-// sdf_out (PT_SDF_QUEUE): the SDF record left for k_wf_sdf_hits (-1: none), not merged here.
+// sdf_out: the SDF record left for k_wf_sdf_hits (-1: none), not merged here.
 template <bool COUNT, class STK>
 __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const STK& stack, Counters& ctr, HitRec& best,
                                           int32_t* sdf_out = nullptr) {
@@ -769,9 +709,9 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
         }
     } else {
         traverse<false, COUNT, false, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr, &pend,
-                                            PT_DEFER_SDF || sdf_out ? &pend_sdf : nullptr);
+                                            sdf_out ? &pend_sdf : nullptr);
     }
-    if (PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
+    march_pending<false>(S, o, d, pend, best);
     if (sdf_out) *sdf_out = pend_sdf;
     else sdf_pending<false>(S, o, d, pend_sdf, best);
     if (best.kind == KIND_TRI && tri_best) best.t = t_in;
@@ -779,7 +719,7 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
 // The analytic half of a split shadow query (light_visible's analytic part): is any analytic
 // primitive strictly nearer than the light?  The refill kernel already cleared the planes and
 // the triangles.
-// sdf_out (PT_SDF_QUEUE): the SDF record left for k_wf_sdf_shadow (-1: none), with the light's t.
+// sdf_out: the SDF record left for k_wf_sdf_shadow (-1: none), with the light's t.
 template <bool COUNT, class STK>
 __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L, v3 o, v3 d, const STK& stack,
                                             Counters& ctr, int32_t* sdf_out = nullptr, double* tl_out = nullptr) {
@@ -795,10 +735,10 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
             if (prim_t<false, true>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return true;
         }
     } else if (traverse<false, COUNT, true, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr,
-                                                   &pend, PT_DEFER_SDF || sdf_out ? &pend_sdf : nullptr)) {
+                                                   &pend, sdf_out ? &pend_sdf : nullptr)) {
         return true;
     }
-    if (PT_COOP_MARCH) {
+    {
         bool blocked = false;
         march_pending<true>(S, o, d, pend, best, &blocked);
         if (blocked) return true;
@@ -842,14 +782,14 @@ __device__ __forceinline__ void trace_heavy(const DevScene& S, v3 o, v3 d, Count
         const uint32_t p = f2u(lo.w);
         if (COUNT) ctr.prims++;
         const float4* r = S.ana_recs + 3 * (size_t)p;
-        if (PT_COOP_MARCH && pend < 0 && march_deferred(S, r)) { pend = (int32_t)p; continue; }
+        if (pend < 0 && march_deferred(S, r)) { pend = (int32_t)p; continue; }
         if (sdf_out && pend_sdf < 0 && sdf_deferred(S, r)) { pend_sdf = (int32_t)p; continue; }
         int32_t kind;
         double tx = 0;
         const double t = prim_t<false, true>(S, S.ana_recs, p, o, d, kind, &tx);
         if (t < best.t) { best.t = t; best.kind = kind; best.idx = (int32_t)p; best.tx = tx; }
     }
-    if (PT_COOP_MARCH) march_pending<false>(S, o, d, pend, best);
+    march_pending<false>(S, o, d, pend, best);
     if (sdf_out) *sdf_out = pend_sdf;
     else sdf_pending<false>(S, o, d, pend_sdf, best);
     if (best.kind == KIND_TRI && tri_best) best.t = t_in;
@@ -870,12 +810,12 @@ __device__ __forceinline__ bool heavy_blocked(const DevScene& S, const DevLight&
         const uint32_t p = f2u(lo.w);
         if (COUNT) ctr.prims++;
         const float4* r = S.ana_recs + 3 * (size_t)p;
-        if (PT_COOP_MARCH && pend < 0 && march_deferred(S, r)) { pend = (int32_t)p; continue; }
+        if (pend < 0 && march_deferred(S, r)) { pend = (int32_t)p; continue; }
         if (sdf_out && pend_sdf < 0 && sdf_deferred(S, r)) { pend_sdf = (int32_t)p; continue; }
         int32_t kind;
         if (prim_t<false, true>(S, S.ana_recs, p, o, d, kind) < tl) return true;
     }
-    if (PT_COOP_MARCH) {
+    {
         bool blocked = false;
         march_pending<true>(S, o, d, pend, best, &blocked);
         if (blocked) return true;

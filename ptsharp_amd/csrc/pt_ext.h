@@ -242,9 +242,6 @@ PT_HD double sdf_value(const DevSdfIns* prog, const double* params, const DevSdf
 PT_HD double sdf_t(const DevSdfIns* prog, const double* params, const DevSdfShape& sh, v3 o, v3 d,
                    uint32_t* evals = nullptr) {
     const double epsilon = (double)0.00001f, start = (double)0.0001f, jump_size = (double)0.001f;
-#ifdef PT_PROBE_NO_SDF   // timing probe only (wrong images): SDF shapes never hit
-    if (epsilon > 0) return kHitInf;
-#endif
     double t1, t2;
     box_span(sh.bmin, sh.bmax, o, d, t1, t2);
     if (t2 < t1 || t2 < 0) return kHitInf;
@@ -376,22 +373,15 @@ PT_HD int vol_material(const DevVolume& v, v3 p, int default_mat) {
     }
     return bm;
 }
-// ---------------------------------------------------------------- Volume march skipping
-#ifndef PT_VOL_TABLE
-#define PT_VOL_TABLE 1   // the cooperative march reads a uniform cell's Sign from its table entry
-#endif
-#ifndef PT_VOL_SKIP
-#define PT_VOL_SKIP 0   // 1: the cooperative march passes runs of uniform cells (measured slower on C5)
-#endif
+// ---------------------------------------------------------------- uniform Volume cells
 // Volume.Intersect acts at a march position only when its Sign is 0 or differs from the last
 // one.  Sample is a convex combination of its cell's eight corners, so a cell whose corner range
 // lies inside one Sign band (with a margin far above the interpolation's rounding) gives every
-// position in it that band's Sign.  A run of positions whose cells all carry the running Sign
-// is therefore passed without any action, and the march can move past it at once: the run's
-// end is found from the exact positions (the reference's own repeated additions, t_after, and
-// fp32 Ray.Position), so the t returned is the loop's, bit for bit.  In the reference's own
-// volume scene (Example.volume) Sample's y-from-z slip puts most of the box beyond the grid's
-// last slice, where every sample is exactly 0.
+// position in it that band's Sign: the cooperative march (pt_device.h coop_vol_t) reads such a
+// cell's Sign from a table and passes runs of such cells at once, at the exact positions (the
+// reference's own repeated additions, t_after, and fp32 Ray.Position), so the t returned is the
+// loop's, bit for bit.  In the reference's own volume scene (Example.volume) Sample's y-from-z slip
+// puts most of the box beyond the grid's last slice, where every sample is exactly 0.
 //
 // The band of a value: 2i for "below window i's lo" (i = nwin: above every window), 2i + 1 for
 // "inside window i" (Sign 0); bands 2i all have Sign 1 except 2·nwin (Sign nwin + 1).
@@ -470,127 +460,12 @@ PT_HD int vol_key_sign(const DevVolume& v, VolKey k) {
     if (k.x < -1 || k.y < -1 || k.z < -1 || k.x >= v.w || k.y >= v.h || k.z >= v.d) return v.zero_sign;
     return v.runs[(k.x + 1) + (size_t)(k.y + 1) * (v.w + 1) + (size_t)(k.z + 1) * (v.w + 1) * (v.h + 1)];
 }
-// Positions k = 0, 1, ... from t (t_after(t, step, k)); kmax: the positions the loop still takes.
-// Returns how many leading positions lie in cells of Sign `sign` (> 0): kmax when all of them do.
-PT_HD long long vol_run(const DevVolume& v, v3 o, v3 d, double t, double step, int sign, long long kmax) {
-    if (!v.runs || sign <= 0 || kmax <= 0) return 0;
-    VolKey c = vol_key(v, o, d, t);
-    if (vol_key_sign(v, c) != sign) return 0;
-    // index directions along the ray (x from d.x; y and z from d.z / zscale)
-    const int dx = d.x > 0 ? 1 : (d.x < 0 ? -1 : 0);
-    const int sdz = d.z > 0 ? 1 : (d.z < 0 ? -1 : 0);
-    const int dz = v.zscale > 0 ? sdz : -sdz;
-    long long k0 = 0;
-    for (int guard = 0; guard < 4096; guard++) {
-        // outside the grid for good: every later cell is a zero cell
-        const bool gone = (c.x == v.w && dx >= 0) || (c.x == -2 && dx <= 0) || (c.y == v.h && dz >= 0) ||
-                          (c.y == -2 && dz <= 0) || (c.z == v.d && dz >= 0) || (c.z == -2 && dz <= 0);
-        if (gone) return kmax;
-        auto same = [&](long long k) {
-            const VolKey q = vol_key(v, o, d, t_after(t, step, k));
-            return q.x == c.x && q.y == c.y && q.z == c.z;
-        };
-        // estimate: the nearest lattice plane ahead on each axis, from the fp64 line
-        double tc = 1e300;
-        const double t0 = t_after(t, step, k0);
-        auto plane = [&](double p0, double dp, double target) {   // the lattice plane ahead on one axis
-            if (dp != 0) {
-                const double tt = (target - p0) / dp;
-                if (tt > t0 && tt < tc) tc = tt;
-            }
-        };
-        if (dx != 0) plane(o.x, d.x, 2.0 * (c.x + (dx > 0 ? 1 : 0)) / v.w - 1.0);
-        if (dz != 0) {
-            plane(o.z, d.z, v.zscale * (2.0 * (c.y + (dz > 0 ? 1 : 0)) / v.h - 1.0));
-            plane(o.z, d.z, v.zscale * (2.0 * (c.z + (dz > 0 ? 1 : 0)) / v.d - 2.0));
-        }
-        long long g = k0 + 1;
-        if (tc < 1e300) {
-            const double kk = floor((tc - t0) / step);
-            if (kk > 1 && kk < 1e15) g = k0 + (long long)kk;
-        }
-        if (g > kmax) g = kmax;
-        // the first k > k0 with another cell (or kmax): same() is true on [k0, first) and false after
-        long long lo = k0, hi;
-        if (g == kmax || !same(g)) {
-            hi = g;
-            for (long long s = 1; hi - lo > 1;) {   // gallop down from the estimate
-                const long long m = hi - s > lo ? hi - s : lo + 1;
-                if (same(m)) { lo = m; break; }
-                hi = m;
-                s *= 2;
-            }
-        } else {
-            lo = g;
-            for (long long s = 1;; s *= 2) {   // gallop up
-                const long long m = lo + s < kmax ? lo + s : kmax;
-                if (m == kmax || !same(m)) { hi = m; break; }
-                lo = m;
-            }
-        }
-        while (hi - lo > 1) {
-            const long long m = lo + (hi - lo) / 2;
-            if (same(m)) lo = m;
-            else hi = m;
-        }
-        if (hi >= kmax) return kmax;
-        c = vol_key(v, o, d, t_after(t, step, hi));
-        if (vol_key_sign(v, c) != sign) return hi;
-        k0 = hi;
-    }
-    return k0;   // (never: a ray crosses at most w + h + d + 6 planes)
-}
-// The positions the loop still takes from t: t_after(t, step, k) <= tmax and iters + k < 2^24.
-PT_HD long long vol_positions_left(double t, double step, double tmax, int iters) {
-    const long long cap = (1ll << 24) - iters;
-    if (cap <= 0 || !(t <= tmax)) return 0;
-    double est = floor((tmax - t) / step) + 1;
-    long long k = est < (double)cap ? (long long)est : cap;
-    if (k < 1) k = 1;
-    while (k > 1 && !(t_after(t, step, k - 1) <= tmax)) k--;   // the estimate is exact or one high
-    while (k < cap && t_after(t, step, k) <= tmax) k++;
-    return k;
-}
-
-// The positions from t the march can pass without acting (vol_run), given the running Sign (-1
-// before the first position: then the first cell's), the loop bound and the iterations so far.
-// Returned: the positions passed (k), the march's t, Sign and iterations after them, and `all`
-// when that is every position the loop has left (the loop then ends with no hit).  Taken by the
-// cooperative march only (coop_vol_t, inside the non-inlined coop_record_t): inlined into the
-// FULL traversal kernels' own march, or made a call, it cost their step loops spills.
-#define PT_HD_CALL PT_HD
-struct VolSkip {
-    double t;
-    uint32_t k;
-    int32_t sign, iters, all;
-};
-PT_HD_CALL VolSkip vol_skip(const DevVolume& v, v3 o, v3 d, double t, double step, int sign, double tmax, int iters) {
-    VolSkip r{t, 0u, sign, iters, 0};
-    if (!v.runs) return r;
-    const int s = vol_key_sign(v, vol_key(v, o, d, t));
-    if (s <= 0 || (sign >= 0 && s != sign)) return r;
-    const long long left = vol_positions_left(t, step, tmax, iters);
-    const long long k = vol_run(v, o, d, t, step, s, left);
-    r.all = k >= left;
-    if (k > 0) {
-        r.k = (uint32_t)k;
-        r.sign = s;
-        r.t = t_after(t, step, k);
-        r.iters = iters + (int)k;
-    }
-    return r;
-}
-
 // Volume.Intersect (Volume.cs:168-197).  The reference loop has no bound; 2^24 steps
 // stand in for it (a ray that needs more never finishes in the reference either).
-// `samples` (instrumentation, may be null): the Volume.Sample calls the march made.
-// skip: pass runs of uniform cells (vol_skip); the traversal kernels' per-lane march leaves it
-// off (its registers would cost their step loops), the cooperative march (coop_vol_t) and the
-// host paths take it.
-PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr, bool skip = false) {
-#ifdef PT_PROBE_NO_VOL   // timing probe only (wrong images): Volumes never hit
-    if (samples) return kHitInf;
-#endif
+// `samples` (instrumentation, may be null): the Volume.Sample calls the march made.  Each position
+// reads its cell's corners once per cell (vol_sample_cell).  A serial search for the end of a run of
+// uniform cells measured slower than the wave's strided pass.
+PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr) {
     double tmin, tmax;
     box_span(v.bmin, v.bmax, o, d, tmin, tmax);
     double step = (double)(1.0f / 512.0f);
@@ -610,14 +485,6 @@ PT_HD double vol_t(const DevVolume& v, v3 o, v3 d, uint32_t* samples = nullptr, 
         return vol_sign_of(v, vol_sample_cell(v, a.x, a.y, a.z, k));
     };
     for (double t = start; t <= tmax && iters < (1 << 24); t += step, iters++) {
-        if (skip && v.runs && (sign < 0 || vol_key_sign(v, VolKey{k.x0, k.y0, k.z0}) == sign)) {
-            // the first position, or the last position's cell carries the running Sign: pass the
-            // run of positions that cannot act
-            const VolSkip r = vol_skip(v, o, d, t, step, sign, tmax, iters);
-            n += r.k;   // counted: the reference samples them
-            if (r.all) return done(kHitInf);
-            t = r.t; sign = r.sign; iters = r.iters;
-        }
         const int sg = sign_at(t);
         if (sg == 0 || (sign >= 0 && sg != sign)) {
             t -= step;

@@ -55,10 +55,7 @@ struct WfQueues {
 // Every counter sits on a line of its own: returning atomics execute at the memory side,
 // one line at a time, so cursors packed into one 128-B line serialise every partition's
 // claims on one channel.  kCountStride words (4 B each) between slots.
-#ifndef PT_COUNT_STRIDE
-#define PT_COUNT_STRIDE 64
-#endif
-constexpr int kCountStride = PT_COUNT_STRIDE;
+constexpr int kCountStride = 64;
 static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
 constexpr int kFetchSlot = 2 * kParts;   // 8 cursors (k = 0..7) per partition
 constexpr int kKeptSlot = 10 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
@@ -89,14 +86,10 @@ constexpr int kLdsStack = PT_LDS_STACK;          // LDS stack entries per lane (
 constexpr uint32_t kWfMaxBlocks = 256 * 8;        // grid cap of the traversal kernels
 
 // k_wf_camera deals a chunk's camera samples to the partitions in runs of deal_run 256-sample
-// blocks, the runs round-robin (pt_wavefront.hip).  PT_DEAL_TILES=1: a run is one 32x32 tile's
-// samples (1024·spp / 256 blocks), so each XCD traces compact patches of the scene; measured
-// slower (C4 5899 → 5831 Mrays/s, closest hit 47.96 → 48.65 ms per pass, the 1/8 share and C2
-// unchanged; profiles/r03e_ab_deal.txt), so runs are one block (16 pixels' samples).
-#ifndef PT_DEAL_TILES
-#define PT_DEAL_TILES 0
-#endif
-__host__ __device__ inline uint32_t deal_run(int32_t spp_launch) { return PT_DEAL_TILES ? 4u * (uint32_t)spp_launch : 1u; }
+// blocks, the runs round-robin (pt_wavefront.hip): one block (16 pixels' samples) per run.  Runs of
+// one 32x32 tile's samples, so that each XCD traces compact patches of the scene, measured slower
+// (C4 5899 → 5831 Mrays/s; profiles/r03e_ab_deal.txt).
+__host__ __device__ inline uint32_t deal_run(int32_t) { return 1u; }
 // Camera samples the fullest partition receives from a chunk of `samples`.
 __host__ __device__ inline uint64_t deal_group_max(uint64_t samples, int32_t spp_launch) {
     const uint64_t run = deal_run(spp_launch), nblk = (samples + 255) / 256, nruns = (nblk + run - 1) / run;
@@ -113,7 +106,6 @@ struct WfPlan {
     uint32_t shade_blocks;     // shade, lockstep shadow; the refill and FULL traversal kernels below)
     uint32_t shadow_blocks;
     uint32_t lanes_trace_blocks, lanes_shadow_blocks, full_trace_blocks, full_shadow_blocks;
-    uint32_t full_lanes_trace_blocks, full_lanes_shadow_blocks;   // k_wf_*_lanes_full (row-4 scenes with a mesh)
     int32_t shade_form;        // k_wf_shade form: 0 chosen per depth from the kept count, 1 direct, 2 SCAN
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
     int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always

@@ -61,13 +61,10 @@ __device__ __forceinline__ void q_store(float4* p, float4 v) { *p = v; }
 __device__ __forceinline__ void q_store(uint4* p, uint4 v) { *p = v; }
 __device__ __forceinline__ void q_store(double2* p, double2 v) { *p = v; }
 __device__ __forceinline__ void q_store(ulonglong2* p, ulonglong2 v) { *p = v; }
-// Queue stores are non-temporal (PT_QSTORE_NT=2): with the child-major fill every store
-// instruction writes whole lines, and keeping the streamed queues out of the caches helped
-// k_wf_shade (C4 shade 29.9 → 28.2 ms/step, 4963 → 5040 Mrays/s; 1 = only the data read two
-// kernels later — throughput, key, light terms: 29.2 ms).  3 adds the closest-hit records.
-#ifndef PT_QSTORE_NT
-#define PT_QSTORE_NT 2
-#endif
+// Queue stores are non-temporal: with the child-major fill every store instruction writes whole
+// lines, and keeping the streamed queues out of the caches helped k_wf_shade (C4 shade 29.9 → 28.2
+// ms/step, 4963 → 5040 Mrays/s; only the data read two kernels later — throughput, key, light terms:
+// 29.2 ms).  Hit records go through the default policy (non-temporal measured no better).
 typedef float f4s __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void q_store_nt(double2* p, double2 v) {
     __builtin_nontemporal_store(__builtin_bit_cast(f4s, v), (f4s*)p);
@@ -79,19 +76,10 @@ __device__ __forceinline__ void q_store_nt(float4* p, float4 v) {
     __builtin_nontemporal_store(__builtin_bit_cast(f4s, v), (f4s*)p);
 }
 template <class T>
-__device__ __forceinline__ void q_store_late(T* p, T v) {
-    if (PT_QSTORE_NT >= 1) q_store_nt(p, v); else q_store(p, v);
-}
+__device__ __forceinline__ void q_store_late(T* p, T v) { q_store_nt(p, v); }
 template <class T>
-__device__ __forceinline__ void q_store_next(T* p, T v) {
-    if (PT_QSTORE_NT >= 2) q_store_nt(p, v); else q_store(p, v);
-}
-__device__ __forceinline__ void q_store_nt(uint4* p, uint4 v) {
-    __builtin_nontemporal_store(__builtin_bit_cast(f4s, v), (f4s*)p);
-}
-__device__ __forceinline__ void hit_store(uint4* p, uint4 v) {
-    if (PT_QSTORE_NT >= 3) q_store_nt(p, v); else q_store(p, v);
-}
+__device__ __forceinline__ void q_store_next(T* p, T v) { q_store_nt(p, v); }
+__device__ __forceinline__ void hit_store(uint4* p, uint4 v) { q_store(p, v); }
 __device__ __forceinline__ float4 nt_load(const float4* p) {
     f4v x = __builtin_nontemporal_load((const f4v*)p);
     return make_float4(x.x, x.y, x.z, x.w);
@@ -137,15 +125,6 @@ constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that
 constexpr int kBlockMajorFH = 16;
 constexpr int kBlockMajorChildren = 32;
 constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera slot (k_wf_trace)
-#ifndef PT_SCAN_HIT_LDS
-#define PT_SCAN_HIT_LDS 1   // SCAN: the shade rounds take the hit records the scan read (LDS) instead of reloading them
-#endif
-#ifndef PT_SCAN_CLAIMS
-#define PT_SCAN_CLAIMS 1   // SCAN claims per block at least (the claim shrinks for small partitions; 4 and 8 measured, no better)
-#endif
-#ifndef PT_SCAN_MOST
-#define PT_SCAN_MOST 1   // lean shade kernels take the SCAN form below 31/32 kept (0: below half, round 1)
-#endif
 #ifndef PT_SHADE_SCAN
 #define PT_SHADE_SCAN 8    // rows of 256 per SCAN claim: 16 best before claims carried their partial round, 8 since
                            // (C4 5836 / 5885 / 5743 for 16 / 8 / 32; the 1/8 share 5099 / 5208 / 4735)
@@ -212,12 +191,9 @@ __device__ __forceinline__ void ray_store_camera(const WfQueues& Q, int q, uint3
 }
 
 // ---------------------------------------------------------------- camera
-// Camera samples go to the XCD partitions in runs of `run` 256-sample blocks, the runs dealt
-// round-robin.  PT_DEAL_TILES=1: a run is one 32x32 tile's samples of the pass (4·spp blocks),
-// so each XCD traces whole tiles — 1/8 of the frame's tiles, each a compact patch of the scene
-// whose BVH nodes and shading records its own L2 then holds (measured 1.2 % slower on C4, see
-// pt_wavefront.h); 0 (default): runs of one block (16 pixels' samples), every XCD touching every
-// tile, the finest balance.
+// Camera samples go to the XCD partitions in runs of `run` 256-sample blocks (deal_run: one block,
+// 16 pixels' samples, so every XCD touches every tile — the finest balance), the runs dealt
+// round-robin.
 __global__ __launch_bounds__(256) void k_wf_camera(DevCamera cam, DevPass P, WfQueues Q, uint64_t begin,
                                                    uint32_t count, int32_t spp_launch, int32_t sample_base) {
     // The deal is fixed, so each sample's queue slot is too: no slot needs an atomic (one
@@ -355,9 +331,9 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
                 h.idx = (int32_t)r.w;
                 h.tx = h.t;
                 int32_t sdf = -1;
-                if (route) trace_heavy<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, ctr, h, PT_SDF_QUEUE ? &sdf : nullptr);
-                else trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h, PT_SDF_QUEUE ? &sdf : nullptr);
-                if (PT_SDF_QUEUE) {   // k_wf_sdf_hits traces it, every lane busy (the active lanes append here)
+                if (route) trace_heavy<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, ctr, h, &sdf);
+                else trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h, &sdf);
+                {   // k_wf_sdf_hits traces it, every lane busy (the active lanes append here)
                     const uint64_t m = __ballot(sdf >= 0);
                     if (m) {
                         const int lead = __builtin_ctzll(m);
@@ -404,7 +380,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 // atomic per refill).  A new ray's head work is two queue loads and the planes (none in
 // C4), so a refill holds the busy lanes for one load round trip.  Same visit order,
 // same arithmetic as trace(): bit-identical hits.
-// The SDF records the analytic half of a split closest hit queued (PT_SDF_QUEUE): one lane per
+// The SDF records the analytic half of a split closest hit queued: one lane per
 // entry, so SDFShape's sphere tracing (up to 1000 dependent steps) runs with every lane busy
 // instead of with the few lanes of a wave whose rays reach the shape.  Merged into the hit record
 // as the traversal would have: nearer wins, and an equal t beats a triangle (the analytic BVH
@@ -432,7 +408,7 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevSce
     if ((threadIdx.x & 63) == 0 && gained) atomicAdd(Q.counts + kept_word(qi), gained);
 }
 
-// The SDF records the analytic half of split shadow rays queued (PT_SDF_QUEUE_SHADOW): one lane per
+// The SDF records the analytic half of split shadow rays queued: one lane per
 // entry; a ray whose SDF is strictly nearer than its light is blocked.
 __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_shadow(DevScene S, WfQueues Q, int qo) {
     const uint32_t n = min(Q.counts[kSdfShWord], Q.s_cap);
@@ -446,133 +422,15 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_shadow(DevS
     }
 }
 
-#ifndef PT_COOP
-#define PT_COOP 0            // 1: the per-lane refill kernels fetch lines cooperatively (measured slower)
-#endif
-static_assert(!(PT_COOP && PT_NODE16), "the cooperative fetch stages the 7-piece node layout only");
-#ifndef PT_COOP_STAGE
-#define PT_COOP_STAGE 32     // lines staged in LDS per wave per pass (64: one pass, 32: two)
-#endif
-#ifndef PT_LANES_VGPRS
-// the register budget of the per-lane refill kernels: 512 / waves, rounded down to 8.  Pinned
-// explicitly because the compiler sizes it for the occupancy it computes from LDS, and with the
-// coop staging rows that estimate is below what the CU's 160 KB actually holds
+// The register budget of the per-lane refill kernels: 512 / waves, rounded down to 8, pinned
+// explicitly (the compiler would size it for the occupancy it computes from LDS).
 #define PT_LANES_VGPRS ((512 / PT_LANES_WAVES) & ~7)
-#endif
-constexpr uint32_t kNoLine = 0xFFFFFFFFu;
-constexpr int kCoopStage = PT_COOP_STAGE;
-[[maybe_unused]] constexpr int kCoopRows = 4 * kCoopStage * 7;   // float4 of LDS per block (PT_COOP)
-// Cooperative line fetch.  A traversal step reads one 128-B line per lane (a BVH4 node or a
-// leaf chunk) as seven 16-B loads; with every lane on its own line, each load instruction
-// touches 64 distinct lines and the texture-address path charges per line, ~1 cycle each
-// (the per-lane refill kernels ran at that bound).  Here the 8 lanes of a group
-// load the group's 8 lines, one line per instruction (lanes 0..6 of the group take one 16-B
-// piece each, so an instruction touches 8 lines), stage them in LDS through this wave's rows
-// and each lane reads its own line back: 8 load instructions of 8 lines instead of 7 of 64.
-// Every load is issued before the first LDS hand-off (one memory round trip per step);
-// kCoopStage < 64 stages the groups' lines in 64 / kCoopStage passes through fewer rows.
-// Wave-uniform call: every lane takes part, `line` = kNoLine for a lane with nothing to fetch.
-template <int J>
-__device__ __forceinline__ uint32_t bcast8(uint32_t x) {   // lane J of each group of 8 (ds_swizzle bit mode)
-    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18 | (J << 5));
-}
-__device__ __forceinline__ void coop_line(const float4* __restrict__ lines, uint32_t line, float4* st, uint32_t lane,
-                                          float4& q0, float4& q1, float4& q2, float4& q3, float4& q4, float4& q5,
-                                          float4& q6) {
-    const uint32_t piece = lane & 7u, g = lane >> 3;
-    float4 v[8];
-    const uint32_t src[8] = {bcast8<0>(line), bcast8<1>(line), bcast8<2>(line), bcast8<3>(line),
-                             bcast8<4>(line), bcast8<5>(line), bcast8<6>(line), bcast8<7>(line)};
-#pragma unroll
-    for (int j = 0; j < 8; j++) {   // lane (g, piece) loads piece `piece` of the line of lane 8g + j
-        v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (src[j] != kNoLine && piece < 7u) v[j] = lines[8 * (size_t)src[j] + piece];   // cached: the tree is reused
-    }
-    constexpr int kPer = kCoopStage / 8;   // lines per group per pass
-#pragma unroll
-    for (int h = 0; h < 8 / kPer; h++) {
-#pragma unroll
-        for (int jj = 0; jj < kPer; jj++)
-            if (piece < 7u) st[(g * kPer + (uint32_t)jj) * 7u + piece] = v[h * kPer + jj];
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes done
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t mj = piece - (uint32_t)(h * kPer);
-        if (mj < (uint32_t)kPer) {
-            const float4* r = st + (g * kPer + mj) * 7u;
-            q0 = r[0]; q1 = r[1]; q2 = r[2]; q3 = r[3]; q4 = r[4]; q5 = r[5]; q6 = r[6];
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // the reads done before the next pass rewrites the rows
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// Cooperative line fetch without LDS (PT_COOP == 2).  The wave's lanes form 8 groups of 8: group
-// q = lane & 7, member m = lane >> 3 (lanes q, q + 8, ..., q + 56).  Load k (k = 0..7): member m < 7
-// loads piece m of the line of member k of its group, so each load instruction touches at most 8
-// distinct lines (one per group) instead of up to 64, and the texture-address path charges per
-// distinct line.  Lane (m, q) then holds piece m of its group's 8 lines; an 8x8 transpose of 16-B
-// elements across the members gives lane (k, q) the pieces of its own line: three butterfly stages
-// over member bits 4 / 2 / 1 = lane bits 32 / 16 / 8, done with gfx950's v_permlane32_swap and
-// v_permlane16_swap (one instruction per dword pair, no selects) and a DPP row_ror:8 exchange.
-// Wave-uniform call; `line` = kNoLine for a lane with nothing to fetch.
-__device__ __forceinline__ void swap32(float& a, float& b) {   // a's upper 32 lanes <-> b's lower 32 lanes
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    a = __uint_as_float(r[0]);
-    b = __uint_as_float(r[1]);
-}
-__device__ __forceinline__ void swap16(float& a, float& b) {   // a's odd rows of 16 <-> b's even rows
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    a = __uint_as_float(r[0]);
-    b = __uint_as_float(r[1]);
-}
-__device__ __forceinline__ void swap8(float& a, float& b, bool top) {   // a's lanes 8-15 <-> b's lanes 0-7 of each row
-    const float u = __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(a), 0x128, 0xf, 0xf, false));
-    const float v = __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(b), 0x128, 0xf, 0xf, false));
-    b = top ? u : b;
-    a = top ? a : v;
-}
-__device__ __forceinline__ void swap32(float4& a, float4& b) { swap32(a.x, b.x); swap32(a.y, b.y); swap32(a.z, b.z); swap32(a.w, b.w); }
-__device__ __forceinline__ void swap16(float4& a, float4& b) { swap16(a.x, b.x); swap16(a.y, b.y); swap16(a.z, b.z); swap16(a.w, b.w); }
-__device__ __forceinline__ void swap8(float4& a, float4& b, bool top) {
-    swap8(a.x, b.x, top); swap8(a.y, b.y, top); swap8(a.z, b.z, top); swap8(a.w, b.w, top);
-}
-__device__ __forceinline__ void coop_line_x(const float4* __restrict__ lines, uint32_t line, uint32_t lane, float4& q0,
-                                            float4& q1, float4& q2, float4& q3, float4& q4, float4& q5, float4& q6) {
-    const uint32_t m = lane >> 3, q = lane & 7u;
-    float4 x[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {   // member m loads piece m of member k's line
-        const uint32_t src = (uint32_t)__shfl((int)line, 8 * k + (int)q, 64);
-        x[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (src != kNoLine && m < 7u) x[k] = lines[8 * (size_t)src + m];
-    }
-    // x[k] of lane (m, q) = element (m, k); transposed: x[j] of lane (k, q) = piece j of member k's line
-#pragma unroll
-    for (int k = 0; k < 4; k++) swap32(x[k], x[k | 4]);
-    swap16(x[0], x[2]); swap16(x[1], x[3]); swap16(x[4], x[6]); swap16(x[5], x[7]);
-    const bool top = (lane & 8u) == 0u;
-    swap8(x[0], x[1], top); swap8(x[2], x[3], top); swap8(x[4], x[5], top); swap8(x[6], x[7], top);
-    q0 = x[0]; q1 = x[1]; q2 = x[2]; q3 = x[3]; q4 = x[4]; q5 = x[5]; q6 = x[6];
-}
-
-// The line a traversal lane reads at its next step (coop_line's index; the arrays are one
-// allocation, pt_scene.h `lines`); an analytic leaf reads its records instead.
-__device__ __forceinline__ uint32_t step_line(const DevScene& S, bool has, bool tri, uint32_t ref) {
-    const bool leaf = (ref & 0x80000000u) != 0;
-    if (!has) return kNoLine;
-    if (tri) return (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu);
-    return leaf ? kNoLine : ref;
-}
 
 // Does the ray reach the triangle BVH at all (its root box within tmax)?  A child box lies inside
 // the root box and the fp32 slab arithmetic is monotone in the bounds, so a miss here is a miss of
 // every root child: skipping the root step changes no hit, only the step count.
-#ifndef PT_ROOT_CULL
-#define PT_ROOT_CULL 1
-#endif
 __device__ __forceinline__ bool tri_reach(const DevScene& S, v3 o, v3 invd, float tmax) {
     if (S.tri_num_nodes <= 0) return false;
-    if (!PT_ROOT_CULL) return true;
     return slab1(S.tri_box[0], S.tri_box[3], S.tri_box[1], S.tri_box[4], S.tri_box[2], S.tri_box[5], o, invd, tmax) !=
            __int_as_float(0x7f800000);
 }
@@ -580,71 +438,31 @@ __device__ __forceinline__ bool tri_reach(const DevScene& S, v3 o, v3 invd, floa
 #ifndef PT_REFILL_IDLE
 #define PT_REFILL_IDLE 40   // closest hit: 8 / 16 / 24 / 32 / 40 / 48 measured on C4, 40 best
 #endif
-// Leaf turns (PT_LEAF_VOTE = T > 0).  A wave whose lanes sit partly at inner nodes and partly
-// at leaves runs both the node test and the leaf's triangle loop every step, and the triangle
-// loop (up to 3 Moeller-Trumbore tests with their fp64 tail) costs more VALU than the node
-// test.  With leaf turns the wave votes: a step is a leaf step only once T of its active lanes
-// wait at a leaf (or no active lane is at an inner node); otherwise it is a node step and the
-// leaf lanes keep their leaf for a later step.  Every ray still takes its own steps in its own
-// order, so hits are unchanged.  Wave-uniform call.
-#ifndef PT_LEAF_VOTE
-#define PT_LEAF_VOTE 0
-#endif
-__device__ __forceinline__ bool leaf_turn(bool act, bool leaf) {
-    const uint64_t am = __ballot(act), lm = __ballot(act && leaf);
-    const bool leaf_step = lm == am || (uint32_t)__popcll(lm) >= (uint32_t)PT_LEAF_VOTE;
-    return leaf == leaf_step;
-}
-// Prefetch (PT_PREFETCH): a node step that pushes a second child also reads one word of that
-// child's line, so the line is on its way to the L2 when the lane pops it (after the nearest
-// child's subtree).  An empty asm after the next step's loads keeps the word alive.
-#ifndef PT_PREFETCH
-#define PT_PREFETCH 0
-#endif
-__device__ __forceinline__ uint32_t line_of(const DevScene& S, bool tri, uint32_t ref) {
-    const bool leaf = (ref & 0x80000000u) != 0;
-    return tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu) : (leaf ? 0u : ref);
-}
-#ifndef PT_SDF_QUEUE_SHADOW
-#define PT_SDF_QUEUE_SHADOW 1   // split shadow rays queue their SDF records too (k_wf_sdf_shadow)
-#endif
-#ifndef PT_SPLIT
-#define PT_SPLIT 1   // row-4 scenes with a triangle BVH: split traversal (depth_loop)
-#endif
-#ifndef PT_LANES_MIN_NODES
-#define PT_LANES_MIN_NODES 64
-#endif
-constexpr int kLanesMinNodes = PT_LANES_MIN_NODES;
-#ifndef PT_STEAL
-#define PT_STEAL 0   // 1: a refill wave whose partition is drained claims from the others (measured slower)
-#endif
-#ifndef PT_SHADOW_HELP
-#define PT_SHADOW_HELP 1   // shadow refill kernel: idle lanes help the tail's rays (k_wf_shadow_lanes)
-#endif
 #ifndef PT_SHADOW_REFILL_IDLE
 #define PT_SHADOW_REFILL_IDLE 32   // shadow: 16 / 24 / 32 / 48 measured, 32 best
 #endif
-// FULL: the same kernel over scenes with §8f row 4 shapes (SDF, Volume, TransformedShape) in the
-// analytic BVH; their intersects are calls (inner_t / xform_t), made by the lanes that reach them.
-#ifndef PT_FULL_LANES_WAVES
-#define PT_FULL_LANES_WAVES 4
-#endif
-#define PT_FULL_LANES_VGPRS ((512 / PT_FULL_LANES_WAVES) & ~7)
-#ifndef PT_FULL_LANES_SHADOW
-#define PT_FULL_LANES_SHADOW PT_FULL_LANES   // the shadow side of PT_FULL_LANES
-#endif
-#ifndef PT_FULL_LANES
-#define PT_FULL_LANES 0   // 1: row-4 scenes with a mesh take these (C5 634 vs 667 Mrays/s lockstep: DESIGN §8)
-#endif
-// split: the planes and the triangle BVH only (the refill half of a split closest hit; the FULL
-// k_wf_trace<.., SPLIT> pass adds the analytic BVH and counts the kept rays).
-template <bool COUNT, bool FULL, bool SPLIT = false>
+// The refill kernels run on scenes whose triangle BVH has more than this many nodes (gopher3's five
+// analytic shapes: trace 16.0 → 23.5 ms with refill).
+constexpr int kLanesMinNodes = 64;
+
+// Closest hit with per-lane refill over lean scenes (no §8f row-4 shapes; the refill half of a split
+// closest hit).  See k_wf_trace for the lockstep form.  Each lane keeps one ray in flight through ONE
+// step loop: a step is one node (or leaf) of the analytic BVH or of the triangle BVH (the same
+// seven-load 128-B line), the analytic phase hands over to the triangle phase at an empty stack, and
+// a lane whose ray is done takes the next one when PT_REFILL_IDLE lanes of the wave are idle (one
+// claim atomic per refill).  A new ray's head work is two queue loads, the planes and (ana_linear /
+// route) the few analytic shapes, so a refill holds the busy lanes for one load round trip.  Same
+// visit order, same arithmetic as trace(): bit-identical hits.
+// SPLIT: the planes, the lean analytic records (routed split) and the triangle BVH only; the FULL
+// k_wf_trace<.., SPLIT> pass adds the analytic BVH (or, routed, the heavy records of the rays that
+// reach their boxes) and counts the kept rays it finishes.
+// Measured and not kept: a cooperative line fetch through LDS (round 2) and through
+// a permlane transpose (round 4), leaf turns, a line read ahead, partition stealing, refill kernels
+// for the row-4 scenes.
+template <bool COUNT, bool SPLIT = false>
 __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q, int qi, unsigned long long* counters) {
     constexpr bool split = SPLIT;   // a template flag: the unsplit kernel keeps its registers
     __shared__ uint32_t s_stack[kLdsStack * kTB];
-#if PT_COOP == 1
-    __shared__ float4 s_coop[kCoopRows];
-#endif
     const WStack stack{s_stack + threadIdx.x, Q.ovf + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;              // consumed: free for k_wf_shade's output
@@ -652,11 +470,9 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
         Q.counts[fetch_word(7, threadIdx.x)] = 0u;               // (the FULL one's of a routed shade)
     }
     const Group G = xcd_group();
-    // claims start in the XCD's own partition; with PT_STEAL a wave whose partition is drained
-    // goes on to the next ones (hits are stored by slot, so which XCD traces a ray changes nothing)
-    uint32_t part = G.g, hops = 0;
-    uint32_t n = min(*ray_count(Q, qi, part), Q.pcap), base = part * Q.pcap;
-    uint32_t* cursor = Q.counts + fetch_word(0, part);
+    const uint32_t part = G.g;   // the XCD's own partition
+    const uint32_t n = min(*ray_count(Q, qi, part), Q.pcap), base = part * Q.pcap;
+    uint32_t* const cursor = Q.counts + fetch_word(0, part);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     Counters ctr{0, 0, 0, 0};
@@ -664,19 +480,16 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     uint32_t kept = 0;
     const float inf = __int_as_float(0x7f800000);
     bool has = false, tri = false, more = true;
-    uint32_t pf_val = 0;   // PT_PREFETCH: the word read ahead (kept alive until the next step)
-    int32_t pend = -1;    // FULL: a Volume record left for the wave's cooperative march (march_pending)
-    bool mwait = false;   // FULL: this lane's traversal is done, its pending Volume not yet marched
     uint32_t i = 0, ref = 0;   // i: the ray's slot; bit 31 set = the ray misses the triangle BVH's root box
     int sp = 0;
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
-    double bt = kHitInf, btx = 0.0;   // btx (FULL): HitRec::tx of the best
+    double bt = kHitInf;
     int32_t bkind = -1, bidx = -1;
     float tmax = 0.f;
     const bool route = split && S.route;   // routed split: only rays that reach a heavy box go on (hq)
     bool hpend = false;                       // this lane's finished ray goes to the heavy queue (at the loop top)
     auto finish = [&]() {
-        unsigned long long tb = (unsigned long long)__double_as_longlong(FULL && bkind == KIND_XFORM ? btx : bt);
+        unsigned long long tb = (unsigned long long)__double_as_longlong(bt);
         hit_store(&Q.hits[i & 0x7FFFFFFFu], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
         if (route) hpend = heavy_reach(S, o, invd, tmax_bound(bt));
         if (!split || (route && !hpend)) kept += (bkind >= 0 || !env_black) ? 1u : 0u;
@@ -697,45 +510,16 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                 }
             }
         }
-        if constexpr (FULL && PT_COOP_MARCH) {   // wave-uniform: every lane is here
-            const uint64_t mq = __ballot(mwait);
-            for (uint64_t todo = mq; todo; todo &= todo - 1ull) {   // each waiting ray, marched by the whole wave
-                const int src = __builtin_ctzll(todo);
-                const int32_t p = __shfl(pend, src, 64);
-                const v3 so{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
-                const v3 sd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
-                int32_t kind;
-                double tx = 0;
-                const double t = coop_record_t(S, p, so, sd, kind, tx);
-                if (lane == (uint32_t)src && (t < bt || (t == bt && bkind == KIND_TRI))) {
-                    bt = t; bkind = kind; bidx = p; btx = tx;
-                }
-            }
-            if (mwait) {
-                mwait = false;
-                pend = -1;
-                finish();
-            }
-        }
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (more && (nidle >= PT_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
             uint32_t kc = 0;
             if (lane == 0) kc = atomicAdd(cursor, nidle);
             kc = __builtin_amdgcn_readfirstlane(kc);   // every lane is active here: lane 0's claim, in an SGPR
-            const uint32_t k = kc + (uint32_t)__popcll(idle & below), cn = n, cbase = base;
-            if (kc + nidle >= n) {   // this partition is drained
-                if (PT_STEAL && ++hops < (uint32_t)kParts) {
-                    part = (part + 1u) % (uint32_t)kParts;
-                    n = min(*ray_count(Q, qi, part), Q.pcap);
-                    base = part * Q.pcap;
-                    cursor = Q.counts + fetch_word(0, part);
-                } else {
-                    more = false;
-                }
-            }
-            if (!has && k < cn) {
-                i = cbase + k;
+            const uint32_t k = kc + (uint32_t)__popcll(idle & below);
+            if (kc + nidle >= n) more = false;   // this partition is drained
+            if (!has && k < n) {
+                i = base + k;
                 const float4 b = nt_load(&Q.q_d[qi][i]);
                 const float4 a = nt_load(&Q.q_o[qi][i]);
                 if (__float_as_uint(b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
@@ -757,9 +541,8 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                             if (route && f2u(S.ana_recs[3 * p].w) > (uint32_t)KIND_CUBE) continue;   // heavy: its box at finish
                             if (COUNT) ctr.prims++;
                             int32_t kind;
-                            double tx = 0;
-                            const double t = prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind, FULL ? &tx : nullptr);
-                            if (t < bt) { bt = t; bkind = kind; bidx = p; if (FULL) btx = tx; }
+                            const double t = prim_t<false, false>(S, S.ana_recs, (uint32_t)p, o, d, kind);
+                            if (t < bt) { bt = t; bkind = kind; bidx = p; }
                         }
                     }
                     tmax = tmax_bound(bt);
@@ -768,37 +551,25 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                     // tested at the refill's bound (planes only), kept as a bit of i: no register for it
                     if (!tri_reach(S, o, invd, tmax)) i |= 0x80000000u;
                     tri = split || S.ana_linear || S.ana_num_nodes <= 0;
-                    if (tri && (i >> 31)) finish();   // (FULL scenes traverse the analytic BVH first: tri false)
+                    if (tri && (i >> 31)) finish();
                 }
             }
         }
         if (!more && __ballot(has) == 0ull) break;
-        // one step: inner node or leaf of the current BVH (one 128-B line)
+        if (!has) continue;
+        // one step: inner node or leaf of the current BVH, one 128-B line of seven 16-B pieces, by a
+        // 32-bit offset into the one allocation of all traversal lines (no per-BVH 64-bit base: the
+        // step loop then holds its state without spilling).  An analytic leaf reads its records in
+        // prim_t; its line is not used.
         const bool leaf = (ref & 0x80000000u) != 0;
-        float4 q0, q1, q2, q3, q4, q5, q6;   // the step's line
-#if PT_COOP == 1
-        coop_line(S.lines, step_line(S, has && !(FULL && mwait), tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7),
-                  lane, q0, q1, q2, q3, q4, q5, q6);
-        if (!has || (FULL && mwait)) continue;
-#elif PT_COOP == 2
-        coop_line_x(S.lines, step_line(S, has && !(FULL && mwait), tri, ref), lane, q0, q1, q2, q3, q4, q5, q6);
-        if (!has || (FULL && mwait)) continue;
-#else
-        if (PT_LEAF_VOTE && !leaf_turn(has && !(FULL && mwait), leaf)) continue;
-        if (!has || (FULL && mwait)) continue;
-        {   // one 128-B line, seven 16-B pieces, by a 32-bit offset into the one allocation of all
-            // traversal lines (no per-BVH 64-bit base: the step loop then holds its state without
-            // spilling).  An analytic leaf reads its records in prim_t; its line is not used.
+        float4 q0, q1, q2, q3, q4, q5, q6;
+        {
             const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
                                           : (leaf ? 0u : ref));
             q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
-            q4 = S.lines[at + 4u];
-            if (kNodePieces > 5 || (tri && leaf)) { q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; }   // a chunk's last two
-            else { q5 = make_float4(0.f, 0.f, 0.f, 0.f); q6 = q5; }
+            q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u];
         }
-#endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
-        if (PT_PREFETCH) asm volatile("" ::"v"(pf_val));
         bool pop = true;
         if (!leaf) {
             if (COUNT) ctr.nodes++;
@@ -814,7 +585,6 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                 push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
                 ref = v0;
                 pop = false;
-                if (PT_PREFETCH && k1 != inf) pf_val = __float_as_uint(S.lines[8u * line_of(S, tri, v1)].x);
             }
         } else if (tri) {
             const uint32_t cntl = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q0.x);
@@ -835,15 +605,9 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
             for (uint32_t k = 0; k < cntl; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
-                if (FULL && PT_COOP_MARCH && pend < 0 && march_deferred(S, S.ana_recs + 3 * (size_t)(first + k))) {
-                    pend = (int32_t)(first + k);
-                    continue;
-                }
-                double tx = 0;
-                const double t = prim_t<false, FULL>(S, S.ana_recs, first + k, o, d, kind, FULL ? &tx : nullptr);
+                const double t = prim_t<false, false>(S, S.ana_recs, first + k, o, d, kind);
                 if (t < bt) {
                     bt = t; bkind = kind; bidx = (int32_t)(first + k);
-                    if (FULL) btx = tx;
                     tmax = tmax_bound(t);
                 }
             }
@@ -855,8 +619,6 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
             } else if (!tri && !(i >> 31)) {
                 tri = true;
                 ref = 0;
-            } else if (FULL && pend >= 0) {
-                mwait = true;   // the wave marches it at the top of the loop
             } else {
                 finish();
             }
@@ -876,20 +638,10 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
 }
 template <bool COUNT, bool SPLIT = false>
 __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_trace_lanes(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
-    trace_lanes<COUNT, false, SPLIT>(S, Q, qi, counters);
-}
-template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_FULL_LANES_VGPRS))) void k_wf_trace_lanes_full(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
-    trace_lanes<COUNT, true>(S, Q, qi, counters);
+    trace_lanes<COUNT, SPLIT>(S, Q, qi, counters);
 }
 
 // ---------------------------------------------------------------- shade / bounce
-#ifndef PT_NEE_VERTEX_MAJOR
-// 1: a vertex' shadow rays take consecutive slots (its children's light terms then sit in one
-// run, summed in registers by k_wf_nee_accum's wave aggregation); 0: child-major like the
-// extension rays (child c of every vertex of the block, then child c + 1)
-#define PT_NEE_VERTEX_MAJOR 0
-#endif
 #ifndef PT_SHADE_WAVES
 #define PT_SHADE_WAVES 3
 #endif
@@ -1009,7 +761,6 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     // whole lines.  Which children exist is unchanged, so is every child's key.  With
     // more children per vertex than s_cc holds, each wave fills its own share that way.
     uint32_t ej = block_major ? blk_e : __shfl(ebase, 0, 64), nj = block_major ? blk_n : __shfl(nbase, 0, 64);
-    uint32_t nk = nbase;   // PT_NEE_VERTEX_MAJOR: this vertex' next shadow-ray slot
     for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
         const int mode = ma + c % nm;
         const uint64_t E = child_key(node, (uint32_t)c);
@@ -1028,10 +779,9 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
                 te += ce; tn += cn;
             }
         }
-        const uint32_t my_n = PT_NEE_VERTEX_MAJOR ? nk : nj + (pn + (uint32_t)__popcll(bn & below)) * rays_per_nee;
+        const uint32_t my_n = nj + (pn + (uint32_t)__popcll(bn & below)) * rays_per_nee;
         const uint32_t my_e = ej + pe + (uint32_t)__popcll(be & below);
         nj += tn * rays_per_nee;
-        if (emit_nee) nk += rays_per_nee;
         ej += te;
         if (!live) continue;
         const double fp = mode == 0 ? 1.0 : (refl ? pv : 1 - pv);
@@ -1102,7 +852,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     const bool routed = S.shade_route != 0;
     const bool scan = routed ? true
                     : form ? form == 2
-                           : (FULL || !PT_SCAN_MOST) ? 2ull * kept < (unsigned long long)queued
+                           : FULL ? 2ull * kept < (unsigned long long)queued
                                                      : 32ull * kept < 31ull * (unsigned long long)queued;
     if (scan != SCAN) return;
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
@@ -1141,9 +891,9 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         __shared__ uint32_t s_list[kShadeScan * 256 + 256];
         __shared__ uint4 s_hit[kShadeScan * 256 + 256];   // their hit records (read once, by the scan)
         uint32_t carry = 0;   // block-uniform
-        // rows of 256 slots per claim: kShadeScan, fewer when the partition would give a block
-        // fewer than PT_SCAN_CLAIMS claims (small chunks: one rank's share of a multi-GPU frame)
-        const uint32_t rows = max(1u, min((uint32_t)kShadeScan, n / (G.nb * 256u * (uint32_t)PT_SCAN_CLAIMS)));
+        // rows of 256 slots per claim: kShadeScan, fewer when the partition would not give every block a
+        // claim (small chunks: one rank's share of a multi-GPU frame; 4 or 8 claims per block: no better)
+        const uint32_t rows = max(1u, min((uint32_t)kShadeScan, n / (G.nb * 256u)));
         for (;;) {
             if (threadIdx.x == 0) s_k0 = atomicAdd(shade_cursor, 256u * rows);
             __syncthreads();
@@ -1190,7 +940,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             for (uint32_t r = 0; r < full; r += 256u) {   // block-uniform
                 const bool listed = r + threadIdx.x < full;
                 shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed, ctr,
-                                          PT_SCAN_HIT_LDS ? &s_hit[r + threadIdx.x] : nullptr);
+                                          &s_hit[r + threadIdx.x]);
                 __syncthreads();   // the next round rewrites shade_vertex's LDS child counts
             }
             if (last) break;
@@ -1244,10 +994,10 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
                 double tl = 0;
                 const bool blocked =
                     route ? heavy_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, ctr,
-                                                 PT_SDF_QUEUE_SHADOW ? &sdf : nullptr, &tl)
+                                                 &sdf, &tl)
                           : ana_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr,
-                                               PT_SDF_QUEUE_SHADOW ? &sdf : nullptr, &tl);
-                if (PT_SDF_QUEUE_SHADOW) {   // k_wf_sdf_shadow tests it, every lane busy
+                                               &sdf, &tl);
+                {   // k_wf_sdf_shadow tests it, every lane busy
                     const uint64_t m = __ballot(!blocked && sdf >= 0);
                     if (m) {
                         const int lead = __builtin_ctzll(m);
@@ -1286,20 +1036,22 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // light's own t and the planes at refill, then one step loop over the analytic BVH and
 // the triangle BVH, any-hit (a primitive strictly nearer than the light ends the ray
 // unlit).  The outcome goes to n_lit; k_wf_nee_accum adds the lit rays' terms.
-// split: the planes and the triangle BVH only; the FULL k_wf_shadow<.., SPLIT> pass then tests the
-// analytic BVH of the rays left lit.
-template <bool COUNT, bool FULL, bool SPLIT = false>
+// split: the planes, the lean analytic records (routed split) and the triangle BVH only; the FULL
+// k_wf_shadow<.., SPLIT> pass then tests the analytic BVH (routed: the heavy records) of the rays
+// left lit.
+// The tail (queue drained): idle lanes take stack entries of busy lanes' rays and traverse those
+// subtrees (any-hit: the ray is blocked iff some subtree holds a blocker, in any order).
+// s_help[root]: helpers still running on root's ray, bit 31 = blocked.  A root that ends its own
+// traversal waits for its helpers before it reports the ray lit.
+template <bool COUNT, bool SPLIT = false>
 __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters) {
     constexpr bool split = SPLIT;
     __shared__ uint32_t s_stack[kLdsStack * kTB];
-#if PT_COOP == 1
-    __shared__ float4 s_coop[kCoopRows];
-#endif
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
-    uint32_t part = G.g, hops = 0;   // as k_wf_trace_lanes: own partition first, then (PT_STEAL) the others
-    uint32_t n = min(*nee_count(Q, qo, part), Q.spcap), base = part * Q.spcap;
-    uint32_t* cursor = Q.counts + fetch_word(2 + qo, part);
+    const uint32_t part = G.g;   // the XCD's own partition
+    const uint32_t n = min(*nee_count(Q, qo, part), Q.spcap), base = part * Q.spcap;
+    uint32_t* const cursor = Q.counts + fetch_word(2 + qo, part);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     Counters ctr{0, 0, 0, 0};
@@ -1310,8 +1062,12 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f}, invd{0.f, 0.f, 0.f};
     double tl = kHitInf;
     float tmax = 0.f;
-    uint32_t pf_val = 0;   // PT_PREFETCH: the word read ahead (kept alive until the next step)
     bool waiting = false;   // a root whose traversal is done, waiting for its tail helpers
+    __shared__ uint32_t s_help[kTB];
+    __shared__ uint32_t s_map[kTB];   // per wave: donor lane by rank
+    bool helper = false;
+    uint32_t root = threadIdx.x;
+    const uint32_t wbase = threadIdx.x & ~63u;
     const bool route = split && S.route;   // routed split: lit rays that reach a heavy box go on (hq_sh)
     bool hpend = false;
     // a root ray found nothing nearer than its light: lit (a phantom light never is); under the routed
@@ -1320,17 +1076,6 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
         Q.n_lit[qo][i] = phantom ? 0 : 1;
         if (route && !phantom) hpend = heavy_reach(S, o, invd, tmax);
     };
-#if PT_SHADOW_HELP
-    // The tail (queue drained): idle lanes take stack entries of busy lanes' rays and traverse
-    // those subtrees (any-hit: the ray is blocked iff some subtree holds a blocker, in any order).
-    // s_help[root]: helpers still running on root's ray, bit 31 = blocked.  A root that ends its
-    // own traversal waits for its helpers before it reports the ray lit.
-    __shared__ uint32_t s_help[kTB];
-    __shared__ uint32_t s_map[kTB];   // per wave: donor lane by rank
-    bool helper = false;
-    uint32_t root = threadIdx.x;
-    const uint32_t wbase = threadIdx.x & ~63u;
-#endif
     for (;;) {
         if (route) {   // wave-uniform: the provisionally lit rays that reach a heavy box, one atomic per wave
             const uint64_t hm = __ballot(hpend);
@@ -1352,19 +1097,10 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
             uint32_t kc = 0;
             if (lane == 0) kc = atomicAdd(cursor, nidle);
             kc = __builtin_amdgcn_readfirstlane(kc);   // every lane is active here: lane 0's claim, in an SGPR
-            const uint32_t k = kc + (uint32_t)__popcll(idle & below), cn = n, cbase = base;
-            if (kc + nidle >= n) {
-                if (PT_STEAL && ++hops < (uint32_t)kParts) {
-                    part = (part + 1u) % (uint32_t)kParts;
-                    n = min(*nee_count(Q, qo, part), Q.spcap);
-                    base = part * Q.spcap;
-                    cursor = Q.counts + fetch_word(2 + qo, part);
-                } else {
-                    more = false;
-                }
-            }
-            if (!has && k < cn) {
-                i = cbase + k;
+            const uint32_t k = kc + (uint32_t)__popcll(idle & below);
+            if (kc + nidle >= n) more = false;
+            if (!has && k < n) {
+                i = base + k;
                 const float4 b = nt_load(&Q.n_n[qo][i]);
                 const float4 a = nt_load(&Q.n_o[qo][i]);
                 const uint32_t li = __float_as_uint(b.w);
@@ -1383,7 +1119,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                         run = S.tri_num_nodes > 0;
                         tri = true;
                     } else {
-                        tl = light_t<FULL>(S, L, o, d);
+                        tl = light_t<false>(S, L, o, d);
                         run = tl < kHitInf;
                         for (int p = 0; run && p < S.num_planes; p++) {
                             const float4 pa = S.planes[2 * p], pb = S.planes[2 * p + 1];
@@ -1394,7 +1130,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                                 if (route && f2u(S.ana_recs[3 * p].w) > (uint32_t)KIND_CUBE) continue;   // heavy: its box at the end
                                 if (COUNT) ctr.prims++;
                                 int32_t kind;
-                                if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) run = false;
+                                if (prim_t<false, false>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) run = false;
                             }
                         tri = split || S.ana_linear || S.ana_num_nodes <= 0;
                     }
@@ -1408,14 +1144,11 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                         Q.n_lit[qo][i] = 0;
                     }
                     has = run;
-#if PT_SHADOW_HELP
                     s_help[threadIdx.x] = 0u;
-#endif
                 }
             }
         }
         if (!more && __ballot(has) == 0ull) break;
-#if PT_SHADOW_HELP
         if (!COUNT && !more) {   // wave-uniform: the tail (not in the counting pass: its node counts stay sequential)
             if (has) {
                 const uint32_t st = s_help[root];
@@ -1464,33 +1197,17 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                 }
             }
         }
-#endif
-        // one step: inner node or leaf of the current BVH (one 128-B line)
+        if (!has || waiting) continue;
+        // one step: inner node or leaf of the current BVH (one 128-B line; see k_wf_trace_lanes)
         const bool leaf = (ref & 0x80000000u) != 0;
-        float4 q0, q1, q2, q3, q4, q5, q6;   // the step's line
-#if PT_COOP == 1
-        coop_line(S.lines, step_line(S, has && !waiting, tri, ref), s_coop + (threadIdx.x >> 6) * (kCoopStage * 7), lane, q0, q1, q2,
-                  q3, q4, q5, q6);
-        if (!has || waiting) continue;
-#elif PT_COOP == 2
-        coop_line_x(S.lines, step_line(S, has && !waiting, tri, ref), lane, q0, q1, q2, q3, q4, q5, q6);
-        if (!has || waiting) continue;
-#else
-        if (PT_LEAF_VOTE && !leaf_turn(has && !waiting, leaf)) continue;
-        if (!has || waiting) continue;
-        {   // one 128-B line, seven 16-B pieces, by a 32-bit offset into the one allocation of all
-            // traversal lines (no per-BVH 64-bit base: the step loop then holds its state without
-            // spilling).  An analytic leaf reads its records in prim_t; its line is not used.
+        float4 q0, q1, q2, q3, q4, q5, q6;
+        {
             const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
                                           : (leaf ? 0u : ref));
             q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
-            q4 = S.lines[at + 4u];
-            if (kNodePieces > 5 || (tri && leaf)) { q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; }   // a chunk's last two
-            else { q5 = make_float4(0.f, 0.f, 0.f, 0.f); q6 = q5; }
+            q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u];
         }
-#endif
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
-        if (PT_PREFETCH) asm volatile("" ::"v"(pf_val));
         bool pop = true, blocked = false;
         if (!leaf) {
             if (COUNT) ctr.nodes++;
@@ -1506,7 +1223,6 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                 push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
                 ref = v0;
                 pop = false;
-                if (PT_PREFETCH && k1 != inf) pf_val = __float_as_uint(S.lines[8u * line_of(S, tri, v1)].x);
             }
         } else if (tri) {
             const uint32_t cntl = ((ref >> 29) & 3u) + 1u;
@@ -1523,10 +1239,9 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
             for (uint32_t k = 0; k < cntl; k++) {
                 if (COUNT) ctr.prims++;
                 int32_t kind;
-                if (prim_t<false, FULL>(S, S.ana_recs, first + k, o, d, kind) < tl) { blocked = true; break; }
+                if (prim_t<false, false>(S, S.ana_recs, first + k, o, d, kind) < tl) { blocked = true; break; }
             }
         }
-#if PT_SHADOW_HELP
         if (blocked) {
             has = false;
             if (helper) atomicOr(&s_help[root], 0x80000000u);
@@ -1544,30 +1259,13 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
             } else if (!tri && tri_reach(S, o, invd, tmax)) {
                 tri = true;
                 ref = 0;
-            } else if (s_help[root] == 0u) {   // no primitive nearer than the light: lit (a phantom light never is)
+            } else if (s_help[root] == 0u) {   // no primitive nearer than the light
                 has = false;
                 report_lit();
             } else {
                 waiting = true;   // the tail block above decides once the helpers are done
             }
         }
-#else
-        if (blocked) {
-            has = false;
-            Q.n_lit[qo][i] = 0;
-        } else if (pop) {
-            if (sp > 0) {
-                sp--;
-                ref = stack.get(sp);
-            } else if (!tri && tri_reach(S, o, invd, tmax)) {
-                tri = true;
-                ref = 0;
-            } else {   // no primitive nearer than the light: lit (a phantom light never is)
-                has = false;
-                report_lit();
-            }
-        }
-#endif
     }
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
@@ -1581,11 +1279,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
 }
 template <bool COUNT, bool SPLIT = false>
 __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
-    shadow_lanes<COUNT, false, SPLIT>(S, Q, qo, counters);
-}
-template <bool COUNT>
-__global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_FULL_LANES_VGPRS))) void k_wf_shadow_lanes_full(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
-    shadow_lanes<COUNT, true>(S, Q, qo, counters);
+    shadow_lanes<COUNT, SPLIT>(S, Q, qo, counters);
 }
 
 // ---------------------------------------------------------------- direct-light terms
@@ -1594,18 +1288,9 @@ __global__ __launch_bounds__(kTB, PT_FULL_LANES_WAVES) __attribute__((amdgpu_num
 // (a pixel's rays sit in runs of consecutive slots, so fix_add_wave sums most of them in
 // registers).  Keeping the accumulation out of the traversal kernels keeps their refill path
 // and registers lean.  Group g takes partition g (written on its XCD by k_wf_shade).
-#ifndef PT_ACCUM_LDS
-#define PT_ACCUM_LDS 1   // k_wf_nee_accum sums a window's runs per pixel in LDS before the atomics
-#endif
-#ifndef PT_ACC_WIN
-#define PT_ACC_WIN 16
-#endif
-constexpr uint32_t kAccWin = PT_ACC_WIN;       // 256-slot rows per block window (one shade block's child-major region
-                                       // of FirstHitSamples 16 children)
-#ifndef PT_ACC_TABLE
-#define PT_ACC_TABLE 512
-#endif
-constexpr uint32_t kAccTable = PT_ACC_TABLE;   // LDS table entries (a power of two)
+constexpr uint32_t kAccWin = 16;      // 256-slot rows per block window (one shade block's child-major region
+                                      // of FirstHitSamples 16 children)
+constexpr uint32_t kAccTable = 512;   // LDS table entries (a power of two)
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsigned long long* counters) {
     const Group G = xcd_group();
@@ -1630,7 +1315,6 @@ __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsign
         const uint32_t r = fix_add_wave(Q.acc, pixel, lit, w01.x, w01.y, w2.x, T);
         if (COUNT) { runs += r; lit_n += (uint32_t)__popcll(__ballot(lit)); }
     };
-#if PT_ACCUM_LDS
     // A pixel's light terms of one depth sit in runs of consecutive slots, one run per child index
     // of its vertex (the child-major fill): a block takes windows of kAccWin·256 slots, sums the
     // wave runs of a window per pixel in LDS and flushes one atomic set per pixel (for
@@ -1658,10 +1342,6 @@ __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsign
         }
         __syncthreads();
     }
-#else
-    const uint32_t wave = G.lb * 4u + (threadIdx.x >> 6), nwaves = G.nb * 4u;
-    for (uint32_t j0 = wave * 64u; j0 < n; j0 += nwaves * 64u) row(j0 + lane, nullptr);   // wave-uniform
-#endif
     if (COUNT && lane == 0) {
         atomicAdd(&counters[7], (unsigned long long)lit_n);
         atomicAdd(&counters[8], (unsigned long long)runs);
@@ -1789,17 +1469,15 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     const bool full = S.full != 0;        // shade: textures or row-4 shapes
     const bool fullg = S.full_geom != 0;  // traversal: row-4 shapes only
     // Per-lane refill traversal (k_wf_trace_lanes, k_wf_shadow_lanes) where rays are long
-    // enough to pay for it: scenes with a triangle BVH of more than kLanesMinNodes nodes
-    // (gopher3's five analytic shapes: trace 16.0 → 23.5 ms with refill).
-    const bool lanes = plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes && (PT_FULL_LANES || !fullg);
-    const bool lanes_sh = plan.lanes >= 0 ? plan.lanes == 1
-                                          : S.tri_num_nodes > kLanesMinNodes && (PT_FULL_LANES_SHADOW || !fullg);
+    // enough to pay for it: lean scenes with a triangle BVH of more than kLanesMinNodes nodes.
+    const bool lanes = !fullg && (plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes);
     // Split traversal (row-4 scenes with a triangle BVH): the lean refill kernels take the planes and
     // the triangles at their occupancy, then the FULL lockstep kernels add the analytic BVH (where
-    // the §8f row-4 shapes live) from that result (pt_device.h trace_ana / ana_blocked).  Shadow rays
-    // split only when every light's own t is a lean intersect (spheres, cubes, planes).
-    const bool split = PT_SPLIT && plan.lanes < 0 && fullg && !PT_FULL_LANES && S.tri_num_nodes > kLanesMinNodes;
-    const bool split_sh = split && !PT_FULL_LANES_SHADOW && S.lights_lean;
+    // the §8f row-4 shapes live) from that result (pt_device.h trace_ana / ana_blocked; routed:
+    // trace_heavy / heavy_blocked for the rays that reach a heavy box).  Shadow rays split only when
+    // every light's own t is a lean intersect (spheres, cubes, planes).
+    const bool split = plan.lanes < 0 && fullg && S.tri_num_nodes > kLanesMinNodes;
+    const bool split_sh = split && S.lights_lean;
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
         begin_k(1, stream);
@@ -1814,21 +1492,16 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
-            if (PT_SDF_QUEUE && S.num_sdf > 0)
+            if (S.num_sdf > 0)
                 hipLaunchKernelGGL(k_wf_sdf_hits, dim3(grid_for(n, 256, 8192)), dim3(256), 0, stream, S, Q, qi);
             end_k(1, stream);
             return;
         }
-        const unsigned tg = grid_for(n, kTB, fullg ? (lanes ? plan.full_lanes_trace_blocks : plan.full_trace_blocks)
-                                                  : lanes ? plan.lanes_trace_blocks : plan.trace_blocks);
-        if (fullg && lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes_full<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-        else if (fullg && lanes) hipLaunchKernelGGL((k_wf_trace_lanes_full<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-        else if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        const unsigned tg = grid_for(n, kTB, fullg ? plan.full_trace_blocks : lanes ? plan.lanes_trace_blocks : plan.trace_blocks);
+        if (count && fullg) hipLaunchKernelGGL((k_wf_trace<true, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-#ifndef PT_NO_TRACE_LANES
         else if (lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (lanes) hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
-#endif
         else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         end_k(1, stream);
@@ -1868,13 +1541,12 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
         }
         const uint64_t children = bound * (uint64_t)(depth == 0 ? plan.root_children : plan.children);
         const unsigned hg = grid_for(children * plan.lights_per_child, kTB,
-                                     fullg ? (lanes_sh ? plan.full_lanes_shadow_blocks : plan.full_shadow_blocks)
-                                           : lanes_sh ? plan.lanes_shadow_blocks : plan.shadow_blocks);
+                                     fullg ? plan.full_shadow_blocks : lanes ? plan.lanes_shadow_blocks : plan.shadow_blocks);
         begin_k(3, side);
         if (split_sh) {
             const unsigned hl = grid_for(children * plan.lights_per_child, kTB, plan.lanes_shadow_blocks);
             const unsigned ha = grid_for(children * plan.lights_per_child, kTB, plan.full_shadow_blocks);
-            const bool sq = PT_SDF_QUEUE_SHADOW && S.num_sdf > 0;
+            const bool sq = S.num_sdf > 0;
             if (sq) {
                 const hipError_t e = hipMemsetAsync(Q.counts + kSdfShWord, 0, sizeof(uint32_t), side);
                 if (e != hipSuccess) return e;
@@ -1893,20 +1565,15 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
             if (sq)
                 hipLaunchKernelGGL(k_wf_sdf_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256), 0,
                                    side, S, Q, 1 - qi);
-        } else if (fullg && lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes_full<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-        else if (fullg && lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes_full<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-        else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        } else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-#ifndef PT_NO_SHADOW_LANES
-        else if (lanes_sh && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-        else if (lanes_sh) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
-#endif
+        else if (lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (lanes) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         end_k(3, side);
         begin_k(6, side);   // PT_K_ACCUM
-        const unsigned ag = PT_ACCUM_LDS ? grid_for(children * plan.lights_per_child, 256u * kAccWin, 4096)
-                                         : grid_for(children * plan.lights_per_child, 256, 8192);
+        const unsigned ag = grid_for(children * plan.lights_per_child, 256u * kAccWin, 4096);
         if (count) hipLaunchKernelGGL((k_wf_nee_accum<true>), dim3(ag), dim3(256), 0, side, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_nee_accum<false>), dim3(ag), dim3(256), 0, side, Q, 1 - qi, B.counters);
         end_k(6, side);
@@ -1953,11 +1620,6 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     return hipGetLastError();
 }
 
-#ifndef PT_EXTRA_CHUNK
-// camera samples per chunk of the extra phases (0: the pass' chunk); their per-sample accumulators
-// (48 B each) are the light terms' atomic targets
-#define PT_EXTRA_CHUNK 0
-#endif
 hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                            const DevBuffer& B, const WfQueues& Q, const WfPlan& plan, bool count, hipStream_t stream,
                            LaunchTimer* timer, int firefly, int32_t K, uint32_t sample_base, uint64_t entries,
@@ -1967,9 +1629,8 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
     auto end_k = [&](int cls) { if (timer) timer->end(cls, stream); };
     WfQueues Qx = Q;
     Qx.acc = Q.acc_s;  // per-sample accumulators
-    uint64_t chunk = plan.chunk;
-    if (PT_EXTRA_CHUNK > 0 && chunk > (uint64_t)PT_EXTRA_CHUNK) chunk = (uint64_t)PT_EXTRA_CHUNK;
-    uint64_t per_chunk = chunk / (uint64_t)K;  // entries per chunk (whole pixels)
+    // entries per chunk (whole pixels; smaller extra-phase chunks measured slower)
+    uint64_t per_chunk = plan.chunk / (uint64_t)K;
     if (per_chunk < 1) per_chunk = 1;
     for (uint64_t e0 = 0; e0 < entries; e0 += per_chunk) {
         const uint64_t ne = (entries - e0) < per_chunk ? (entries - e0) : per_chunk;
@@ -2009,10 +1670,6 @@ hipError_t wavefront_grids(WfPlan& plan) {
     if (e == hipSuccess) plan.lanes_trace_blocks = resident(nb, kWfMaxBlocks);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow_lanes<false>, kTB, 0);
     if (e == hipSuccess) plan.lanes_shadow_blocks = resident(nb, kWfMaxBlocks);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace_lanes_full<false>, kTB, 0);
-    if (e == hipSuccess) plan.full_lanes_trace_blocks = resident(nb, kWfMaxBlocks);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow_lanes_full<false>, kTB, 0);
-    if (e == hipSuccess) plan.full_lanes_shadow_blocks = resident(nb, kWfMaxBlocks);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace<false, true>, kTB, 0);
     if (e == hipSuccess) plan.full_trace_blocks = resident(nb, kWfMaxBlocks);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false, true>, kTB, 0);

@@ -1,5 +1,6 @@
-// Host check of the Volume march skip (ptsharp_amd/csrc/pt_ext.h vol_run / vol_skip / t_after):
-// vol_t, which passes runs of uniform cells at once, against the reference loop of
+// Host check of the Volume marches (ptsharp_amd/csrc/pt_ext.h vol_t / vol_build_runs / t_after):
+// vol_t (the per-lane march) and the cooperative march with its strided pass over runs of uniform
+// cells (emulated lane by lane) against the reference loop of
 // Volume.Intersect (Volume.cs:168-197) restated here position by position, on seeded volumes
 // (smooth blobs with noise and exact-zero regions, the reference's narrow windows, Sample's
 // y-from-z slip) and seeded rays, bit for bit; and t_after against k repeated additions.
@@ -41,7 +42,7 @@ static double naive_t(const DevVolume& v, v3 o, v3 d) {
     return kHitInf;
 }
 
-// pt_device.h coop_vol_t with its strided pass over uniform runs (PT_VOL_STRIDE) and the table
+// pt_device.h coop_vol_t with its strided pass over uniform runs (kVolStride) and the table
 // Sign (vol_sign_fast), its 64 lanes as loops: lane r of a round takes the r-th position.
 static int sign_fast(const DevVolume& v, v3 o, v3 d, double t) {
     const int s = vol_key_sign(v, vol_key(v, o, d, t));
@@ -204,7 +205,7 @@ int main(int argc, char** argv) {
                 if (!(dir.x == dir.x)) continue;
                 uint32_t n = 0;
                 const auto c0 = std::chrono::steady_clock::now();
-                const double a = vol_t(v, o, dir, &n, PT_VOL_SKIP != 0);
+                const double a = vol_t(v, o, dir, &n);
                 const auto c1 = std::chrono::steady_clock::now();
                 const double b = naive_t(v, o, dir);
                 const auto c2 = std::chrono::steady_clock::now();
@@ -221,7 +222,7 @@ int main(int argc, char** argv) {
                 hits += b < kHitInf;
                 if (a != b && !(a != a && b != b)) {
                     if (vbad < 5)
-                        printf("vol %d ray %d: skip %.17g naive %.17g  o=(%a,%a,%a) d=(%a,%a,%a)\n", vi, i, a, b, o.x, o.y, o.z,
+                        printf("vol %d ray %d: vol_t %.17g naive %.17g  o=(%a,%a,%a) d=(%a,%a,%a)\n", vi, i, a, b, o.x, o.y, o.z,
                                dir.x, dir.y, dir.z);
                     vbad++;
                 }

@@ -1,9 +1,9 @@
-"""The Volume march skip (ptsharp_amd/csrc/pt_ext.h vol_run / vol_skip / t_after), host build:
-vol_t, which passes runs of uniform cells at once, equals Volume.Intersect's loop as written
+"""The Volume marches (ptsharp_amd/csrc/pt_ext.h vol_t / vol_build_runs / t_after), host build:
+vol_t, the per-lane march, equals Volume.Intersect's loop as written
 (Volume.cs:168-197, restated position by position in tests/native/vol_skip_check.cpp) bit for bit
 on seeded volumes and rays, including grazing rays and rays along lattice planes; t_after equals
 k repeated fp64 additions across binade crossings; and the GPU's cooperative march with its strided
-pass over uniform runs (pt_device.h coop_vol_t, PT_VOL_STRIDE; its 64 lanes emulated as loops) gives
+pass over uniform runs (pt_device.h coop_vol_t, kVolStride; its 64 lanes emulated as loops) gives
 the same t as the loop as written, at strides 8, 16 and 32."""
 import os
 import subprocess
