@@ -22,8 +22,8 @@ struct WfQueues {
     double2* q_t[2];     // {throughput.r, throughput.g} (fp64, as the reference's Colour)
     ulonglong2* q_k[2];  // {RNG node key of the vertex the ray leads to, throughput.b (fp64 bits)}
     uint4* hits;         // {t (fp64 bits), kind, record}
-    uint4* sdfq;         // split closest hit, PT_SDF_QUEUE: {slot, SDF record, best world t (fp64 bits)} (k_wf_sdf_hits)
-    uint4* sdfq_sh;      // split shadow rays, PT_SDF_QUEUE: {slot, SDF record, the light's t (fp64 bits)} (k_wf_sdf_shadow)
+    uint4* sdfq;         // split closest hit: {slot, SDF record, best world t (fp64 bits)} (k_wf_sdf_hits)
+    uint4* sdfq_sh;      // split shadow rays: {slot, SDF record, the light's t (fp64 bits)} (k_wf_sdf_shadow)
     // Routed split (DevScene::route): the slots of the rays whose segment reaches a §8f row-4 shape's box,
     // per partition (pcap / spcap entries each): only these go through the FULL analytic half
     uint32_t* hq;        // closest-hit rays (k_wf_trace_lanes → k_wf_trace<.., SPLIT>)
@@ -50,7 +50,12 @@ struct WfQueues {
     uint32_t* ovf;       // closest-hit traversal stack entries beyond kLdsStack: [kStackMax - kLdsStack][kWfMaxThreads]
     uint32_t* ovf_sh;    // the same for the shadow kernels, which may run beside a closest-hit kernel (side stream)
     FixAcc acc_s;        // [chunk] per-sample accumulators of the adaptive / firefly phases
+    // Origin-region deal (WfPlan::deal): vertices at depth >= 1 on the triangle mesh send their children to
+    // the partition of their triangle's region, so each XCD's L2 holds one eighth of the mesh's BVH lines
+    unsigned long long* region_hist;   // [kRegionBins] such vertices per bin of BVH-order triangle index, all passes
+    uint32_t* region_bounds;           // [kParts] first triangle of region r (r >= 1; k_wf_region_bounds)
 };
+constexpr int kRegionBins = 256;
 
 // Every counter sits on a line of its own: returning atomics execute at the memory side,
 // one line at a time, so cursors packed into one 128-B line serialise every partition's
@@ -110,6 +115,7 @@ struct WfPlan {
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
     int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always
                                // (PT_LANES=0|1 in the environment; tests)
+    int32_t deal;              // origin-region deal of depth >= 1 children (WfQueues::region_hist)
     // Optional second stream: each depth's shadow pass runs there, beside the next depth's
     // closest-hit pass (independent queues), so one fills the other's ramp and tail.
     // ev_main orders shade(d) → shadow(d); ev_side[q], recorded after the light terms of

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../ptsharp_amd/csrc/pt_bvh.h"
@@ -68,6 +69,7 @@ struct Tracer {
     v3 tv3(uint32_t p) const { uint32_t s = T.order[p]; return v3{m.v3[3 * s], m.v3[3 * s + 1], m.v3[3 * s + 2]}; }
 
     // closest hit (any = false) or any hit before tlim (any = true); ordered BVH4 traversal, near child first
+    std::vector<uint32_t>* lines = nullptr;   // (cache study) the 128-B lines a traversal touches, in order
     double trace(v3 o, v3 d, bool any, double tlim, Count& c, int32_t& prim) const {
         c.rays++;
         const v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
@@ -78,6 +80,7 @@ struct Tracer {
         int sp = 0;
         uint32_t ref = 0;
         for (;;) {
+            if (lines) lines->push_back(ref & 0x80000000u ? (uint32_t)T.nodes + (ref & 0x1FFFFFFFu) : ref);
             if (!(ref & 0x80000000u)) {
                 c.nodes++;
                 const float* w = reinterpret_cast<const float*>(&T.words[(size_t)ref * kNode4Words]);
@@ -187,6 +190,75 @@ static void build(const Mesh& m, const std::string& variant, Tree& T, double& bu
         }
 }
 
+// L2 study: rays leaving random points of the mesh (cosine bounces about the outward face normal,
+// the deep rays of the C4 frame), their traversal lines fed through 8 LRU caches of 4 MB (32768
+// 128-B lines, one per XCD), with the rays dealt to the caches round-robin (the kernels today) or by
+// the region of the mesh their origin lies in (the origin triangle's position in BVH order, in 8
+// contiguous ranges).  Reports the hit rate of each deal.
+struct Lru {
+    size_t cap;
+    std::vector<uint32_t> key;                 // slot -> line
+    std::vector<int> prev, next;
+    std::unordered_map<uint32_t, int> where;
+    int head = -1, tail = -1, used = 0;
+    explicit Lru(size_t c) : cap(c), key(c), prev(c, -1), next(c, -1) { where.reserve(c * 2); }
+    void unlink(int s) {
+        if (prev[s] >= 0) next[prev[s]] = next[s]; else head = next[s];
+        if (next[s] >= 0) prev[next[s]] = prev[s]; else tail = prev[s];
+    }
+    void front(int s) { prev[s] = -1; next[s] = head; if (head >= 0) prev[head] = s; head = s; if (tail < 0) tail = s; }
+    bool access(uint32_t line) {
+        auto it = where.find(line);
+        if (it != where.end()) { unlink(it->second); front(it->second); return true; }
+        int s;
+        if ((size_t)used < cap) s = used++;
+        else { s = tail; unlink(s); where.erase(key[s]); }
+        key[s] = line; where[line] = s; front(s);
+        return false;
+    }
+};
+static void cache_study(const Mesh& m, const Tree& T, long nrays) {
+    Tracer tr{m, T};
+    std::vector<uint32_t> pos_of(m.n);
+    for (size_t p = 0; p < T.order.size(); p++) pos_of[T.order[p]] = (uint32_t)p;
+    double cx = 0, cy = 0, cz = 0;
+    for (int i = 0; i < m.n; i++) { cx += m.v1[3 * i]; cy += m.v1[3 * i + 1]; cz += m.v1[3 * i + 2]; }
+    cx /= m.n; cy /= m.n; cz /= m.n;
+    std::mt19937_64 rng(777);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    std::vector<Lru> rr, reg;
+    for (int k = 0; k < 8; k++) { rr.emplace_back(32768); reg.emplace_back(32768); }
+    long acc = 0, hit_rr = 0, hit_reg = 0;
+    Count c;
+    std::vector<uint32_t> lines;
+    for (long r = 0; r < nrays; r++) {
+        const int tri = (int)(U(rng) * m.n) % m.n;
+        const v3 a{m.v1[3 * tri], m.v1[3 * tri + 1], m.v1[3 * tri + 2]}, b{m.v2[3 * tri], m.v2[3 * tri + 1], m.v2[3 * tri + 2]};
+        const v3 cc{m.v3[3 * tri], m.v3[3 * tri + 1], m.v3[3 * tri + 2]};
+        double u = U(rng), v = U(rng);
+        if (u + v > 1) { u = 1 - u; v = 1 - v; }
+        const v3 p = add(add(a, muls(sub(b, a), u)), muls(sub(cc, a), v));
+        v3 nrm = normalize(cross(sub(b, a), sub(cc, a)));
+        if ((p.x - cx) * nrm.x + (p.y - cy) * nrm.y + (p.z - cz) * nrm.z < 0) nrm = neg(nrm);
+        const double r1 = U(rng) * 2 * kPi, r2 = U(rng), r2s = std::sqrt(r2);
+        const v3 ax = std::fabs(nrm.x) > 0.1f ? v3{0.f, 1.f, 0.f} : v3{1.f, 0.f, 0.f};
+        const v3 e1 = normalize(cross(ax, nrm)), e2 = cross(nrm, e1);
+        const v3 d = normalize(add(add(muls(e1, std::cos(r1) * r2s), muls(e2, std::sin(r1) * r2s)), muls(nrm, std::sqrt(1 - r2))));
+        lines.clear();
+        tr.lines = &lines;
+        int32_t prim;
+        tr.trace(p, d, false, 0, c, prim);
+        const int xr = (int)(r % 8), xg = (int)((uint64_t)pos_of[tri] * 8 / (uint64_t)m.n);
+        for (uint32_t l : lines) {
+            acc++;
+            hit_rr += rr[xr].access(l);
+            hit_reg += reg[xg].access(l);
+        }
+    }
+    std::printf("cache study: %ld surface rays, %.2f lines/ray; L2 (8 x 4 MB LRU) hit rate: round-robin deal %.3f, "
+                "deal by origin region %.3f\n", nrays, (double)acc / nrays, (double)hit_rr / acc, (double)hit_reg / acc);
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: %s MESH.bin [stride] [variant ...]\n", argv[0]); return 2; }
     Mesh m;
@@ -201,8 +273,12 @@ int main(int argc, char** argv) {
         Tree T;
         double bs = 0;
         build(m, var, T, bs);
+        if (const char* cs = std::getenv("CACHE_RAYS")) { cache_study(m, T, std::atol(cs)); continue; }
         Tracer tr{m, T};
         Count cd[kDepth + 1], csh;
+        std::vector<uint32_t> pos_of(m.n);
+        for (size_t q = 0; q < T.order.size(); q++) pos_of[T.order[q]] = (uint32_t)q;
+        long region[kDepth + 1][8] = {{0}};   // mesh hits per origin region (8 ranges of BVH order), by depth
         std::mt19937_64 rng(12345);
         std::uniform_real_distribution<double> U(0.0, 1.0);
         const v3 cp{m.cam_p[0], m.cam_p[1], m.cam_p[2]}, cu{m.cam_u[0], m.cam_u[1], m.cam_u[2]};
@@ -226,6 +302,7 @@ int main(int argc, char** argv) {
                     const v3 p = add(o, muls(d, t));
                     if (prim == -2) nrm = v3{0.f, 1.f, 0.f};
                     else {
+                        region[depth][(uint64_t)prim * 8 / (uint64_t)m.n]++;
                         const v3 a = tr.tv1((uint32_t)prim);
                         nrm = normalize(cross(sub(tr.tv2((uint32_t)prim), a), sub(tr.tv3((uint32_t)prim), a)));
                         if (dotf(nrm, d) > 0) nrm = neg(nrm);
@@ -262,6 +339,13 @@ int main(int argc, char** argv) {
             row(nm, cd[k]);
         }
         row("shadow", csh);
+        for (int k = 0; k <= kDepth; k++) {
+            long t = 0;
+            for (int g = 0; g < 8; g++) t += region[k][g];
+            std::printf("  mesh hits of depth %d by region:", k);
+            for (int g = 0; g < 8; g++) std::printf(" %.3f", t ? (double)region[k][g] / t : 0.0);
+            std::printf("\n");
+        }
         std::fflush(stdout);
     }
     return 0;
