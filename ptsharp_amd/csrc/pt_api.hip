@@ -1278,7 +1278,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     plan.lanes = -1;
     if (const char* f = std::getenv("PT_LANES")) plan.lanes = !std::strcmp(f, "0") ? 0 : !std::strcmp(f, "1") ? 1 : -1;
     plan.deal = PT_REGION_DEAL;
-    if (const char* f = std::getenv("PT_DEAL")) plan.deal = std::atoi(f) != 0;
+    if (const char* f = std::getenv("PT_DEAL")) plan.deal = std::atoi(f);   // 2: every region 0 (tests)
     plan.root_children = (uint32_t)std::max(1, n_root * n_root * nm_root);
     plan.children = (uint32_t)nm;
     plan.lights_per_child = (uint32_t)(sampler->light_mode == PT_LIGHT_ALL ? std::max(1, c->S.num_lights) : 1);

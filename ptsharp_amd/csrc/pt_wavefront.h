@@ -115,7 +115,8 @@ struct WfPlan {
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
     int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always
                                // (PT_LANES=0|1 in the environment; tests)
-    int32_t deal;              // origin-region deal of depth >= 1 children (WfQueues::region_hist)
+    int32_t deal;              // origin-region deal of depth >= 1 children (WfQueues::region_hist); 2: every
+                               // triangle in region 0 (tests: the full-partition fallback)
     // Optional second stream: each depth's shadow pass runs there, beside the next depth's
     // closest-hit pass (independent queues), so one fills the other's ramp and tail.
     // ev_main orders shade(d) → shadow(d); ev_side[q], recorded after the light terms of

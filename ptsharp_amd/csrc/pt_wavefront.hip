@@ -177,25 +177,60 @@ __device__ __forceinline__ void block_reserve2(unsigned long long* word, uint32_
 }
 
 // The origin-region deal's reservation (WfPlan::deal): lane slots in the partition `tgt` of each lane,
-// one returning atomic per target partition the block sends to.  Block-uniform call sites only.
-__device__ __forceinline__ void block_reserve_deal(const WfQueues& Q, int qo, int tgt, uint32_t a, uint32_t b,
+// one returning atomic per target partition the block sends to.  A target without room for the block's
+// share (a full partition) takes none of it: the lanes mark the slots they got below the cap dead (the
+// traversal kernels skip them) and try the next partition, up to every partition once; the queues then
+// hold every child as long as all of them fit in all partitions less one block's share each (k_wf_shade
+// checks that before it deals).  Block-uniform call sites only.
+__device__ __forceinline__ void block_reserve_deal(const WfQueues& Q, int qo, int& tgt, uint32_t a, uint32_t b,
                                                    uint32_t& abase, uint32_t& bbase) {
     __shared__ uint32_t s_n[kParts][2];
     __shared__ uint32_t s_at[kParts][2];
-    if (threadIdx.x < 2 * kParts) s_n[threadIdx.x >> 1][threadIdx.x & 1] = 0u;
-    __syncthreads();
-    const uint32_t oa = a ? atomicAdd(&s_n[tgt][0], a) : 0u, ob = b ? atomicAdd(&s_n[tgt][1], b) : 0u;
-    __syncthreads();
-    if (threadIdx.x < kParts) {
-        const uint32_t ta = s_n[threadIdx.x][0], tb = s_n[threadIdx.x][1];
-        unsigned long long base = 0;
-        if (ta | tb) base = atomicAdd(pair_word(Q, qo, (int)threadIdx.x), ((unsigned long long)tb << 32) | ta);
-        s_at[threadIdx.x][0] = (uint32_t)base;
-        s_at[threadIdx.x][1] = (uint32_t)(base >> 32);
+    __shared__ uint32_t s_ok;
+    bool placed = false;
+    for (int attempt = 0;; attempt++) {
+        __syncthreads();   // the last attempt's reads of s_at are done
+        if (threadIdx.x < 2 * kParts) s_n[threadIdx.x >> 1][threadIdx.x & 1] = 0u;
+        __syncthreads();
+        uint32_t oa = 0, ob = 0;
+        if (!placed) {
+            if (a) oa = atomicAdd(&s_n[tgt][0], a);
+            if (b) ob = atomicAdd(&s_n[tgt][1], b);
+        }
+        __syncthreads();
+        if (threadIdx.x < kParts) {
+            const uint32_t ta = s_n[threadIdx.x][0], tb = s_n[threadIdx.x][1];
+            unsigned long long base = 0;
+            if (ta | tb) base = atomicAdd(pair_word(Q, qo, (int)threadIdx.x), ((unsigned long long)tb << 32) | ta);
+            s_at[threadIdx.x][0] = (uint32_t)base;
+            s_at[threadIdx.x][1] = (uint32_t)(base >> 32);
+            const bool fits = (uint64_t)(uint32_t)base + ta <= Q.pcap && (uint64_t)(uint32_t)(base >> 32) + tb <= Q.spcap;
+            const uint64_t bad = __ballot(!fits) & ((1ull << kParts) - 1ull);
+            if (threadIdx.x == 0) s_ok = bad ? (uint32_t)bad : 0u;   // bit t: partition t had no room
+        }
+        __syncthreads();
+        const uint32_t bad = s_ok;
+        if (!placed) {
+            abase = s_at[tgt][0] + oa;
+            bbase = s_at[tgt][1] + ob;
+            if ((bad >> tgt) & 1u) {   // no room in tgt: mark the slots below the cap dead, try the next partition
+                for (uint32_t k = 0; k < a; k++)
+                    if (abase + k < Q.pcap)
+                        Q.q_d[qo][(size_t)tgt * Q.pcap + abase + k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(kDead));
+                for (uint32_t k = 0; k < b; k++)
+                    if (bbase + k < Q.spcap)
+                        Q.n_n[qo][(size_t)tgt * Q.spcap + bbase + k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(kDead));
+                tgt = (tgt + 1) % kParts;
+            } else {
+                placed = true;
+            }
+        }
+        if (!bad) break;   // block-uniform
+        if (attempt == kParts - 1) {   // every partition full: the queues overflowed
+            if (!placed) { abase = Q.pcap; bbase = Q.spcap; *Q.overflow = 1ull; }
+            break;
+        }
     }
-    __syncthreads();
-    abase = s_at[tgt][0] + oa;
-    bbase = s_at[tgt][1] + ob;
 }
 
 // Region of BVH-order triangle `idx` (WfQueues::region_bounds) and its histogram bin.
@@ -207,9 +242,14 @@ __device__ __forceinline__ int tri_region(const WfQueues& Q, uint32_t idx) {
 }
 
 // Region bounds from the histogram of the passes so far: region r starts at the bin where the
-// cumulative count reaches r/kParts of the total (equal triangle counts before any pass).
-__global__ __launch_bounds__(64) void k_wf_region_bounds(WfQueues Q, uint32_t num_tris) {
+// cumulative count reaches r/kParts of the total (equal triangle counts before any pass).  `skew`
+// (PT_DEAL=2, tests): every triangle in region 0, so partition 0 fills and block_reserve_deal falls back.
+__global__ __launch_bounds__(64) void k_wf_region_bounds(WfQueues Q, uint32_t num_tris, int skew) {
     if (threadIdx.x != 0) return;
+    if (skew) {
+        for (int r = 0; r < kParts; r++) Q.region_bounds[r] = r ? num_tris : 0u;
+        return;
+    }
     unsigned long long total = 0;
     for (int b = 0; b < kRegionBins; b++) total += Q.region_hist[b];
     Q.region_bounds[0] = 0u;
@@ -775,7 +815,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     }
     fix_add_wave(Q.acc, pixel, has_c, cc[0], cc[1], cc[2]);
     int tgt = (int)G.g;   // the partition this vertex' children go to
-    if (DEAL && alive && h.kind == KIND_TRI) {
+    if (DEAL && s_hist && alive && h.kind == KIND_TRI) {
         const uint32_t tri = (uint32_t)h.idx;
         atomicAdd(&s_hist[(uint32_t)(((uint64_t)tri * kRegionBins) / (uint32_t)S.num_tris)], 1u);
         tgt = tri_region(Q, tri);
@@ -933,9 +973,16 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     Counters ctr{0, 0, 0, 0};
     __shared__ uint32_t s_k0;
     __shared__ uint32_t s_hist[kRegionBins];   // the origin-region deal's histogram of this block's vertices
+    // deal only while every child of this depth fits the queues less one block's share per partition (the
+    // room block_reserve_deal's full-partition fallback may leave unused): at most `fan` children per vertex
+    uint32_t* deal_hist = nullptr;
     if (DEAL) {
         for (int b = threadIdx.x; b < kRegionBins; b += 256) s_hist[b] = 0u;
         __syncthreads();
+        const uint64_t fan = smp.spec_mode == 2 ? 2u : 1u;
+        const uint64_t fan_n = fan * (smp.light_mode == 1 ? (uint64_t)S.num_lights : 1u);
+        const uint64_t room = (uint64_t)kParts * (Q.pcap - 256u * fan), room_n = (uint64_t)kParts * (Q.spcap - 256u * fan_n);
+        if (Q.pcap > 256u * fan && Q.spcap > 256u * fan_n && kept * fan <= room && kept * fan_n <= room_n) deal_hist = s_hist;
     }
     if constexpr (!SCAN) {
         for (;;) {  // block-uniform: the block takes 256 vertices of its partition at a time
@@ -943,7 +990,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             __syncthreads();
             const uint32_t k0 = s_k0;  // thread 0 rewrites it only after block_reserve2's barriers
             if (k0 >= n) break;
-            shade_vertex<COUNT, FULL, DEAL>(S, smp, Q, qi, G, base + k0 + threadIdx.x, k0 + threadIdx.x < n, ctr, s_hist);
+            shade_vertex<COUNT, FULL, DEAL>(S, smp, Q, qi, G, base + k0 + threadIdx.x, k0 + threadIdx.x < n, ctr, deal_hist);
         }
     } else {
         const bool env_black = (!FULL || S.env_tex < 0) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
@@ -1009,7 +1056,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             for (uint32_t r = 0; r < full; r += 256u) {   // block-uniform
                 const bool listed = r + threadIdx.x < full;
                 shade_vertex<COUNT, FULL, DEAL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed,
-                                                ctr, s_hist, &s_hit[r + threadIdx.x]);
+                                                ctr, deal_hist, &s_hit[r + threadIdx.x]);
                 __syncthreads();   // the next round rewrites shade_vertex's LDS child counts
             }
             if (last) break;
@@ -1585,7 +1632,8 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     // XCD traces rays that start in one eighth of the mesh (tools/bvh_quality.cpp cache study: C4's
     // surface rays hit the 8 x 4 MB L2s 58 % of the time dealt round-robin, 82 % dealt by region)
     const bool deal_on = plan.deal && lanes && S.num_tris > 0;
-    if (deal_on) hipLaunchKernelGGL(k_wf_region_bounds, dim3(1), dim3(64), 0, stream, Q, (uint32_t)S.num_tris);
+    if (deal_on)
+        hipLaunchKernelGGL(k_wf_region_bounds, dim3(1), dim3(64), 0, stream, Q, (uint32_t)S.num_tris, plan.deal == 2 ? 1 : 0);
     int qi = 0;
     trace(qi, bound);
     for (int depth = 0; depth <= smp.mb; depth++) {
