@@ -251,8 +251,8 @@ __device__ __forceinline__ int tri_region(const WfQueues& Q, uint32_t idx) {
 // (PT_DEAL=2, tests): every triangle in region 0, so partition 0 fills and block_reserve_deal falls back.
 __global__ __launch_bounds__(64) void k_wf_region_bounds(WfQueues Q, uint32_t num_tris, int skew) {
     if (threadIdx.x != 0) return;
-    if (skew) {
-        for (int r = 0; r < kParts; r++) Q.region_bounds[r] = r ? num_tris : 0u;
+    if (skew) {   // 1: every triangle in region 0; 2 (PT_DEAL=3, A/B): each vertex' own partition (marker word)
+        for (int r = 0; r < kParts; r++) Q.region_bounds[r] = r ? num_tris : skew == 2 ? 0xFFFFFFFFu : 0u;
         return;
     }
     unsigned long long total = 0;
@@ -649,7 +649,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                 }
             }
         }
-        if (!more && __ballot(has) == 0ull) break;
+        if (!more && __ballot(has || hpend) == 0ull) break;   // (a ray finished at refill may wait for the append)
         if (!has) continue;
         // one step: inner node or leaf of the current BVH, one 128-B line of seven 16-B pieces, by a
         // 32-bit offset into the one allocation of all traversal lines (no per-BVH 64-bit base: the
@@ -823,7 +823,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     if (DEAL && s_hist && alive && h.kind == KIND_TRI) {
         const uint32_t tri = (uint32_t)h.idx;
         atomicAdd(&s_hist[(uint32_t)(((uint64_t)tri * kRegionBins) / (uint32_t)S.num_tris)], 1u);
-        tgt = tri_region(Q, tri);
+        tgt = Q.region_bounds[0] ? (int)G.g : tri_region(Q, tri);
     }
     const DevMaterial& m = S.mats[mat];
     const int ma = nm == 2 ? 1 : 0;
@@ -1288,7 +1288,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                 }
             }
         }
-        if (!more && __ballot(has) == 0ull) break;
+        if (!more && __ballot(has || hpend) == 0ull) break;   // (a ray finished at refill may wait for the append)
         if (!COUNT && !more) {   // wave-uniform: the tail (not in the counting pass: its node counts stay sequential)
             if (has) {
                 const uint32_t st = s_help[root];
@@ -1652,7 +1652,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     // surface rays hit the 8 x 4 MB L2s 58 % of the time dealt round-robin, 82 % dealt by region)
     const bool deal_on = plan.deal && lanes && S.num_tris > 0;
     if (deal_on)
-        hipLaunchKernelGGL(k_wf_region_bounds, dim3(1), dim3(64), 0, stream, Q, (uint32_t)S.num_tris, plan.deal == 2 ? 1 : 0);
+        hipLaunchKernelGGL(k_wf_region_bounds, dim3(1), dim3(64), 0, stream, Q, (uint32_t)S.num_tris, plan.deal == 2 ? 1 : plan.deal == 3 ? 2 : 0);
     int qi = 0;
     trace(qi, bound);
     for (int depth = 0; depth <= smp.mb; depth++) {
