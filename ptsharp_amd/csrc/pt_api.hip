@@ -272,9 +272,9 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     if (want_heavy && (rc = wf_alloc(c, &Q.hq, cap))) return rc;
     if (want_heavy && (rc = wf_alloc(c, &Q.hq_sh, scap))) return rc;   // one shadow pass at a time uses it
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
-    if ((rc = wf_alloc(c, &Q.region_hist, pt::kRegionBins))) return rc;
-    if ((rc = wf_alloc(c, &Q.region_bounds, pt::kParts))) return rc;
-    PT_HIP(hipMemsetAsync(Q.region_hist, 0, pt::kRegionBins * sizeof(unsigned long long), c->stream));
+    if ((rc = wf_alloc(c, &Q.region_hist, pt::kDealSets * pt::kRegionBins))) return rc;
+    if ((rc = wf_alloc(c, &Q.region_bounds, pt::kDealSets * pt::kParts))) return rc;
+    PT_HIP(hipMemsetAsync(Q.region_hist, 0, pt::kDealSets * pt::kRegionBins * sizeof(unsigned long long), c->stream));
     Q.overflow = c->d_counters + pt::kOverflowCounter;
     // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
     // can run at the same time on the side stream)

@@ -52,10 +52,12 @@ struct WfQueues {
     FixAcc acc_s;        // [chunk] per-sample accumulators of the adaptive / firefly phases
     // Origin-region deal (WfPlan::deal): vertices at depth >= 1 on the triangle mesh send their children to
     // the partition of their triangle's region, so each XCD's L2 holds one eighth of the mesh's BVH lines
-    unsigned long long* region_hist;   // [kRegionBins] such vertices per bin of BVH-order triangle index, all passes
-    uint32_t* region_bounds;           // [kParts] first triangle of region r (r >= 1; k_wf_region_bounds)
+    unsigned long long* region_hist;   // [kDealSets][kRegionBins] such vertices per bin of BVH-order triangle
+                                       // index, per depth (min(depth, kDealSets - 1)), all passes
+    uint32_t* region_bounds;           // [kDealSets][kParts] first triangle of region r (k_wf_region_bounds)
 };
 constexpr int kRegionBins = 256;
+constexpr int kDealSets = 8;
 
 // Every counter sits on a line of its own: returning atomics execute at the memory side,
 // one line at a time, so cursors packed into one 128-B line serialise every partition's

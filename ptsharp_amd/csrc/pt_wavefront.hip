@@ -246,28 +246,30 @@ __device__ __forceinline__ int tri_region(const WfQueues& Q, uint32_t idx) {
     return r;
 }
 
-// Region bounds from the histogram of the passes so far: region r starts at the bin where the
+// Region bounds from the histograms of the passes so far, one set per depth (the first bounce's vertices
+// crowd the mesh's camera-facing side, deeper ones less): region r starts at the bin where the
 // cumulative count reaches r/kParts of the total (equal triangle counts before any pass).  `skew`
-// (PT_DEAL=2, tests): every triangle in region 0, so partition 0 fills and block_reserve_deal falls back.
+// (tests and A/B): 1 every triangle in region 0; 2 each vertex' own partition (a marker word).
 __global__ __launch_bounds__(64) void k_wf_region_bounds(WfQueues Q, uint32_t num_tris, int skew) {
-    if (threadIdx.x != 0) return;
-    if (skew) {   // 1: every triangle in region 0; 2 (PT_DEAL=3, A/B): each vertex' own partition (marker word)
-        for (int r = 0; r < kParts; r++) Q.region_bounds[r] = r ? num_tris : skew == 2 ? 0xFFFFFFFFu : 0u;
+    if (threadIdx.x >= (unsigned)kDealSets) return;
+    const unsigned long long* hist = Q.region_hist + threadIdx.x * kRegionBins;
+    uint32_t* bounds = Q.region_bounds + threadIdx.x * kParts;
+    if (skew) {
+        for (int r = 0; r < kParts; r++) bounds[r] = r ? num_tris : skew == 2 ? 0xFFFFFFFFu : 0u;
         return;
     }
     unsigned long long total = 0;
-    for (int b = 0; b < kRegionBins; b++) total += Q.region_hist[b];
-    Q.region_bounds[0] = 0u;
+    for (int b = 0; b < kRegionBins; b++) total += hist[b];
+    bounds[0] = 0u;
     int r = 1;
     unsigned long long run = 0;
+    const unsigned long long all = total ? total : (unsigned long long)kRegionBins;
     for (int b = 0; b < kRegionBins && r < kParts; b++) {
-        run += total ? Q.region_hist[b] : 1ull;
-        const unsigned long long all = total ? total : (unsigned long long)kRegionBins;
-        while (r < kParts && run * kParts >= all * (unsigned long long)r) {
-            Q.region_bounds[r++] = (uint32_t)(((uint64_t)(b + 1) * num_tris) / kRegionBins);
-        }
+        run += total ? hist[b] : 1ull;
+        while (r < kParts && run * kParts >= all * (unsigned long long)r)
+            bounds[r++] = (uint32_t)(((uint64_t)(b + 1) * num_tris) / kRegionBins);
     }
-    while (r < kParts) Q.region_bounds[r++] = num_tris;
+    while (r < kParts) bounds[r++] = num_tris;
 }
 
 // Throughput (fp64) rides in two 16-B fields: {r, g} and {key, b}.
@@ -1657,36 +1659,42 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     trace(qi, bound);
     for (int depth = 0; depth <= smp.mb; depth++) {
         const bool deal = deal_on && depth >= 1;   // (lean scenes only: never with `full`)
+        WfQueues Qs = Q;   // the shade's view: this depth's region histogram and bounds
+        if (deal) {
+            const int set = depth < kDealSets ? depth : kDealSets - 1;
+            Qs.region_hist += (size_t)set * kRegionBins;
+            Qs.region_bounds += (size_t)set * kParts;
+        }
         const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
         begin_k(2, stream);
         // both forms (the one the kept count selects runs, the other returns at once); a routed shade runs
         // the lean and the FULL SCAN kernels, each on its own vertices
         if (full && S.shade_route) {
             if (count) {
-                hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
-                hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
             } else {
-                hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
-                hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
             }
         } else if (count && full) {
-            hipLaunchKernelGGL((k_wf_shade<true, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
         } else if (count && deal) {
-            hipLaunchKernelGGL((k_wf_shade<true, false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<true, false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
         } else if (count) {
-            hipLaunchKernelGGL((k_wf_shade<true, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
         } else if (full) {
-            hipLaunchKernelGGL((k_wf_shade<false, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
         } else if (deal) {
-            hipLaunchKernelGGL((k_wf_shade<false, false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<false, false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
         } else {
-            hipLaunchKernelGGL((k_wf_shade<false, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
         }
         end_k(2, stream);
         if (plan.side) {
