@@ -129,11 +129,6 @@ constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera sl
 #define PT_SHADE_SCAN 8    // rows of 256 per SCAN claim: 16 best before claims carried their partial round, 8 since
                            // (C4 5836 / 5885 / 5743 for 16 / 8 / 32; the 1/8 share 5099 / 5208 / 4735)
 #endif
-#ifndef PT_SHADE_PREFETCH
-#define PT_SHADE_PREFETCH 0   // SCAN shade: pull the next round's lines toward L2 during this round
-#endif
-typedef __attribute__((address_space(1))) void* glb_ptr_t;
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr int kShadeScan = PT_SHADE_SCAN;   // 256-vertex groups a SCAN shade block claims and lists
 // The environment may be textured (non-black per direction) only where the shade kernel
 // runs its FULL instantiation; the traversal kernels see S.env_tex either way.
@@ -1013,7 +1008,6 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         // claim's partial last round, a quarter to a half of the rounds at C4's first bounce)
         __shared__ uint32_t s_list[kShadeScan * 256 + 256];
         __shared__ uint4 s_hit[kShadeScan * 256 + 256];   // their hit records (read once, by the scan)
-        __shared__ uint32_t s_pf[PT_SHADE_PREFETCH ? 256 : 1];   // the prefetches' scratch row (never read)
         uint32_t carry = 0;   // block-uniform
         // rows of 256 slots per claim: kShadeScan, fewer when the partition would not give every block a
         // claim (small chunks: one rank's share of a multi-GPU frame; 4 or 8 claims per block: no better)
@@ -1063,19 +1057,6 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             const uint32_t full = last ? total : total & ~255u;
             for (uint32_t r = 0; r < full; r += 256u) {   // block-uniform
                 const bool listed = r + threadIdx.x < full;
-                if (PT_SHADE_PREFETCH && r + 256u + threadIdx.x < full) {
-                    // the next round's queue-entry and triangle lines toward L2, while this round's loads are
-                    // in flight: LDS-DMA loads into a scratch row (no registers; nothing reads the row)
-                    const uint32_t sl = base + s_list[r + 256u + threadIdx.x];
-                    const uint4 hn = s_hit[r + 256u + threadIdx.x];
-                    const lds_ptr_t pf = (lds_ptr_t)(s_pf + wid * 64);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)&Q.q_d[qi][sl], pf, 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)&Q.q_o[qi][sl], pf, 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)&Q.q_t[qi][sl], pf, 4, 0, 0);
-                    __builtin_amdgcn_global_load_lds((glb_ptr_t)&Q.q_k[qi][sl], pf, 4, 0, 0);
-                    if ((int32_t)hn.z == KIND_TRI)
-                        __builtin_amdgcn_global_load_lds((glb_ptr_t)(S.tri_recs + (size_t)S.tri_rstride * hn.w), pf, 4, 0, 0);
-                }
                 shade_vertex<COUNT, FULL, DEAL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed,
                                                 ctr, deal_hist, &s_hit[r + threadIdx.x]);
                 __syncthreads();   // the next round rewrites shade_vertex's LDS child counts
