@@ -272,9 +272,6 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     if (want_heavy && (rc = wf_alloc(c, &Q.hq, cap))) return rc;
     if (want_heavy && (rc = wf_alloc(c, &Q.hq_sh, scap))) return rc;   // one shadow pass at a time uses it
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
-    if ((rc = wf_alloc(c, &Q.region_hist, pt::kDealSets * pt::kRegionBins))) return rc;
-    if ((rc = wf_alloc(c, &Q.region_bounds, pt::kDealSets * pt::kParts))) return rc;
-    PT_HIP(hipMemsetAsync(Q.region_hist, 0, pt::kDealSets * pt::kRegionBins * sizeof(unsigned long long), c->stream));
     Q.overflow = c->d_counters + pt::kOverflowCounter;
     // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
     // can run at the same time on the side stream)
@@ -377,9 +374,6 @@ inline void pad_box(float* lo, float* hi) {
 #endif
 #ifndef PT_SHADE_ROUTE
 #define PT_SHADE_ROUTE 1   // the routed shade (pt_scene.h shade_route); 0: every vertex of a FULL scene through the FULL shade
-#endif
-#ifndef PT_REGION_DEAL
-#define PT_REGION_DEAL 0   // the origin-region deal of depth >= 1 children (pt_wavefront.hip depth_loop); PT_DEAL=0|1 overrides
 #endif
 #ifndef PT_ROUTE
 #define PT_ROUTE 1   // the routed split traversal (pt_scene.h route); 0: every ray through the FULL analytic half
@@ -1177,7 +1171,6 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     S.full_geom = (d->num_sdf_shapes > 0 || d->num_volumes > 0 || d->num_transformed > 0) ? 1 : 0;
     S.full = (d->num_textures > 0 || S.full_geom) ? 1 : 0;
     S.tri_num_nodes = tri_num_nodes;
-    S.num_tris = (int32_t)nt;
     S.ana_num_nodes = ana_num_nodes;
     S.ana_count = (int32_t)na;
     // C4's floor cube and two light spheres: a linear test of 3 records at refill costs less than a BVH
@@ -1277,8 +1270,6 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     if (const char* f = std::getenv("PT_SHADE_FORM")) plan.shade_form = !std::strcmp(f, "direct") ? 1 : !std::strcmp(f, "scan") ? 2 : 0;
     plan.lanes = -1;
     if (const char* f = std::getenv("PT_LANES")) plan.lanes = !std::strcmp(f, "0") ? 0 : !std::strcmp(f, "1") ? 1 : -1;
-    plan.deal = PT_REGION_DEAL;
-    if (const char* f = std::getenv("PT_DEAL")) plan.deal = std::atoi(f);   // 2: every region 0 (tests)
     plan.root_children = (uint32_t)std::max(1, n_root * n_root * nm_root);
     plan.children = (uint32_t)nm;
     plan.lights_per_child = (uint32_t)(sampler->light_mode == PT_LIGHT_ALL ? std::max(1, c->S.num_lights) : 1);

@@ -54,7 +54,6 @@ struct DevScene {
     // triangle BVH (world-space mesh + directly-added triangles)
     const float4* tri_nodes;   // 2 float4 per node (pt::BvhNode)
     int32_t tri_num_nodes;
-    int32_t num_tris;          // world-mesh triangles (tri_recs entries, BVH order)
     const float4* tri_recs;    // 3 float4 per triangle: {v1.xyz,e1.x} {e1.yz,e2.xy} {e2.z,-,-,-}
     const float4* tri_chunks;  // 8 float4 per triangle leaf (pt_api.hip make_leaf_chunks)
     const float4* tri_shade;   // 3 float4 per triangle: {n1.xyz,n2.x} {n2.yz,n3.xy} {n3.z,mat,-,-}

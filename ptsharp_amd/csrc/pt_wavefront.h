@@ -50,14 +50,7 @@ struct WfQueues {
     uint32_t* ovf;       // closest-hit traversal stack entries beyond kLdsStack: [kStackMax - kLdsStack][kWfMaxThreads]
     uint32_t* ovf_sh;    // the same for the shadow kernels, which may run beside a closest-hit kernel (side stream)
     FixAcc acc_s;        // [chunk] per-sample accumulators of the adaptive / firefly phases
-    // Origin-region deal (WfPlan::deal): vertices at depth >= 1 on the triangle mesh send their children to
-    // the partition of their triangle's region, so each XCD's L2 holds one eighth of the mesh's BVH lines
-    unsigned long long* region_hist;   // [kDealSets][kRegionBins] such vertices per bin of BVH-order triangle
-                                       // index, per depth (min(depth, kDealSets - 1)), all passes
-    uint32_t* region_bounds;           // [kDealSets][kParts] first triangle of region r (k_wf_region_bounds)
 };
-constexpr int kRegionBins = 256;
-constexpr int kDealSets = 8;
 
 // Every counter sits on a line of its own: returning atomics execute at the memory side,
 // one line at a time, so cursors packed into one 128-B line serialise every partition's
@@ -117,8 +110,6 @@ struct WfPlan {
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
     int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always
                                // (PT_LANES=0|1 in the environment; tests)
-    int32_t deal;              // origin-region deal of depth >= 1 children (WfQueues::region_hist); 2: every
-                               // triangle in region 0 (tests: the full-partition fallback)
     // Optional second stream: each depth's shadow pass runs there, beside the next depth's
     // closest-hit pass (independent queues), so one fills the other's ramp and tail.
     // ev_main orders shade(d) → shadow(d); ev_side[q], recorded after the light terms of

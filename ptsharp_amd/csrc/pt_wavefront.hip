@@ -176,97 +176,6 @@ __device__ __forceinline__ void block_reserve2(unsigned long long* word, uint32_
     bbase = s_base[1][wid] + xb - b;
 }
 
-// The origin-region deal's reservation (WfPlan::deal): lane slots in the partition `tgt` of each lane,
-// one returning atomic per target partition the block sends to.  A target without room for the block's
-// share (a full partition) takes none of it: the lanes mark the slots they got below the cap dead (the
-// traversal kernels skip them) and try the next partition, up to every partition once; the queues then
-// hold every child as long as all of them fit in all partitions less one block's share each (k_wf_shade
-// checks that before it deals).  Block-uniform call sites only.
-__device__ __forceinline__ void block_reserve_deal(const WfQueues& Q, int qo, int& tgt, uint32_t a, uint32_t b,
-                                                   uint32_t& abase, uint32_t& bbase) {
-    __shared__ uint32_t s_n[kParts][2];
-    __shared__ uint32_t s_at[kParts][2];
-    __shared__ uint32_t s_ok;
-    bool placed = false;
-    for (int attempt = 0;; attempt++) {
-        __syncthreads();   // the last attempt's reads of s_at are done
-        if (threadIdx.x < 2 * kParts) s_n[threadIdx.x >> 1][threadIdx.x & 1] = 0u;
-        __syncthreads();
-        uint32_t oa = 0, ob = 0;
-        if (!placed) {
-            if (a) oa = atomicAdd(&s_n[tgt][0], a);
-            if (b) ob = atomicAdd(&s_n[tgt][1], b);
-        }
-        __syncthreads();
-        if (threadIdx.x < kParts) {
-            const uint32_t ta = s_n[threadIdx.x][0], tb = s_n[threadIdx.x][1];
-            unsigned long long base = 0;
-            if (ta | tb) base = atomicAdd(pair_word(Q, qo, (int)threadIdx.x), ((unsigned long long)tb << 32) | ta);
-            s_at[threadIdx.x][0] = (uint32_t)base;
-            s_at[threadIdx.x][1] = (uint32_t)(base >> 32);
-            const bool fits = (uint64_t)(uint32_t)base + ta <= Q.pcap && (uint64_t)(uint32_t)(base >> 32) + tb <= Q.spcap;
-            const uint64_t bad = __ballot(!fits) & ((1ull << kParts) - 1ull);
-            if (threadIdx.x == 0) s_ok = bad ? (uint32_t)bad : 0u;   // bit t: partition t had no room
-        }
-        __syncthreads();
-        const uint32_t bad = s_ok;
-        if (!placed) {
-            abase = s_at[tgt][0] + oa;
-            bbase = s_at[tgt][1] + ob;
-            if ((bad >> tgt) & 1u) {   // no room in tgt: mark the slots below the cap dead, try the next partition
-                for (uint32_t k = 0; k < a; k++)
-                    if (abase + k < Q.pcap)
-                        Q.q_d[qo][(size_t)tgt * Q.pcap + abase + k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(kDead));
-                for (uint32_t k = 0; k < b; k++)
-                    if (bbase + k < Q.spcap)
-                        Q.n_n[qo][(size_t)tgt * Q.spcap + bbase + k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(kDead));
-                tgt = (tgt + 1) % kParts;
-            } else {
-                placed = true;
-            }
-        }
-        if (!bad) break;   // block-uniform
-        if (attempt == kParts - 1) {   // every partition full: the queues overflowed
-            if (!placed) { abase = Q.pcap; bbase = Q.spcap; *Q.overflow = 1ull; }
-            break;
-        }
-    }
-}
-
-// Region of BVH-order triangle `idx` (WfQueues::region_bounds) and its histogram bin.
-__device__ __forceinline__ int tri_region(const WfQueues& Q, uint32_t idx) {
-    int r = 0;
-#pragma unroll
-    for (int k = 1; k < kParts; k++) r += idx >= Q.region_bounds[k] ? 1 : 0;
-    return r;
-}
-
-// Region bounds from the histograms of the passes so far, one set per depth (the first bounce's vertices
-// crowd the mesh's camera-facing side, deeper ones less): region r starts at the bin where the
-// cumulative count reaches r/kParts of the total (equal triangle counts before any pass).  `skew`
-// (tests and A/B): 1 every triangle in region 0; 2 each vertex' own partition (a marker word).
-__global__ __launch_bounds__(64) void k_wf_region_bounds(WfQueues Q, uint32_t num_tris, int skew) {
-    if (threadIdx.x >= (unsigned)kDealSets) return;
-    const unsigned long long* hist = Q.region_hist + threadIdx.x * kRegionBins;
-    uint32_t* bounds = Q.region_bounds + threadIdx.x * kParts;
-    if (skew) {
-        for (int r = 0; r < kParts; r++) bounds[r] = r ? num_tris : skew == 2 ? 0xFFFFFFFFu : 0u;
-        return;
-    }
-    unsigned long long total = 0;
-    for (int b = 0; b < kRegionBins; b++) total += hist[b];
-    bounds[0] = 0u;
-    int r = 1;
-    unsigned long long run = 0;
-    const unsigned long long all = total ? total : (unsigned long long)kRegionBins;
-    for (int b = 0; b < kRegionBins && r < kParts; b++) {
-        run += total ? hist[b] : 1ull;
-        while (r < kParts && run * kParts >= all * (unsigned long long)r)
-            bounds[r++] = (uint32_t)(((uint64_t)(b + 1) * num_tris) / kRegionBins);
-    }
-    while (r < kParts) bounds[r++] = num_tris;
-}
-
 // Throughput (fp64) rides in two 16-B fields: {r, g} and {key, b}.
 __device__ __forceinline__ void ray_store(const WfQueues& Q, int q, uint32_t i, v3 o, v3 d, const double thr[3],
                                           uint32_t pixel, uint32_t meta, uint64_t key) {
@@ -746,12 +655,10 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
 // traversal kernel (ray + stack state only).
 // One queued vertex (slot i of partition G.g; `alive` false: the lane only takes part in
 // the block's reservation and ballots).  Block-uniform call.
-// DEAL: the origin-region deal (WfPlan::deal) — a vertex on the mesh counts in s_hist and
-// sends its children to its triangle's region partition, slots per lane.
-template <bool COUNT, bool FULL, bool DEAL>
+template <bool COUNT, bool FULL>
 __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler& smp, const WfQueues& Q, int qi,
                                              const Group& G, uint32_t i, bool alive, Counters& ctr,
-                                             uint32_t* s_hist, const uint4* hl = nullptr) {   // hl: the hit record, already in LDS
+                                             const uint4* hl = nullptr) {   // hl: the hit record, already in LDS
     const int qo = 1 - qi;
     const bool nee_on = smp.dl && S.num_lights > 0;
     const int nl = S.num_lights;
@@ -816,12 +723,6 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         pv = vertex_p(m, sh, d, n1, n2);
     }
     fix_add_wave(Q.acc, pixel, has_c, cc[0], cc[1], cc[2]);
-    int tgt = (int)G.g;   // the partition this vertex' children go to
-    if (DEAL && s_hist && alive && h.kind == KIND_TRI) {
-        const uint32_t tri = (uint32_t)h.idx;
-        atomicAdd(&s_hist[(uint32_t)(((uint64_t)tri * kRegionBins) / (uint32_t)S.num_tris)], 1u);
-        tgt = Q.region_bounds[0] ? (int)G.g : tri_region(Q, tri);
-    }
     const DevMaterial& m = S.mats[mat];
     const int ma = nm == 2 ? 1 : 0;
     const bool ext_on = depth + 1 <= smp.mb;   // deeper samples return black without an Intersect
@@ -833,7 +734,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
     int cmax = nch;
     for (int off = 32; off > 0; off >>= 1) cmax = max(cmax, __shfl_xor(cmax, off, 64));
     __shared__ uint32_t s_cc[kBlockMajorChildren][4][2];
-    const bool block_major = !DEAL && smp.fh <= kBlockMajorFH;   // kernel-uniform: every depth's children fit s_cc
+    const bool block_major = smp.fh <= kBlockMajorFH;   // kernel-uniform: every depth's children fit s_cc
     uint32_t n_ext = 0, n_nee = 0;
     for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
         const int mode = ma + c % nm;
@@ -848,9 +749,8 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         }
     }
     if (block_major && lane >= cmax && lane < kBlockMajorChildren) { s_cc[lane][wid][0] = 0u; s_cc[lane][wid][1] = 0u; }
-    uint32_t ebase, nbase, blk_e = 0, blk_n = 0;
-    if (DEAL) block_reserve_deal(Q, qo, tgt, n_ext, n_nee, ebase, nbase);
-    else block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase, &blk_e, &blk_n);
+    uint32_t ebase, nbase, blk_e, blk_n;
+    block_reserve2(pair_word(Q, qo, G.g), n_ext, n_nee, ebase, nbase, &blk_e, &blk_n);
     if (ebase + n_ext > Q.pcap || nbase + n_nee > Q.spcap) *Q.overflow = 1ull;
     // Child-major slots: the block's reservation is filled child index by child index,
     // child c of every lane of the block on consecutive slots (waves in order, a ballot
@@ -879,16 +779,10 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
                 te += ce; tn += cn;
             }
         }
-        uint32_t my_n = nj + (pn + (uint32_t)__popcll(bn & below)) * rays_per_nee;
-        uint32_t my_e = ej + pe + (uint32_t)__popcll(be & below);
+        const uint32_t my_n = nj + (pn + (uint32_t)__popcll(bn & below)) * rays_per_nee;
+        const uint32_t my_e = ej + pe + (uint32_t)__popcll(be & below);
         nj += tn * rays_per_nee;
         ej += te;
-        if (DEAL) {   // each lane's children on consecutive slots of its own reservation
-            my_n = nbase;
-            my_e = ebase;
-            nbase += emit_nee ? rays_per_nee : 0u;
-            ebase += emit_ext ? 1u : 0u;
-        }
         if (!live) continue;
         const double fp = mode == 0 ? 1.0 : (refl ? pv : 1 - pv);
         double w[3];
@@ -912,7 +806,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
                     if (all_lights) { lc.x /= nl; lc.y /= nl; lc.z /= nl; }
                     else { lc.x *= nl; lc.y *= nl; lc.z *= nl; }
                     if (my_n + j < Q.spcap) {
-                        const uint32_t at = (uint32_t)tgt * Q.spcap + my_n + j;
+                        const uint32_t at = G.g * Q.spcap + my_n + j;
                         q_store_next(&Q.n_o[qo][at], make_float4(sh.pos.x, sh.pos.y, sh.pos.z, __uint_as_float(pixel)));
                         q_store_next(&Q.n_n[qo][at], make_float4(ldir.x, ldir.y, ldir.z, __uint_as_float(cast ? (uint32_t)li : kDead)));
                         q_store_late(&Q.n_w[qo][2 * (size_t)at], make_double2((t2[0] * w[0]) * lc.x, (t2[1] * w[1]) * lc.y));
@@ -931,7 +825,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         bounce_dir(m, sh, d, fu, fv, refl, n1, n2, E, no, nd);
         if (my_e < Q.pcap) {
             const double nthr[3] = {t2[0] * w[0], t2[1] * w[1], t2[2] * w[2]};
-            ray_store(Q, qo, (uint32_t)tgt * Q.pcap + my_e, no, nd, nthr, pixel, (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8),
+            ray_store(Q, qo, G.g * Q.pcap + my_e, no, nd, nthr, pixel, (uint32_t)(depth + 1) | ((reflected ? 1u : 0u) << 8),
                       E);
         }
     }
@@ -945,7 +839,7 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
 // at a time: each round trip of the chain (claim, queue loads, triangle record,
 // reservation) serves four times as many vertices.  Otherwise the block shades every
 // claimed slot (no extra read of the hit records, fewer live registers).
-template <bool COUNT, bool FULL, bool SCAN, bool DEAL = false>
+template <bool COUNT, bool FULL, bool SCAN>
 __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters, int form) {
     uint32_t queued = 0;
@@ -974,25 +868,13 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
     Counters ctr{0, 0, 0, 0};
     __shared__ uint32_t s_k0;
-    __shared__ uint32_t s_hist[kRegionBins];   // the origin-region deal's histogram of this block's vertices
-    // deal only while every child of this depth fits the queues less one block's share per partition (the
-    // room block_reserve_deal's full-partition fallback may leave unused): at most `fan` children per vertex
-    uint32_t* deal_hist = nullptr;
-    if (DEAL) {
-        for (int b = threadIdx.x; b < kRegionBins; b += 256) s_hist[b] = 0u;
-        __syncthreads();
-        const uint64_t fan = smp.spec_mode == 2 ? 2u : 1u;
-        const uint64_t fan_n = fan * (smp.light_mode == 1 ? (uint64_t)S.num_lights : 1u);
-        const uint64_t room = (uint64_t)kParts * (Q.pcap - 256u * fan), room_n = (uint64_t)kParts * (Q.spcap - 256u * fan_n);
-        if (Q.pcap > 256u * fan && Q.spcap > 256u * fan_n && kept * fan <= room && kept * fan_n <= room_n) deal_hist = s_hist;
-    }
     if constexpr (!SCAN) {
         for (;;) {  // block-uniform: the block takes 256 vertices of its partition at a time
             if (threadIdx.x == 0) s_k0 = atomicAdd(Q.counts + fetch_word(1, G.g), 256u);
             __syncthreads();
             const uint32_t k0 = s_k0;  // thread 0 rewrites it only after block_reserve2's barriers
             if (k0 >= n) break;
-            shade_vertex<COUNT, FULL, DEAL>(S, smp, Q, qi, G, base + k0 + threadIdx.x, k0 + threadIdx.x < n, ctr, deal_hist);
+            shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + k0 + threadIdx.x, k0 + threadIdx.x < n, ctr);
         }
     } else {
         const bool env_black = (!FULL || S.env_tex < 0) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
@@ -1057,8 +939,8 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             const uint32_t full = last ? total : total & ~255u;
             for (uint32_t r = 0; r < full; r += 256u) {   // block-uniform
                 const bool listed = r + threadIdx.x < full;
-                shade_vertex<COUNT, FULL, DEAL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed,
-                                                ctr, deal_hist, &s_hit[r + threadIdx.x]);
+                shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed, ctr,
+                                          &s_hit[r + threadIdx.x]);
                 __syncthreads();   // the next round rewrites shade_vertex's LDS child counts
             }
             if (last) break;
@@ -1069,11 +951,6 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             if (threadIdx.x < carry) { s_list[threadIdx.x] = held; s_hit[threadIdx.x] = hheld; }
             __syncthreads();
         }
-    }
-    if (DEAL) {
-        __syncthreads();
-        for (int b = threadIdx.x; b < kRegionBins; b += 256)
-            if (s_hist[b]) atomicAdd(Q.region_hist + b, (unsigned long long)s_hist[b]);
     }
     if (COUNT) {
         uint32_t shades = wave_sum(ctr.shades);
@@ -1629,53 +1506,33 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
         else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         end_k(1, stream);
     };
-    // Origin-region deal (refill scenes): the vertices of depth >= 1 on the mesh send their children to the
-    // partition of their triangle's region — regions of equal vertex counts over the passes so far — so each
-    // XCD traces rays that start in one eighth of the mesh (tools/bvh_quality.cpp cache study: C4's
-    // surface rays hit the 8 x 4 MB L2s 58 % of the time dealt round-robin, 82 % dealt by region)
-    const bool deal_on = plan.deal && lanes && S.num_tris > 0;
-    if (deal_on)
-        hipLaunchKernelGGL(k_wf_region_bounds, dim3(1), dim3(64), 0, stream, Q, (uint32_t)S.num_tris, plan.deal == 2 ? 1 : plan.deal == 3 ? 2 : 0);
     int qi = 0;
     trace(qi, bound);
     for (int depth = 0; depth <= smp.mb; depth++) {
-        const bool deal = deal_on && depth >= 1;   // (lean scenes only: never with `full`)
-        WfQueues Qs = Q;   // the shade's view: this depth's region histogram and bounds
-        if (deal) {
-            const int set = depth < kDealSets ? depth : kDealSets - 1;
-            Qs.region_hist += (size_t)set * kRegionBins;
-            Qs.region_bounds += (size_t)set * kParts;
-        }
         const unsigned sg = grid_for(bound, 256, plan.shade_blocks);
         begin_k(2, stream);
         // both forms (the one the kept count selects runs, the other returns at once); a routed shade runs
         // the lean and the FULL SCAN kernels, each on its own vertices
         if (full && S.shade_route) {
             if (count) {
-                hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-                hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
             } else {
-                hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-                hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+                hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
             }
         } else if (count && full) {
-            hipLaunchKernelGGL((k_wf_shade<true, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-        } else if (count && deal) {
-            hipLaunchKernelGGL((k_wf_shade<true, false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<true, false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
         } else if (count) {
-            hipLaunchKernelGGL((k_wf_shade<true, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<true, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
         } else if (full) {
-            hipLaunchKernelGGL((k_wf_shade<false, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-        } else if (deal) {
-            hipLaunchKernelGGL((k_wf_shade<false, false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<false, false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
         } else {
-            hipLaunchKernelGGL((k_wf_shade<false, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
-            hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Qs, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, false, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
+            hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
         }
         end_k(2, stream);
         if (plan.side) {

@@ -26,19 +26,6 @@ def test_c4_mesh1m_tiles(gpu):
     check(g, gr, o, orr)
 
 
-@pytest.mark.parametrize("deal", ["0", "1"])
-def test_c4_mesh1m_tiles_region_deal(gpu, monkeypatch, deal):
-    """C4 with the origin-region deal of depth >= 1 children off and on (PT_DEAL): which partition a
-    ray is traced in changes, no result may; 3 passes, so passes 2-3 deal by the regions the earlier
-    passes' histogram set (pass 1 by equal triangle counts)."""
-    monkeypatch.setenv("PT_DEAL", deal)
-    s, c, smp = scenes.bunny_frame(1_000_000)
-    tiles = tiles_for_rank(1920, 1080, 2, 128)
-    g, gr, o, orr = render_both(s, c, smp, 1920, 1080, spp=1, passes=3, seed=4321, tiles=tiles,
-                                engine=_abi.ENGINE_WAVEFRONT)
-    check(g, gr, o, orr)
-
-
 def test_c3_mesh70k_tiles(gpu):
     """C3: the ~70k-triangle mesh frame at 1920x1080 on one 64th of the tiles, 2 passes of 2 spp."""
     s, c, smp = scenes.bunny_frame(69_451)

@@ -140,23 +140,6 @@ def test_wavefront_many_chunks(gpu, monkeypatch):
     same_buffer(a, b)
 
 
-@pytest.mark.parametrize("deal", ["1", "2"])
-def test_region_deal_matches_megakernel(gpu, monkeypatch, deal):
-    """The origin-region deal (PT_DEAL=1: depth >= 1 children to their triangle's region partition)
-    with the queues held to 64K entries; PT_DEAL=2 puts every triangle in region 0, so partition 0
-    fills and the full-partition fallback moves children on (dead slots left behind).  Which
-    partition traces a ray may change, the Buffer and the ray count may not: the megakernel's."""
-    monkeypatch.setenv("PT_LANES", "1")
-    monkeypatch.setenv("PT_DEAL", deal)
-    monkeypatch.setenv("PT_WF_MAX_CAP", str(1 << 16))
-    s, c, smp = scenes.bunny_frame(20000, seed=5)
-    smp.MaxBounces = 3
-    a, ra = render_gpu(s, c, smp, 160, 90, spp=4, seed=7, engine=_abi.ENGINE_MEGAKERNEL)
-    b, rb = render_gpu(s, c, smp, 160, 90, spp=4, seed=7, engine=_abi.ENGINE_WAVEFRONT)
-    assert ra == rb
-    same_buffer(a, b)
-
-
 def test_wavefront_full_frame_one_stream(gpu):
     """1920x1080 at 16 spp with 8 first-bounce children: one 33M-sample chunk, above the side-stream
     threshold, so shadow passes run on the main stream (the C4 bench's configuration); the Buffer

@@ -18,7 +18,8 @@ def main():
     with open(path) as f:
         rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
     for r in rows:
-        runs[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        name = r["Kernel_Name"].replace("void ", "").replace("pt::", "").split("(")[0]
+        runs[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     for name, ds in sorted(runs.items()):
         if not name.startswith("k_wf_") or len(ds) % depths:
             continue
