@@ -59,11 +59,11 @@ constexpr int kCountStride = 64;
 static_assert(kCountStride >= 2, "a slot holds a packed 64-bit pair");
 constexpr int kFetchSlot = 2 * kParts;   // 8 cursors (k = 0..7) per partition
 constexpr int kKeptSlot = 10 * kParts;   // two slots (depth parity): rays k_wf_trace left work for k_wf_shade
-constexpr int kSdfSlot = 10 * kParts + 2;   // entries of Q.sdfq (PT_SDF_QUEUE)
-constexpr int kSdfShSlot = 10 * kParts + 3;   // entries of Q.sdfq_sh
-constexpr int kHeavySlot = 10 * kParts + 4;     // kParts slots: entries of Q.hq per partition
-constexpr int kHeavyShSlot = 11 * kParts + 4;  // kParts slots: entries of Q.hq_sh per partition
-constexpr int kEndSlot = 12 * kParts + 4;
+constexpr int kSdfSlot = 10 * kParts + 2;   // entries of Q.sdfq
+constexpr int kSdfShSlot = 10 * kParts + 3;   // two slots (shadow set q): entries of Q.sdfq_sh
+constexpr int kHeavySlot = 10 * kParts + 5;     // kParts slots: entries of Q.hq per partition
+constexpr int kHeavyShSlot = 11 * kParts + 5;  // 2 x kParts slots (shadow set q): entries of Q.hq_sh per partition
+constexpr int kEndSlot = 13 * kParts + 5;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kCountWords = count_word(kEndSlot);
@@ -75,9 +75,13 @@ constexpr int kOverflowCounter = 15;            // DevBuffer::counters word of W
 constexpr int fetch_word(int k, int g) { return count_word(kFetchSlot + k * kParts + g); }
 constexpr int kept_word(int q) { return count_word(kKeptSlot + q); }
 constexpr int kSdfWord = count_word(kSdfSlot);
-constexpr int kSdfShWord = count_word(kSdfShSlot);
+// Every counter a depth's kernels append to is zeroed by a kernel ahead of them on the same stream
+// (k_wf_shade's block 0: the next closest hit's heavy queue, the shadow set it writes), never by a
+// hipMemsetAsync: a fill kernel queued behind the other stream's persistent grid waits for a free CU
+// and holds its stream (C5: 500 such fills per pass, 0.47 ms each).
+constexpr int sdf_sh_word(int q) { return count_word(kSdfShSlot + q); }
 constexpr int heavy_word(int g) { return count_word(kHeavySlot + g); }
-constexpr int heavy_sh_word(int g) { return count_word(kHeavyShSlot + g); }
+constexpr int heavy_sh_word(int q, int g) { return count_word(kHeavyShSlot + q * kParts + g); }
 
 #ifndef PT_LDS_STACK
 #define PT_LDS_STACK 16

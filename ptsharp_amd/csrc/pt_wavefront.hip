@@ -411,7 +411,7 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevSce
 // The SDF records the analytic half of split shadow rays queued: one lane per
 // entry; a ray whose SDF is strictly nearer than its light is blocked.
 __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_shadow(DevScene S, WfQueues Q, int qo) {
-    const uint32_t n = min(Q.counts[kSdfShWord], Q.s_cap);
+    const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         const uint4 e = Q.sdfq_sh[k];
         const double tl = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
@@ -860,6 +860,9 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         Q.counts[fetch_word(0, threadIdx.x)] = 0u;              // the next k_wf_trace's (it may run beside k_wf_shadow)
         Q.counts[fetch_word(4, threadIdx.x)] = 0u;              // its analytic half's (split)
         if (threadIdx.x == 0) Q.counts[kSdfWord] = 0u;          // and that half's SDF queue
+        Q.counts[heavy_word(threadIdx.x)] = 0u;                 // and the routed split's heavy queue
+        Q.counts[heavy_sh_word(1 - qi, threadIdx.x)] = 0u;      // the shadow set it writes: its heavy queue
+        if (threadIdx.x == 0) Q.counts[sdf_sh_word(1 - qi)] = 0u;   // and its SDF queue
         Q.counts[fetch_word(5 + (1 - qi), threadIdx.x)] = 0u;   // the split shadow rays' analytic half
         if (threadIdx.x == 0) Q.counts[kept_word(1 - qi)] = 0u;   // the next k_wf_trace's kept count
     }
@@ -971,7 +974,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
     const bool route = SPLIT && S.route;   // the heavy queue's rays only (the refill half decided the others)
-    const uint32_t cnt = route ? Q.counts[heavy_sh_word((int)G.g)] : *nee_count(Q, qo, G.g);
+    const uint32_t cnt = route ? Q.counts[heavy_sh_word(qo, (int)G.g)] : *nee_count(Q, qo, G.g);
     const uint32_t n = cnt < Q.spcap ? cnt : Q.spcap, base = G.g * Q.spcap;
     uint32_t* cursor = Q.counts + fetch_word(SPLIT ? 5 + qo : 2 + qo, G.g);
     const uint32_t lane = threadIdx.x & 63;
@@ -1002,7 +1005,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
                     if (m) {
                         const int lead = __builtin_ctzll(m);
                         uint32_t at = 0;
-                        if ((int)lane == lead) at = atomicAdd(Q.counts + kSdfShWord, (uint32_t)__popcll(m));
+                        if ((int)lane == lead) at = atomicAdd(Q.counts + sdf_sh_word(qo), (uint32_t)__popcll(m));
                         at = (uint32_t)__shfl((int)at, lead, 64) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                         if (!blocked && sdf >= 0 && at < Q.s_cap) {
                             const unsigned long long tb = (unsigned long long)__double_as_longlong(tl);
@@ -1082,7 +1085,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
             if (hm) {
                 const int lead = __builtin_ctzll(hm);
                 uint32_t at = 0;
-                if ((int)lane == lead) at = atomicAdd(Q.counts + heavy_sh_word((int)part), (uint32_t)__popcll(hm));
+                if ((int)lane == lead) at = atomicAdd(Q.counts + heavy_sh_word(qo, (int)part), (uint32_t)__popcll(hm));
                 at = (uint32_t)__shfl((int)at, lead, 64) + (uint32_t)__popcll(hm & below);
                 if (hpend) {
                     if (at < Q.spcap) Q.hq_sh[part * Q.spcap + at] = i;
@@ -1481,8 +1484,6 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
         begin_k(1, stream);
-        if (split && S.route)   // the routed split's heavy queue counts, before the refill half appends
-            (void)hipMemsetAsync(Q.counts + heavy_word(0), 0, sizeof(uint32_t) * count_word(kParts), stream);
         if (split) {
             const unsigned tl = grid_for(n, kTB, plan.lanes_trace_blocks), ta = grid_for(n, kTB, plan.full_trace_blocks);
             if (count) {
@@ -1547,14 +1548,6 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
             const unsigned hl = grid_for(children * plan.lights_per_child, kTB, plan.lanes_shadow_blocks);
             const unsigned ha = grid_for(children * plan.lights_per_child, kTB, plan.full_shadow_blocks);
             const bool sq = S.num_sdf > 0;
-            if (sq) {
-                const hipError_t e = hipMemsetAsync(Q.counts + kSdfShWord, 0, sizeof(uint32_t), side);
-                if (e != hipSuccess) return e;
-            }
-            if (S.route) {   // the routed split's heavy shadow queue counts
-                const hipError_t e = hipMemsetAsync(Q.counts + heavy_sh_word(0), 0, sizeof(uint32_t) * count_word(kParts), side);
-                if (e != hipSuccess) return e;
-            }
             if (count) {
                 hipLaunchKernelGGL((k_wf_shadow_lanes<true, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<true, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
