@@ -193,9 +193,16 @@ struct Ctx {
 // and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
 // MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
+#ifndef PT_VOL_LDS_MAX
+#define PT_VOL_LDS_MAX 40960   // LDS bytes k_wf_vol_* may stage a Volume in (4 blocks per CU fit 160 KB); 0: never
+#endif
+#ifndef PT_VOL_DEFER
+#define PT_VOL_DEFER 1   // split traversal: Volumes deferred to k_wf_vol_hits / k_wf_vol_shadow (0: marched in place)
+#endif
 constexpr double kSideStreamMaxRays = (double)(64ull << 20);   // a chunk's widest depth, extension rays
-// (a scene with SDF shapes adds its two SDF queues, 32 B per entry, outside this budget: counted in,
-// they halved C4's queues from 2^28 to 2^27 entries and split its pass in two chunks, -3 %)
+// (a scene with SDF shapes or Volumes adds its two deferred-record queues, 32 B per entry, and with
+// Volumes their record words, 8 B, outside this budget: counted in, they halved C4's queues from 2^28 to
+// 2^27 entries and split its pass in two chunks, -3 %)
 constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 2 * (64 + 1);
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
@@ -243,9 +250,11 @@ int wf_alloc(Ctx* c, T** out, size_t n) {
 }
 
 int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
-    const bool want_sdf = c->S.num_sdf > 0;   // the split traversal's SDF queues (pt_wavefront.hip k_wf_sdf_*)
+    // the split traversal's deferred-record queues (pt_wavefront.hip k_wf_vol_* / k_wf_sdf_*)
+    const bool want_sdf = c->S.num_sdf > 0 || (PT_VOL_DEFER && c->S.num_vol > 0);
+    const bool want_vol = PT_VOL_DEFER && c->S.num_vol > 0;
     const bool want_heavy = c->S.route != 0;  // the routed split's queues of rays that reach a row-4 shape's box
-    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes && (!want_sdf || c->Q.sdfq) &&
+    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes && (!want_sdf || c->Q.sdfq) && (!want_vol || c->Q.volq) &&
         (!want_heavy || c->Q.hq))
         return PT_OK;
     cap = std::max(cap, c->wf_cap);
@@ -262,6 +271,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     }
     if ((rc = wf_alloc(c, &Q.hits, cap))) return rc;
     if (want_sdf && (rc = wf_alloc(c, &Q.sdfq, cap))) return rc;
+    if (want_vol && (rc = wf_alloc(c, &Q.volq, cap))) return rc;
     for (int q = 0; q < 2; q++) {   // shadow-ray sets by depth parity
         if ((rc = wf_alloc(c, &Q.n_o[q], scap))) return rc;
         if ((rc = wf_alloc(c, &Q.n_n[q], scap))) return rc;
@@ -269,6 +279,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
         if ((rc = wf_alloc(c, &Q.n_lit[q], scap))) return rc;
     }
     if (want_sdf && (rc = wf_alloc(c, &Q.sdfq_sh, scap))) return rc;   // one shadow pass at a time uses it
+    if (want_vol && (rc = wf_alloc(c, &Q.volq_sh, scap))) return rc;
     if (want_heavy && (rc = wf_alloc(c, &Q.hq, cap))) return rc;
     if (want_heavy && (rc = wf_alloc(c, &Q.hq_sh, scap))) return rc;   // one shadow pass at a time uses it
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
@@ -1153,11 +1164,38 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, windows, &d_win); if (rc) return rc;
     const int8_t* d_runs = nullptr;
     rc = upload(c, vol_runs, &d_runs); if (rc) return rc;
+    // grids whose every value is k/255 (Volume.cs:63's 8-bit slices) also as bytes: k_wf_vol_* stage such a
+    // grid in LDS with the 256-entry table k/255.0 (the same division: the same doubles)
+    std::vector<uint8_t> vol_bytes;
+    std::vector<size_t> bytes_off((size_t)std::max(d->num_volumes, 0), SIZE_MAX);
+    for (int i = 0; i < d->num_volumes; i++) {
+        const size_t n = (size_t)d->volumes[i].w * d->volumes[i].h * d->volumes[i].d;
+        const double* g = vox.data() + vol_off[(size_t)i];
+        bool exact = true;
+        for (size_t k = 0; k < n && exact; k++) {
+            const double b = std::nearbyint(g[k] * 255.0);
+            exact = b >= 0.0 && b <= 255.0 && b / 255.0 == g[k];
+        }
+        if (!exact) continue;
+        bytes_off[(size_t)i] = vol_bytes.size();
+        for (size_t k = 0; k < n; k++) vol_bytes.push_back((uint8_t)std::nearbyint(g[k] * 255.0));
+        vol_bytes.resize((vol_bytes.size() + 15) & ~(size_t)15);
+    }
+    const uint8_t* d_bytes = nullptr;
+    rc = upload(c, vol_bytes, &d_bytes); if (rc) return rc;
     std::vector<pt::DevVolume> vols;
     for (int i = 0; i < d->num_volumes; i++) {
         vols.push_back(dev_volume(d->volumes[i], d_vox + vol_off[(size_t)i], d_win ? d_win + win_off[(size_t)i] : nullptr));
         vols.back().runs = d_runs ? d_runs + runs_off[(size_t)i] : nullptr;
         vols.back().zero_sign = zero_sign[(size_t)i];
+        vols.back().bytes_src = (d_bytes && bytes_off[(size_t)i] != SIZE_MAX) ? d_bytes + bytes_off[(size_t)i] : nullptr;
+    }
+    S.vol_lds = 0;
+    if (d->num_volumes == 1 && vols[0].bytes_src) {   // lut, runs, bytes; 16-B aligned pieces
+        const pt_volume& v = d->volumes[0];
+        const size_t runs_b = vols[0].runs ? ((size_t)(v.w + 1) * (v.h + 1) * (v.d + 1) + 15) & ~(size_t)15 : 0;
+        const size_t need = 256 * sizeof(double) + runs_b + (((size_t)v.w * v.h * v.d + 15) & ~(size_t)15);
+        if (need <= (size_t)PT_VOL_LDS_MAX) S.vol_lds = (int32_t)need;
     }
     rc = upload(c, vols, &S.volumes); if (rc) return rc;
     rc = upload(c, xforms, &S.xforms); if (rc) return rc;
@@ -1177,6 +1215,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     // node step (seven loads through the texture path) and leaf record loads per ray
     S.ana_linear = (na > 0 && na <= (size_t)PT_ANA_LINEAR && !S.full_geom) ? 1 : 0;
     S.num_sdf = d->num_sdf_shapes;
+    S.num_vol = d->num_volumes;
     S.lights_lean = 1;
     for (const pt::DevLight& L : lights)
         if (!L.phantom && (L.kind == pt::KIND_SDF || L.kind == pt::KIND_VOLUME || L.kind == pt::KIND_XFORM)) S.lights_lean = 0;

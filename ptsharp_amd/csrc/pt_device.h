@@ -543,18 +543,21 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     }
 }
 // Intersect of analytic record p (march_deferred) by the active lanes together: prim_t's t.
-__device__ __noinline__ double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj) {
+// STAGED: the scene's one Volume as k_wf_vol_* staged it in LDS (vl), instead of S.volumes.
+template <bool STAGED = false>
+__device__ __forceinline__ double coop_record_t_body(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind,
+                                                    double& tobj, const DevVolume& vl = DevVolume{}) {
     const float4* r = S.ana_recs + 3 * (size_t)p;
     kind = (int32_t)f2u(r[0].w);
     uint32_t n = 0;
     double t;
     if (kind == KIND_VOLUME) {
-        t = coop_vol_t(S.volumes[rec_ext(r)], o, d, n);
+        t = STAGED ? coop_vol_t(vl, o, d, n) : coop_vol_t(S.volumes[rec_ext(r)], o, d, n);
         tobj = t;
     } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
         const DevXform& X = S.xforms[rec_ext(r)];
         const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
-        t = coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n);
+        t = STAGED ? coop_vol_t(vl, so, sd, n) : coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n);
         tobj = t;
         if (t < kHitInf) {
             const v3 position = mat_position(X.m, add(so, muls(sd, t)));
@@ -564,13 +567,39 @@ __device__ __noinline__ double coop_record_t(const DevScene& S, int32_t p, v3 o,
     if (S.march && (threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) atomicAdd(S.march, (unsigned long long)n);
     return t;
 }
+// Out of line in the FULL traversal kernels (their registers), inlined in k_wf_vol_* (INL).
+__device__ __noinline__ double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj) {
+    return coop_record_t_body(S, p, o, d, kind, tobj);
+}
+// The lanes' pending Volume records, one ray at a time by all active lanes (at least kCoopMinLanes):
+// march_pending's merge, without its few-lanes fallback (k_wf_vol_hits / k_wf_vol_shadow run full waves).
+template <bool ANY, bool INL = false, bool STAGED = false>
+__device__ inline void march_coop(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked,
+                                  const DevVolume& vl = DevVolume{}) {
+    const int lane = threadIdx.x & 63;
+    for (uint64_t todo = __ballot(pend >= 0); todo; todo &= todo - 1ull) {   // wave-uniform
+        const int src = __builtin_ctzll(todo);
+        const int32_t p = __shfl(pend, src, 64);
+        const v3 so{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
+        const v3 sd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+        int32_t kind;
+        double tx = 0;
+        const double t = INL ? coop_record_t_body<STAGED>(S, p, so, sd, kind, tx, vl) : coop_record_t(S, p, so, sd, kind, tx);
+        if (lane == src) {
+            if (ANY) {
+                if (t < best.t) *blocked = true;
+            } else if (t < best.t || (t == best.t && best.kind == KIND_TRI)) {
+                best.t = t; best.kind = kind; best.idx = p; best.tx = tx;
+            }
+        }
+    }
+}
 // The lanes' pending Volume records (traverse's pend), one ray at a time by all active lanes.
 // Closest hit: the march's t replaces the best when nearer, and on a tie with a triangle (the
 // analytic BVH is traversed before the triangles, which replace only a strictly farther best);
 // any-hit (ANY): *blocked when nearer than the light.
 template <bool ANY>
 __device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked = nullptr) {
-    const int lane = threadIdx.x & 63;
     auto merge = [&](double t, int32_t kind, int32_t p, double tx) {
         if (ANY) {
             if (t < best.t) *blocked = true;
@@ -587,16 +616,7 @@ __device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend
         }
         return;
     }
-    for (uint64_t todo = __ballot(pend >= 0); todo; todo &= todo - 1ull) {   // wave-uniform
-        const int src = __builtin_ctzll(todo);
-        const int32_t p = __shfl(pend, src, 64);
-        const v3 so{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
-        const v3 sd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
-        int32_t kind;
-        double tx = 0;
-        const double t = coop_record_t(S, p, so, sd, kind, tx);
-        if (lane == src) merge(t, kind, p, tx);
-    }
+    march_coop<ANY>(S, o, d, pend, best, blocked);
 }
 
 // Scene.Intersect (Scene.cs:75-79): closest hit over planes, analytic BVH, triangle BVH.
@@ -690,10 +710,11 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
 // best its t is raised by one ulp for the analytic pass (no double lies between), and restored
 // when no analytic hit took it.  The triangles the refill kernel found without the analytic
 // hit's tighter bound are the same: a bound only prunes, it never reorders the visits.
-// sdf_out: the SDF record left for k_wf_sdf_hits (-1: none), not merged here.
+// sdf_out: the SDF record left for k_wf_sdf_hits (-1: none), not merged here; vol_out: likewise the
+// Volume record left for k_wf_vol_hits, which merges it first.
 template <bool COUNT, class STK>
 __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const STK& stack, Counters& ctr, HitRec& best,
-                                          int32_t* sdf_out = nullptr) {
+                                          int32_t* sdf_out = nullptr, int32_t* vol_out = nullptr) {
     const double t_in = best.t;
     const bool tri_best = best.kind == KIND_TRI;
     if (tri_best) best.t = nextafter(best.t, (double)INFINITY);
@@ -711,7 +732,8 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
         traverse<false, COUNT, false, true>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack, ctr, &pend,
                                             sdf_out ? &pend_sdf : nullptr);
     }
-    march_pending<false>(S, o, d, pend, best);
+    if (vol_out) *vol_out = pend;
+    else march_pending<false>(S, o, d, pend, best);
     if (sdf_out) *sdf_out = pend_sdf;
     else sdf_pending<false>(S, o, d, pend_sdf, best);
     if (best.kind == KIND_TRI && tri_best) best.t = t_in;
@@ -719,10 +741,12 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
 // The analytic half of a split shadow query (light_visible's analytic part): is any analytic
 // primitive strictly nearer than the light?  The refill kernel already cleared the planes and
 // the triangles.
-// sdf_out: the SDF record left for k_wf_sdf_shadow (-1: none), with the light's t.
+// sdf_out: the SDF record left for k_wf_sdf_shadow (-1: none), with the light's t; vol_out: the
+// Volume record left for k_wf_vol_shadow.
 template <bool COUNT, class STK>
 __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L, v3 o, v3 d, const STK& stack,
-                                            Counters& ctr, int32_t* sdf_out = nullptr, double* tl_out = nullptr) {
+                                            Counters& ctr, int32_t* sdf_out = nullptr, double* tl_out = nullptr,
+                                            int32_t* vol_out = nullptr) {
     const double tl = light_t<true>(S, L, o, d);
     if (!(tl < kHitInf)) return true;   // (the refill kernel found it lit, so tl is finite)
     HitRec best{tl, -1, -1};
@@ -738,7 +762,9 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
                                                    &pend, sdf_out ? &pend_sdf : nullptr)) {
         return true;
     }
-    {
+    if (vol_out) {
+        *vol_out = pend;
+    } else {
         bool blocked = false;
         march_pending<true>(S, o, d, pend, best, &blocked);
         if (blocked) return true;
@@ -770,7 +796,7 @@ __device__ __forceinline__ bool heavy_reach(const DevScene& S, v3 o, v3 invd, fl
 // and the triangles): the same merge rules, the same deferred Volume march and SDF queue.
 template <bool COUNT>
 __device__ __forceinline__ void trace_heavy(const DevScene& S, v3 o, v3 d, Counters& ctr, HitRec& best,
-                                            int32_t* sdf_out) {
+                                            int32_t* sdf_out, int32_t* vol_out) {
     const double t_in = best.t;
     const bool tri_best = best.kind == KIND_TRI;
     if (tri_best) best.t = nextafter(best.t, (double)INFINITY);
@@ -789,7 +815,8 @@ __device__ __forceinline__ void trace_heavy(const DevScene& S, v3 o, v3 d, Count
         const double t = prim_t<false, true>(S, S.ana_recs, p, o, d, kind, &tx);
         if (t < best.t) { best.t = t; best.kind = kind; best.idx = (int32_t)p; best.tx = tx; }
     }
-    march_pending<false>(S, o, d, pend, best);
+    if (vol_out) *vol_out = pend;
+    else march_pending<false>(S, o, d, pend, best);
     if (sdf_out) *sdf_out = pend_sdf;
     else sdf_pending<false>(S, o, d, pend_sdf, best);
     if (best.kind == KIND_TRI && tri_best) best.t = t_in;
@@ -797,7 +824,7 @@ __device__ __forceinline__ void trace_heavy(const DevScene& S, v3 o, v3 d, Count
 // ana_blocked over the heavy records only.
 template <bool COUNT>
 __device__ __forceinline__ bool heavy_blocked(const DevScene& S, const DevLight& L, v3 o, v3 d, Counters& ctr,
-                                              int32_t* sdf_out, double* tl_out) {
+                                              int32_t* sdf_out, double* tl_out, int32_t* vol_out) {
     const double tl = light_t<true>(S, L, o, d);
     if (!(tl < kHitInf)) return true;
     HitRec best{tl, -1, -1};
@@ -815,7 +842,9 @@ __device__ __forceinline__ bool heavy_blocked(const DevScene& S, const DevLight&
         int32_t kind;
         if (prim_t<false, true>(S, S.ana_recs, p, o, d, kind) < tl) return true;
     }
-    {
+    if (vol_out) {
+        *vol_out = pend;
+    } else {
         bool blocked = false;
         march_pending<true>(S, o, d, pend, best, &blocked);
         if (blocked) return true;

@@ -16,6 +16,7 @@ namespace pt {
 // working on one region of the image at every depth, and the reservation
 // atomics spread over kParts counter words.
 constexpr int kParts = 8;
+constexpr uint32_t kNoRecord = 0xFFFFFFFFu;
 struct WfQueues {
     float4* q_o[2];      // {origin.xyz, pixel}
     float4* q_d[2];      // {direction.xyz, depth | emission << 8}
@@ -24,6 +25,11 @@ struct WfQueues {
     uint4* hits;         // {t (fp64 bits), kind, record}
     uint4* sdfq;         // split closest hit: {slot, SDF record, best world t (fp64 bits)} (k_wf_sdf_hits)
     uint4* sdfq_sh;      // split shadow rays: {slot, SDF record, the light's t (fp64 bits)} (k_wf_sdf_shadow)
+    // Volume records deferred the same way (one per sdfq / sdfq_sh entry, kNoRecord: none; the entry's
+    // SDF record may be kNoRecord too): k_wf_vol_hits / k_wf_vol_shadow march them before the SDF
+    // kernels run, lowering the entry's t when the Volume is nearer.  Null: no Volume in the scene.
+    uint32_t* volq;
+    uint32_t* volq_sh;
     // Routed split (DevScene::route): the slots of the rays whose segment reaches a §8f row-4 shape's box,
     // per partition (pcap / spcap entries each): only these go through the FULL analytic half
     uint32_t* hq;        // closest-hit rays (k_wf_trace_lanes → k_wf_trace<.., SPLIT>)

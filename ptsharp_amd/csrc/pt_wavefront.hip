@@ -330,21 +330,24 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
                 h.kind = (int32_t)r.z;
                 h.idx = (int32_t)r.w;
                 h.tx = h.t;
-                int32_t sdf = -1;
-                if (route) trace_heavy<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, ctr, h, &sdf);
-                else trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h, &sdf);
-                {   // k_wf_sdf_hits traces it, every lane busy (the active lanes append here)
-                    const uint64_t m = __ballot(sdf >= 0);
+                int32_t sdf = -1, vol = -1;
+                int32_t* const vol_out = Q.volq ? &vol : nullptr;   // Volumes deferred to k_wf_vol_hits
+                if (route) trace_heavy<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, ctr, h, &sdf, vol_out);
+                else trace_ana<COUNT>(S, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr, h, &sdf, vol_out);
+                {   // k_wf_vol_hits and k_wf_sdf_hits trace them, every lane busy (the active lanes append here)
+                    const bool defer = sdf >= 0 || vol >= 0;
+                    const uint64_t m = __ballot(defer);
                     if (m) {
                         const int lead = __builtin_ctzll(m);
                         uint32_t at = 0;
                         if ((int)lane == lead) at = atomicAdd(Q.counts + kSdfWord, (uint32_t)__popcll(m));
                         at = (uint32_t)__shfl((int)at, lead, 64) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                        if (sdf >= 0 && at < Q.cap) {
+                        if (defer && at < Q.cap) {
                             const unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
                             Q.sdfq[at] = make_uint4(i, (uint32_t)sdf, (uint32_t)tb, (uint32_t)(tb >> 32));
-                        } else if (sdf >= 0) {
-                            *Q.overflow = 1ull;   // a dropped entry would lose the SDF hit: the pass reports it
+                            if (Q.volq) Q.volq[at] = (uint32_t)vol;
+                        } else if (defer) {
+                            *Q.overflow = 1ull;   // a dropped entry would lose the hit: the pass reports it
                         }
                     }
                 }
@@ -380,6 +383,103 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 // atomic per refill).  A new ray's head work is two queue loads and the planes (none in
 // C4), so a refill holds the busy lanes for one load round trip.  Same visit order,
 // same arithmetic as trace(): bit-identical hits.
+#ifndef PT_VOL_WAVES
+#define PT_VOL_WAVES 4   // the cooperative march needs ~130 VGPRs (5 / 6 / 8 waves: 37-146 spilled)
+#endif
+// The scene's one Volume staged in this block's LDS (DevScene::vol_lds > 0): the 256 doubles k/255,
+// the uniform-cell table and the grid as bytes, so the march's table and corner reads are LDS reads
+// (flat loads of LDS addresses; the grid's doubles, 8× the bytes, would not fit 4 blocks per CU).
+// Returns the view to march with.  Block-uniform call, STAGED kernels only (DevScene::vol_lds > 0).
+__device__ __forceinline__ DevVolume stage_volume(const DevScene& S) {
+    extern __shared__ __align__(16) unsigned char s_vol[];
+    DevVolume vl = S.volumes[0];
+    double* lut = reinterpret_cast<double*>(s_vol);
+    const uint32_t runs_n = vl.runs ? (uint32_t)((vl.w + 1) * (vl.h + 1) * (vl.d + 1)) : 0u;
+    int8_t* runs = reinterpret_cast<int8_t*>(s_vol + 256 * sizeof(double));
+    uint8_t* bytes = reinterpret_cast<uint8_t*>(runs) + ((runs_n + 15u) & ~15u);
+    const uint32_t bytes_n = (uint32_t)(vl.w * vl.h * vl.d);
+    for (uint32_t k = threadIdx.x; k < 256u; k += blockDim.x) lut[k] = (double)k / 255.0;   // Volume.cs:63
+    for (uint32_t k = threadIdx.x; k < runs_n; k += blockDim.x) runs[k] = vl.runs[k];
+    for (uint32_t k = threadIdx.x; k < (bytes_n + 3u) / 4u; k += blockDim.x)   // the source is padded to 16 B
+        reinterpret_cast<uint32_t*>(bytes)[k] = reinterpret_cast<const uint32_t*>(vl.bytes_src)[k];
+    __syncthreads();
+    vl.lut = lut;
+    vl.bytes = bytes;
+    if (vl.runs) vl.runs = runs;
+    return vl;
+}
+
+// The Volume records the analytic half of a split closest hit deferred (trace_ana / trace_heavy
+// vol_out), merged before the entry's SDF record (k_wf_sdf_hits then reads the t this kernel lowered:
+// the traversal's order, the Volume's march before the SDF).  A wave takes 64 entries and marches their
+// Volumes one at a time with all its lanes (march_pending, the cooperative march), in a kernel that
+// holds nothing else and so runs more waves than the FULL kernel that found them.
+template <bool STAGED>
+__global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, WfQueues Q, int qi) {
+    const uint32_t n = min(Q.counts[kSdfWord], Q.cap);
+    const bool env_black = S.env_tex < 0 && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    uint32_t gained = 0;   // misses that became hits: rays with work for k_wf_shade (kept_word)
+    const DevVolume vl = STAGED ? stage_volume(S) : DevVolume{};
+    for (uint32_t k0 = w * 64u; k0 < n; k0 += nw * 64u) {   // wave-uniform: every lane takes part in the march
+        const uint32_t k = k0 + lane;
+        int32_t pend = k < n ? (int32_t)Q.volq[k] : -1;
+        if (__ballot(pend >= 0) == 0ull) continue;
+        uint4 e = make_uint4(0u, 0u, 0u, 0u);
+        HitRec best{kHitInf, -1, -1};
+        v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f};
+        if (pend >= 0) {
+            e = Q.sdfq[k];
+            const uint4 hr = Q.hits[e.x];
+            best.t = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
+            best.kind = (int32_t)hr.z;
+            best.idx = (int32_t)hr.w;
+            const float4 a = nt_load(&Q.q_o[qi][e.x]), b = nt_load(&Q.q_d[qi][e.x]);
+            o = v3{a.x, a.y, a.z};
+            d = v3{b.x, b.y, b.z};
+        }
+        const int32_t kind0 = best.kind;
+        march_coop<false, true, STAGED>(S, o, d, pend, best, nullptr, vl);
+        if (pend >= 0 && best.idx == pend && (best.kind == KIND_VOLUME || best.kind == KIND_XFORM)) {   // nearer
+            const unsigned long long tb = (unsigned long long)__double_as_longlong(best.kind == KIND_XFORM ? best.tx : best.t);
+            hit_store(&Q.hits[e.x], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)best.kind, (uint32_t)pend));
+            const unsigned long long tw = (unsigned long long)__double_as_longlong(best.t);
+            Q.sdfq[k] = make_uint4(e.x, e.y, (uint32_t)tw, (uint32_t)(tw >> 32));   // the SDF kernel's bound
+            gained += (kind0 < 0 && env_black) ? 1u : 0u;
+        }
+    }
+    gained = wave_sum(gained);
+    if (lane == 0 && gained) atomicAdd(Q.counts + kept_word(qi), gained);
+}
+// The Volume records split shadow rays deferred: blocked (unlit) when the march's t is nearer than
+// the light; k_wf_sdf_shadow then skips the ray.
+template <bool STAGED>
+__global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S, WfQueues Q, int qo) {
+    const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const DevVolume vl = STAGED ? stage_volume(S) : DevVolume{};
+    for (uint32_t k0 = w * 64u; k0 < n; k0 += nw * 64u) {   // wave-uniform
+        const uint32_t k = k0 + lane;
+        int32_t pend = k < n ? (int32_t)Q.volq_sh[k] : -1;
+        if (__ballot(pend >= 0) == 0ull) continue;
+        uint4 e = make_uint4(0u, 0u, 0u, 0u);
+        HitRec best{kHitInf, -1, -1};
+        v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f};
+        if (pend >= 0) {
+            e = Q.sdfq_sh[k];
+            best.t = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));   // the light's t
+            const float4 a = nt_load(&Q.n_o[qo][e.x]), b = nt_load(&Q.n_n[qo][e.x]);
+            o = v3{a.x, a.y, a.z};
+            d = v3{b.x, b.y, b.z};
+        }
+        bool blocked = false;
+        march_coop<true, true, STAGED>(S, o, d, pend, best, &blocked, vl);
+        if (pend >= 0 && blocked) Q.n_lit[qo][e.x] = 0;
+    }
+}
+
 // The SDF records the analytic half of a split closest hit queued: one lane per
 // entry, so SDFShape's sphere tracing (up to 1000 dependent steps) runs with every lane busy
 // instead of with the few lanes of a wave whose rays reach the shape.  Merged into the hit record
@@ -391,6 +491,7 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevSce
     uint32_t gained = 0;   // misses that became hits: rays with work for k_wf_shade (kept_word)
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         const uint4 e = Q.sdfq[k];
+        if (e.y == kNoRecord) continue;   // a Volume-only entry (k_wf_vol_hits)
         const uint32_t i = e.x;
         const double bt = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
         const float4 a = nt_load(&Q.q_o[qi][i]), b = nt_load(&Q.q_d[qi][i]);
@@ -414,6 +515,7 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_shadow(DevS
     const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         const uint4 e = Q.sdfq_sh[k];
+        if (e.y == kNoRecord || Q.n_lit[qo][e.x] == 0) continue;   // Volume-only, or blocked by its Volume
         const double tl = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
         const float4 a = nt_load(&Q.n_o[qo][e.x]), b = nt_load(&Q.n_n[qo][e.x]);
         int32_t kind;
@@ -993,24 +1095,27 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
             const uint32_t li = __float_as_uint(b.w);
             if (SPLIT) {
                 const float4 a = nt_load(&Q.n_o[qo][i]);
-                int32_t sdf = -1;
+                int32_t sdf = -1, vol = -1;
+                int32_t* const vol_out = Q.volq_sh ? &vol : nullptr;   // Volumes deferred to k_wf_vol_shadow
                 double tl = 0;
                 const bool blocked =
                     route ? heavy_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, ctr,
-                                                 &sdf, &tl)
+                                                 &sdf, &tl, vol_out)
                           : ana_blocked<COUNT>(S, S.lights[li], v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr,
-                                               &sdf, &tl);
-                {   // k_wf_sdf_shadow tests it, every lane busy
-                    const uint64_t m = __ballot(!blocked && sdf >= 0);
+                                               &sdf, &tl, vol_out);
+                {   // k_wf_vol_shadow and k_wf_sdf_shadow test them, every lane busy
+                    const bool defer = !blocked && (sdf >= 0 || vol >= 0);
+                    const uint64_t m = __ballot(defer);
                     if (m) {
                         const int lead = __builtin_ctzll(m);
                         uint32_t at = 0;
                         if ((int)lane == lead) at = atomicAdd(Q.counts + sdf_sh_word(qo), (uint32_t)__popcll(m));
                         at = (uint32_t)__shfl((int)at, lead, 64) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                        if (!blocked && sdf >= 0 && at < Q.s_cap) {
+                        if (defer && at < Q.s_cap) {
                             const unsigned long long tb = (unsigned long long)__double_as_longlong(tl);
                             Q.sdfq_sh[at] = make_uint4(i, (uint32_t)sdf, (uint32_t)tb, (uint32_t)(tb >> 32));
-                        } else if (!blocked && sdf >= 0) {
+                            if (Q.volq_sh) Q.volq_sh[at] = (uint32_t)vol;
+                        } else if (defer) {
                             *Q.overflow = 1ull;
                         }
                     }
@@ -1493,6 +1598,10 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
+            if (Q.volq && S.vol_lds > 0)
+                hipLaunchKernelGGL(k_wf_vol_hits<true>, dim3(grid_for(n, 256, 2048)), dim3(256), (size_t)S.vol_lds, stream, S, Q, qi);
+            else if (Q.volq)
+                hipLaunchKernelGGL(k_wf_vol_hits<false>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
             if (S.num_sdf > 0)
                 hipLaunchKernelGGL(k_wf_sdf_hits, dim3(grid_for(n, 256, 8192)), dim3(256), 0, stream, S, Q, qi);
             end_k(1, stream);
@@ -1555,6 +1664,12 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
+            if (Q.volq_sh && S.vol_lds > 0)
+                hipLaunchKernelGGL(k_wf_vol_shadow<true>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256),
+                                   (size_t)S.vol_lds, side, S, Q, 1 - qi);
+            else if (Q.volq_sh)
+                hipLaunchKernelGGL(k_wf_vol_shadow<false>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)),
+                                   dim3(256), 0, side, S, Q, 1 - qi);
             if (sq)
                 hipLaunchKernelGGL(k_wf_sdf_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256), 0,
                                    side, S, Q, 1 - qi);
