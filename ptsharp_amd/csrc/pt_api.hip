@@ -196,6 +196,9 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #ifndef PT_VOL_LDS_MAX
 #define PT_VOL_LDS_MAX 40960   // LDS bytes k_wf_vol_* may stage a Volume in (4 blocks per CU fit 160 KB); 0: never
 #endif
+#ifndef PT_SDF_LDS_MAX
+#define PT_SDF_LDS_MAX 16384   // LDS bytes k_wf_sdf_* may stage the SDF programs in; 0: never
+#endif
 #ifndef PT_VOL_DEFER
 #define PT_VOL_DEFER 1   // split traversal: Volumes deferred to k_wf_vol_hits / k_wf_vol_shadow (0: marched in place)
 #endif
@@ -1157,6 +1160,11 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     S.env_angle = d->env_texture_angle;
     rc = upload(c, sdfc.prog, &S.sdf_prog); if (rc) return rc;
     rc = upload(c, sdfc.params, &S.sdf_params); if (rc) return rc;
+    {   // the SDF programs, staged in LDS by the SDF queue kernels when small (pt_wavefront.hip stage_sdf)
+        const size_t need = sdfc.prog.size() * sizeof(pt::DevSdfIns) + sdfc.params.size() * sizeof(double);
+        S.sdf_prog_n = (int32_t)sdfc.prog.size();
+        S.sdf_lds = (!sdfc.prog.empty() && need <= (size_t)PT_SDF_LDS_MAX) ? (int32_t)need : 0;
+    }
     rc = upload(c, sdf_shapes, &S.sdf_shapes); if (rc) return rc;
     const double* d_vox = nullptr;
     const pt::DevWindow* d_win = nullptr;

@@ -87,6 +87,8 @@ struct DevScene {
     // SDF shapes, volumes, transformed shapes (§8f row 4; pt_ext.h)
     const DevSdfIns* sdf_prog;
     const double* sdf_params;
+    int32_t sdf_lds;           // LDS bytes k_wf_sdf_* stage sdf_prog and sdf_params in (8-B aligned halves); 0: none
+    int32_t sdf_prog_n;        // entries of sdf_prog
     const DevSdfShape* sdf_shapes;
     const DevVolume* volumes;
     const DevXform* xforms;

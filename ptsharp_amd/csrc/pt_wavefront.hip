@@ -480,12 +480,34 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S,
     }
 }
 
+// The SDF programs (instructions, then parameters: DevSdfIns is 8 B) staged in this block's LDS when
+// small (DevScene::sdf_lds): the march reads an instruction and its parameters at every step, one
+// address for the wave (one shape), from LDS instead of through the vector L1.  Returns the scene
+// view that reads them there.  Block-uniform call, STAGED kernels only.
+static_assert(sizeof(DevSdfIns) == 8, "stage_sdf copies 8-B words");
+__device__ __forceinline__ DevScene stage_sdf(const DevScene& S) {
+    extern __shared__ __align__(16) unsigned char s_sdf[];
+    DevScene V = S;
+    const uint32_t words = (uint32_t)S.sdf_lds / 8u;
+    const unsigned long long* prog = reinterpret_cast<const unsigned long long*>(S.sdf_prog);
+    const uint32_t pn = (uint32_t)S.sdf_prog_n;   // program entries (8 B each), then the parameters
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(s_sdf);
+    for (uint32_t k = threadIdx.x; k < words; k += blockDim.x)
+        dst[k] = k < pn ? prog[k] : reinterpret_cast<const unsigned long long*>(S.sdf_params)[k - pn];
+    __syncthreads();
+    V.sdf_prog = reinterpret_cast<const DevSdfIns*>(s_sdf);
+    V.sdf_params = reinterpret_cast<const double*>(s_sdf + (size_t)pn * sizeof(DevSdfIns));
+    return V;
+}
+
 // The SDF records the analytic half of a split closest hit queued: one lane per
 // entry, so SDFShape's sphere tracing (up to 1000 dependent steps) runs with every lane busy
 // instead of with the few lanes of a wave whose rays reach the shape.  Merged into the hit record
 // as the traversal would have: nearer wins, and an equal t beats a triangle (the analytic BVH
 // precedes the triangles in Scene.Intersect).  One entry per ray: no two lanes write one record.
-__global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevScene S, WfQueues Q, int qi) {
+template <bool STAGED>
+__global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevScene S0, WfQueues Q, int qi) {
+    const DevScene S = STAGED ? stage_sdf(S0) : S0;
     const uint32_t n = min(Q.counts[kSdfWord], Q.cap);
     const bool env_black = S.env_tex < 0 && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
     uint32_t gained = 0;   // misses that became hits: rays with work for k_wf_shade (kept_word)
@@ -511,7 +533,9 @@ __global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_hits(DevSce
 
 // The SDF records the analytic half of split shadow rays queued: one lane per
 // entry; a ray whose SDF is strictly nearer than its light is blocked.
-__global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_shadow(DevScene S, WfQueues Q, int qo) {
+template <bool STAGED>
+__global__ __launch_bounds__(256, PT_FULL_TRACE_WAVES) void k_wf_sdf_shadow(DevScene S0, WfQueues Q, int qo) {
+    const DevScene S = STAGED ? stage_sdf(S0) : S0;
     const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         const uint4 e = Q.sdfq_sh[k];
@@ -1602,8 +1626,10 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL(k_wf_vol_hits<true>, dim3(grid_for(n, 256, 2048)), dim3(256), (size_t)S.vol_lds, stream, S, Q, qi);
             else if (Q.volq)
                 hipLaunchKernelGGL(k_wf_vol_hits<false>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
-            if (S.num_sdf > 0)
-                hipLaunchKernelGGL(k_wf_sdf_hits, dim3(grid_for(n, 256, 8192)), dim3(256), 0, stream, S, Q, qi);
+            if (S.num_sdf > 0 && S.sdf_lds > 0)
+                hipLaunchKernelGGL(k_wf_sdf_hits<true>, dim3(grid_for(n, 256, 8192)), dim3(256), (size_t)S.sdf_lds, stream, S, Q, qi);
+            else if (S.num_sdf > 0)
+                hipLaunchKernelGGL(k_wf_sdf_hits<false>, dim3(grid_for(n, 256, 8192)), dim3(256), 0, stream, S, Q, qi);
             end_k(1, stream);
             return;
         }
@@ -1670,9 +1696,12 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
             else if (Q.volq_sh)
                 hipLaunchKernelGGL(k_wf_vol_shadow<false>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)),
                                    dim3(256), 0, side, S, Q, 1 - qi);
-            if (sq)
-                hipLaunchKernelGGL(k_wf_sdf_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256), 0,
-                                   side, S, Q, 1 - qi);
+            if (sq && S.sdf_lds > 0)
+                hipLaunchKernelGGL(k_wf_sdf_shadow<true>, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256),
+                                   (size_t)S.sdf_lds, side, S, Q, 1 - qi);
+            else if (sq)
+                hipLaunchKernelGGL(k_wf_sdf_shadow<false>, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256),
+                                   0, side, S, Q, 1 - qi);
         } else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
