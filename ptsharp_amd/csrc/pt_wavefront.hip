@@ -409,6 +409,32 @@ __device__ __forceinline__ DevVolume stage_volume(const DevScene& S) {
     return vl;
 }
 
+#ifndef PT_VOL_SERIAL
+#define PT_VOL_SERIAL 1   // k_wf_vol_*: each lane marches its own entry (vol_t); 0: the wave's lanes march one entry together
+#endif
+// Intersect of Volume record p (a Volume, or a TransformedShape of one) by this lane alone: vol_t, the
+// reference's loop (prim_t's t; tobj: the inner t of a TransformedShape).  `n`: its Volume.Sample calls.
+__device__ __forceinline__ double vol_record_t(const DevScene& S, const DevVolume& vg, bool staged, int32_t p, v3 o,
+                                               v3 d, int32_t& kind, double& tobj, uint32_t& n) {
+    const float4* r = S.ana_recs + 3 * (size_t)p;
+    kind = (int32_t)f2u(r[0].w);
+    double t;
+    if (kind == KIND_VOLUME) {
+        t = vol_t(staged ? vg : S.volumes[rec_ext(r)], o, d, &n);
+        tobj = t;
+    } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
+        const DevXform& X = S.xforms[rec_ext(r)];
+        const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
+        t = vol_t(staged ? vg : S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, &n);
+        tobj = t;
+        if (t < kHitInf) {
+            const v3 position = mat_position(X.m, add(so, muls(sd, t)));
+            t = (double)lengthf(sub(position, o));
+        }
+    }
+    return t;
+}
+
 // The Volume records the analytic half of a split closest hit deferred (trace_ana / trace_heavy
 // vol_out), merged before the entry's SDF record (k_wf_sdf_hits then reads the t this kernel lowered:
 // the traversal's order, the Volume's march before the SDF).  A wave takes 64 entries and marches their
@@ -421,6 +447,7 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t gained = 0;   // misses that became hits: rays with work for k_wf_shade (kept_word)
+    uint32_t samples = 0;  // Volume.Sample calls (counted passes; the cooperative march counts its own)
     const DevVolume vl = STAGED ? stage_volume(S) : DevVolume{};
     for (uint32_t k0 = w * 64u; k0 < n; k0 += nw * 64u) {   // wave-uniform: every lane takes part in the march
         const uint32_t k = k0 + lane;
@@ -440,7 +467,18 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
             d = v3{b.x, b.y, b.z};
         }
         const int32_t kind0 = best.kind;
-        march_coop<false, true, STAGED>(S, o, d, pend, best, nullptr, vl);
+        if (PT_VOL_SERIAL) {
+            if (pend >= 0) {
+                int32_t kind;
+                double tx = 0;
+                uint32_t ns = 0;
+                const double t = vol_record_t(S, vl, STAGED, pend, o, d, kind, tx, ns);
+                samples += ns;
+                if (t < best.t || (t == best.t && best.kind == KIND_TRI)) { best.t = t; best.kind = kind; best.idx = pend; best.tx = tx; }
+            }
+        } else {
+            march_coop<false, true, STAGED>(S, o, d, pend, best, nullptr, vl);
+        }
         if (pend >= 0 && best.idx == pend && (best.kind == KIND_VOLUME || best.kind == KIND_XFORM)) {   // nearer
             const unsigned long long tb = (unsigned long long)__double_as_longlong(best.kind == KIND_XFORM ? best.tx : best.t);
             hit_store(&Q.hits[e.x], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)best.kind, (uint32_t)pend));
@@ -451,6 +489,8 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
     }
     gained = wave_sum(gained);
     if (lane == 0 && gained) atomicAdd(Q.counts + kept_word(qi), gained);
+    samples = wave_sum(samples);
+    if (S.march && lane == 0 && samples) atomicAdd(S.march, (unsigned long long)samples);
 }
 // The Volume records split shadow rays deferred: blocked (unlit) when the march's t is nearer than
 // the light; k_wf_sdf_shadow then skips the ray.
@@ -459,6 +499,7 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S,
     const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    uint32_t samples = 0;
     const DevVolume vl = STAGED ? stage_volume(S) : DevVolume{};
     for (uint32_t k0 = w * 64u; k0 < n; k0 += nw * 64u) {   // wave-uniform
         const uint32_t k = k0 + lane;
@@ -475,9 +516,21 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S,
             d = v3{b.x, b.y, b.z};
         }
         bool blocked = false;
-        march_coop<true, true, STAGED>(S, o, d, pend, best, &blocked, vl);
+        if (PT_VOL_SERIAL) {
+            if (pend >= 0) {
+                int32_t kind;
+                double tx = 0;
+                uint32_t ns = 0;
+                blocked = vol_record_t(S, vl, STAGED, pend, o, d, kind, tx, ns) < best.t;
+                samples += ns;
+            }
+        } else {
+            march_coop<true, true, STAGED>(S, o, d, pend, best, &blocked, vl);
+        }
         if (pend >= 0 && blocked) Q.n_lit[qo][e.x] = 0;
     }
+    samples = wave_sum(samples);
+    if (S.march && lane == 0 && samples) atomicAdd(S.march, (unsigned long long)samples);
 }
 
 // The SDF programs (instructions, then parameters: DevSdfIns is 8 B) staged in this block's LDS when
