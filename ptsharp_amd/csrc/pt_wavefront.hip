@@ -666,16 +666,21 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
     int32_t bkind = -1, bidx = -1;
     float tmax = 0.f;
     const bool route = split && S.route;   // routed split: only rays that reach a heavy box go on (hq)
-    bool hpend = false;                       // this lane's finished ray goes to the heavy queue (at the loop top)
+    bool hpend = false;                       // this lane's finished ray waits for the heavy-box test (at the loop top)
     auto finish = [&]() {
         unsigned long long tb = (unsigned long long)__double_as_longlong(bt);
         hit_store(&Q.hits[i & 0x7FFFFFFFu], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)bkind, (uint32_t)bidx));
-        if (route) hpend = heavy_reach(S, o, invd, tmax_bound(bt));
-        if (!split || (route && !hpend)) kept += (bkind >= 0 || !env_black) ? 1u : 0u;
+        if (route) hpend = true;
+        else if (!split) kept += (bkind >= 0 || !env_black) ? 1u : 0u;
         has = false;
     };
     for (;;) {
         if (route) {   // wave-uniform: the finished rays that reach a heavy box, appended with one atomic per wave
+            // (one call site of the box test: the step loop keeps its registers)
+            if (hpend) {
+                hpend = heavy_reach(S, o, invd, tmax_bound(bt));
+                if (!hpend) kept += (bkind >= 0 || !env_black) ? 1u : 0u;
+            }
             const uint64_t hm = __ballot(hpend);
             if (hm) {
                 const int lead = __builtin_ctzll(hm);
@@ -1259,10 +1264,11 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     // split, provisionally when the ray reaches a heavy box (the FULL half decides: k_wf_shadow<.., SPLIT>)
     auto report_lit = [&]() {
         Q.n_lit[qo][i] = phantom ? 0 : 1;
-        if (route && !phantom) hpend = heavy_reach(S, o, invd, tmax);
+        if (route && !phantom) hpend = true;   // the heavy-box test at the loop top
     };
     for (;;) {
         if (route) {   // wave-uniform: the provisionally lit rays that reach a heavy box, one atomic per wave
+            if (hpend) hpend = heavy_reach(S, o, invd, tmax);
             const uint64_t hm = __ballot(hpend);
             if (hm) {
                 const int lead = __builtin_ctzll(hm);
