@@ -410,7 +410,7 @@ __device__ __forceinline__ DevVolume stage_volume(const DevScene& S) {
 }
 
 #ifndef PT_VOL_SERIAL
-#define PT_VOL_SERIAL 1   // k_wf_vol_*: each lane marches its own entry (vol_t); 0: the wave's lanes march one entry together
+#define PT_VOL_SERIAL 0   // k_wf_vol_*: 1 each lane marches its own entry (vol_t); 0: the wave's lanes march one entry together
 #endif
 // Intersect of Volume record p (a Volume, or a TransformedShape of one) by this lane alone: vol_t, the
 // reference's loop (prim_t's t; tobj: the inner t of a TransformedShape).  `n`: its Volume.Sample calls.
