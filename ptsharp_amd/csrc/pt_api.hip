@@ -193,9 +193,6 @@ struct Ctx {
 // and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
 // MI355X's 288 GB).
 constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
-#ifndef PT_VOL_LDS_MAX
-#define PT_VOL_LDS_MAX 40960   // LDS bytes k_wf_vol_* may stage a Volume in (4 blocks per CU fit 160 KB); 0: never
-#endif
 #ifndef PT_SDF_LDS_MAX
 #define PT_SDF_LDS_MAX 16384   // LDS bytes k_wf_sdf_* may stage the SDF programs in; 0: never
 #endif
@@ -1172,38 +1169,11 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, windows, &d_win); if (rc) return rc;
     const int8_t* d_runs = nullptr;
     rc = upload(c, vol_runs, &d_runs); if (rc) return rc;
-    // grids whose every value is k/255 (Volume.cs:63's 8-bit slices) also as bytes: k_wf_vol_* stage such a
-    // grid in LDS with the 256-entry table k/255.0 (the same division: the same doubles)
-    std::vector<uint8_t> vol_bytes;
-    std::vector<size_t> bytes_off((size_t)std::max(d->num_volumes, 0), SIZE_MAX);
-    for (int i = 0; i < d->num_volumes; i++) {
-        const size_t n = (size_t)d->volumes[i].w * d->volumes[i].h * d->volumes[i].d;
-        const double* g = vox.data() + vol_off[(size_t)i];
-        bool exact = true;
-        for (size_t k = 0; k < n && exact; k++) {
-            const double b = std::nearbyint(g[k] * 255.0);
-            exact = b >= 0.0 && b <= 255.0 && b / 255.0 == g[k];
-        }
-        if (!exact) continue;
-        bytes_off[(size_t)i] = vol_bytes.size();
-        for (size_t k = 0; k < n; k++) vol_bytes.push_back((uint8_t)std::nearbyint(g[k] * 255.0));
-        vol_bytes.resize((vol_bytes.size() + 15) & ~(size_t)15);
-    }
-    const uint8_t* d_bytes = nullptr;
-    rc = upload(c, vol_bytes, &d_bytes); if (rc) return rc;
     std::vector<pt::DevVolume> vols;
     for (int i = 0; i < d->num_volumes; i++) {
         vols.push_back(dev_volume(d->volumes[i], d_vox + vol_off[(size_t)i], d_win ? d_win + win_off[(size_t)i] : nullptr));
         vols.back().runs = d_runs ? d_runs + runs_off[(size_t)i] : nullptr;
         vols.back().zero_sign = zero_sign[(size_t)i];
-        vols.back().bytes_src = (d_bytes && bytes_off[(size_t)i] != SIZE_MAX) ? d_bytes + bytes_off[(size_t)i] : nullptr;
-    }
-    S.vol_lds = 0;
-    if (d->num_volumes == 1 && vols[0].bytes_src) {   // lut, runs, bytes; 16-B aligned pieces
-        const pt_volume& v = d->volumes[0];
-        const size_t runs_b = vols[0].runs ? ((size_t)(v.w + 1) * (v.h + 1) * (v.d + 1) + 15) & ~(size_t)15 : 0;
-        const size_t need = 256 * sizeof(double) + runs_b + (((size_t)v.w * v.h * v.d + 15) & ~(size_t)15);
-        if (need <= (size_t)PT_VOL_LDS_MAX) S.vol_lds = (int32_t)need;
     }
     rc = upload(c, vols, &S.volumes); if (rc) return rc;
     rc = upload(c, xforms, &S.xforms); if (rc) return rc;

@@ -543,21 +543,19 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     }
 }
 // Intersect of analytic record p (march_deferred) by the active lanes together: prim_t's t.
-// STAGED: the scene's one Volume as k_wf_vol_* staged it in LDS (vl), instead of S.volumes.
-template <bool STAGED = false>
 __device__ __forceinline__ double coop_record_t_body(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind,
-                                                    double& tobj, const DevVolume& vl = DevVolume{}) {
+                                                    double& tobj) {
     const float4* r = S.ana_recs + 3 * (size_t)p;
     kind = (int32_t)f2u(r[0].w);
     uint32_t n = 0;
     double t;
     if (kind == KIND_VOLUME) {
-        t = STAGED ? coop_vol_t(vl, o, d, n) : coop_vol_t(S.volumes[rec_ext(r)], o, d, n);
+        t = coop_vol_t(S.volumes[rec_ext(r)], o, d, n);
         tobj = t;
     } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
         const DevXform& X = S.xforms[rec_ext(r)];
         const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
-        t = STAGED ? coop_vol_t(vl, so, sd, n) : coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n);
+        t = coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n);
         tobj = t;
         if (t < kHitInf) {
             const v3 position = mat_position(X.m, add(so, muls(sd, t)));
@@ -573,9 +571,8 @@ __device__ __noinline__ double coop_record_t(const DevScene& S, int32_t p, v3 o,
 }
 // The lanes' pending Volume records, one ray at a time by all active lanes (at least kCoopMinLanes):
 // march_pending's merge, without its few-lanes fallback (k_wf_vol_hits / k_wf_vol_shadow run full waves).
-template <bool ANY, bool INL = false, bool STAGED = false>
-__device__ inline void march_coop(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked,
-                                  const DevVolume& vl = DevVolume{}) {
+template <bool ANY, bool INL = false>
+__device__ inline void march_coop(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked) {
     const int lane = threadIdx.x & 63;
     for (uint64_t todo = __ballot(pend >= 0); todo; todo &= todo - 1ull) {   // wave-uniform
         const int src = __builtin_ctzll(todo);
@@ -584,7 +581,7 @@ __device__ inline void march_coop(const DevScene& S, v3 o, v3 d, int32_t pend, H
         const v3 sd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
         int32_t kind;
         double tx = 0;
-        const double t = INL ? coop_record_t_body<STAGED>(S, p, so, sd, kind, tx, vl) : coop_record_t(S, p, so, sd, kind, tx);
+        const double t = INL ? coop_record_t_body(S, p, so, sd, kind, tx) : coop_record_t(S, p, so, sd, kind, tx);
         if (lane == src) {
             if (ANY) {
                 if (t < best.t) *blocked = true;

@@ -60,11 +60,6 @@ struct DevVolume {
     // for; null: no skipping.  zero_sign: the Sign of a cell with every corner outside the grid.
     const int8_t* runs;
     int32_t zero_sign, _pad;
-    // Every value k/255 (the reference's Volume from 8-bit slices, Volume.cs:63): the grid as bytes (for
-    // k_wf_vol_* to stage in LDS), else null.  bytes / lut: when set (an LDS view), Get reads lut[bytes[i]].
-    const uint8_t* bytes_src;
-    const uint8_t* bytes;
-    const double* lut;
 };
 struct DevBlas {          // object-space BVH4 of a mesh instanced by TransformedShape
     int32_t node_off;     // first node in blas_nodes
@@ -283,8 +278,7 @@ PT_HD v3 sdf_normal(const DevSdfIns* prog, const double* params, const DevSdfSha
 // ---------------------------------------------------------------- Volume (Volume.cs)
 PT_HD double vol_get(const DevVolume& v, int x, int y, int z) {   // Volume.Get (Volume.cs:40-46)
     if (x < 0 || y < 0 || z < 0 || x >= v.w || y >= v.h || z >= v.d) return 0;
-    const size_t i = (size_t)x + (size_t)y * (size_t)v.w + (size_t)z * (size_t)v.w * (size_t)v.h;
-    return v.bytes ? v.lut[v.bytes[i]] : v.data[i];
+    return v.data[(size_t)x + (size_t)y * (size_t)v.w + (size_t)z * (size_t)v.w * (size_t)v.h];
 }
 // Volume.Sample (Volume.cs:73-105), with its y-from-z slip (:77).  Coordinates outside
 // the int range (an OverflowException in the reference) sample 0, as in the oracle.

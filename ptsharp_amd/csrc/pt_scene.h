@@ -108,7 +108,6 @@ struct DevScene {
     int32_t lights_lean;       // 1: every light's own t is a lean intersect (no SDF / Volume light): split shadow rays
     int32_t num_sdf;           // SDFShapes (the split closest hit queues their records: k_wf_sdf_hits)
     int32_t num_vol;           // Volumes (likewise: k_wf_vol_hits)
-    int32_t vol_lds;           // LDS bytes k_wf_vol_* stage the one Volume's grid in (lut, runs, bytes); 0: none
     // Routed split traversal (a scene with §8f row-4 shapes, at most 8 analytic records, lean lights and a
     // large triangle BVH): the refill kernels test the lean analytic records (spheres, cubes) linearly and
     // the row-4 ("heavy") records' boxes; only rays whose segment reaches such a box take the FULL half

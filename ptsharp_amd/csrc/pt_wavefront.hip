@@ -386,46 +386,23 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 #ifndef PT_VOL_WAVES
 #define PT_VOL_WAVES 4   // the cooperative march needs ~130 VGPRs (5 / 6 / 8 waves: 37-146 spilled)
 #endif
-// The scene's one Volume staged in this block's LDS (DevScene::vol_lds > 0): the 256 doubles k/255,
-// the uniform-cell table and the grid as bytes, so the march's table and corner reads are LDS reads
-// (flat loads of LDS addresses; the grid's doubles, 8× the bytes, would not fit 4 blocks per CU).
-// Returns the view to march with.  Block-uniform call, STAGED kernels only (DevScene::vol_lds > 0).
-__device__ __forceinline__ DevVolume stage_volume(const DevScene& S) {
-    extern __shared__ __align__(16) unsigned char s_vol[];
-    DevVolume vl = S.volumes[0];
-    double* lut = reinterpret_cast<double*>(s_vol);
-    const uint32_t runs_n = vl.runs ? (uint32_t)((vl.w + 1) * (vl.h + 1) * (vl.d + 1)) : 0u;
-    int8_t* runs = reinterpret_cast<int8_t*>(s_vol + 256 * sizeof(double));
-    uint8_t* bytes = reinterpret_cast<uint8_t*>(runs) + ((runs_n + 15u) & ~15u);
-    const uint32_t bytes_n = (uint32_t)(vl.w * vl.h * vl.d);
-    for (uint32_t k = threadIdx.x; k < 256u; k += blockDim.x) lut[k] = (double)k / 255.0;   // Volume.cs:63
-    for (uint32_t k = threadIdx.x; k < runs_n; k += blockDim.x) runs[k] = vl.runs[k];
-    for (uint32_t k = threadIdx.x; k < (bytes_n + 3u) / 4u; k += blockDim.x)   // the source is padded to 16 B
-        reinterpret_cast<uint32_t*>(bytes)[k] = reinterpret_cast<const uint32_t*>(vl.bytes_src)[k];
-    __syncthreads();
-    vl.lut = lut;
-    vl.bytes = bytes;
-    if (vl.runs) vl.runs = runs;
-    return vl;
-}
-
 #ifndef PT_VOL_SERIAL
 #define PT_VOL_SERIAL 0   // k_wf_vol_*: 1 each lane marches its own entry (vol_t); 0: the wave's lanes march one entry together
 #endif
 // Intersect of Volume record p (a Volume, or a TransformedShape of one) by this lane alone: vol_t, the
 // reference's loop (prim_t's t; tobj: the inner t of a TransformedShape).  `n`: its Volume.Sample calls.
-__device__ __forceinline__ double vol_record_t(const DevScene& S, const DevVolume& vg, bool staged, int32_t p, v3 o,
-                                               v3 d, int32_t& kind, double& tobj, uint32_t& n) {
+__device__ __forceinline__ double vol_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj,
+                                               uint32_t& n) {
     const float4* r = S.ana_recs + 3 * (size_t)p;
     kind = (int32_t)f2u(r[0].w);
     double t;
     if (kind == KIND_VOLUME) {
-        t = vol_t(staged ? vg : S.volumes[rec_ext(r)], o, d, &n);
+        t = vol_t(S.volumes[rec_ext(r)], o, d, &n);
         tobj = t;
     } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
         const DevXform& X = S.xforms[rec_ext(r)];
         const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
-        t = vol_t(staged ? vg : S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, &n);
+        t = vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, &n);
         tobj = t;
         if (t < kHitInf) {
             const v3 position = mat_position(X.m, add(so, muls(sd, t)));
@@ -440,7 +417,6 @@ __device__ __forceinline__ double vol_record_t(const DevScene& S, const DevVolum
 // the traversal's order, the Volume's march before the SDF).  A wave takes 64 entries and marches their
 // Volumes one at a time with all its lanes (march_pending, the cooperative march), in a kernel that
 // holds nothing else and so runs more waves than the FULL kernel that found them.
-template <bool STAGED>
 __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, WfQueues Q, int qi) {
     const uint32_t n = min(Q.counts[kSdfWord], Q.cap);
     const bool env_black = S.env_tex < 0 && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
@@ -448,7 +424,6 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t gained = 0;   // misses that became hits: rays with work for k_wf_shade (kept_word)
     uint32_t samples = 0;  // Volume.Sample calls (counted passes; the cooperative march counts its own)
-    const DevVolume vl = STAGED ? stage_volume(S) : DevVolume{};
     for (uint32_t k0 = w * 64u; k0 < n; k0 += nw * 64u) {   // wave-uniform: every lane takes part in the march
         const uint32_t k = k0 + lane;
         int32_t pend = k < n ? (int32_t)Q.volq[k] : -1;
@@ -472,12 +447,12 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
                 int32_t kind;
                 double tx = 0;
                 uint32_t ns = 0;
-                const double t = vol_record_t(S, vl, STAGED, pend, o, d, kind, tx, ns);
+                const double t = vol_record_t(S, pend, o, d, kind, tx, ns);
                 samples += ns;
                 if (t < best.t || (t == best.t && best.kind == KIND_TRI)) { best.t = t; best.kind = kind; best.idx = pend; best.tx = tx; }
             }
         } else {
-            march_coop<false, true, STAGED>(S, o, d, pend, best, nullptr, vl);
+            march_coop<false, true>(S, o, d, pend, best, nullptr);
         }
         if (pend >= 0 && best.idx == pend && (best.kind == KIND_VOLUME || best.kind == KIND_XFORM)) {   // nearer
             const unsigned long long tb = (unsigned long long)__double_as_longlong(best.kind == KIND_XFORM ? best.tx : best.t);
@@ -494,13 +469,11 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
 }
 // The Volume records split shadow rays deferred: blocked (unlit) when the march's t is nearer than
 // the light; k_wf_sdf_shadow then skips the ray.
-template <bool STAGED>
 __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S, WfQueues Q, int qo) {
     const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t samples = 0;
-    const DevVolume vl = STAGED ? stage_volume(S) : DevVolume{};
     for (uint32_t k0 = w * 64u; k0 < n; k0 += nw * 64u) {   // wave-uniform
         const uint32_t k = k0 + lane;
         int32_t pend = k < n ? (int32_t)Q.volq_sh[k] : -1;
@@ -521,11 +494,11 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S,
                 int32_t kind;
                 double tx = 0;
                 uint32_t ns = 0;
-                blocked = vol_record_t(S, vl, STAGED, pend, o, d, kind, tx, ns) < best.t;
+                blocked = vol_record_t(S, pend, o, d, kind, tx, ns) < best.t;
                 samples += ns;
             }
         } else {
-            march_coop<true, true, STAGED>(S, o, d, pend, best, &blocked, vl);
+            march_coop<true, true>(S, o, d, pend, best, &blocked);
         }
         if (pend >= 0 && blocked) Q.n_lit[qo][e.x] = 0;
     }
@@ -1681,10 +1654,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
-            if (Q.volq && S.vol_lds > 0)
-                hipLaunchKernelGGL(k_wf_vol_hits<true>, dim3(grid_for(n, 256, 2048)), dim3(256), (size_t)S.vol_lds, stream, S, Q, qi);
-            else if (Q.volq)
-                hipLaunchKernelGGL(k_wf_vol_hits<false>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
+            if (Q.volq) hipLaunchKernelGGL(k_wf_vol_hits, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
             if (S.num_sdf > 0 && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_hits<true>, dim3(grid_for(n, 256, 8192)), dim3(256), (size_t)S.sdf_lds, stream, S, Q, qi);
             else if (S.num_sdf > 0)
@@ -1749,12 +1719,9 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
-            if (Q.volq_sh && S.vol_lds > 0)
-                hipLaunchKernelGGL(k_wf_vol_shadow<true>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256),
-                                   (size_t)S.vol_lds, side, S, Q, 1 - qi);
-            else if (Q.volq_sh)
-                hipLaunchKernelGGL(k_wf_vol_shadow<false>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)),
-                                   dim3(256), 0, side, S, Q, 1 - qi);
+            if (Q.volq_sh)
+                hipLaunchKernelGGL(k_wf_vol_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256), 0,
+                                   side, S, Q, 1 - qi);
             if (sq && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_shadow<true>, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256),
                                    (size_t)S.sdf_lds, side, S, Q, 1 - qi);
