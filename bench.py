@@ -353,10 +353,14 @@ def main(argv=None):
     full = fullg or len(fl.texture_list) > 0 or fl.env_texture > 0   # (1-based texture slots, 0 = none)
     lanes = st.bvh_nodes - 1 > 64
     # (row-4 scenes with a mesh split each traversal: the lean refill kernel <false, true>, then the FULL
-    # kernel <false, true, true>; the class below times both)
-    trace_name = ("k_wf_trace<false, true>" if fullg else "k_wf_trace_lanes<false, false>" if lanes
+    # kernel <false, true, true> on the rays that reach a row-4 box, then the deferred Volume and SDF
+    # records' kernels; the class times them together)
+    split = fullg and lanes
+    trace_name = ("k_wf_trace_lanes<false, true> + k_wf_trace<false, true, true> + k_wf_vol_hits + k_wf_sdf_hits"
+                  if split else "k_wf_trace<false, true>" if fullg else "k_wf_trace_lanes<false, false>" if lanes
                   else "k_wf_trace<false, false>")
-    shadow_name = ("k_wf_shadow<false, true>" if fullg else "k_wf_shadow_lanes<false, false>" if lanes
+    shadow_name = ("k_wf_shadow_lanes<false, true> + k_wf_shadow<false, true, true> + k_wf_vol_shadow + k_wf_sdf_shadow"
+                   if split else "k_wf_shadow<false, true>" if fullg else "k_wf_shadow_lanes<false, false>" if lanes
                    else "k_wf_shadow<false, false>")
     shade_name = "k_wf_shade<false, true, *>" if full else "k_wf_shade<false, false, *>"
 
