@@ -1235,13 +1235,14 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     bool hpend = false;
     // a root ray found nothing nearer than its light: lit (a phantom light never is); under the routed
     // split, provisionally when the ray reaches a heavy box (the FULL half decides: k_wf_shadow<.., SPLIT>)
+    // (the box test runs here, on this lane's own ray: in the tail a lane that reported may turn helper and
+    // take another root's ray into o / invd before the loop top)
     auto report_lit = [&]() {
         Q.n_lit[qo][i] = phantom ? 0 : 1;
-        if (route && !phantom) hpend = true;   // the heavy-box test at the loop top
+        if (route && !phantom) hpend = heavy_reach(S, o, invd, tmax);
     };
     for (;;) {
         if (route) {   // wave-uniform: the provisionally lit rays that reach a heavy box, one atomic per wave
-            if (hpend) hpend = heavy_reach(S, o, invd, tmax);
             const uint64_t hm = __ballot(hpend);
             if (hm) {
                 const int lead = __builtin_ctzll(hm);
