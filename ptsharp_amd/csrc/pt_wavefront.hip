@@ -389,20 +389,20 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 #ifndef PT_VOL_SERIAL
 #define PT_VOL_SERIAL 0   // k_wf_vol_*: 1 each lane marches its own entry (vol_t); 0: the wave's lanes march one entry together
 #endif
-// Intersect of Volume record p (a Volume, or a TransformedShape of one) by this lane alone: vol_t, the
-// reference's loop (prim_t's t; tobj: the inner t of a TransformedShape).  `n`: its Volume.Sample calls.
+// Intersect of Volume record p (a Volume, or a TransformedShape of one) by this lane alone: the reference's
+// loop (vol_t_runs; prim_t's t; tobj: the inner t of a TransformedShape).  `n`: its Volume.Sample calls.
 __device__ __forceinline__ double vol_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj,
                                                uint32_t& n) {
     const float4* r = S.ana_recs + 3 * (size_t)p;
     kind = (int32_t)f2u(r[0].w);
     double t;
     if (kind == KIND_VOLUME) {
-        t = vol_t(S.volumes[rec_ext(r)], o, d, &n);
+        t = vol_t_runs(S.volumes[rec_ext(r)], o, d, &n);
         tobj = t;
     } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
         const DevXform& X = S.xforms[rec_ext(r)];
         const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
-        t = vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, &n);
+        t = vol_t_runs(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, &n);
         tobj = t;
         if (t < kHitInf) {
             const v3 position = mat_position(X.m, add(so, muls(sd, t)));
