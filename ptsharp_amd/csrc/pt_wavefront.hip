@@ -412,6 +412,129 @@ __device__ __forceinline__ double vol_record_t(const DevScene& S, int32_t p, v3 
     return t;
 }
 
+// PT_VOL_SERIAL 2: the deferred Volume records marched one per lane with per-lane refill (as the
+// traversal kernels): the reference loop (vol_t_runs) unrolled into one position per step of a single
+// loop, so a lane whose march is done takes the next entry instead of waiting for the wave's longest
+// march.  ANY: shadow entries (blocked when nearer than the light's t), else closest-hit entries (merged
+// as k_wf_vol_hits does).  q: the ray queue (closest) or shadow set (ANY).
+template <bool ANY>
+__global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_refill(DevScene S, WfQueues Q, int q) {
+    const uint32_t n = ANY ? min(Q.counts[sdf_sh_word(q)], Q.s_cap) : min(Q.counts[kSdfWord], Q.cap);
+    const uint4* const E = ANY ? Q.sdfq_sh : Q.sdfq;
+    const uint32_t* const V = ANY ? Q.volq_sh : Q.volq;
+    uint32_t* const cursor = Q.counts + vol_cur_word(ANY ? 1 : 0, q);
+    const bool env_black = S.env_tex < 0 && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t gained = 0, samples = 0;
+    bool has = false, more = true;
+    uint32_t k = 0;              // this lane's entry
+    int32_t rec = -1, xf = -1;   // its Volume record; the TransformedShape's xform index (-1: none)
+    v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f};   // the ray in the Volume's space
+    double t = 0, tmax = 0, step = 0;
+    int sign = -1, iters = 0, ri = -1, pend_sign = 0;   // ri: -1 coarse steps, 0..63 the refinement's
+    auto finish = [&](double tv) {   // the march's t (kHitInf: none), as prim_t returns it
+        has = false;
+        const uint4 e = E[k];
+        double tw = tv;
+        if (tv < kHitInf && xf >= 0) {   // TransformedShape.Intersect: back to world space (TransformedShape.cs:43-73)
+            const DevXform& X = S.xforms[xf];
+            const float4 ao = ANY ? nt_load(&Q.n_o[q][e.x]) : nt_load(&Q.q_o[q][e.x]);
+            const v3 position = mat_position(X.m, add(o, muls(d, tv)));
+            tw = (double)lengthf(sub(position, v3{ao.x, ao.y, ao.z}));
+        }
+        const double bt = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
+        if (ANY) {
+            if (tw < bt) Q.n_lit[q][e.x] = 0;
+            return;
+        }
+        const uint4 hr = Q.hits[e.x];
+        const int32_t hk = (int32_t)hr.z;
+        if (tw < bt || (tw == bt && hk == KIND_TRI)) {
+            const int32_t kind = xf >= 0 ? KIND_XFORM : KIND_VOLUME;
+            const unsigned long long tb = (unsigned long long)__double_as_longlong(xf >= 0 ? tv : tw);
+            hit_store(&Q.hits[e.x], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)kind, (uint32_t)rec));
+            const unsigned long long twb = (unsigned long long)__double_as_longlong(tw);
+            Q.sdfq[k] = make_uint4(e.x, e.y, (uint32_t)twb, (uint32_t)(twb >> 32));
+            gained += (hk < 0 && env_black) ? 1u : 0u;
+        }
+    };
+    for (;;) {
+        const uint64_t idle = __ballot(!has);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (more && (nidle >= 32u || nidle == 64u)) {   // wave-uniform
+            uint32_t kc = 0;
+            if (lane == 0) kc = atomicAdd(cursor, nidle);
+            kc = __builtin_amdgcn_readfirstlane(kc);
+            const uint32_t kk = kc + (uint32_t)__popcll(idle & below);
+            if (kc + nidle >= n) more = false;
+            if (!has && kk < n && (int32_t)V[kk] >= 0) {
+                k = kk;
+                rec = (int32_t)V[kk];
+                const uint32_t slot = E[kk].x;
+                const float4 a = ANY ? nt_load(&Q.n_o[q][slot]) : nt_load(&Q.q_o[q][slot]);
+                const float4 b = ANY ? nt_load(&Q.n_n[q][slot]) : nt_load(&Q.q_d[q][slot]);
+                o = v3{a.x, a.y, a.z};
+                d = v3{b.x, b.y, b.z};
+                const float4* r = S.ana_recs + 3 * (size_t)rec;
+                int32_t vi;
+                if ((int32_t)f2u(r[0].w) == KIND_XFORM) {   // the inner Volume, in its own space
+                    xf = rec_ext(r);
+                    const DevXform& X = S.xforms[xf];
+                    o = mat_position(X.inv, v3{a.x, a.y, a.z});
+                    d = mat_direction(X.inv, v3{b.x, b.y, b.z});
+                    vi = rec_ext(S.ext_recs + 3 * (size_t)X.rec);
+                } else {
+                    xf = -1;
+                    vi = rec_ext(r);
+                }
+                const DevVolume& v = S.volumes[vi];
+                double tmin;
+                box_span(v.bmin, v.bmax, o, d, tmin, tmax);
+                step = (double)(1.0f / 512.0f);
+                t = net_max(step, tmin);
+                sign = -1; iters = 0; ri = -1;
+                has = true;
+            }
+        }
+        if (!more && __ballot(has) == 0ull) break;
+        if (!has) continue;
+        // one position of Volume.Intersect's loop (Volume.cs:168-197; vol_t_runs)
+        const float4* r = S.ana_recs + 3 * (size_t)rec;
+        const DevVolume& v = S.volumes[xf >= 0 ? rec_ext(S.ext_recs + 3 * (size_t)S.xforms[xf].rec) : rec_ext(r)];
+        if (ri < 0) {
+            if (!(t <= tmax && iters < (1 << 24))) { finish(kHitInf); continue; }
+            samples++;
+            const int sg = vol_sign_fast(v, o, d, t);
+            if (sg == 0 || (sign >= 0 && sg != sign)) {   // the refinement
+                t -= step;
+                step /= 64;
+                t += step;
+                ri = 0;
+                pend_sign = sg;
+            } else {
+                sign = sg;
+                t += step;
+                iters++;
+            }
+        } else {
+            samples++;
+            if (vol_sign_fast(v, o, d, t) == 0) { finish(t - step); continue; }
+            t += step;
+            if (++ri == 64) {   // no zero: the loop goes on at the fine step
+                ri = -1;
+                sign = pend_sign;
+                t += step;
+                iters++;
+            }
+        }
+    }
+    gained = wave_sum(gained);
+    if (!ANY && lane == 0 && gained) atomicAdd(Q.counts + kept_word(q), gained);
+    samples = wave_sum(samples);
+    if (S.march && lane == 0 && samples) atomicAdd(S.march, (unsigned long long)samples);
+}
+
 // The Volume records the analytic half of a split closest hit deferred (trace_ana / trace_heavy
 // vol_out), merged before the entry's SDF record (k_wf_sdf_hits then reads the t this kernel lowered:
 // the traversal's order, the Volume's march before the SDF).  A wave takes 64 entries and marches their
@@ -1018,6 +1141,8 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         Q.counts[fetch_word(4, threadIdx.x)] = 0u;              // its analytic half's (split)
         if (threadIdx.x == 0) Q.counts[kSdfWord] = 0u;          // and that half's SDF queue
         Q.counts[heavy_word(threadIdx.x)] = 0u;                 // and the routed split's heavy queue
+        if (threadIdx.x == 0) Q.counts[vol_cur_word(0, 0)] = 0u;   // and its Volume queue's claim cursor
+        if (threadIdx.x == 0) Q.counts[vol_cur_word(1, 1 - qi)] = 0u;   // (that of the shadow set it writes)
         Q.counts[heavy_sh_word(1 - qi, threadIdx.x)] = 0u;      // the shadow set it writes: its heavy queue
         if (threadIdx.x == 0) Q.counts[sdf_sh_word(1 - qi)] = 0u;   // and its SDF queue
         Q.counts[fetch_word(5 + (1 - qi), threadIdx.x)] = 0u;   // the split shadow rays' analytic half
@@ -1655,7 +1780,10 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
-            if (Q.volq) hipLaunchKernelGGL(k_wf_vol_hits, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
+            if (Q.volq && PT_VOL_SERIAL == 2)
+                hipLaunchKernelGGL((k_wf_vol_refill<false>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
+            else if (Q.volq)
+                hipLaunchKernelGGL(k_wf_vol_hits, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
             if (S.num_sdf > 0 && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_hits<true>, dim3(grid_for(n, 256, 8192)), dim3(256), (size_t)S.sdf_lds, stream, S, Q, qi);
             else if (S.num_sdf > 0)
@@ -1720,7 +1848,10 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
-            if (Q.volq_sh)
+            if (Q.volq_sh && PT_VOL_SERIAL == 2)
+                hipLaunchKernelGGL((k_wf_vol_refill<true>), dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256),
+                                   0, side, S, Q, 1 - qi);
+            else if (Q.volq_sh)
                 hipLaunchKernelGGL(k_wf_vol_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256), 0,
                                    side, S, Q, 1 - qi);
             if (sq && S.sdf_lds > 0)
