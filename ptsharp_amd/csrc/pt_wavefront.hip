@@ -429,7 +429,7 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_refill(DevScene S,
     uint32_t gained = 0, samples = 0;
     bool has = false, more = true;
     uint32_t k = 0;              // this lane's entry
-    int32_t rec = -1, xf = -1;   // its Volume record; the TransformedShape's xform index (-1: none)
+    int32_t rec = -1, xf = -1, vi = 0;   // its Volume record; the TransformedShape's xform index (-1: none); the Volume
     v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f};   // the ray in the Volume's space
     double t = 0, tmax = 0, step = 0;
     int sign = -1, iters = 0, ri = -1, pend_sign = 0;   // ri: -1 coarse steps, 0..63 the refinement's
@@ -477,7 +477,6 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_refill(DevScene S,
                 o = v3{a.x, a.y, a.z};
                 d = v3{b.x, b.y, b.z};
                 const float4* r = S.ana_recs + 3 * (size_t)rec;
-                int32_t vi;
                 if ((int32_t)f2u(r[0].w) == KIND_XFORM) {   // the inner Volume, in its own space
                     xf = rec_ext(r);
                     const DevXform& X = S.xforms[xf];
@@ -500,8 +499,7 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_refill(DevScene S,
         if (!more && __ballot(has) == 0ull) break;
         if (!has) continue;
         // one position of Volume.Intersect's loop (Volume.cs:168-197; vol_t_runs)
-        const float4* r = S.ana_recs + 3 * (size_t)rec;
-        const DevVolume& v = S.volumes[xf >= 0 ? rec_ext(S.ext_recs + 3 * (size_t)S.xforms[xf].rec) : rec_ext(r)];
+        const DevVolume& v = S.volumes[vi];
         if (ri < 0) {
             if (!(t <= tmax && iters < (1 << 24))) { finish(kHitInf); continue; }
             samples++;
