@@ -412,6 +412,10 @@ __device__ __forceinline__ double vol_record_t(const DevScene& S, int32_t p, v3 
     return t;
 }
 
+#ifndef PT_VOL_JUMP
+#define PT_VOL_JUMP 24   // positions a lane's march may pass in one step over uniform cells (a cell spans ~32)
+#endif
+constexpr int kVolJump = PT_VOL_JUMP;
 // PT_VOL_SERIAL 2: the deferred Volume records marched one per lane with per-lane refill (as the
 // traversal kernels): the reference loop (vol_t_runs) unrolled into one position per step of a single
 // loop, so a lane whose march is done takes the next entry instead of waiting for the wave's longest
@@ -502,6 +506,21 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_refill(DevScene S,
         const DevVolume& v = S.volumes[vi];
         if (ri < 0) {
             if (!(t <= tmax && iters < (1 << 24))) { finish(kHitInf); continue; }
+            if (v.runs) {   // a run of uniform cells: the next kVolJump positions in one step (coop_vol_t's strided pass)
+                const VolKey k0 = vol_key(v, o, d, t);
+                const int s0 = vol_key_sign(v, k0);
+                if (s0 > 0 && (sign < 0 || s0 == sign)) {
+                    const double tj = t_after(t, step, kVolJump);
+                    if (tj <= tmax && iters + kVolJump < (1 << 24) && vol_box_sign(v, k0, vol_key(v, o, d, tj), s0)) {
+                        // positions t .. tj all lie in cells of Sign s0: none acts
+                        samples += kVolJump + 1;
+                        sign = s0;
+                        t = tj + step;
+                        iters += kVolJump + 1;
+                        continue;
+                    }
+                }
+            }
             samples++;
             const int sg = vol_sign_fast(v, o, d, t);
             if (sg == 0 || (sign >= 0 && sg != sign)) {   // the refinement

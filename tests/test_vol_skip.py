@@ -19,5 +19,5 @@ def test_vol_skip_bit_identical():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "t_after: 200000 cases, 0 differences" in r.stdout
-    assert "(strides 8, 16, 32), emulated: 0 differences" in r.stdout
+    assert "and the lane march with jumps (8, 24, 40), emulated: 0 differences" in r.stdout
     assert " 0 differences;" in r.stdout.splitlines()[-1]
