@@ -442,36 +442,6 @@ __device__ __forceinline__ int vol_sign_fast(const DevVolume& v, v3 o, v3 d, dou
     }
     return vol_sign(v, add(o, muls(d, t)));
 }
-// vol_t with vol_sign_fast's Sign: a position in a uniform cell (vol_build_runs) takes the cell's Sign
-// from the table instead of the eight corner reads and the interpolation; the positions, the actions
-// and the t returned are vol_t's (the cooperative march relies on the same table).
-__device__ __forceinline__ double vol_t_runs(const DevVolume& v, v3 o, v3 d, uint32_t* samples) {
-    double tmin, tmax;
-    box_span(v.bmin, v.bmax, o, d, tmin, tmax);
-    double step = (double)(1.0f / 512.0f);
-    const double start = net_max(step, tmin);
-    int sign = -1, iters = 0;
-    uint32_t n = 0;
-    auto sign_at = [&](double t) { n++; return vol_sign_fast(v, o, d, t); };
-    for (double t = start; t <= tmax && iters < (1 << 24); t += step, iters++) {
-        const int sg = sign_at(t);
-        if (sg == 0 || (sign >= 0 && sg != sign)) {
-            t -= step;
-            step /= 64;
-            t += step;
-            for (int i = 0; i < 64; i++) {
-                if (sign_at(t) == 0) {
-                    *samples = n;
-                    return t - step;
-                }
-                t += step;
-            }
-        }
-        sign = sg;
-    }
-    *samples = n;
-    return kHitInf;
-}
 // Every cell of the index box spanned by cells a and b (at most one step apart per axis) has
 // Sign `sign`: then every position between a position in a and a later one in b lies in such a
 // cell (each index is monotone along the ray, so the cells between lie in that box).

@@ -69,8 +69,7 @@ constexpr int kSdfSlot = 10 * kParts + 2;   // entries of Q.sdfq
 constexpr int kSdfShSlot = 10 * kParts + 3;   // two slots (shadow set q): entries of Q.sdfq_sh
 constexpr int kHeavySlot = 10 * kParts + 5;     // kParts slots: entries of Q.hq per partition
 constexpr int kHeavyShSlot = 11 * kParts + 5;  // 2 x kParts slots (shadow set q): entries of Q.hq_sh per partition
-constexpr int kVolCurSlot = 13 * kParts + 5;   // three slots: k_wf_vol_refill's claim cursors (closest hit, shadow set q)
-constexpr int kEndSlot = 13 * kParts + 8;
+constexpr int kEndSlot = 13 * kParts + 5;
 constexpr int count_word(int slot) { return slot * kCountStride; }
 constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kCountWords = count_word(kEndSlot);
@@ -87,7 +86,6 @@ constexpr int kSdfWord = count_word(kSdfSlot);
 // hipMemsetAsync: a fill kernel queued behind the other stream's persistent grid waits for a free CU
 // and holds its stream (C5: 500 such fills per pass, 0.47 ms each).
 constexpr int sdf_sh_word(int q) { return count_word(kSdfShSlot + q); }
-constexpr int vol_cur_word(int any, int q) { return count_word(kVolCurSlot + (any ? 1 + q : 0)); }
 constexpr int heavy_word(int g) { return count_word(kHeavySlot + g); }
 constexpr int heavy_sh_word(int q, int g) { return count_word(kHeavyShSlot + q * kParts + g); }
 

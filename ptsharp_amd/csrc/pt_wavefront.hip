@@ -386,172 +386,6 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 #ifndef PT_VOL_WAVES
 #define PT_VOL_WAVES 4   // the cooperative march needs ~130 VGPRs (5 / 6 / 8 waves: 37-146 spilled)
 #endif
-#ifndef PT_VOL_SERIAL
-#define PT_VOL_SERIAL 0   // k_wf_vol_*: 1 each lane marches its own entry (vol_t); 0: the wave's lanes march one entry together
-#endif
-// Intersect of Volume record p (a Volume, or a TransformedShape of one) by this lane alone: the reference's
-// loop (vol_t_runs; prim_t's t; tobj: the inner t of a TransformedShape).  `n`: its Volume.Sample calls.
-__device__ __forceinline__ double vol_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj,
-                                               uint32_t& n) {
-    const float4* r = S.ana_recs + 3 * (size_t)p;
-    kind = (int32_t)f2u(r[0].w);
-    double t;
-    if (kind == KIND_VOLUME) {
-        t = vol_t_runs(S.volumes[rec_ext(r)], o, d, &n);
-        tobj = t;
-    } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
-        const DevXform& X = S.xforms[rec_ext(r)];
-        const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
-        t = vol_t_runs(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, &n);
-        tobj = t;
-        if (t < kHitInf) {
-            const v3 position = mat_position(X.m, add(so, muls(sd, t)));
-            t = (double)lengthf(sub(position, o));
-        }
-    }
-    return t;
-}
-
-#ifndef PT_VOL_JUMP
-#define PT_VOL_JUMP 24   // positions a lane's march may pass in one step over uniform cells (a cell spans ~32)
-#endif
-constexpr int kVolJump = PT_VOL_JUMP;
-// PT_VOL_SERIAL 2: the deferred Volume records marched one per lane with per-lane refill (as the
-// traversal kernels): the reference loop (vol_t_runs) unrolled into one position per step of a single
-// loop, so a lane whose march is done takes the next entry instead of waiting for the wave's longest
-// march.  ANY: shadow entries (blocked when nearer than the light's t), else closest-hit entries (merged
-// as k_wf_vol_hits does).  q: the ray queue (closest) or shadow set (ANY).
-template <bool ANY>
-__global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_refill(DevScene S, WfQueues Q, int q) {
-    const uint32_t n = ANY ? min(Q.counts[sdf_sh_word(q)], Q.s_cap) : min(Q.counts[kSdfWord], Q.cap);
-    const uint4* const E = ANY ? Q.sdfq_sh : Q.sdfq;
-    const uint32_t* const V = ANY ? Q.volq_sh : Q.volq;
-    uint32_t* const cursor = Q.counts + vol_cur_word(ANY ? 1 : 0, q);
-    const bool env_black = S.env_tex < 0 && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t below = (1ull << lane) - 1ull;
-    uint32_t gained = 0, samples = 0;
-    bool has = false, more = true;
-    uint32_t k = 0;              // this lane's entry
-    int32_t rec = -1, xf = -1, vi = 0;   // its Volume record; the TransformedShape's xform index (-1: none); the Volume
-    v3 o{0.f, 0.f, 0.f}, d{0.f, 0.f, 0.f};   // the ray in the Volume's space
-    double t = 0, tmax = 0, step = 0;
-    int sign = -1, iters = 0, ri = -1, pend_sign = 0;   // ri: -1 coarse steps, 0..63 the refinement's
-    auto finish = [&](double tv) {   // the march's t (kHitInf: none), as prim_t returns it
-        has = false;
-        const uint4 e = E[k];
-        double tw = tv;
-        if (tv < kHitInf && xf >= 0) {   // TransformedShape.Intersect: back to world space (TransformedShape.cs:43-73)
-            const DevXform& X = S.xforms[xf];
-            const float4 ao = ANY ? nt_load(&Q.n_o[q][e.x]) : nt_load(&Q.q_o[q][e.x]);
-            const v3 position = mat_position(X.m, add(o, muls(d, tv)));
-            tw = (double)lengthf(sub(position, v3{ao.x, ao.y, ao.z}));
-        }
-        const double bt = __longlong_as_double((long long)(((unsigned long long)e.w << 32) | e.z));
-        if (ANY) {
-            if (tw < bt) Q.n_lit[q][e.x] = 0;
-            return;
-        }
-        const uint4 hr = Q.hits[e.x];
-        const int32_t hk = (int32_t)hr.z;
-        if (tw < bt || (tw == bt && hk == KIND_TRI)) {
-            const int32_t kind = xf >= 0 ? KIND_XFORM : KIND_VOLUME;
-            const unsigned long long tb = (unsigned long long)__double_as_longlong(xf >= 0 ? tv : tw);
-            hit_store(&Q.hits[e.x], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)kind, (uint32_t)rec));
-            const unsigned long long twb = (unsigned long long)__double_as_longlong(tw);
-            Q.sdfq[k] = make_uint4(e.x, e.y, (uint32_t)twb, (uint32_t)(twb >> 32));
-            gained += (hk < 0 && env_black) ? 1u : 0u;
-        }
-    };
-    for (;;) {
-        const uint64_t idle = __ballot(!has);
-        const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (more && (nidle >= 32u || nidle == 64u)) {   // wave-uniform
-            uint32_t kc = 0;
-            if (lane == 0) kc = atomicAdd(cursor, nidle);
-            kc = __builtin_amdgcn_readfirstlane(kc);
-            const uint32_t kk = kc + (uint32_t)__popcll(idle & below);
-            if (kc + nidle >= n) more = false;
-            if (!has && kk < n && (int32_t)V[kk] >= 0) {
-                k = kk;
-                rec = (int32_t)V[kk];
-                const uint32_t slot = E[kk].x;
-                const float4 a = ANY ? nt_load(&Q.n_o[q][slot]) : nt_load(&Q.q_o[q][slot]);
-                const float4 b = ANY ? nt_load(&Q.n_n[q][slot]) : nt_load(&Q.q_d[q][slot]);
-                o = v3{a.x, a.y, a.z};
-                d = v3{b.x, b.y, b.z};
-                const float4* r = S.ana_recs + 3 * (size_t)rec;
-                if ((int32_t)f2u(r[0].w) == KIND_XFORM) {   // the inner Volume, in its own space
-                    xf = rec_ext(r);
-                    const DevXform& X = S.xforms[xf];
-                    o = mat_position(X.inv, v3{a.x, a.y, a.z});
-                    d = mat_direction(X.inv, v3{b.x, b.y, b.z});
-                    vi = rec_ext(S.ext_recs + 3 * (size_t)X.rec);
-                } else {
-                    xf = -1;
-                    vi = rec_ext(r);
-                }
-                const DevVolume& v = S.volumes[vi];
-                double tmin;
-                box_span(v.bmin, v.bmax, o, d, tmin, tmax);
-                step = (double)(1.0f / 512.0f);
-                t = net_max(step, tmin);
-                sign = -1; iters = 0; ri = -1;
-                has = true;
-            }
-        }
-        if (!more && __ballot(has) == 0ull) break;
-        if (!has) continue;
-        // one position of Volume.Intersect's loop (Volume.cs:168-197; vol_t_runs)
-        const DevVolume& v = S.volumes[vi];
-        if (ri < 0) {
-            if (!(t <= tmax && iters < (1 << 24))) { finish(kHitInf); continue; }
-            if (v.runs) {   // a run of uniform cells: the next kVolJump positions in one step (coop_vol_t's strided pass)
-                const VolKey k0 = vol_key(v, o, d, t);
-                const int s0 = vol_key_sign(v, k0);
-                if (s0 > 0 && (sign < 0 || s0 == sign)) {
-                    const double tj = t_after(t, step, kVolJump);
-                    if (tj <= tmax && iters + kVolJump < (1 << 24) && vol_box_sign(v, k0, vol_key(v, o, d, tj), s0)) {
-                        // positions t .. tj all lie in cells of Sign s0: none acts
-                        samples += kVolJump + 1;
-                        sign = s0;
-                        t = tj + step;
-                        iters += kVolJump + 1;
-                        continue;
-                    }
-                }
-            }
-            samples++;
-            const int sg = vol_sign_fast(v, o, d, t);
-            if (sg == 0 || (sign >= 0 && sg != sign)) {   // the refinement
-                t -= step;
-                step /= 64;
-                t += step;
-                ri = 0;
-                pend_sign = sg;
-            } else {
-                sign = sg;
-                t += step;
-                iters++;
-            }
-        } else {
-            samples++;
-            if (vol_sign_fast(v, o, d, t) == 0) { finish(t - step); continue; }
-            t += step;
-            if (++ri == 64) {   // no zero: the loop goes on at the fine step
-                ri = -1;
-                sign = pend_sign;
-                t += step;
-                iters++;
-            }
-        }
-    }
-    gained = wave_sum(gained);
-    if (!ANY && lane == 0 && gained) atomicAdd(Q.counts + kept_word(q), gained);
-    samples = wave_sum(samples);
-    if (S.march && lane == 0 && samples) atomicAdd(S.march, (unsigned long long)samples);
-}
-
 // The Volume records the analytic half of a split closest hit deferred (trace_ana / trace_heavy
 // vol_out), merged before the entry's SDF record (k_wf_sdf_hits then reads the t this kernel lowered:
 // the traversal's order, the Volume's march before the SDF).  A wave takes 64 entries and marches their
@@ -563,7 +397,6 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     uint32_t gained = 0;   // misses that became hits: rays with work for k_wf_shade (kept_word)
-    uint32_t samples = 0;  // Volume.Sample calls (counted passes; the cooperative march counts its own)
     for (uint32_t k0 = w * 64u; k0 < n; k0 += nw * 64u) {   // wave-uniform: every lane takes part in the march
         const uint32_t k = k0 + lane;
         int32_t pend = k < n ? (int32_t)Q.volq[k] : -1;
@@ -582,18 +415,7 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
             d = v3{b.x, b.y, b.z};
         }
         const int32_t kind0 = best.kind;
-        if (PT_VOL_SERIAL) {
-            if (pend >= 0) {
-                int32_t kind;
-                double tx = 0;
-                uint32_t ns = 0;
-                const double t = vol_record_t(S, pend, o, d, kind, tx, ns);
-                samples += ns;
-                if (t < best.t || (t == best.t && best.kind == KIND_TRI)) { best.t = t; best.kind = kind; best.idx = pend; best.tx = tx; }
-            }
-        } else {
-            march_coop<false, true>(S, o, d, pend, best, nullptr);
-        }
+        march_coop<false, true>(S, o, d, pend, best, nullptr);
         if (pend >= 0 && best.idx == pend && (best.kind == KIND_VOLUME || best.kind == KIND_XFORM)) {   // nearer
             const unsigned long long tb = (unsigned long long)__double_as_longlong(best.kind == KIND_XFORM ? best.tx : best.t);
             hit_store(&Q.hits[e.x], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)best.kind, (uint32_t)pend));
@@ -604,8 +426,6 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
     }
     gained = wave_sum(gained);
     if (lane == 0 && gained) atomicAdd(Q.counts + kept_word(qi), gained);
-    samples = wave_sum(samples);
-    if (S.march && lane == 0 && samples) atomicAdd(S.march, (unsigned long long)samples);
 }
 // The Volume records split shadow rays deferred: blocked (unlit) when the march's t is nearer than
 // the light; k_wf_sdf_shadow then skips the ray.
@@ -613,7 +433,6 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S,
     const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-    uint32_t samples = 0;
     for (uint32_t k0 = w * 64u; k0 < n; k0 += nw * 64u) {   // wave-uniform
         const uint32_t k = k0 + lane;
         int32_t pend = k < n ? (int32_t)Q.volq_sh[k] : -1;
@@ -629,21 +448,9 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S,
             d = v3{b.x, b.y, b.z};
         }
         bool blocked = false;
-        if (PT_VOL_SERIAL) {
-            if (pend >= 0) {
-                int32_t kind;
-                double tx = 0;
-                uint32_t ns = 0;
-                blocked = vol_record_t(S, pend, o, d, kind, tx, ns) < best.t;
-                samples += ns;
-            }
-        } else {
-            march_coop<true, true>(S, o, d, pend, best, &blocked);
-        }
+        march_coop<true, true>(S, o, d, pend, best, &blocked);
         if (pend >= 0 && blocked) Q.n_lit[qo][e.x] = 0;
     }
-    samples = wave_sum(samples);
-    if (S.march && lane == 0 && samples) atomicAdd(S.march, (unsigned long long)samples);
 }
 
 // The SDF programs (instructions, then parameters: DevSdfIns is 8 B) staged in this block's LDS when
@@ -1158,8 +965,6 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
         Q.counts[fetch_word(4, threadIdx.x)] = 0u;              // its analytic half's (split)
         if (threadIdx.x == 0) Q.counts[kSdfWord] = 0u;          // and that half's SDF queue
         Q.counts[heavy_word(threadIdx.x)] = 0u;                 // and the routed split's heavy queue
-        if (threadIdx.x == 0) Q.counts[vol_cur_word(0, 0)] = 0u;   // and its Volume queue's claim cursor
-        if (threadIdx.x == 0) Q.counts[vol_cur_word(1, 1 - qi)] = 0u;   // (that of the shadow set it writes)
         Q.counts[heavy_sh_word(1 - qi, threadIdx.x)] = 0u;      // the shadow set it writes: its heavy queue
         if (threadIdx.x == 0) Q.counts[sdf_sh_word(1 - qi)] = 0u;   // and its SDF queue
         Q.counts[fetch_word(5 + (1 - qi), threadIdx.x)] = 0u;   // the split shadow rays' analytic half
@@ -1797,10 +1602,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
-            if (Q.volq && PT_VOL_SERIAL == 2)
-                hipLaunchKernelGGL((k_wf_vol_refill<false>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
-            else if (Q.volq)
-                hipLaunchKernelGGL(k_wf_vol_hits, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
+            if (Q.volq) hipLaunchKernelGGL(k_wf_vol_hits, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
             if (S.num_sdf > 0 && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_hits<true>, dim3(grid_for(n, 256, 8192)), dim3(256), (size_t)S.sdf_lds, stream, S, Q, qi);
             else if (S.num_sdf > 0)
@@ -1865,10 +1667,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
-            if (Q.volq_sh && PT_VOL_SERIAL == 2)
-                hipLaunchKernelGGL((k_wf_vol_refill<true>), dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256),
-                                   0, side, S, Q, 1 - qi);
-            else if (Q.volq_sh)
+            if (Q.volq_sh)
                 hipLaunchKernelGGL(k_wf_vol_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256), 0,
                                    side, S, Q, 1 - qi);
             if (sq && S.sdf_lds > 0)

@@ -1,7 +1,6 @@
 // Host check of the Volume marches (ptsharp_amd/csrc/pt_ext.h vol_t / vol_build_runs / t_after):
-// vol_t (the per-lane march), the cooperative march with its strided pass over runs of uniform
-// cells (emulated lane by lane) and the refill kernel's per-lane march with its jumps over uniform
-// runs, against the reference loop of
+// vol_t (the per-lane march) and the cooperative march with its strided pass over runs of uniform
+// cells (emulated lane by lane) against the reference loop of
 // Volume.Intersect (Volume.cs:168-197) restated here position by position, on seeded volumes
 // (smooth blobs with noise and exact-zero regions, the reference's narrow windows, Sample's
 // y-from-z slip) and seeded rays, bit for bit; and t_after against k repeated additions.
@@ -126,56 +125,6 @@ static double coop_emul(const DevVolume& v, v3 o, v3 d, int S) {
     }
 }
 
-// pt_wavefront.hip k_wf_vol_refill's march (PT_VOL_SERIAL 2), one lane: single positions, and over a run of
-// uniform cells J positions in one step when the cells between t and the J-th next position all have the
-// running Sign (the same test as the strided pass).
-static double jump_emul(const DevVolume& v, v3 o, v3 d, int J) {
-    double tmin, tmax;
-    box_span(v.bmin, v.bmax, o, d, tmin, tmax);
-    double step = (double)(1.0f / 512.0f);
-    double t = net_max(step, tmin);
-    int sign = -1, iters = 0, ri = -1, pend = 0;
-    for (;;) {
-        if (ri < 0) {
-            if (!(t <= tmax && iters < (1 << 24))) return kHitInf;
-            if (v.runs) {
-                const VolKey k0 = vol_key(v, o, d, t);
-                const int s0 = vol_key_sign(v, k0);
-                if (s0 > 0 && (sign < 0 || s0 == sign)) {
-                    const double tj = t_after(t, step, J);
-                    if (tj <= tmax && iters + J < (1 << 24) && box_sign(v, k0, vol_key(v, o, d, tj), s0)) {
-                        sign = s0;
-                        t = tj + step;
-                        iters += J + 1;
-                        continue;
-                    }
-                }
-            }
-            const int sg = sign_fast(v, o, d, t);
-            if (sg == 0 || (sign >= 0 && sg != sign)) {
-                t -= step;
-                step /= 64;
-                t += step;
-                ri = 0;
-                pend = sg;
-            } else {
-                sign = sg;
-                t += step;
-                iters++;
-            }
-        } else {
-            if (sign_fast(v, o, d, t) == 0) return t - step;
-            t += step;
-            if (++ri == 64) {
-                ri = -1;
-                sign = pend;
-                t += step;
-                iters++;
-            }
-        }
-    }
-}
-
 int main(int argc, char** argv) {
     const int rays = argc > 1 ? atoi(argv[1]) : 20000;
     std::mt19937_64 rng(12345);
@@ -269,13 +218,6 @@ int main(int argc, char** argv) {
                         cbad++;
                     }
                 }
-                for (int J : {8, 24, 40}) {
-                    const double c = jump_emul(v, o, dir, J);
-                    if (c != b && !(c != c && b != b)) {
-                        if (cbad < 5) printf("vol %d ray %d jump %d: lane march %.17g naive %.17g\n", vi, i, J, c, b);
-                        cbad++;
-                    }
-                }
                 total++;
                 hits += b < kHitInf;
                 if (a != b && !(a != a && b != b)) {
@@ -290,7 +232,7 @@ int main(int argc, char** argv) {
             bad += vbad;
             vi++;
         }
-    printf("cooperative march with the strided pass (strides 8, 16, 32) and the lane march with jumps (8, 24, 40), emulated: %lld differences\n", cbad);
+    printf("cooperative march with the strided pass (strides 8, 16, 32), emulated: %lld differences\n", cbad);
     bad += cbad;
     printf("%lld rays, %lld hits, %lld differences; vol_t %.3f s, the loop as written %.3f s\n", total, hits, bad, t_skip,
            t_naive);

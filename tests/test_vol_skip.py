@@ -3,9 +3,8 @@ vol_t, the per-lane march, equals Volume.Intersect's loop as written
 (Volume.cs:168-197, restated position by position in tests/native/vol_skip_check.cpp) bit for bit
 on seeded volumes and rays, including grazing rays and rays along lattice planes; t_after equals
 k repeated fp64 additions across binade crossings; and the GPU's cooperative march with its strided
-pass over uniform runs (pt_device.h coop_vol_t, kVolStride; its 64 lanes emulated as loops) and the
-refill kernel's per-lane march with its jumps over uniform runs (pt_wavefront.hip k_wf_vol_refill,
-kVolJump) give the same t as the loop as written, at strides 8, 16 and 32 and jumps 8, 24 and 40."""
+pass over uniform runs (pt_device.h coop_vol_t, kVolStride; its 64 lanes emulated as loops) gives
+the same t as the loop as written, at strides 8, 16 and 32."""
 import os
 import subprocess
 
@@ -20,5 +19,5 @@ def test_vol_skip_bit_identical():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "t_after: 200000 cases, 0 differences" in r.stdout
-    assert "and the lane march with jumps (8, 24, 40), emulated: 0 differences" in r.stdout
+    assert "(strides 8, 16, 32), emulated: 0 differences" in r.stdout
     assert " 0 differences;" in r.stdout.splitlines()[-1]
