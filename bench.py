@@ -574,6 +574,17 @@ def main(argv=None):
         },
     }
 
+    def whole_traffic(rays_timed):   # C2 / C5 (kernel "whole pass"): L2-fabric bytes per step, all kernels
+        pw = os.path.join(ROOT, "profiles", f"pmc_traffic_{a.workload}.json")
+        if not os.path.exists(pw):
+            return {"traffic": None}
+        with open(pw) as f:
+            tw = json.load(f)
+        return {"traffic": round(tw["traffic_bytes_per_ray"] * rays_timed / a.steps),
+                "traffic_kind": f"L2-fabric bytes per step, every kernel of the pass (FETCH_SIZE x2 + WRITE_SIZE; "
+                                f"Infinity-Cache hits included), profiles/pmc_traffic_{a.workload}.json ({tw.get('tag')}), "
+                                f"same workload"}
+
     if a.workload == "c5":
         # C5: the marches (Volume.Intersect's fixed 1/512 steps, SDFShape's sphere tracing) are fp64
         # scalar work: the pass' algorithmic flops (BVH nodes and primitive tests in fp32 as C2's,
@@ -584,7 +595,7 @@ def main(argv=None):
         tflops = fl_ray * rays / (kernel_ms * 1e-3) / 1e12
         out["roofline"] = {
             "bound": "valu", "kernel": "whole pass", "achieved": round(tflops, 4), "peak": FP64_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(tflops / FP64_PEAK_TFLOPS, 6), "traffic": None,
+            "unit": "TFLOP/s", "frac": round(tflops / FP64_PEAK_TFLOPS, 6), **whole_traffic(rays),
             "flops_per_ray": round(fl_ray, 2),
             "volume_samples_per_ray": round(ctr.volume_samples / max(ctr.rays, 1), 3),
             "sdf_evals_per_ray": round(ctr.sdf_evals / max(ctr.rays, 1), 3),
@@ -593,6 +604,11 @@ def main(argv=None):
             "flop_model": f"{F_NODE}/BVH4 node, {F_PRIM}/primitive test, {F_SHADE}/shading fetch (fp32), "
                           f"{F_VOX}/Volume.Sample, {F_SDF}/SDF evaluation (fp64)",
         }
+
+    # keys that do not apply to this run are left out rather than null (one GPU: no gather; C2: no mesh)
+    for k in ("gather_check", "mesh_source"):
+        if out["config"].get(k, 0) is None:
+            del out["config"][k]
 
     if a.workload == "c2":
         # C2 is priced in flops against the FP32 vector peak (whole pass), with the
@@ -607,7 +623,7 @@ def main(argv=None):
             valu = vj.get("kernels", {}).get(names[dom], {}).get("valu_issue_frac")
         out["roofline"] = {
             "bound": "valu", "kernel": "whole pass", "achieved": round(tflops, 4), "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(tflops / FP32_PEAK_TFLOPS, 6), "traffic": None,
+            "unit": "TFLOP/s", "frac": round(tflops / FP32_PEAK_TFLOPS, 6), **whole_traffic(rays),
             "flops_per_ray": round(flops_ray, 2),
             "dominant_kernel": names[dom], "dominant_kernel_ms_per_step": round(float(kms[dom]) / a.steps, 3),
             "dominant_kernel_valu_issue_frac": valu,
