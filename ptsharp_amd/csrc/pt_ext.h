@@ -460,6 +460,43 @@ PT_HD int vol_key_sign(const DevVolume& v, VolKey k) {
     if (k.x < -1 || k.y < -1 || k.z < -1 || k.x >= v.w || k.y >= v.h || k.z >= v.d) return v.zero_sign;
     return v.runs[(k.x + 1) + (size_t)(k.y + 1) * (v.w + 1) + (size_t)(k.z + 1) * (v.w + 1) * (v.h + 1)];
 }
+// The Sign of march position t (vol_key_sign of a uniform cell, else Volume.Sign of the sample) with the
+// lattice coordinates computed once: vol_key and Volume.Sample (vol_sample) scale the same position by
+// the same operations, so the key and the sample share them (one fp64 division by zscale, not two).
+PT_HD int vol_sign_at(const DevVolume& v, v3 o, v3 d, double t) {
+    const v3 a = add(o, muls(d, t));   // Ray.Position
+    double x = a.x, z = a.z;
+    z /= v.zscale;
+    x = ((x + 1) / 2) * (double)v.w;
+    double y = ((z + 1) / 2) * (double)v.h;   // Sample's y-from-z slip (Volume.cs:77)
+    z = ((z + 2) / 2) * (double)v.d;
+    if (v.runs) {
+        auto cl = [](double c, int n) {   // vol_key's floor, clamped to -2..n
+            if (!(c > -2.0)) return -2;
+            if (!(c < (double)n)) return n;
+            return (int)floor(c);
+        };
+        const int s = vol_key_sign(v, VolKey{cl(x, v.w), cl(y, v.h), cl(z, v.d)});
+        if (s > 0) return s;
+    }
+    const double lim = 2147483647.0;   // vol_sample from the scaled coordinates on
+    if (!(fabs(x) < lim && fabs(y) < lim && fabs(z) < lim)) return vol_sign_of(v, 0.0);
+    const int x0 = (int)floor(x), y0 = (int)floor(y), z0 = (int)floor(z);
+    const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
+    const double v000 = vol_get(v, x0, y0, z0), v001 = vol_get(v, x0, y0, z1), v010 = vol_get(v, x0, y1, z0);
+    const double v011 = vol_get(v, x0, y1, z1), v100 = vol_get(v, x1, y0, z0), v101 = vol_get(v, x1, y0, z1);
+    const double v110 = vol_get(v, x1, y1, z0), v111 = vol_get(v, x1, y1, z1);
+    x -= (double)x0;
+    y -= (double)y0;
+    z -= (double)z0;
+    const double c00 = v000 * (1 - x) + v100 * x;
+    const double c01 = v001 * (1 - x) + v101 * x;
+    const double c10 = v010 * (1 - x) + v110 * x;
+    const double c11 = v011 * (1 - x) + v111 * x;
+    const double c0 = c00 * (1 - y) + c10 * y;
+    const double c1 = c01 * (1 - y) + c11 * y;
+    return vol_sign_of(v, c0 * (1 - z) + c1 * z);
+}
 // Volume.Intersect (Volume.cs:168-197).  The reference loop has no bound; 2^24 steps
 // stand in for it (a ray that needs more never finishes in the reference either).
 // `samples` (instrumentation, may be null): the Volume.Sample calls the march made.  Each position

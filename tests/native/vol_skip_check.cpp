@@ -130,7 +130,7 @@ int main(int argc, char** argv) {
     std::mt19937_64 rng(12345);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     std::normal_distribution<double> N(0.0, 1.0);
-    long long bad = 0, total = 0, hits = 0, cbad = 0;
+    long long bad = 0, total = 0, hits = 0, cbad = 0, sbad = 0;
     double t_skip = 0, t_naive = 0;
     // t_after against repeated addition, across binade crossings
     for (int i = 0; i < 200000; i++) {
@@ -211,6 +211,19 @@ int main(int argc, char** argv) {
                 const auto c2 = std::chrono::steady_clock::now();
                 t_skip += std::chrono::duration<double>(c1 - c0).count();
                 t_naive += std::chrono::duration<double>(c2 - c1).count();
+                {   // pt_ext.h vol_sign_at (the device march's Sign) against the key and the sample taken apart
+                    double tmn, tmx;
+                    box_span(v.bmin, v.bmax, o, dir, tmn, tmx);
+                    if (tmx > tmn)
+                        for (int j = 0; j < 16; j++) {
+                            const double t = std::fmax(tmn, 0.0) + (tmx - std::fmax(tmn, 0.0)) * U(rng);
+                            if (vol_sign_at(v, o, dir, t) != sign_fast(v, o, dir, t)) {
+                                if (sbad < 5) printf("vol %d ray %d t %.17g: vol_sign_at %d, key / sample %d\n", vi, i, t,
+                                                     vol_sign_at(v, o, dir, t), sign_fast(v, o, dir, t));
+                                sbad++;
+                            }
+                        }
+                }
                 for (int S : {8, 16, 32}) {
                     const double c = coop_emul(v, o, dir, S);
                     if (c != b && !(c != c && b != b)) {
@@ -232,6 +245,7 @@ int main(int argc, char** argv) {
             bad += vbad;
             vi++;
         }
+    printf("vol_sign_at against the key and the sample taken apart: %lld differences\n", sbad);
     printf("cooperative march with the strided pass (strides 8, 16, 32), emulated: %lld differences\n", cbad);
     bad += cbad;
     printf("%lld rays, %lld hits, %lld differences; vol_t %.3f s, the loop as written %.3f s\n", total, hits, bad, t_skip,
