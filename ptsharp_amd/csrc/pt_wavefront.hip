@@ -125,6 +125,9 @@ constexpr uint32_t kDead = 0xFFFFFFFFu;  // queue slot reserved for a child that
 constexpr int kBlockMajorFH = 16;
 constexpr int kBlockMajorChildren = 32;
 constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera slot (k_wf_trace)
+#ifndef PT_SHADE_MISS
+#define PT_SHADE_MISS 1   // routed shade: a textured environment's misses in k_wf_shade_miss (0: in the FULL shade)
+#endif
 #ifndef PT_SHADE_SCAN
 #define PT_SHADE_SCAN 8    // rows of 256 per SCAN claim: 16 best before claims carried their partial round, 8 since
                            // (C4 5836 / 5885 / 5743 for 16 / 8 / 32; the 1/8 share 5099 / 5208 / 4735)
@@ -986,7 +989,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     } else {
         const bool env_black = (!FULL || S.env_tex < 0) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
         // routed: the lean kernel takes the hits on spheres, cubes, planes and triangles, and the misses unless the
-        // environment is textured; the FULL kernel takes the rest
+        // environment is textured (then k_wf_shade_miss takes them); the FULL kernel takes the rest
         const bool env_lean = S.env_tex < 0;
         uint32_t* const shade_cursor = Q.counts + fetch_word(routed && FULL ? 7 : 1, G.g);
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1017,7 +1020,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                     if ((uint32_t)j < rows && sl < n) hv[j] = nt_load(&Q.hits[base + sl]);
                     const int32_t kind = (int32_t)hv[j].z;
                     bool k = kind != kDeadKind && (kind >= 0 || !env_black);
-                    if (routed) k = k && ((kind >= 0 ? kind <= KIND_TRI : env_lean) != FULL);
+                    if (routed) k = k && (kind >= 0 ? (kind <= KIND_TRI) != FULL : PT_SHADE_MISS ? env_lean && !FULL : env_lean != FULL);
                     keep |= k ? 1u << j : 0u;
                 }
                 uint64_t bal[kShadeScan];
@@ -1062,6 +1065,35 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
     if (COUNT) {
         uint32_t shades = wave_sum(ctr.shades);
         if ((threadIdx.x & 63) == 0) atomicAdd(&counters[3], (unsigned long long)shades);
+    }
+}
+
+// The misses of a routed shade under a textured environment (DevScene::shade_route, S.env_tex >= 0):
+// sampleEnvironment (Sampler.cs:64-67, 177-189), throughput · Scene.Texture lookup, added to the
+// vertex' pixel; a miss has no children.  The SCAN shades skip these vertices, so the texture lookup
+// runs here at a small kernel's occupancy instead of in the FULL shade (2 waves).
+__global__ __launch_bounds__(256) void k_wf_shade_miss(DevScene S, WfQueues Q, int qi) {
+    const Group G = xcd_group();
+    const uint32_t cnt = *ray_count(Q, qi, G.g);
+    const uint32_t n = cnt < Q.pcap ? cnt : Q.pcap, base = G.g * Q.pcap;
+    for (uint32_t k0 = G.lb * 256u; k0 < n; k0 += G.nb * 256u) {   // block-uniform: fix_add_wave takes every lane
+        const uint32_t sl = k0 + threadIdx.x;
+        bool has = false;
+        uint32_t pixel = 0;
+        double c[3] = {0.0, 0.0, 0.0};
+        if (sl < n && (int32_t)nt_load(&Q.hits[base + sl]).z == -1) {   // a miss (dead slots are kDeadKind)
+            const size_t i = base + sl;
+            const float4 rd = nt_load(&Q.q_d[qi][i]), ro = nt_load(&Q.q_o[qi][i]);
+            const double2 rt = nt_load(&Q.q_t[qi][i]);
+            const ulonglong2 rk = nt_load(&Q.q_k[qi][i]);
+            const double3 env = environment<true>(S, v3{rd.x, rd.y, rd.z});
+            c[0] = rt.x * env.x;
+            c[1] = rt.y * env.y;
+            c[2] = __longlong_as_double((long long)rk.y) * env.z;
+            pixel = __float_as_uint(ro.w);
+            has = true;
+        }
+        fix_add_wave(Q.acc, pixel, has, c[0], c[1], c[2]);
     }
 }
 
@@ -1634,6 +1666,8 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shade<false, false, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
                 hipLaunchKernelGGL((k_wf_shade<false, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
             }
+            if (PT_SHADE_MISS && S.env_tex >= 0)   // the textured environment's misses
+                hipLaunchKernelGGL(k_wf_shade_miss, dim3(grid_for(bound, 256, 8192)), dim3(256), 0, stream, S, Q, qi);
         } else if (count && full) {
             hipLaunchKernelGGL((k_wf_shade<true, true, false>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
             hipLaunchKernelGGL((k_wf_shade<true, true, true>), dim3(sg), dim3(256), 0, stream, S, smp, Q, qi, B.counters, plan.shade_form);
