@@ -435,16 +435,8 @@ __device__ __forceinline__ bool march_exact(double t, double step) {   // t > 0
 }
 // The Sign of march position t: a uniform cell's (pt_ext.h vol_build_runs: every sample in it has
 // that Sign) without the eight corner loads and the interpolation, else Volume.Sign of the sample.
-#ifndef PT_VOL_FUSED
-#define PT_VOL_FUSED 1
-#endif
 __device__ __forceinline__ int vol_sign_fast(const DevVolume& v, v3 o, v3 d, double t) {
-    if (PT_VOL_FUSED) return vol_sign_at(v, o, d, t);   // the key and the sample from one scaling of the position
-    if (v.runs) {
-        const int s = vol_key_sign(v, vol_key(v, o, d, t));
-        if (s > 0) return s;
-    }
-    return vol_sign(v, add(o, muls(d, t)));
+    return vol_sign_at(v, o, d, t);   // the key and the sample from one scaling of the position
 }
 // Every cell of the index box spanned by cells a and b (at most one step apart per axis) has
 // Sign `sign`: then every position between a position in a and a later one in b lies in such a
