@@ -561,7 +561,7 @@ struct SdfCompiler {
 pt::DevVolume dev_volume(const pt_volume& v, const double* data, const pt::DevWindow* windows) {
     pt::DevVolume o{};
     o.data = data; o.windows = windows;
-    o.w = v.w; o.h = v.h; o.d = v.d; o.nwin = v.num_windows; o.zscale = v.zscale;
+    o.w = v.w; o.h = v.h; o.d = v.d; o.nwin = v.num_windows; o.zscale = v.zscale; o.zinv = pt::vol_zinv(v.zscale);
     for (int k = 0; k < 3; k++) { o.bmin[k] = v.box_min[k]; o.bmax[k] = v.box_max[k]; }
     return o;
 }

@@ -54,6 +54,7 @@ struct DevVolume {
     const DevWindow* windows;
     int32_t w, h, d, nwin;
     double zscale;
+    double zinv;          // RN(1 / zscale) for vol_zdiv; 0: divide (host views, a zscale without a normal reciprocal)
     float bmin[3], bmax[3];
     // Uniform cells (vol_build_runs): per cell (x0, y0, z0) of Sample's lattice, indices -1..w-1
     // etc., the Sign every sample inside it has (1 or nwin + 1), or 0 when it cannot be vouched
@@ -276,6 +277,26 @@ PT_HD v3 sdf_normal(const DevSdfIns* prog, const double* params, const DevSdfSha
 }
 
 // ---------------------------------------------------------------- Volume (Volume.cs)
+// z / zscale (Volume.Sample's `z /= ZScale`, Volume.cs:76), correctly rounded, from the reciprocal y =
+// RN(1/zscale): q0 = RN(z·y) is within 1.5 ulp of z/zscale, the first correction makes it faithful, and
+// Markstein's theorem makes the second, RN(q1 + (z − zscale·q1)·y) with the residual exact by the FMA,
+// the correctly rounded quotient.  Five dependent fp64 operations instead of the division's sequence;
+// tests/native/vol_skip_check.cpp compares it with the division (also on divisors with all-ones and
+// few-bit significands).  A zero z gives +0 for −0, which Sample's next step (z + 1, z + 2) erases.
+PT_HD double vol_zdiv(const DevVolume& v, double z) {
+    if (v.zinv == 0.0) return z / v.zscale;
+    const double b = v.zscale, y = v.zinv;
+    double q = z * y;
+    double r = fma(-q, b, z);
+    q = fma(r, y, q);
+    r = fma(-q, b, z);
+    return fma(r, y, q);
+}
+// The reciprocal vol_zdiv takes: normal zscale and 1/zscale only (no overflow or underflow in the steps).
+inline double vol_zinv(double zscale) {
+    const double y = 1.0 / zscale;
+    return (isnormal(zscale) && isnormal(y)) ? y : 0.0;
+}
 PT_HD double vol_get(const DevVolume& v, int x, int y, int z) {   // Volume.Get (Volume.cs:40-46)
     if (x < 0 || y < 0 || z < 0 || x >= v.w || y >= v.h || z >= v.d) return 0;
     return v.data[(size_t)x + (size_t)y * (size_t)v.w + (size_t)z * (size_t)v.w * (size_t)v.h];
@@ -284,7 +305,7 @@ PT_HD double vol_get(const DevVolume& v, int x, int y, int z) {   // Volume.Get 
 // the int range (an OverflowException in the reference) sample 0, as in the oracle.
 PT_HD double vol_sample(const DevVolume& v, double x, double y, double z) {
     (void)y;
-    z /= v.zscale;
+    z = vol_zdiv(v, z);
     x = ((x + 1) / 2) * (double)v.w;
     y = ((z + 1) / 2) * (double)v.h;
     z = ((z + 2) / 2) * (double)v.d;
@@ -316,7 +337,7 @@ struct VolCell {
 };
 PT_HD double vol_sample_cell(const DevVolume& v, double x, double y, double z, VolCell& k) {
     (void)y;
-    z /= v.zscale;
+    z = vol_zdiv(v, z);
     x = ((x + 1) / 2) * (double)v.w;
     y = ((z + 1) / 2) * (double)v.h;
     z = ((z + 2) / 2) * (double)v.d;
@@ -445,7 +466,7 @@ struct VolKey {
 PT_HD VolKey vol_key(const DevVolume& v, v3 o, v3 d, double t) {
     const v3 a = add(o, muls(d, t));   // Ray.Position, as vol_t's positions
     double x = a.x, z = a.z;
-    z /= v.zscale;
+    z = vol_zdiv(v, z);
     x = ((x + 1) / 2) * (double)v.w;
     const double y = ((z + 1) / 2) * (double)v.h;
     z = ((z + 2) / 2) * (double)v.d;
@@ -466,7 +487,7 @@ PT_HD int vol_key_sign(const DevVolume& v, VolKey k) {
 PT_HD int vol_sign_at(const DevVolume& v, v3 o, v3 d, double t) {
     const v3 a = add(o, muls(d, t));   // Ray.Position
     double x = a.x, z = a.z;
-    z /= v.zscale;
+    z = vol_zdiv(v, z);
     x = ((x + 1) / 2) * (double)v.w;
     double y = ((z + 1) / 2) * (double)v.h;   // Sample's y-from-z slip (Volume.cs:77)
     z = ((z + 2) / 2) * (double)v.d;

@@ -145,6 +145,46 @@ int main(int argc, char** argv) {
         }
     }
     printf("t_after: 200000 cases, %lld differences\n", bad);
+    {   // vol_zdiv (the reciprocal and two corrections) against the division: fp32 positions and
+        // random doubles over zscales with random, all-ones and few-bit significands
+        long long zbad = 0, zn = 0;
+        std::mt19937_64 g(99);
+        for (int s = 0; s < 600; s++) {
+            double zs;
+            if (s < 3) zs = s == 0 ? 3.4 / 0.9765625 : s == 1 ? (double)(3.4f / 0.9765625f) : 0.37;
+            else {
+                uint64_t mant = g() & 0x000FFFFFFFFFFFFFull;
+                if (s % 3 == 1) mant = 0x000FFFFFFFFFFFFFull - (g() % 64);
+                if (s % 3 == 2) mant &= ~((1ull << (g() % 52)) - 1);
+                const uint64_t u = mant | ((uint64_t)(1023 + (int)(g() % 16) - 8) << 52);
+                memcpy(&zs, &u, 8);
+            }
+            DevVolume zv{};
+            zv.zscale = zs;
+            zv.zinv = vol_zinv(zs);
+            for (int i = 0; i < 100000; i++) {
+                double z;
+                if (i & 1) {
+                    uint32_t u = (uint32_t)g();
+                    u = (u & 0x807FFFFFu) | ((uint32_t)(127 - 40 + (int)(g() % 50)) << 23);
+                    float f;
+                    memcpy(&f, &u, 4);
+                    z = f;
+                } else {
+                    uint64_t u = g();
+                    u = (u & 0x800FFFFFFFFFFFFFull) | ((uint64_t)(1023 - 60 + (int)(g() % 120)) << 52);
+                    memcpy(&z, &u, 8);
+                }
+                zn++;
+                if (vol_zdiv(zv, z) != z / zs) {
+                    if (zbad < 5) printf("vol_zdiv(%a) by %a: %a, division %a\n", z, zs, vol_zdiv(zv, z), z / zs);
+                    zbad++;
+                }
+            }
+        }
+        printf("vol_zdiv against the division: %lld cases, %lld differences\n", zn, zbad);
+        bad += zbad;
+    }
     // the last volume has 256 narrow windows: a cell above all of them has Sign 257, past the run
     // table's int8 (stored as "no shortcut")
     const int dims[][3] = {{32, 32, 16}, {16, 16, 8}, {48, 48, 24}, {7, 5, 3}, {9, 7, 4}};
@@ -181,6 +221,7 @@ int main(int argc, char** argv) {
             v.windows = win.data();
             v.w = w; v.h = h; v.d = dd; v.nwin = (int)win.size();
             v.zscale = zs;
+            v.zinv = vol_zinv(zs);   // the device's Sample arithmetic (vol_zdiv); naive_t divides (vref)
             const float bmn[3] = {-1, -1, -0.2f}, bmx[3] = {1, 1, 1};
             for (int k = 0; k < 3; k++) { v.bmin[k] = bmn[k]; v.bmax[k] = bmx[k]; }
             std::vector<int8_t> runs((size_t)(w + 1) * (h + 1) * (dd + 1));
@@ -207,7 +248,9 @@ int main(int argc, char** argv) {
                 const auto c0 = std::chrono::steady_clock::now();
                 const double a = vol_t(v, o, dir, &n);
                 const auto c1 = std::chrono::steady_clock::now();
-                const double b = naive_t(v, o, dir);
+                DevVolume vref = v;
+                vref.zinv = 0.0;
+                const double b = naive_t(vref, o, dir);
                 const auto c2 = std::chrono::steady_clock::now();
                 t_skip += std::chrono::duration<double>(c1 - c0).count();
                 t_naive += std::chrono::duration<double>(c2 - c1).count();

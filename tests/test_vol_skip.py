@@ -20,6 +20,7 @@ def test_vol_skip_bit_identical():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "t_after: 200000 cases, 0 differences" in r.stdout
+    assert "vol_zdiv against the division: 60000000 cases, 0 differences" in r.stdout
     assert "(strides 8, 16, 32), emulated: 0 differences" in r.stdout
     assert "vol_sign_at against the key and the sample taken apart: 0 differences" in r.stdout
     assert " 0 differences;" in r.stdout.splitlines()[-1]
