@@ -26,6 +26,7 @@ namespace PTSharpCore
         public const int PT_OK = 0;
         public const int PT_ERR_UNSUPPORTED = -4;
         public const int PT_PASS_KERNEL_TIMING = 1, PT_PASS_SERIAL = 2;
+        public const int PT_MARCH_LANE = 1, PT_MARCH_WAVE = 2;   // pt_intersect / pt_occluded flags
         public const int SHAPE_SPHERE = 0, SHAPE_CUBE = 1, SHAPE_PLANE = 2, SHAPE_TRIANGLE = 3, SHAPE_MESH = 4;
         public const int SHAPE_SDF = 5, SHAPE_VOLUME = 6, SHAPE_TRANSFORMED = 7;
 
@@ -169,6 +170,9 @@ namespace PTSharpCore
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_write_tiles(IntPtr ctx, int[] tiles, int num_tiles, double[] m, double[] v, int[] n);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_reset_buffer(IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_stats_get(IntPtr ctx, out pt_stats stats);
+        // Scene.Intersect of a batch of rays / the shadow query against a t (PT_MARCH_* flags: the Volume march form)
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_intersect(IntPtr ctx, long n, float[] origins, float[] dirs, int flags, double[] t, int[] kind);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_occluded(IntPtr ctx, long n, float[] origins, float[] dirs, double[] tMax, int flags, int[] blocked);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern IntPtr pt_last_error();
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern void pt_destroy(IntPtr ctx);
         // multi-GPU (include/ptsharp_hip.h "Multi-GPU"): one process per GPU (unique id + init per rank) or

@@ -24,6 +24,8 @@
  *   pt_write_buffer    resuming IterativeRender from a saved PBuffer       Renderer.cs:702-765
  *   pt_read_tiles /    (new) a tile list's pixels, packed: progressive    SURVEY.md §8e
  *   pt_write_tiles     display of a rank's tiles, host-side gathers
+ *   pt_intersect /     Scene.Intersect of a host's rays; the shadow query   Scene.cs:75-79, Sampler.cs:261-265
+ *   pt_occluded
  *   pt_stats           Scene.rays (Interlocked counter, never printed)     Scene.cs:70-79
  *                      + the "time elapsed" stopwatch                      Renderer.cs:212-213,470
  *   pt_last_error      oidnGetDeviceError(device, out msg)                 OIDN.cs:85-86
@@ -49,7 +51,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 6
+#define PT_ABI_VERSION 7
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -386,6 +388,25 @@ int pt_comm_gather_all(void* const* ctxs, int32_t n, int32_t root);   /* the gro
 int pt_gather_layout(int32_t nranks, int32_t root, const int32_t* counts, int32_t image_tiles,
                      int64_t* out_offsets, int64_t* out_total);
 int pt_tile_lists_check(const int32_t* ids, int64_t n, int32_t image_tiles);
+
+/* Ray queries on the uploaded scene, one lane per ray (the megakernel's traversal).  Rays are
+ * [n][3] float origins and directions (Ray.Origin / Ray.Direction, Vector = Vector3).
+ *   pt_intersect  Scene.Intersect (Scene.cs:75-79 → Tree.Intersect, Tree.cs:31-42): out_t[i] the
+ *                 nearest hit's T (Hit.T, 1e9 = Hit.INF on a miss, Hit.cs:6), out_kind[i] its
+ *                 pt_shape_kind (a mesh triangle is PT_SHAPE_TRIANGLE) or -1.
+ *   pt_occluded   the shadow query after the light's own t (Sampler.cs:261-265 as the wavefront engine
+ *                 answers it): out_blocked[i] = 1 if some shape is hit strictly nearer
+ *                 than t_max[i].
+ * flags choose how a ray's Volume (Volume.Intersect, Volume.cs:168-197) is marched; every choice
+ * returns the same bits, which is what the flags are for: 0 as in a render (a wave's lanes march
+ * together unless fewer than 8 are active), PT_MARCH_LANE every lane its own march, PT_MARCH_WAVE
+ * always together. */
+#define PT_MARCH_LANE 1
+#define PT_MARCH_WAVE 2
+int pt_intersect(void* ctx, int64_t n, const float* origins, const float* dirs, int32_t flags, double* out_t,
+                 int32_t* out_kind);
+int pt_occluded(void* ctx, int64_t n, const float* origins, const float* dirs, const double* t_max, int32_t flags,
+                int32_t* out_blocked);
 
 /* Instrumentation (bench / roofline): last pass' traversal counters, summed. */
 typedef struct pt_trace_counters {

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptsharp_hip.so")
 
-ABI_VERSION = 6   # PT_ABI_VERSION
+ABI_VERSION = 7   # PT_ABI_VERSION
 PT_OK = 0
 PT_ERR_INVALID_ARG = -1
 PT_ERR_HIP = -2
@@ -30,6 +30,7 @@ K_SLOTS = 8   # PT_K_SLOTS
 
 SHAPE_SPHERE, SHAPE_CUBE, SHAPE_PLANE, SHAPE_TRIANGLE, SHAPE_MESH = 0, 1, 2, 3, 4
 SHAPE_SDF, SHAPE_VOLUME, SHAPE_TRANSFORMED = 5, 6, 7
+MARCH_LANE, MARCH_WAVE = 1, 2   # pt_intersect / pt_occluded flags (PT_MARCH_*)
 
 _f = C.POINTER(C.c_float)
 _d = C.POINTER(C.c_double)
@@ -163,6 +164,8 @@ SIGNATURES = {
     "pt_tile_lists_check": (C.c_int, [_i, C.c_int64, C.c_int32]),
     "pt_render_pass_counted": (C.c_int, [C.c_void_p, C.POINTER(pt_camera), C.POINTER(pt_sampler),
                                          C.POINTER(pt_pass_params), C.POINTER(pt_trace_counters)]),
+    "pt_intersect": (C.c_int, [C.c_void_p, C.c_int64, _f, _f, C.c_int32, _d, _i]),
+    "pt_occluded": (C.c_int, [C.c_void_p, C.c_int64, _f, _f, _d, C.c_int32, _i]),
     "pt_obj_load": (C.c_int, [C.c_char_p, C.POINTER(pt_mesh_data)]),
     "pt_mesh_free": (None, [C.POINTER(pt_mesh_data)]),
     "pt_obj_last_error": (C.c_char_p, []),

@@ -71,6 +71,8 @@ __global__ void k_iota(int32_t* a, int32_t n) {
 }
 hipError_t launch_render_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                               const DevBuffer& B, int num_tiles, bool count, hipStream_t stream);
+hipError_t launch_intersect(const DevScene& S, uint32_t n, const float* o3, const float* d3, const double* tl,
+                            double* out_t, int32_t* out_kind, hipStream_t stream);
 }
 
 namespace {
@@ -200,9 +202,11 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #define PT_VOL_DEFER 1   // split traversal: Volumes deferred to k_wf_vol_hits / k_wf_vol_shadow (0: marched in place)
 #endif
 constexpr double kSideStreamMaxRays = (double)(64ull << 20);   // a chunk's widest depth, extension rays
-// (a scene with SDF shapes or Volumes adds its two deferred-record queues, 32 B per entry, and with
-// Volumes their record words, 8 B, outside this budget: counted in, they halved C4's queues from 2^28 to
-// 2^27 entries and split its pass in two chunks, -3 %)
+// Outside this budget, for row-4 scenes only (counted in, they halved C4-sized queues from 2^28 to 2^27
+// entries and split the pass in two chunks, -3 %): the two deferred-record queues of a scene with SDF
+// shapes or Volumes (sdfq, sdfq_sh: 32 B per entry), with Volumes their record words (volq, volq_sh: 8 B),
+// and under the routed split the heavy queues (hq, hq_sh: 8 B).  At most 48 B per entry, 17 % over the
+// 274 B: 12.9 GB at 2^28 entries, inside the three quarters of the device the budget leaves free.
 constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 2 * (64 + 1);
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
@@ -1199,7 +1203,11 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         if (!L.phantom && (L.kind == pt::KIND_SDF || L.kind == pt::KIND_VOLUME || L.kind == pt::KIND_XFORM)) S.lights_lean = 0;
     // Routed split (C5's kind of scene: the 1M-triangle mesh, a floor cube, light spheres, one SDF shape and
     // one transformed Volume): only the rays whose segment reaches a row-4 box take the FULL kernels
-    S.route = (PT_ROUTE && S.full_geom && S.lights_lean && na <= (size_t)PT_ANA_LINEAR && !heavy.empty() &&
+    // (environment PT_ROUTE=0 at upload: every ray through the FULL analytic half, as a -DPT_ROUTE=0 build;
+    // tests compare the two, whose only possible difference is the exact-t tie order of DESIGN.md §5)
+    const char* route_env = std::getenv("PT_ROUTE");
+    const bool route_on = PT_ROUTE && !(route_env && !std::strcmp(route_env, "0"));
+    S.route = (route_on && S.full_geom && S.lights_lean && na <= (size_t)PT_ANA_LINEAR && !heavy.empty() &&
                tri_num_nodes > 64) ? 1 : 0;
     S.heavy_count = (int32_t)(heavy.size() / 2);
     bool mat_tex = false;
@@ -1608,6 +1616,55 @@ int pt_read_tiles(void* ctx, const int32_t* tiles, int32_t num_tiles, double* ou
 int pt_write_tiles(void* ctx, const int32_t* tiles, int32_t num_tiles, const double* m, const double* v,
                    const int32_t* n) {
     return tiles_io(ctx, tiles, num_tiles, const_cast<double*>(m), const_cast<double*>(v), const_cast<int32_t*>(n), true);
+}
+
+// pt_intersect / pt_occluded: the rays to the device, one launch of k_intersect, the answers back.
+static int ray_queries(void* ctx, int64_t n, const float* origins, const float* dirs, const double* t_light,
+                       int32_t flags, double* out_t, int32_t* out_i) {
+    Ctx* c = (Ctx*)ctx;
+    if (!c || (n > 0 && (!origins || !dirs || !out_i || (!t_light && !out_t)))) return fail(PT_ERR_INVALID_ARG, "NULL argument");
+    if (n < 0 || n > (int64_t)1 << 30) return fail(PT_ERR_INVALID_ARG, "n out of range [0, 2^30]");
+    if (flags & ~(PT_MARCH_LANE | PT_MARCH_WAVE) || (flags & PT_MARCH_LANE && flags & PT_MARCH_WAVE))
+        return fail(PT_ERR_INVALID_ARG, "flags: PT_MARCH_LANE or PT_MARCH_WAVE, not both");
+    if (!c->has_scene) return fail(PT_ERR_NO_SCENE, "no scene uploaded");
+    if (n == 0) return PT_OK;
+    PT_HIP(hipSetDevice(c->device));
+    const size_t N = (size_t)n;
+    const size_t bytes = N * (6 * sizeof(float) + sizeof(double) + sizeof(double) + sizeof(int32_t));
+    unsigned char* d = nullptr;
+    hipError_t e = hipMalloc(&d, bytes);
+    if (e != hipSuccess) return fail(PT_ERR_OUT_OF_MEMORY, std::string("hipMalloc ray queries: ") + hipGetErrorString(e));
+    float* d_o = (float*)d;
+    float* d_d = d_o + 3 * N;
+    double* d_tl = (double*)(d_d + 3 * N);   // 8-B aligned: 24·N bytes precede it
+    double* d_t = d_tl + N;
+    int32_t* d_i = (int32_t*)(d_t + N);
+    pt::DevScene S = c->S;
+    if (flags & PT_MARCH_LANE) S.coop_min_lanes = 65;   // fewer than 65 active lanes: always
+    if (flags & PT_MARCH_WAVE) S.coop_min_lanes = 1;    // every wave with a pending Volume marches it together
+    int rc = PT_OK;
+    auto step = [&](hipError_t err, const char* what) {
+        if (rc == PT_OK && err != hipSuccess) rc = fail(PT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(err));
+    };
+    step(hipMemcpyAsync(d_o, origins, 3 * N * sizeof(float), hipMemcpyHostToDevice, c->stream), "origins");
+    step(hipMemcpyAsync(d_d, dirs, 3 * N * sizeof(float), hipMemcpyHostToDevice, c->stream), "dirs");
+    if (t_light) step(hipMemcpyAsync(d_tl, t_light, N * sizeof(double), hipMemcpyHostToDevice, c->stream), "t_light");
+    if (rc == PT_OK) step(pt::launch_intersect(S, (uint32_t)N, d_o, d_d, t_light ? d_tl : nullptr, d_t, d_i, c->stream), "k_intersect");
+    if (rc == PT_OK && out_t && !t_light) step(hipMemcpyAsync(out_t, d_t, N * sizeof(double), hipMemcpyDeviceToHost, c->stream), "out_t");
+    if (rc == PT_OK) step(hipMemcpyAsync(out_i, d_i, N * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream), "out");
+    step(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    (void)hipFree(d);
+    return rc;
+}
+int pt_intersect(void* ctx, int64_t n, const float* origins, const float* dirs, int32_t flags, double* out_t,
+                 int32_t* out_kind) {
+    if (!out_t) return fail(PT_ERR_INVALID_ARG, "out_t is NULL");
+    return ray_queries(ctx, n, origins, dirs, nullptr, flags, out_t, out_kind);
+}
+int pt_occluded(void* ctx, int64_t n, const float* origins, const float* dirs, const double* t_max, int32_t flags,
+                int32_t* out_blocked) {
+    if (n > 0 && !t_max) return fail(PT_ERR_INVALID_ARG, "t_max is NULL");
+    return ray_queries(ctx, n, origins, dirs, t_max, flags, nullptr, out_blocked);
 }
 
 int pt_stats_get(void* ctx, pt_stats* out) {

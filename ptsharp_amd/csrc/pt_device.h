@@ -33,9 +33,6 @@ struct Counters {
     uint32_t rays, nodes, prims, shades;
 };
 
-// Volume marches by the wave's active lanes together (coop_vol_t); with fewer than this many active
-// lanes each marches its own ray (vol_t, one grid read per cell)
-constexpr int kCoopMinLanes = 8;
 
 __device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
 
@@ -565,7 +562,7 @@ __device__ __forceinline__ double coop_record_t_body(const DevScene& S, int32_t 
 __device__ __noinline__ double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj) {
     return coop_record_t_body(S, p, o, d, kind, tobj);
 }
-// The lanes' pending Volume records, one ray at a time by all active lanes (at least kCoopMinLanes):
+// The lanes' pending Volume records, one ray at a time by all active lanes (at least S.coop_min_lanes):
 // march_pending's merge, without its few-lanes fallback (k_wf_vol_hits / k_wf_vol_shadow run full waves).
 template <bool ANY, bool INL = false>
 __device__ inline void march_coop(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked) {
@@ -600,7 +597,7 @@ __device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend
             best.t = t; best.kind = kind; best.idx = p; best.tx = tx;
         }
     };
-    if (__popcll(__ballot(true)) < kCoopMinLanes) {   // too few lanes to share a march: each its own
+    if (__popcll(__ballot(true)) < S.coop_min_lanes) {   // too few lanes to share a march: each its own
         if (pend >= 0) {
             int32_t kind;
             double tx = 0;
@@ -652,6 +649,36 @@ __device__ __forceinline__ double light_t(const DevScene& S, const DevLight& L, 
     return prim_t<false, FULL>(S, S.ana_recs, (uint32_t)L.index, o, d, kind);
 }
 
+// Is any primitive strictly nearer than tl along (o, d)?  The any-hit half of the shadow query
+// (light_visible) after the light's own t; pt_occluded runs it for a host's rays.
+template <bool COUNT, bool FULL, class STK>
+__device__ __forceinline__ bool any_nearer(const DevScene& S, v3 o, v3 d, double tl, const STK& stack, Counters& ctr) {
+    HitRec best{tl, -1, -1};
+    for (int i = 0; i < S.num_planes; i++) {
+        float4 a = S.planes[2 * i], b = S.planes[2 * i + 1];
+        if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return true;
+    }
+    v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    int32_t pend = -1;   // FULL: a Volume left for the cooperative march
+    if (S.ana_linear) {
+        for (int p = 0; p < S.ana_count; p++) {
+            if (COUNT) ctr.prims++;
+            int32_t kind;
+            if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return true;
+        }
+    } else if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack,
+                                                 ctr, FULL ? &pend : nullptr)) {
+        return true;
+    }
+    if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return true;
+    if (FULL) {   // the lanes still unblocked march their pending Volume together
+        bool blocked = false;
+        march_pending<true>(S, o, d, pend, best, &blocked);
+        if (blocked) return true;
+    }
+    return false;
+}
+
 // Shadow visibility (Sampler.cs:261-265): the reference takes the nearest hit and
 // compares it with the light by reference.  Equivalent query: the light's own t,
 // then "is any primitive strictly nearer" (any-hit, early exit).  Counts one ray.
@@ -667,34 +694,10 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         traverse_tri<COUNT, true>(S, o, d, invd, h, stack, ctr);
         return false;
     }
-    double tl = light_t<FULL>(S, L, o, d);
+    const double tl = light_t<FULL>(S, L, o, d);
     if (!(tl < kHitInf)) return false;
-    HitRec best{tl, -1, -1};
-    for (int i = 0; i < S.num_planes; i++) {
-        float4 a = S.planes[2 * i], b = S.planes[2 * i + 1];
-        if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
-    }
-    v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    int32_t pend = -1;   // FULL: a Volume left for the cooperative march
-    if (S.ana_linear) {
-        for (int p = 0; p < S.ana_count; p++) {
-            if (COUNT) ctr.prims++;
-            int32_t kind;
-            if (prim_t<false, FULL>(S, S.ana_recs, (uint32_t)p, o, d, kind) < tl) return false;
-        }
-    } else if (traverse<false, COUNT, true, FULL>(S, S.ana_nodes, S.ana_num_nodes, S.ana_recs, o, d, invd, best, stack,
-                                                 ctr, FULL ? &pend : nullptr)) {
-        return false;
-    }
-    if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return false;
-    if (FULL) {   // the lanes still unblocked march their pending Volume together
-        bool blocked = false;
-        march_pending<true>(S, o, d, pend, best, &blocked);
-        if (blocked) return false;
-    }
-    return true;
+    return !any_nearer<COUNT, FULL>(S, o, d, tl, stack, ctr);
 }
-
 // Split traversal (scenes with §8f row 4 shapes and a large triangle BVH, pt_wavefront.hip
 // "split"): the lean refill kernels take the planes and the triangle BVH, then the FULL kernel
 // takes the analytic BVH of the same ray, starting from that hit.  Scene.Intersect visits planes,

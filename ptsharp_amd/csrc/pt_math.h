@@ -123,7 +123,8 @@ PT_HD void sincos_kernel(double x, double y, double& s, double& c) {
 // k·(π/2)_hi with its exact fma error, r = x − k·hi exact by Sterbenz — and evaluates the
 // fdlibm kernels: within 1 ulp of glibc's sin / cos, and the fp32 vectors the reference builds
 // from them (r·sin, r·cos rounded to float) identical on 2·10^7 sampled arguments
-// (tools/check_sincos.cpp).  It replaces the general library routine, whose large-argument
+// (tools/check_sincos.cpp, removed in 188afd0; its successor tools/sincos_flip_rate.cpp covers random
+// radii and the call sites' float expressions, profiles/r03_sincos_flip_rate.txt).  It replaces the general library routine, whose large-argument
 // path alone took the shade kernel from 11 to 34 spilled VGPRs.  No large-argument path here:
 // the reduction stays accurate to ~1e-29 absolute for |x| up to ~1e4, far beyond any caller.
 PT_HD void pt_sincos(double x, double* s, double* c) {

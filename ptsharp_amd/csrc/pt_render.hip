@@ -254,6 +254,40 @@ __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera ca
     if (lane == 0) atomicAdd(&B.counters[0], (unsigned long long)rays);
 }
 
+// Scene.Intersect (Scene.cs:75-79) of a host's rays (pt_intersect), or the any-hit shadow query against
+// a given t (pt_occluded, light_visible's any_nearer): one lane per ray, the megakernel's trace() with its
+// LDS stack.  S.coop_min_lanes (set by the host) picks how a pending Volume is marched.
+template <bool FULL, bool ANY>
+__global__ __launch_bounds__(kBlock) void k_intersect(DevScene S, uint32_t n, const float* __restrict__ o3,
+                                                      const float* __restrict__ d3, const double* __restrict__ tl,
+                                                      double* __restrict__ out_t, int32_t* __restrict__ out_kind) {
+    __shared__ uint32_t s_stack[kStackMax * kBlock];
+    const MStack stack{s_stack + threadIdx.x};
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const v3 o{o3[3 * (size_t)i], o3[3 * (size_t)i + 1], o3[3 * (size_t)i + 2]};
+    const v3 d{d3[3 * (size_t)i], d3[3 * (size_t)i + 1], d3[3 * (size_t)i + 2]};
+    Counters ctr{0, 0, 0, 0};
+    if (ANY) {
+        out_kind[i] = any_nearer<false, FULL>(S, o, d, tl[i], stack, ctr) ? 1 : 0;
+    } else {
+        const HitRec h = trace<false, FULL>(S, o, d, stack, ctr);
+        out_t[i] = h.t;
+        out_kind[i] = h.t < kHitInf ? h.kind : -1;
+    }
+}
+
+hipError_t launch_intersect(const DevScene& S, uint32_t n, const float* o3, const float* d3, const double* tl,
+                            double* out_t, int32_t* out_kind, hipStream_t stream) {
+    const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
+    const bool full = S.full_geom != 0;
+    if (tl && full) hipLaunchKernelGGL((k_intersect<true, true>), grid, block, 0, stream, S, n, o3, d3, tl, out_t, out_kind);
+    else if (tl) hipLaunchKernelGGL((k_intersect<false, true>), grid, block, 0, stream, S, n, o3, d3, tl, out_t, out_kind);
+    else if (full) hipLaunchKernelGGL((k_intersect<true, false>), grid, block, 0, stream, S, n, o3, d3, tl, out_t, out_kind);
+    else hipLaunchKernelGGL((k_intersect<false, false>), grid, block, 0, stream, S, n, o3, d3, tl, out_t, out_kind);
+    return hipGetLastError();
+}
+
 // Host-side launch (called from pt_api.hip).
 hipError_t launch_render_pass(const DevScene& S, const DevCamera& cam, const DevSampler& smp, const DevPass& P,
                               const DevBuffer& B, int num_tiles, bool count, hipStream_t stream) {

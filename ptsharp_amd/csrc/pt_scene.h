@@ -118,6 +118,10 @@ struct DevScene {
     int32_t shade_route;
     int32_t heavy_count;
     const float4* heavy;       // 2 float4 per heavy record: {box lo.xyz, record index (bits)} {box hi.xyz, 0}
+    // march_pending: a wave with fewer active lanes than this marches each pending Volume by its own lane
+    // (vol_t, one grid read per cell), else by all active lanes together (coop_vol_t).  8 in every render;
+    // pt_intersect / pt_occluded set 65 (every lane its own) or 1 (always together) to test both forms
+    int32_t coop_min_lanes = 8;
     // counted passes only (else null): [0] Volume.Sample calls and [1] SDF evaluations of the
     // Volume / SDFShape intersect marches (DevBuffer::counters words 9 and 10)
     unsigned long long* march;

@@ -1081,7 +1081,13 @@ __global__ __launch_bounds__(256) void k_wf_shade_miss(DevScene S, WfQueues Q, i
         bool has = false;
         uint32_t pixel = 0;
         double c[3] = {0.0, 0.0, 0.0};
-        if (sl < n && (int32_t)nt_load(&Q.hits[base + sl]).z == -1) {   // a miss (dead slots are kDeadKind)
+        // a miss, by shade_vertex's own test (t = Hit.INF; a dead slot has kind kDeadKind and t 0).  Every hit
+        // store writes kind -1 exactly with t = kHitInf (trace / refill kernels: HitRec{kHitInf, -1, -1} until
+        // a hit; k_wf_vol_hits / k_wf_sdf_hits write hits only), so this agrees with the SCAN listing's
+        // kind < 0 that routes these vertices here and not to the FULL shade.
+        const uint4 hr = sl < n ? nt_load(&Q.hits[base + sl]) : make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u);
+        const double ht = __longlong_as_double((long long)(((unsigned long long)hr.y << 32) | hr.x));
+        if ((int32_t)hr.z != kDeadKind && !(ht < kHitInf)) {
             const size_t i = base + sl;
             const float4 rd = nt_load(&Q.q_d[qi][i]), ro = nt_load(&Q.q_o[qi][i]);
             const double2 rt = nt_load(&Q.q_t[qi][i]);
@@ -1634,7 +1640,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
-            if (Q.volq) hipLaunchKernelGGL(k_wf_vol_hits, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
+            if (Q.volq && S.num_vol > 0) hipLaunchKernelGGL(k_wf_vol_hits, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
             if (S.num_sdf > 0 && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_hits<true>, dim3(grid_for(n, 256, 8192)), dim3(256), (size_t)S.sdf_lds, stream, S, Q, qi);
             else if (S.num_sdf > 0)
@@ -1701,7 +1707,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
-            if (Q.volq_sh)
+            if (Q.volq_sh && S.num_vol > 0)   // (the queues outlive a re-upload of a scene without Volumes)
                 hipLaunchKernelGGL(k_wf_vol_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256), 0,
                                    side, S, Q, 1 - qi);
             if (sq && S.sdf_lds > 0)

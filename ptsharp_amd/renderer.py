@@ -269,6 +269,35 @@ class Renderer:
                                             M.ctypes.data_as(C.POINTER(C.c_double)), V.ctypes.data_as(C.POINTER(C.c_double)),
                                             N.ctypes.data_as(C.POINTER(C.c_int32))), "pt_write_tiles")
 
+    def Intersect(self, origins, dirs, flags: int = 0):
+        """Scene.Intersect (Scene.cs:75-79) of n rays on the device (pt_intersect): (t [n] float64, 1e9 on
+        a miss; kind [n] int32, the pt_shape_kind hit or -1).  flags: _abi.MARCH_LANE / MARCH_WAVE."""
+        self._ensure_scene()
+        o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        assert o.shape == d.shape
+        t = np.zeros(len(o), np.float64)
+        k = np.zeros(len(o), np.int32)
+        _abi.check(self._lib.pt_intersect(self._ctx, len(o), o.ctypes.data_as(C.POINTER(C.c_float)),
+                                          d.ctypes.data_as(C.POINTER(C.c_float)), int(flags),
+                                          t.ctypes.data_as(C.POINTER(C.c_double)), k.ctypes.data_as(C.POINTER(C.c_int32))),
+                   "pt_intersect")
+        return t, k
+
+    def Occluded(self, origins, dirs, t_max, flags: int = 0) -> np.ndarray:
+        """The shadow query after the light's own t (pt_occluded): [n] int32, 1 where a shape is hit
+        strictly nearer than t_max."""
+        self._ensure_scene()
+        o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        tm = np.ascontiguousarray(t_max, np.float64).reshape(-1)
+        assert o.shape == d.shape and len(tm) == len(o)
+        b = np.zeros(len(o), np.int32)
+        _abi.check(self._lib.pt_occluded(self._ctx, len(o), o.ctypes.data_as(C.POINTER(C.c_float)),
+                                         d.ctypes.data_as(C.POINTER(C.c_float)), tm.ctypes.data_as(C.POINTER(C.c_double)),
+                                         int(flags), b.ctypes.data_as(C.POINTER(C.c_int32))), "pt_occluded")
+        return b
+
     def ResetBuffer(self) -> None:
         _abi.check(self._lib.pt_reset_buffer(self._ctx), "pt_reset_buffer")
         self._pass = 0

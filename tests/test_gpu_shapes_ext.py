@@ -81,3 +81,25 @@ def test_march_counters(gpu):
     ctr2 = r.RenderCounted()
     r.close()
     assert ctr2.rays > 0 and ctr2.volume_samples == 0 and ctr2.sdf_evals == 0
+
+
+def test_routed_split_equals_full_analytic_half(gpu, monkeypatch):
+    """The routed split (only rays that reach a row-4 shape's box take the FULL kernels, which test the
+    heavy records in record order) against every ray through the FULL analytic half (PT_ROUTE=0 at
+    upload): they differ only at exact-t ties between shapes (class 3), so on C5's
+    kind of scene the two Buffers must be the same bits.  C5's 1M-triangle mixed scene at 4K, 4 tiles,
+    AdaptiveSamples 8, plus the C5 scene at test size with MaxBounces 3."""
+    from parity import render_gpu, same_buffer
+    from ptsharp_amd.renderer import tiles_for_rank
+    cases = [(scenes.mixed(1_000_000), 3840, 2160, tiles_for_rank(3840, 2160, 5, 2048), 8),
+             (scenes.mixed(3000, seed=5), 96, 64, None, 2)]
+    for (s, c, smp), w, h, tiles, adaptive in cases:
+        smp.MaxBounces = min(smp.MaxBounces, 3)
+        bufs = []
+        for route in ("1", "0"):
+            monkeypatch.setenv("PT_ROUTE", route)
+            bufs.append(render_gpu(s, c, smp, w, h, 1, passes=1, seed=77, tiles=tiles,
+                                   engine=_abi.ENGINE_WAVEFRONT, adaptive=adaptive))
+        (a, ra), (b, rb) = bufs
+        assert ra == rb
+        same_buffer(a, b)
