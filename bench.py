@@ -341,9 +341,14 @@ def main(argv=None):
         t_ok = torch.tensor([ok], dtype=torch.int32)
         dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
         rccl_ok = bool(t_ok[0])
-    _each(rs, lambda i, x: x._ensure_scene())   # every device builds and uploads its replica
+    # every device uploads its replica, from its own thread; the triangle BVH is built once for all of them
+    # (pt_upload_scene shares one host build of identical geometry: pt_scene_bvh_digest)
+    t_up = time.perf_counter()
+    _each(rs, lambda i, x: x._ensure_scene())
+    t_up = time.perf_counter() - t_up
     st = r.Stats()
     build_ms, bvh_bytes = st.build_ms, st.bvh_bytes
+    upload_ms = [round(x.Stats().build_ms, 1) for x in rs]
     # closest-hit and shadow kernels the library runs on this scene: per-lane refill
     # (k_wf_*_lanes) above 64 triangle-BVH nodes (pt_wavefront.hip kLanesMinNodes); the bench scene's
     # analytic BVH (floor cube, two light spheres) is one node
@@ -547,6 +552,7 @@ def main(argv=None):
             "shadow_ray_fraction": round(ctr.shadow_rays / max(ctr.rays, 1), 4),
             "lit_shadow_rays_per_step": int(ctr.lit_shadow_rays), "accum_runs_per_step": int(ctr.accum_runs),
             "engine": a.engine, "scene_build_s": round(t_scene, 3), "bvh_build_ms": round(build_ms, 1),
+            "scene_upload_s": round(t_up, 3), "contexts_upload_ms": upload_ms,
             "mesh_source": None if a.workload == "c2" else a.mesh_source, **(obj_info or {}),
             "bvh_bytes": int(bvh_bytes),
             "kernel_ms_per_step": {names[k]: round(kms[k] / a.steps, 3) for k in range(_abi.K_SLOTS) if klaunch[k]},

@@ -170,6 +170,7 @@ namespace PTSharpCore
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_write_tiles(IntPtr ctx, int[] tiles, int num_tiles, double[] m, double[] v, int[] n);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_reset_buffer(IntPtr ctx);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_stats_get(IntPtr ctx, out pt_stats stats);
+        [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_scene_bvh_digest(ref pt_scene_desc scene, ulong[] out4);
         // Scene.Intersect of a batch of rays / the shadow query against a t (PT_MARCH_* flags: the Volume march form)
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_intersect(IntPtr ctx, long n, float[] origins, float[] dirs, int flags, double[] t, int[] kind);
         [DllImport(Lib, CallingConvention = CallingConvention.Cdecl)] public static extern int pt_occluded(IntPtr ctx, long n, float[] origins, float[] dirs, double[] tMax, int flags, int[] blocked);

@@ -408,6 +408,13 @@ int pt_intersect(void* ctx, int64_t n, const float* origins, const float* dirs, 
 int pt_occluded(void* ctx, int64_t n, const float* origins, const float* dirs, const double* t_max, int32_t flags,
                 int32_t* out_blocked);
 
+/* The triangle BVH is built once per process for identical geometry: N contexts that upload the same
+ * scene (one process driving N GPUs) share one host build (Scene.Compile once, Scene.cs:48-68) and upload
+ * its bytes; a context that uploads while another builds waits for that build.  Host only (no device):
+ * out[0] a 64-bit digest of the BVH bytes a context of this scene receives (node lines, leaf chunks,
+ * triangle order), out[1] their size in bytes, out[2] / out[3] the builds made / builds reused so far. */
+int pt_scene_bvh_digest(const pt_scene_desc* scene, uint64_t out[4]);
+
 /* Instrumentation (bench / roofline): last pass' traversal counters, summed. */
 typedef struct pt_trace_counters {
     uint64_t rays;            /* all Scene.Intersect calls                     */

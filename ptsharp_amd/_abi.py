@@ -164,6 +164,7 @@ SIGNATURES = {
     "pt_tile_lists_check": (C.c_int, [_i, C.c_int64, C.c_int32]),
     "pt_render_pass_counted": (C.c_int, [C.c_void_p, C.POINTER(pt_camera), C.POINTER(pt_sampler),
                                          C.POINTER(pt_pass_params), C.POINTER(pt_trace_counters)]),
+    "pt_scene_bvh_digest": (C.c_int, [C.POINTER(pt_scene_desc), C.POINTER(C.c_uint64)]),
     "pt_intersect": (C.c_int, [C.c_void_p, C.c_int64, _f, _f, C.c_int32, _d, _i]),
     "pt_occluded": (C.c_int, [C.c_void_p, C.c_int64, _f, _f, _d, C.c_int32, _i]),
     "pt_obj_load": (C.c_int, [C.c_char_p, C.POINTER(pt_mesh_data)]),

@@ -131,6 +131,242 @@ struct Tracer {
     }
 };
 
+// ---------------------------------------------------------------- wide-node model
+// A W-wide tree collapsed from the same BVH2 by the SAH dynamic program (Ylitie et al. 2017 §4.1, W
+// slots), child boxes optionally quantized to Q bits per bound relative to the node's own box (an fp32
+// origin and a power-of-two step per axis, decoded as origin + q·step in fp32 and widened until they
+// hold the exact box: the compressed wide BVH's format), leaves of <= 3 triangles as today's 128-B
+// chunks.  A node line: W = 8 with Q = 8 is 80 B (origin 12, exponents 3, mask 1, child and triangle
+// bases 8, per-child meta 8, bounds 48), W = 8 with Q = 16 is 128 B, W = 4 in fp32 is today's 128 B.
+// Every node and every leaf chunk is one 128-B line, so steps = distinct lines a ray reads.
+struct WChild {
+    float lo[3], hi[3];
+    uint32_t ref;   // inner node index, or 0x80000000 | (count-1) << 29 | first
+};
+struct WNode {
+    std::vector<WChild> c;
+};
+struct WideTree {
+    int W = 4, Q = 0;
+    std::vector<WNode> nodes;
+    size_t leaves = 0;
+    double fill = 0;
+    int depth = 0;
+};
+struct WideCollapser {
+    const std::vector<BvhNode>& n2;
+    int W;
+    double c_step = 1.0, c_tri = 0.5;
+    int max_leaf = 3;
+    std::vector<double> cost;    // [node][W]
+    std::vector<int8_t> choice;  // [node][W]
+    std::vector<uint8_t> as_leaf;
+    std::vector<uint32_t> prims, first;
+    bool is_leaf(uint32_t i) const { return n2[i].b != 0; }
+    double area(uint32_t i) const {
+        const BvhNode& n = n2[i];
+        double dx = (double)n.bmax[0] - n.bmin[0], dy = (double)n.bmax[1] - n.bmin[1], dz = (double)n.bmax[2] - n.bmin[2];
+        if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+        return dx * dy + dy * dz + dz * dx;
+    }
+    double dist(uint32_t n, int j, int& kbest) const {
+        const double* CL = &cost[(size_t)n2[n].a * W];
+        const double* CR = &cost[(size_t)(n2[n].a + 1) * W];
+        double best = INFINITY;
+        kbest = -1;
+        for (int k = 1; k < j; k++) {
+            const double c = CL[k - 1] + CR[j - k - 1];
+            if (c < best) { best = c; kbest = k; }
+        }
+        return best;
+    }
+    void solve(uint32_t n) {
+        {
+            double* C = &cost[(size_t)n * W];
+            int8_t* ch = &choice[(size_t)n * W];
+            const double a = area(n);
+            if (is_leaf(n)) {
+                prims[n] = n2[n].b; first[n] = n2[n].a;
+                for (int i = 0; i < W; i++) { C[i] = a * (c_step + c_tri * (double)prims[n]); ch[i] = 0; }
+                as_leaf[n] = 1;
+                return;
+            }
+            const uint32_t l = n2[n].a, r = l + 1;
+            solve(l);
+            solve(r);
+            prims[n] = prims[l] + prims[r];
+            first[n] = std::min(first[l], first[r]);
+            int kw;
+            const double inner = a * c_step + dist(n, W, kw);
+            const double leaf = (int)prims[n] <= max_leaf ? a * (c_step + c_tri * (double)prims[n]) : INFINITY;
+            as_leaf[n] = leaf <= inner;
+            C[0] = std::min(leaf, inner);
+            ch[0] = 0;
+            for (int i = 2; i <= W; i++) {
+                int k;
+                const double d = dist(n, i, k);
+                if (d < C[i - 2]) { C[i - 1] = d; ch[i - 1] = (int8_t)k; }
+                else { C[i - 1] = C[i - 2]; ch[i - 1] = -1; }
+            }
+        }
+    }
+    void slots(uint32_t n, int i, std::vector<uint32_t>& outs) const {
+        const int8_t c = choice[(size_t)n * W + (size_t)(i - 1)];
+        if (c == 0) { outs.push_back(n); return; }
+        if (c < 0) { slots(n, i - 1, outs); return; }
+        slots(n2[n].a, c, outs);
+        slots(n2[n].a + 1, i - c, outs);
+    }
+    void emit(WideTree& T, uint32_t at, uint32_t n, int depth) {
+        T.depth = std::max(T.depth, depth);
+        int k;
+        (void)dist(n, W, k);
+        std::vector<uint32_t> C;
+        slots(n2[n].a, k, C);
+        slots(n2[n].a + 1, W - k, C);
+        std::vector<std::pair<uint32_t, uint32_t>> inner;
+        for (uint32_t c : C) {
+            WChild w;
+            for (int ax = 0; ax < 3; ax++) { w.lo[ax] = n2[c].bmin[ax]; w.hi[ax] = n2[c].bmax[ax]; }
+            if (as_leaf[c]) {
+                w.ref = 0x80000000u | ((prims[c] - 1u) << 29) | (first[c] & 0x1FFFFFFFu);
+                T.leaves++;
+            } else {
+                w.ref = (uint32_t)T.nodes.size();
+                T.nodes.emplace_back();
+                inner.emplace_back(c, w.ref);
+            }
+            T.nodes[at].c.push_back(w);
+        }
+        for (auto& pr : inner) emit(T, pr.second, pr.first, depth + 1);
+    }
+};
+// Q-bit child bounds relative to the node's box: the decoded box holds the exact one.
+static void quantize(WideTree& T) {
+    if (T.Q <= 0) return;
+    const float qmax = (float)((1 << T.Q) - 1);
+    for (WNode& nd : T.nodes) {
+        for (int ax = 0; ax < 3; ax++) {
+            float o = INFINITY, e = -INFINITY;
+            for (const WChild& c : nd.c) { o = std::fmin(o, c.lo[ax]); e = std::fmax(e, c.hi[ax]); }
+            int ex = 0;
+            const double ext = (double)e - (double)o;
+            (void)std::frexp(ext / qmax, &ex);   // 2^ex > ext / qmax
+            for (;;) {
+                const float step = std::ldexp(1.0f, ex);
+                bool ok = true;
+                std::vector<WChild> qc = nd.c;
+                for (WChild& c : qc) {
+                    float ql = std::floor((float)(((double)c.lo[ax] - o) / step)), qh = std::ceil((float)(((double)c.hi[ax] - o) / step));
+                    while (ql > 0 && o + ql * step > c.lo[ax]) ql -= 1.f;
+                    while (o + qh * step < c.hi[ax]) qh += 1.f;
+                    if (ql < 0 || qh > qmax) { ok = false; break; }
+                    c.lo[ax] = o + ql * step;
+                    c.hi[ax] = o + qh * step;
+                    if (c.lo[ax] > nd.c[&c - &qc[0]].lo[ax]) { ok = false; break; }
+                }
+                if (ok) { nd.c = qc; break; }
+                ex++;
+            }
+        }
+    }
+}
+static void build_wide(const Mesh& m, int W, int Q, WideTree& T, std::vector<uint32_t>& order, double& build_s) {
+    const size_t n = (size_t)m.n;
+    std::vector<float> lo(n * 3), hi(n * 3);
+    for (size_t i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++) {
+            const float a = m.v1[3 * i + k], b = m.v2[3 * i + k], c = m.v3[3 * i + k];
+            float l = std::fmin(std::fmin(a, b), c), h = std::fmax(std::fmax(a, b), c);
+            const float e = std::fmax(std::fabs(l), std::fabs(h)) * 2.0e-6f + 1e-30f;
+            lo[3 * i + k] = l - e; hi[3 * i + k] = h + e;
+        }
+    const auto t0 = std::chrono::steady_clock::now();
+    BvhResult b2;
+    build_bvh(lo.data(), hi.data(), (int64_t)n, 0, b2, 3, false, std::getenv("BINS") ? std::atoi(std::getenv("BINS")) : 32);
+    WideCollapser wc{b2.nodes, W};
+    const size_t nn = b2.nodes.size();
+    wc.cost.assign(nn * W, 0.0);
+    wc.choice.assign(nn * W, 0);
+    wc.as_leaf.assign(nn, 0);
+    wc.prims.assign(nn, 0);
+    wc.first.assign(nn, 0);
+    wc.solve(0);
+    T.W = W;
+    T.Q = Q;
+    T.nodes.emplace_back();
+    wc.emit(T, 0, 0, 0);
+    quantize(T);
+    build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    order = b2.order;
+    size_t used = 0;
+    for (const WNode& nd : T.nodes) used += nd.c.size();
+    T.fill = (double)used / ((double)W * (double)T.nodes.size());
+}
+struct WideTracer {
+    const Mesh& m;
+    const WideTree& T;
+    const std::vector<uint32_t>& order;
+    v3 tv(const std::vector<float>& a, uint32_t p) const { uint32_t s = order[p]; return v3{a[3 * s], a[3 * s + 1], a[3 * s + 2]}; }
+    double trace(v3 o, v3 d, bool any, double tlim, Count& c, int32_t& prim, double& tests, int& max_stack) const {
+        c.rays++;
+        const v3 invd{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        double best = any ? tlim : kHitInf;
+        prim = -1;
+        float tmax = (float)best;
+        std::vector<uint32_t> stack;
+        uint32_t ref = 0;
+        for (;;) {
+            if (!(ref & 0x80000000u)) {
+                c.nodes++;
+                const WNode& nd = T.nodes[ref];
+                float key[8];
+                uint32_t ch[8];
+                int nh = 0;
+                for (const WChild& w : nd.c) {
+                    tests++;
+                    const float tx0 = (w.lo[0] - o.x) * invd.x, tx1 = (w.hi[0] - o.x) * invd.x;
+                    const float ty0 = (w.lo[1] - o.y) * invd.y, ty1 = (w.hi[1] - o.y) * invd.y;
+                    const float tz0 = (w.lo[2] - o.z) * invd.z, tz1 = (w.hi[2] - o.z) * invd.z;
+                    const float tn = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmax(std::fmin(tz0, tz1), 0.f));
+                    const float tf = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmin(std::fmax(tz0, tz1), tmax));
+                    if (tn <= tf) {
+                        key[nh] = tn; ch[nh] = w.ref; nh++;
+                        if (o.x >= w.lo[0] && o.x <= w.hi[0] && o.y >= w.lo[1] && o.y <= w.hi[1] && o.z >= w.lo[2] && o.z <= w.hi[2])
+                            c.inside++;
+                    }
+                }
+                for (int a = 1; a < nh; a++)
+                    for (int b = a; b > 0 && key[b] < key[b - 1]; b--) { std::swap(key[b], key[b - 1]); std::swap(ch[b], ch[b - 1]); }
+                if (nh > 0) {
+                    for (int k = nh - 1; k >= 1; k--) stack.push_back(ch[k]);
+                    max_stack = std::max(max_stack, (int)stack.size());
+                    ref = ch[0];
+                    continue;
+                }
+            } else {
+                c.leaves++;
+                const uint32_t first = ref & 0x1FFFFFFFu, cnt = ((ref >> 29) & 3u) + 1u;
+                for (uint32_t k = 0; k < cnt; k++) {
+                    c.tris++;
+                    const v3 a = tv(m.v1, first + k);
+                    const double t = isect_tri(a, sub(tv(m.v2, first + k), a), sub(tv(m.v3, first + k), a), o, d);
+                    if (t < best) {
+                        best = t;
+                        prim = (int32_t)(first + k);
+                        tmax = (float)t * 1.0000002f;
+                        if (any) return best;
+                    }
+                }
+            }
+            if (stack.empty()) break;
+            ref = stack.back();
+            stack.pop_back();
+        }
+        return best;
+    }
+};
+
 static double tree_sah(const Tree& T, double c_tri) {
     // expected steps per ray through the root box: Σ P(node)·1 + Σ P(leaf)·(1 + n·c_tri), P = area ratio
     auto area = [](const float* lo, const float* hi) {
@@ -259,6 +495,77 @@ static void cache_study(const Mesh& m, const Tree& T, long nrays) {
                 "deal by origin region %.3f\n", nrays, (double)acc / nrays, (double)hit_rr / acc, (double)hit_reg / acc);
 }
 
+// The C4 ray mix (main's loop) through a wide tree: steps (lines) per ray by depth and for shadow rays.
+static void run_wide(const Mesh& m, int W, int Q, int stride) {
+    WideTree T;
+    std::vector<uint32_t> order;
+    double bs = 0;
+    build_wide(m, W, Q, T, order, bs);
+    WideTracer tr{m, T, order};
+    const int Wd = 1920, H = 1080, kDepth = 4;
+    const v3 lights[2] = {v3{0.f, 5.f, 0.f}, v3{4.f, 5.f, 4.f}};
+    Count cd[kDepth + 1], csh;
+    double tests_c = 0, tests_s = 0;
+    int max_stack = 0;
+    std::mt19937_64 rng(12345);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    const v3 cp{m.cam_p[0], m.cam_p[1], m.cam_p[2]}, cu{m.cam_u[0], m.cam_u[1], m.cam_u[2]};
+    const v3 cv{m.cam_v[0], m.cam_v[1], m.cam_v[2]}, cw{m.cam_w[0], m.cam_w[1], m.cam_w[2]};
+    for (int y = stride / 2; y < H; y += stride)
+        for (int x = stride / 2; x < Wd; x += stride) {
+            const double aspect = Wd / (double)H;
+            const double px = ((x + 0.5 - 0.5) / (Wd - 1.0)) * 2 - 1, py = ((y + 0.5 - 0.5) / (H - 1.0)) * 2 - 1;
+            v3 d = normalize(add(add(muls(cu, -px * aspect), muls(cv, -py)), muls(cw, m.cam_m)));
+            v3 o = cp;
+            for (int depth = 0; depth <= kDepth; depth++) {
+                int32_t prim;
+                double t = tr.trace(o, d, false, 0, cd[depth], prim, tests_c, max_stack);
+                v3 nrm;
+                if (d.y < 0) {
+                    const double tf = -(double)o.y / (double)d.y;
+                    if (tf > kEps && tf < t) { t = tf; prim = -2; }
+                }
+                if (prim == -1) break;
+                const v3 p = add(o, muls(d, t));
+                if (prim == -2) nrm = v3{0.f, 1.f, 0.f};
+                else {
+                    const v3 a = tr.tv(m.v1, (uint32_t)prim);
+                    nrm = normalize(cross(sub(tr.tv(m.v2, (uint32_t)prim), a), sub(tr.tv(m.v3, (uint32_t)prim), a)));
+                    if (dotf(nrm, d) > 0) nrm = neg(nrm);
+                }
+                for (const v3& L : lights) {
+                    const v3 ld = normalize(sub(L, p));
+                    const double tl = (double)lengthf(sub(L, p)) - 1.0;
+                    int32_t sprim;
+                    tr.trace(p, ld, true, tl, csh, sprim, tests_s, max_stack);
+                }
+                const double r1 = U(rng) * 2 * kPi, r2 = U(rng), r2s = std::sqrt(r2);
+                const v3 ax = std::fabs(nrm.x) > 0.1f ? v3{0.f, 1.f, 0.f} : v3{1.f, 0.f, 0.f};
+                const v3 u = normalize(cross(ax, nrm)), vv = cross(nrm, u);
+                d = normalize(add(add(muls(u, std::cos(r1) * r2s), muls(vv, std::sin(r1) * r2s)), muls(nrm, std::sqrt(1 - r2))));
+                o = p;
+            }
+        }
+    Count all;
+    for (auto& c : cd) all.add(c);
+    std::printf("wide W=%d Q=%d nodes %zu leaves %zu fill %.3f depth %d max stack %d build %.2fs\n", W, Q, T.nodes.size(),
+                T.leaves, T.fill, T.depth, max_stack, bs);
+    auto row = [](const char* name, const Count& c, double tests) {
+        if (c.rays == 0) return;
+        std::printf("  %-9s rays %9.0f  steps/ray %6.3f  nodes/ray %6.3f  leaves/ray %6.3f  tris/ray %6.3f  origin-box %6.3f  box tests/ray %6.2f\n",
+                    name, c.rays, (c.nodes + c.leaves) / c.rays, c.nodes / c.rays, c.leaves / c.rays, c.tris / c.rays,
+                    c.inside / c.rays, tests / c.rays);
+    };
+    row("closest", all, tests_c);
+    for (int k = 0; k <= kDepth; k++) {
+        char nm[16];
+        std::snprintf(nm, sizeof nm, "depth %d", k);
+        row(nm, cd[k], NAN);
+    }
+    row("shadow", csh, tests_s);
+    std::fflush(stdout);
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: %s MESH.bin [stride] [variant ...]\n", argv[0]); return 2; }
     Mesh m;
@@ -270,6 +577,11 @@ int main(int argc, char** argv) {
     const int W = 1920, H = 1080, kDepth = 4;
     const v3 lights[2] = {v3{0.f, 5.f, 0.f}, v3{4.f, 5.f, 4.f}};
     for (const auto& var : variants) {
+        int W = 0, Q = 0;
+        if (std::sscanf(var.c_str(), "w%dq%d", &W, &Q) == 2) {   // wide-node model: w8q8, w8q16, w4q0 ...
+            run_wide(m, W, Q, stride);
+            continue;
+        }
         Tree T;
         double bs = 0;
         build(m, var, T, bs);
