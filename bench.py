@@ -21,10 +21,10 @@ kernel and `cpu_baseline` (the oracle port timed on this host).
 
 --workload c3 / c2 measure the other GPU configs of BASELINE.json the same way (not the
 driver's line): C3 = the 69,451-triangle mesh in the same frame (L2 roofline of its dominant
-kernel), C2 = the gopher 3-sphere scene, NewSampler(16,16), no triangle BVH — a latency /
-VALU-bound path, priced as SURVEY.md §8d says against the FP32 vector peak (157 TFLOP/s) with
-F_ray = 80 flops per BVH4 node + 22 per primitive test + 60 per shading fetch, and beside it the
-dominant kernel's measured VALU issue fraction (profiles/pmc_valu_c2.json, when present).
+kernel), C2 = the gopher 3-sphere scene, NewSampler(16,16), no triangle BVH, and C5 = the mixed 4K
+scene: both VALU-issue-bound (fp64 sampler math; fp64 marches), priced by the pass' measured VALU issue
+cycles per ray (PMC instruction mix by kind, profiles/pmc_valu_mix_<workload>.json) against 1024 SIMDs
+at 2.4 GHz, with the measured fp32 / fp64 FLOP rates beside it.
 
 Roofline: the closest-hit kernel's algorithmic bytes (per ray: 112 B per
 BVH4 node fetch, 36 B per primitive test, 44 B ray in + hit out) over its HIP-event time,
@@ -56,14 +56,11 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md (FP32 vector peak)
 # FP64 vector peak: half the FP32 rate (a wave64 fp64 FMA issues over 4 cycles against 2 for
 # fp32, MI355X_MICROARCH.md "issue cost"; AMD's MI355X specification: 78.6 TFLOP/s)
 FP64_PEAK_TFLOPS = 78.6
-# C5 march steps (algorithmic fp64 flops): one Volume.Sample of Volume.Intersect (Volume.cs:73-131:
-# the coordinate maps 10, seven trilinear lerps 28, the window test 2, the step position 6) and one
-# SDF evaluation of SDFShape.Intersect (SDF.cs:32-76, the C5 torus: TransformSDF's MulPosition 18,
-# TorusSDF's two LengthN 14 + 2, the step 3 + position 6)
-F_VOX, F_SDF = 46, 43
-# C2 flops: slab tests of a BVH4 node's four boxes, a primitive test (gopher3:
-# two cubes ≈30, three spheres ≈14 → 22 on average), and the shading of a closest hit
-F_NODE, F_PRIM, F_SHADE = 80, 22, 60
+# VALU issue peak: 1024 SIMDs (256 CUs x 4) each issuing one cycle's work per cycle at 2.4 GHz, in
+# T SIMD-cycles/s.  C2 and C5 are priced by their measured VALU issue cycles (tools/gpu_valu_mix.sh ->
+# profiles/pmc_valu_mix_*.json): a flop model (round 4: 60 fp32 flops per shading) missed the fp64
+# sincos / acos / sqrt chains that are most of their work.
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 1e12
 WORKLOADS = {
     "c4": "C4: 1M-triangle mesh in Example.bunny's scene, 1920x1080, NewSampler(4,4) SpecularModeFirst",
     "c3": "C3: 69,451-triangle mesh in Example.bunny's scene, 1920x1080, NewSampler(4,4) SpecularModeFirst",
@@ -77,11 +74,11 @@ WORKLOADS = {
 DEFAULTS = {"c5": dict(steps=2, warmup=1, spp=1, width=3840, height=2160, adaptive=32)}
 DEFAULT = dict(steps=64, warmup=2, spp=16, width=1920, height=1080, adaptive=0)
 
-# Algorithmic bytes per unit: per ray 112 B per 4-wide BVH node
-# fetched (four child boxes of 24 B + four 4-B child refs), 36 B per primitive
-# tested (v0, e1, e2), 28 B ray in + 16 B hit out, and 40 B (three normals +
-# material id) per closest-hit shading fetch.
-B_NODE, B_PRIM, B_RAY, B_SHADE = 112, 36, 28 + 16, 40
+# Algorithmic bytes per unit (SURVEY.md §8d with this BVH's node): per ray 128 B per node fetched (the
+# triangle BVH's 8-wide node: origin, steps, child bases and counts 32 B + eight quantized child boxes 96 B;
+# round 4's BVH4 node was 112 B: four 24-B boxes and four refs), 36 B per primitive tested (v0, e1, e2),
+# 28 B ray in + 16 B hit out, and 40 B (three normals + material id) per closest-hit shading fetch.
+B_NODE, B_PRIM, B_RAY, B_SHADE = 128, 36, 28 + 16, 40
 
 
 def _gloo_gather(r, dist, rank, world, mine):
@@ -591,50 +588,49 @@ def main(argv=None):
                                 f"Infinity-Cache hits included), profiles/pmc_traffic_{a.workload}.json ({tw.get('tag')}), "
                                 f"same workload"}
 
-    if a.workload == "c5":
-        # C5: the marches (Volume.Intersect's fixed 1/512 steps, SDFShape's sphere tracing) are fp64
-        # scalar work: the pass' algorithmic flops (BVH nodes and primitive tests in fp32 as C2's,
-        # march steps in fp64) over the whole pass' kernel time, against the FP64 vector peak (the
-        # binding one for the steps that dominate), the dominant kernel and the step counts beside it
-        fl_ray = (F_NODE * ctr.nodes_visited + F_PRIM * ctr.prims_tested + F_SHADE * ctr.shading_fetches
-                  + F_VOX * ctr.volume_samples + F_SDF * ctr.sdf_evals) / max(ctr.rays, 1)
-        tflops = fl_ray * rays / (kernel_ms * 1e-3) / 1e12
-        out["roofline"] = {
-            "bound": "valu", "kernel": "whole pass", "achieved": round(tflops, 4), "peak": FP64_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(tflops / FP64_PEAK_TFLOPS, 6), **whole_traffic(rays),
-            "flops_per_ray": round(fl_ray, 2),
-            "volume_samples_per_ray": round(ctr.volume_samples / max(ctr.rays, 1), 3),
-            "sdf_evals_per_ray": round(ctr.sdf_evals / max(ctr.rays, 1), 3),
+    def valu_roofline():   # C2 / C5: whole pass bound by VALU issue (measured instruction mix, profiles/)
+        pv = os.path.join(ROOT, "profiles", f"pmc_valu_mix_{a.workload}.json")
+        if not os.path.exists(pv):
+            return {"bound": "valu_issue", "kernel": "whole pass", "achieved": None, "peak": VALU_ISSUE_PEAK,
+                    "unit": "T SIMD-cycles/s", "frac": None, "note": f"{pv} missing (tools/gpu_valu_mix.sh)"}
+        with open(pv) as f:
+            vm = json.load(f)
+        pr = vm["per_ray"]
+        sec = kernel_ms * 1e-3
+        achieved = pr["valu_issue_cycles"] * rays / sec / 1e12
+        f32 = pr["fp32_flops"] * rays / sec / 1e12
+        f64 = pr["fp64_flops"] * rays / sec / 1e12
+        dom_k = max(vm["kernels"].items(), key=lambda kv: kv[1]["valu_issue_cycles"])
+        return {
+            "bound": "valu_issue", "kernel": "whole pass",
+            "achieved": round(achieved, 5), "peak": VALU_ISSUE_PEAK, "unit": "T SIMD-cycles/s",
+            "frac": round(achieved / VALU_ISSUE_PEAK, 5), **whole_traffic(rays),
+            "valu_issue_cycles_per_ray": round(pr["valu_issue_cycles"], 2), "valu_insts_per_ray": round(pr["valu_insts"], 2),
+            "f64_insts_per_ray": round(pr["f64_insts"], 2),
+            "measured_fp32_tflops": round(f32, 4), "measured_fp32_frac": round(f32 / FP32_PEAK_TFLOPS, 5),
+            "measured_fp64_tflops": round(f64, 4), "measured_fp64_frac": round(f64 / FP64_PEAK_TFLOPS, 5),
+            "issue_model": "cycles per wave64 instruction: 2 (fp32 / int), 4 (fp64 add / mul / fma), 8 (fp32 transcendental), "
+                           "16 (fp64 transcendental); peak = 1024 SIMDs x 2.4 GHz",
+            "mix_source": f"profiles/pmc_valu_mix_{a.workload}.json ({vm.get('tag')}: SQ_INSTS_VALU and its per-kind "
+                          f"counters, SQ_INSTS_VALU_FLOPS_FP32/FP64, same workload)",
+            "dominant_kernel": dom_k[0], "dominant_kernel_valu_issue_frac_under_counters": dom_k[1]["valu_issue_frac"],
+            "pass_valu_issue_frac_under_counters": vm.get("pass_valu_issue_frac_under_counters"),
             "nodes_per_ray": round(ctr.nodes_visited / max(ctr.rays, 1), 3),
-            "dominant_kernel": names[dom], "dominant_kernel_ms_per_step": round(float(kms[dom]) / a.steps, 3),
-            "flop_model": f"{F_NODE}/BVH4 node, {F_PRIM}/primitive test, {F_SHADE}/shading fetch (fp32), "
-                          f"{F_VOX}/Volume.Sample, {F_SDF}/SDF evaluation (fp64)",
+            **({"volume_samples_per_ray": round(ctr.volume_samples / max(ctr.rays, 1), 3),
+                "sdf_evals_per_ray": round(ctr.sdf_evals / max(ctr.rays, 1), 3)} if a.workload == "c5" else {}),
         }
+
+    if a.workload in ("c2", "c5"):
+        # C2 (fp64 sampler math, 16 children per camera hit) and C5 (the fp64 Volume / SDF marches) are
+        # bound by VALU issue, not by bytes: the pass' measured VALU issue cycles per ray (instruction mix
+        # by kind from PMC counters, priced at each kind's issue cost) over the pass' kernel time, against
+        # 1024 SIMDs issuing every cycle; the measured fp32 / fp64 FLOP rates beside it
+        out["roofline"] = valu_roofline()
 
     # keys that do not apply to this run are left out rather than null (one GPU: no gather; C2: no mesh)
     for k in ("gather_check", "mesh_source"):
         if out["config"].get(k, 0) is None:
             del out["config"][k]
-
-    if a.workload == "c2":
-        # C2 is priced in flops against the FP32 vector peak (whole pass), with the
-        # dominant kernel's measured VALU issue fraction beside it
-        flops_ray = (F_NODE * ctr.nodes_visited + F_PRIM * ctr.prims_tested + F_SHADE * ctr.shading_fetches) / max(ctr.rays, 1)
-        tflops = flops_ray * rays / (kernel_ms * 1e-3) / 1e12
-        valu = None
-        pv = os.path.join(ROOT, "profiles", "pmc_valu_c2.json")
-        if os.path.exists(pv):
-            with open(pv) as f:
-                vj = json.load(f)
-            valu = vj.get("kernels", {}).get(names[dom], {}).get("valu_issue_frac")
-        out["roofline"] = {
-            "bound": "valu", "kernel": "whole pass", "achieved": round(tflops, 4), "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(tflops / FP32_PEAK_TFLOPS, 6), **whole_traffic(rays),
-            "flops_per_ray": round(flops_ray, 2),
-            "dominant_kernel": names[dom], "dominant_kernel_ms_per_step": round(float(kms[dom]) / a.steps, 3),
-            "dominant_kernel_valu_issue_frac": valu,
-            "valu_issue_source": "profiles/pmc_valu_c2.json (SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE))",
-        }
 
     # ---------------- CPU baseline + parity sample (rank 0, N = 1 only)
     if world == 1 and a.workload == "c4" and (a.cpu_seconds > 0 or not a.no_parity):

@@ -409,9 +409,9 @@ constexpr int kTriBins = 128;
 constexpr double kTriCost = 0.5;
 int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_nodes, bool sah = false) {
     pt::Bvh4Result r;
-    if (sah) pt::collapse_bvh4_sah(b, pt::kStackMax, r, 1.0, kTriCost, 3);
-    else pt::collapse_bvh4(b, pt::kStackMax, r);
-    if (r.stack_need > pt::kStackMax) return fail(PT_ERR_UNSUPPORTED, "BVH4 traversal stack bound exceeded");
+    if (sah) pt::collapse_bvh4_sah(b, pt::kStack4Budget, r, 1.0, kTriCost, 3);
+    else pt::collapse_bvh4(b, pt::kStack4Budget, r);
+    if (r.stack_need > pt::kStack4Budget) return fail(PT_ERR_UNSUPPORTED, "BVH4 traversal stack bound exceeded");
     out.resize(r.words.size() / 4);
     std::memcpy(out.data(), r.words.data(), r.words.size() * sizeof(uint32_t));
     num_nodes = (int32_t)r.nodes();
@@ -524,18 +524,43 @@ std::shared_ptr<const TriBvhBuild> build_tri_bvh(const pt_scene_desc* d, const s
         tri_recs[3 * i + 1] = f4(e1.y, e1.z, e2.x, e2.y);
         tri_recs[3 * i + 2] = f4(e2.z, 0.f, 0.f, 0.f);
     }
-    out->rc = pack_nodes(tb, out->nodes, out->num_nodes, true);
-    if (out->rc == PT_OK) out->rc = make_leaf_chunks(out->nodes, tri_recs, out->chunks);
-    if (out->rc != PT_OK) { out->err = g_last_error; return out; }
-    if (!out->nodes.empty()) {   // root box = union of the root node's used child slots (pt_bvh.h layout)
-        const float* w = reinterpret_cast<const float*>(out->nodes.data());
-        const uint32_t* refs = reinterpret_cast<const uint32_t*>(w + 24);
+    // 8-wide nodes with quantized child boxes (pt_bvh.h collapse_bvh8q), leaf chunks as make_leaf_chunks' (one
+    // 128-B line per leaf: the first record in word 0, up to three {v1, e1, e2})
+    pt::Bvh8Result b8;
+    pt::collapse_bvh8q(tb, pt::kStackMax, b8, 1.0, kTriCost, 3);
+    if (b8.stack_need > pt::kStackMax) {
+        out->rc = fail(PT_ERR_UNSUPPORTED, "BVH8 traversal stack bound exceeded");
+        out->err = g_last_error;
+        return out;
+    }
+    if (b8.chunk_first.size() > 0x1FFFFFFFu) {
+        out->rc = fail(PT_ERR_UNSUPPORTED, "too many triangle leaves");
+        out->err = g_last_error;
+        return out;
+    }
+    out->nodes.resize(b8.words.size() / 4);
+    std::memcpy(out->nodes.data(), b8.words.data(), b8.words.size() * sizeof(uint32_t));
+    out->num_nodes = (int32_t)b8.nodes();
+    out->chunks.resize(8 * b8.chunk_first.size());
+    for (size_t ci = 0; ci < b8.chunk_first.size(); ci++) {
+        float w[32] = {0.f};
+        const uint32_t first = b8.chunk_first[ci], cnt = b8.chunk_count[ci];
+        std::memcpy(&w[0], &first, 4);
+        for (uint32_t t = 0; t < cnt; t++) {
+            const float* rf = reinterpret_cast<const float*>(&tri_recs[3 * (size_t)(first + t)]);
+            for (int j = 0; j < 9; j++) w[1 + 9 * t + j] = rf[j];
+        }
+        std::memcpy(&out->chunks[8 * ci], w, sizeof w);
+    }
+    if (!out->nodes.empty()) {   // root box = union of the root node's children (their quantized boxes)
+        const uint32_t* w = b8.words.data();
         for (int ax = 0; ax < 3; ax++) { out->box[ax] = INFINITY; out->box[3 + ax] = -INFINITY; }
-        for (int k = 0; k < 4; k++) {
-            if (refs[k] == pt::kEmpty4) continue;
+        for (int k = 0; k < (int)(w[3] >> 28); k++) {
+            float lo[3], hi[3];
+            pt::bvh8_child_box(w, k, lo, hi);
             for (int ax = 0; ax < 3; ax++) {
-                out->box[ax] = std::min(out->box[ax], w[8 * ax + k]);
-                out->box[3 + ax] = std::max(out->box[3 + ax], w[8 * ax + 4 + k]);
+                out->box[ax] = std::min(out->box[ax], lo[ax]);
+                out->box[3 + ax] = std::max(out->box[3 + ax], hi[ax]);
             }
         }
     }

@@ -421,6 +421,269 @@ void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out,
     c.emit(root, 0, 0, 0);
 }
 
+namespace {
+
+// ---- 8-wide quantized collapse (pt_bvh.h collapse_bvh8q)
+constexpr int kW8 = 8;
+constexpr uint32_t kQMax = 2047;   // child bounds as binary16 integers: 0..2047 are exact
+
+uint16_t half_of_int(uint32_t q) {   // an integer 0..2047 as binary16 bits (exact)
+    if (q == 0) return 0;
+    int e = 31 - __builtin_clz(q);   // 2^e <= q < 2^(e+1), e <= 10
+    return (uint16_t)(((uint32_t)(e + 15) << 10) | ((q - (1u << e)) << (10 - e)));
+}
+uint32_t int_of_half(uint16_t h) {   // the inverse, for the integers half_of_int makes
+    if (h == 0) return 0;
+    const int e = (int)(h >> 10) - 15;
+    return (1u << e) + ((uint32_t)(h & 0x3FFu) >> (10 - e));
+}
+
+struct Wide8 {
+    const std::vector<BvhNode>& n2;
+    Bvh8Result& out;
+    double c_step, c_tri;
+    int max_leaf, budget;
+    std::vector<int> height;       // BVH2 stack need below a node (greedy bound)
+    std::vector<double> cost;      // [node][8]: cost(n, i + 1)
+    std::vector<int8_t> choice;    // [node][8]: 0 one slot, -1 as with one slot fewer, k > 0: k slots to the left child
+    std::vector<uint8_t> as_leaf;  // one slot: a leaf chunk rather than an inner node
+    std::vector<uint32_t> prims, first;
+
+    bool is_leaf(uint32_t i) const { return n2[i].b != 0; }
+    double area(uint32_t i) const {
+        const BvhNode& n = n2[i];
+        double dx = (double)n.bmax[0] - n.bmin[0], dy = (double)n.bmax[1] - n.bmin[1], dz = (double)n.bmax[2] - n.bmin[2];
+        if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+        return dx * dy + dy * dz + dz * dx;
+    }
+    int fill_height(uint32_t i) {
+        if (is_leaf(i)) return height[i] = 0;
+        const int l = fill_height(n2[i].a), r = fill_height(n2[i].a + 1);
+        return height[i] = 1 + std::max(l, r);
+    }
+    double dist(uint32_t n, int j, int& kbest) const {
+        const double* CL = &cost[(size_t)n2[n].a * kW8];
+        const double* CR = &cost[(size_t)(n2[n].a + 1) * kW8];
+        double best = INFINITY;
+        kbest = -1;
+        for (int k = 1; k < j; k++) {
+            const double c = CL[k - 1] + CR[j - k - 1];
+            if (c < best) { best = c; kbest = k; }
+        }
+        return best;
+    }
+    void solve(uint32_t n) {
+        double* C = &cost[(size_t)n * kW8];
+        int8_t* ch = &choice[(size_t)n * kW8];
+        const double a = area(n);
+        if (is_leaf(n)) {
+            prims[n] = n2[n].b;
+            first[n] = n2[n].a;
+            for (int i = 0; i < kW8; i++) { C[i] = a * (c_step + c_tri * (double)prims[n]); ch[i] = 0; }
+            as_leaf[n] = 1;
+            return;
+        }
+        const uint32_t l = n2[n].a, r = l + 1;
+        solve(l);
+        solve(r);
+        prims[n] = prims[l] + prims[r];
+        first[n] = first[l];
+        int kw;
+        const double inner = a * c_step + dist(n, kW8, kw);
+        const double leaf = (int)prims[n] <= max_leaf ? a * (c_step + c_tri * (double)prims[n]) : INFINITY;
+        as_leaf[n] = leaf <= inner;
+        C[0] = std::min(leaf, inner);
+        ch[0] = 0;
+        for (int i = 2; i <= kW8; i++) {
+            int k;
+            const double d = dist(n, i, k);
+            if (d < C[i - 2]) { C[i - 1] = d; ch[i - 1] = (int8_t)k; }
+            else { C[i - 1] = C[i - 2]; ch[i - 1] = -1; }
+        }
+    }
+    void slots(uint32_t n, int i, std::vector<uint32_t>& outs) const {
+        const int8_t c = choice[(size_t)n * kW8 + (size_t)(i - 1)];
+        if (c == 0) { outs.push_back(n); return; }
+        if (c < 0) { slots(n, i - 1, outs); return; }
+        slots(n2[n].a, c, outs);
+        slots(n2[n].a + 1, i - c, outs);
+    }
+    // greedy children of subtree root set C within the budget (collapse_bvh4's rule, 8 slots)
+    void greedy(std::vector<uint32_t>& C, int A) const {
+        while (C.size() < (size_t)kW8) {
+            int pick = -1;
+            double best = -1.0;
+            for (size_t k = 0; k < C.size(); k++) {
+                if (is_leaf(C[k])) continue;
+                int maxh = 0;
+                for (size_t j = 0; j < C.size(); j++)
+                    if (j != k) maxh = std::max(maxh, height[C[j]]);
+                maxh = std::max(maxh, std::max(height[n2[C[k]].a], height[n2[C[k]].a + 1]));
+                if (A + (int)C.size() + maxh > budget) continue;
+                const double a = area(C[k]);
+                if (a > best) { best = a; pick = (int)k; }
+            }
+            if (pick < 0) break;
+            const uint32_t e = C[(size_t)pick];
+            C[(size_t)pick] = n2[e].a;
+            C.push_back(n2[e].a + 1);
+        }
+    }
+    std::vector<int> need_memo;    // [node]: stack entries the DP collapse of subtree n pushes on its worst path
+    void dp_children(uint32_t n, std::vector<uint32_t>& C) const {
+        int k;
+        (void)dist(n, kW8, k);
+        slots(n2[n].a, k, C);
+        slots(n2[n].a + 1, kW8 - k, C);
+    }
+    int need(uint32_t n) {
+        int& r = need_memo[n];
+        if (r >= 0) return r;
+        std::vector<uint32_t> C;
+        dp_children(n, C);
+        int m = 0;
+        for (uint32_t c : C)
+            if (!as_leaf[c]) m = std::max(m, need(c));
+        return r = (int)C.size() - 1 + m;
+    }
+    uint32_t alloc(int k) {
+        const uint32_t at = (uint32_t)out.nodes();
+        out.words.resize(out.words.size() + (size_t)k * kNode8Words, 0u);
+        return at;
+    }
+    // node `at` for BVH2 inner node n, A entries pushed by the ancestors.  The DP's children when its whole
+    // collapse below keeps the stack within the budget (need), else the greedy children, which keep it by
+    // construction (A + height(n) <= budget holds from the root down, the BVH2 depth being bounded).
+    void emit(uint32_t at, uint32_t n, int A, int depth) {
+        out.depth = std::max(out.depth, depth);
+        std::vector<uint32_t> C;
+        bool leafy[kW8] = {false};
+        const bool dp = A + need(n) <= budget;
+        if (dp) {
+            dp_children(n, C);
+        } else {
+            C = {n2[n].a, n2[n].a + 1};
+            greedy(C, A);
+        }
+        for (size_t k = 0; k < C.size(); k++) leafy[k] = dp ? as_leaf[C[k]] != 0 : is_leaf(C[k]);
+        // inner children first, then leaves (pt_bvh.h layout)
+        std::vector<uint32_t> inner, leaves;
+        for (size_t k = 0; k < C.size(); k++) (leafy[k] ? leaves : inner).push_back(C[k]);
+        C = inner;
+        C.insert(C.end(), leaves.begin(), leaves.end());
+        const int nc = (int)C.size(), nin = (int)inner.size();
+        const int pushed = A + nc - 1;
+        out.stack_need = std::max(out.stack_need, pushed);
+        out.children += nc;
+        const uint32_t base_in = nin ? alloc(nin) : 0u;
+        const uint32_t base_chunk = (uint32_t)out.chunk_first.size();
+        uint32_t cnt_bits = 0;
+        for (int k = nin; k < nc; k++) {
+            const uint32_t c = C[(size_t)k];
+            const uint32_t np = dp ? prims[c] : n2[c].b, fp = dp ? first[c] : n2[c].a;
+            out.chunk_first.push_back(fp);
+            out.chunk_count.push_back((uint8_t)np);
+            cnt_bits |= (np - 1u) << (2 * k);
+        }
+        uint32_t* w = &out.words[(size_t)at * kNode8Words];
+        // quantization, per axis: origin = the children's lowest bound, step 2^e the least power of two with
+        // every bound within kQMax steps; q rounded outward (exact arithmetic in double)
+        uint32_t ebits = 0;
+        uint16_t qb[6][kW8];
+        for (int ax = 0; ax < 3; ax++) {
+            float o = INFINITY, top = -INFINITY;
+            for (uint32_t c : C) { o = std::min(o, n2[c].bmin[ax]); top = std::max(top, n2[c].bmax[ax]); }
+            const double ext = (double)top - (double)o;
+            int e = -126;
+            while (e < 127 && std::ldexp((double)kQMax, e) < ext) e++;
+            for (;;) {   // the outward rounding can need one more step
+                bool ok = true;
+                for (int k = 0; k < nc && ok; k++) {
+                    const double hi = std::ceil(((double)n2[C[(size_t)k]].bmax[ax] - (double)o) / std::ldexp(1.0, e));
+                    ok = hi <= (double)kQMax;
+                }
+                if (ok || e >= 127) break;
+                e++;
+            }
+            std::memcpy(&w[ax], &o, 4);
+            ebits |= (uint32_t)(e + 127) << (8 * ax);
+            for (int k = 0; k < kW8; k++) {
+                if (k >= nc) { qb[2 * ax][k] = 0x7C00; qb[2 * ax + 1][k] = 0xFC00; continue; }   // +inf / -inf
+                const double step = std::ldexp(1.0, e);
+                const double lo = std::floor(((double)n2[C[(size_t)k]].bmin[ax] - (double)o) / step);
+                const double hi = std::ceil(((double)n2[C[(size_t)k]].bmax[ax] - (double)o) / step);
+                qb[2 * ax][k] = half_of_int((uint32_t)std::max(0.0, lo));
+                qb[2 * ax + 1][k] = half_of_int((uint32_t)std::min((double)kQMax, std::max(0.0, hi)));
+            }
+        }
+        w[3] = ebits | ((uint32_t)nin << 24) | ((uint32_t)nc << 28);
+        w[4] = base_in;
+        w[5] = base_chunk - (uint32_t)nin;   // leaf slot k's chunk is w[5] + k
+        w[6] = cnt_bits;
+        w[7] = 0;
+        for (int r = 0; r < 6; r++)
+            for (int k = 0; k < kW8; k += 2) w[8 + 4 * r + k / 2] = (uint32_t)qb[r][k] | ((uint32_t)qb[r][k + 1] << 16);
+        for (int k = 0; k < nin; k++) emit(base_in + (uint32_t)k, C[(size_t)k], pushed, depth + 1);
+    }
+};
+
+}  // namespace
+
+void bvh8_child_box(const uint32_t* w, int slot, float lo[3], float hi[3]) {
+    for (int ax = 0; ax < 3; ax++) {
+        float o;
+        std::memcpy(&o, &w[ax], 4);
+        const int e = (int)((w[3] >> (8 * ax)) & 0xFFu) - 127;
+        const uint16_t hl = (uint16_t)(w[8 + 8 * ax + slot / 2] >> (16 * (slot & 1)));
+        const uint16_t hh = (uint16_t)(w[12 + 8 * ax + slot / 2] >> (16 * (slot & 1)));
+        if (hl == 0x7C00) { lo[ax] = INFINITY; hi[ax] = -INFINITY; continue; }
+        const double l = (double)o + std::ldexp((double)int_of_half(hl), e), h = (double)o + std::ldexp((double)int_of_half(hh), e);
+        float fl = (float)l, fh = (float)h;
+        if ((double)fl > l) fl = std::nextafter(fl, -INFINITY);
+        if ((double)fh < h) fh = std::nextafter(fh, INFINITY);
+        lo[ax] = fl;
+        hi[ax] = fh;
+    }
+}
+
+void collapse_bvh8q(const BvhResult& bvh2, int stack_budget, Bvh8Result& out, double c_step, double c_tri, int max_leaf) {
+    out = Bvh8Result{};
+    if (bvh2.nodes.empty()) return;
+    const size_t nn = bvh2.nodes.size();
+    Wide8 c{bvh2.nodes, out, c_step, c_tri, max_leaf, stack_budget, std::vector<int>(nn, 0), std::vector<double>(nn * kW8, 0.0),
+            std::vector<int8_t>(nn * kW8, 0), std::vector<uint8_t>(nn, 0), std::vector<uint32_t>(nn, 0),
+            std::vector<uint32_t>(nn, 0), std::vector<int>(nn, -1)};
+    c.fill_height(0);
+    c.solve(0);
+    const uint32_t root = c.alloc(1);
+    if (c.is_leaf(0)) {   // a lone leaf: the root node holds it in slot 0
+        uint32_t* w = &out.words[0];
+        for (int ax = 0; ax < 3; ax++) std::memcpy(&w[ax], &bvh2.nodes[0].bmin[ax], 4);
+        uint32_t ebits = 0;
+        for (int ax = 0; ax < 3; ax++) {
+            const double ext = (double)bvh2.nodes[0].bmax[ax] - (double)bvh2.nodes[0].bmin[ax];
+            int e = -126;
+            while (e < 127 && std::ldexp((double)kQMax, e) < ext) e++;
+            ebits |= (uint32_t)(e + 127) << (8 * ax);
+            const double hi = std::ceil(ext / std::ldexp(1.0, e));
+            for (int k = 0; k < kW8; k += 2) {
+                const uint32_t lo0 = 0, hi0 = half_of_int((uint32_t)std::min((double)kQMax, hi));
+                w[8 + 8 * ax + k / 2] = k == 0 ? (lo0 | (0x7C00u << 16)) : (0x7C00u | (0x7C00u << 16));
+                w[12 + 8 * ax + k / 2] = k == 0 ? (hi0 | (0xFC00u << 16)) : (0xFC00u | (0xFC00u << 16));
+            }
+        }
+        w[3] = ebits | (0u << 24) | (1u << 28);
+        w[4] = 0;
+        w[5] = 0;   // chunk 0 - n_in (0)
+        w[6] = (bvh2.nodes[0].b - 1u);
+        out.chunk_first.push_back(bvh2.nodes[0].a);
+        out.chunk_count.push_back((uint8_t)bvh2.nodes[0].b);
+        out.children = 1;
+        return;
+    }
+    c.emit(root, 0, 0, 0);
+}
+
 void collapse_bvh4(const BvhResult& bvh2, int stack_budget, Bvh4Result& out) {
     out.words.clear();
     out.stack_need = 0;

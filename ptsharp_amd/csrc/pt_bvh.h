@@ -18,8 +18,11 @@ constexpr int kMaxDepth = 32;     // BVH2 depth bound
 // within it (the traversal kernels hold the first kLdsStack in LDS and the rest in a
 // per-thread global column; the megakernel all in LDS).  A larger budget lets the collapse
 // fill more nodes to four children (fewer, wider steps per ray).
-constexpr int kStackMax = 32;   // (48 or 64 measured: the BVH 1 % smaller, no faster)
-static_assert(kStackMax >= kMaxDepth, "the collapse needs at least the BVH2 depth");
+// The BVH4 collapses keep every path within kStack4Budget pushes (48 or 64 measured: the BVH 1 % smaller, no
+// faster); the 8-wide triangle BVH pushes up to 7 per node and is collapsed within kStackMax.
+constexpr int kStack4Budget = 32;
+constexpr int kStackMax = 64;
+static_assert(kStack4Budget >= kMaxDepth, "the collapse needs at least the BVH2 depth");
 constexpr int kMaxLeafSize = 4;
 
 // 32-byte node; nodes[0] is the root, nodes[1] is padding, every child pair
@@ -79,5 +82,37 @@ void collapse_bvh4(const BvhResult& bvh2, int stack_budget, Bvh4Result& out);
 // collapsed greedily (collapse_bvh4), so the bound holds.
 void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out, double c_step = 1.0,
                        double c_tri = 0.5, int max_leaf = 3);
+
+// 8-wide BVH with quantized child boxes: one 128-byte line per node, as a BVH4 node, for about a quarter
+// fewer steps per ray (tools/bvh_quality.cpp's wide-node model on the C4 ray mix: closest hit 7.97 → 6.08
+// steps, shadow 11.34 → 8.24).  Node = 32 words:
+//   [0..2]  origin x, y, z (fp32: the union of the child boxes' lower corner)
+//   [3]     bits 0-23: exponents ex, ey, ez (biased by 127: step 2^(e-127)), bits 24-27: inner children
+//           n_in, bits 28-31: children n (1..8)
+//   [4]     the first inner child's node index (inner children are consecutive, slots 0 .. n_in-1)
+//   [5]     the first leaf chunk's index minus n_in (leaf slots n_in .. n-1 are consecutive chunks)
+//   [6]     2 bits per slot: a leaf slot's triangle count - 1
+//   [7]     0
+//   [8..31] the child bounds as binary16 integers q (0..2048, exact in binary16), SoA: lo.x[8] hi.x[8]
+//           lo.y[8] hi.y[8] lo.z[8] hi.z[8]; bound = origin + q·step, a superset of the child's box;
+//           an empty slot has lo = +inf, hi = -inf.
+// A traversal computes a slab distance as fma(q, step/d, (origin - o)/d).
+constexpr int kNode8Words = 32;
+struct Bvh8Result {
+    std::vector<uint32_t> words;         // kNode8Words per node; node 0 is the root
+    std::vector<uint32_t> chunk_first;   // per leaf chunk: its first primitive (position in BvhResult::order)
+    std::vector<uint8_t> chunk_count;    // per leaf chunk: its primitives (1 .. max_leaf)
+    int stack_need = 0;                  // worst-case traversal stack entries (<= budget)
+    int depth = 0;
+    int64_t children = 0;
+    size_t nodes() const { return words.size() / kNode8Words; }
+};
+// The SAH-optimal 8-wide collapse (collapse_bvh4_sah's dynamic program with 8 slots; subtrees whose choice
+// would break stack_budget are collapsed greedily, 8-wide) and the quantization.  Leaves: BVH2 subtrees of at
+// most max_leaf primitives, one chunk each.
+void collapse_bvh8q(const BvhResult& bvh2, int stack_budget, Bvh8Result& out, double c_step = 1.0, double c_tri = 0.5,
+                    int max_leaf = 3);
+// The box a slot's quantized bounds describe, in exact arithmetic rounded outward to fp32 (host checks).
+void bvh8_child_box(const uint32_t* node, int slot, float lo[3], float hi[3]);
 
 }  // namespace pt

@@ -192,6 +192,93 @@ __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, floa
     if (v3r == kEmpty4) k3 = inf;
 }
 
+// ---- The triangle BVH as 8-wide nodes with quantized child boxes (pt_bvh.h collapse_bvh8q: one 128-B line,
+// eight 16-B pieces q0..q7).  A child's slab distances are fma(q, step/d, (origin - o)/d) per axis, the
+// near and far bounds chosen once per node by the ray's direction signs; the hit children's entry distances
+// (fp32 bits, non-negative, so ordered as integers) carry the slot in their low 3 bits and are sorted by a
+// 19-comparator network; the nearest is descended, the rest pushed far-to-near.  The slab test keeps
+// slab1's widening of the far distance (the fma form's rounding is of the same order).
+typedef _Float16 pt_half2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void halves(float w, float& a, float& b) {
+    const pt_half2 h = __builtin_bit_cast(pt_half2, w);
+    a = (float)h.x;
+    b = (float)h.y;
+}
+__device__ __forceinline__ void usort2(uint32_t& a, uint32_t& b) {
+    const uint32_t lo = min(a, b), hi = max(a, b);
+    a = lo;
+    b = hi;
+}
+// The ref a sorted key names: slot k of the node (inner children first: base_in + k; leaf chunks after them:
+// base_leaf - n_in + k, with the count from 2 bits per slot).
+__device__ __forceinline__ uint32_t node8_ref(uint32_t key, uint32_t nin, uint32_t base_in, uint32_t base_leaf,
+                                              uint32_t cntb) {
+    const uint32_t k = key & 7u;
+    const uint32_t leaf = 0x80000000u | (((cntb >> (2u * k)) & 3u) << 29) | (base_leaf + k);
+    return k < nin ? base_in + k : leaf;
+}
+template <class STK>
+__device__ __forceinline__ bool node8_step(float4 q0, float4 q1, float4 q2, float4 q3, float4 q4, float4 q5, float4 q6,
+                                           float4 q7, v3 o, v3 invd, float tmax, const STK& st, int& sp, uint32_t& ref) {
+    const uint32_t hdr = __float_as_uint(q0.w);
+    const float sx = __uint_as_float((hdr & 0xFFu) << 23), sy = __uint_as_float(((hdr >> 8) & 0xFFu) << 23);
+    const float sz = __uint_as_float(((hdr >> 16) & 0xFFu) << 23);
+    const float ax = (q0.x - o.x) * invd.x, ay = (q0.y - o.y) * invd.y, az = (q0.z - o.z) * invd.z;
+    const float bx = sx * invd.x, by = sy * invd.y, bz = sz * invd.z;
+    const bool fx = invd.x < 0.f, fy = invd.y < 0.f, fz = invd.z < 0.f;   // the near bound is hi on that axis
+    const float4 nx = fx ? q3 : q2, gx = fx ? q2 : q3;
+    const float4 ny = fy ? q5 : q4, gy = fy ? q4 : q5;
+    const float4 nz = fz ? q7 : q6, gz = fz ? q6 : q7;
+    const uint32_t nc = hdr >> 28;
+    uint32_t key[8];
+    int nh = 0;
+    auto slab = [&](int k, float wnx, float wgx, float wny, float wgy, float wnz, float wgz, bool hi) {
+        float a0, a1, b0, b1, c0, c1, d0, d1, e0, e1, f0, f1;
+        halves(wnx, a0, a1); halves(wgx, b0, b1);
+        halves(wny, c0, c1); halves(wgy, d0, d1);
+        halves(wnz, e0, e1); halves(wgz, f0, f1);
+        const float tnx = fmaf(hi ? a1 : a0, bx, ax), tfx = fmaf(hi ? b1 : b0, bx, ax);
+        const float tny = fmaf(hi ? c1 : c0, by, ay), tfy = fmaf(hi ? d1 : d0, by, ay);
+        const float tnz = fmaf(hi ? e1 : e0, bz, az), tfz = fmaf(hi ? f1 : f0, bz, az);
+        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
+        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
+        const bool hit = (uint32_t)k < nc && tn <= tf * 1.0000005f;
+        key[k] = hit ? ((__float_as_uint(tn) & 0x7FFFFFF8u) | (uint32_t)k) : 0xFFFFFFFFu;
+        nh += hit ? 1 : 0;
+    };
+    slab(0, nx.x, gx.x, ny.x, gy.x, nz.x, gz.x, false);
+    slab(1, nx.x, gx.x, ny.x, gy.x, nz.x, gz.x, true);
+    slab(2, nx.y, gx.y, ny.y, gy.y, nz.y, gz.y, false);
+    slab(3, nx.y, gx.y, ny.y, gy.y, nz.y, gz.y, true);
+    slab(4, nx.z, gx.z, ny.z, gy.z, nz.z, gz.z, false);
+    slab(5, nx.z, gx.z, ny.z, gy.z, nz.z, gz.z, true);
+    slab(6, nx.w, gx.w, ny.w, gy.w, nz.w, gz.w, false);
+    slab(7, nx.w, gx.w, ny.w, gy.w, nz.w, gz.w, true);
+    if (nh == 0) return false;
+    // Batcher's odd-even merge sort of 8
+    usort2(key[0], key[1]); usort2(key[2], key[3]); usort2(key[4], key[5]); usort2(key[6], key[7]);
+    usort2(key[0], key[2]); usort2(key[1], key[3]); usort2(key[4], key[6]); usort2(key[5], key[7]);
+    usort2(key[1], key[2]); usort2(key[5], key[6]);
+    usort2(key[0], key[4]); usort2(key[1], key[5]); usort2(key[2], key[6]); usort2(key[3], key[7]);
+    usort2(key[2], key[4]); usort2(key[3], key[5]);
+    usort2(key[1], key[2]); usort2(key[3], key[4]); usort2(key[5], key[6]);
+    const uint32_t nin = (hdr >> 24) & 15u, base_in = __float_as_uint(q1.x), base_leaf = __float_as_uint(q1.y);
+    const uint32_t cntb = __float_as_uint(q1.z);
+    ref = node8_ref(key[0], nin, base_in, base_leaf, cntb);
+    if (__builtin_expect(sp <= STK::kLds - 7, 1)) {   // far-to-near, every slot written, sp advanced by the hits
+#pragma unroll
+        for (int j = 7; j >= 1; j--) {
+            st.lds[sp * STK::kStride] = node8_ref(key[j], nin, base_in, base_leaf, cntb);
+            sp += j < nh ? 1 : 0;
+        }
+    } else {
+#pragma unroll
+        for (int j = 7; j >= 1; j--)
+            if (j < nh) { st.put(sp, node8_ref(key[j], nin, base_in, base_leaf, cntb)); sp++; }
+    }
+    return true;
+}
+
 // SDF records (an SDFShape, or a TransformedShape of one): their sphere tracing runs up to 1000
 // dependent steps, taken by the lane whose traversal meets the leaf.  The analytic half of a split
 // closest hit (k_wf_trace<.., SPLIT>) and of split shadow rays leaves the first SDF record of a ray in a
@@ -336,24 +423,11 @@ __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 i
     for (;;) {
         const bool leaf = (ref & 0x80000000u) != 0;
         const float4* c = (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu);
-        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6];
-        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
+        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6], q7 = c[7];
+        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6); PT_PIN4(q7);
         if (!leaf) {
             if (COUNT) ctr.nodes++;
-            const float inf = __int_as_float(0x7f800000);
-            float k0, k1, k2, k3;
-            uint32_t v0, v1, v2, v3r;
-            node4_test(q0, q1, q2, q3, q4, q5, q6, o, invd, tmax, k0, k1, k2, k3, v0, v1, v2, v3r);
-            cswap(k0, v0, k1, v1);
-            cswap(k2, v2, k3, v3r);
-            cswap(k0, v0, k2, v2);
-            cswap(k1, v1, k3, v3r);
-            cswap(k1, v1, k2, v2);
-            if (k0 != inf) {
-                push_hits(stack, sp, 1 + (k1 != inf) + (k2 != inf) + (k3 != inf), v1, v2, v3r);
-                ref = v0;
-                continue;
-            }
+            if (node8_step(q0, q1, q2, q3, q4, q5, q6, q7, o, invd, tmax, stack, sp, ref)) continue;
         } else {
             const uint32_t cnt = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q0.x);
             PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6);

@@ -62,8 +62,8 @@ static void bvh_case(int64_t n, int threads, unsigned seed) {
             }
     }
     pt::Bvh4Result b4;
-    pt::collapse_bvh4(b2, pt::kStackMax, b4);
-    CHECK(b4.stack_need <= pt::kStackMax);
+    pt::collapse_bvh4(b2, pt::kStack4Budget, b4);
+    CHECK(b4.stack_need <= pt::kStack4Budget);
     CHECK(b4.nodes() > 0);
     std::printf("bvh: %lld prims, %d threads: %zu BVH2 nodes (depth %d), %zu BVH4 nodes (stack %d)\n", (long long)n,
                 threads, b2.nodes.size(), b2.max_depth, b4.nodes(), b4.stack_need);

@@ -408,10 +408,10 @@ static void build(const Mesh& m, const std::string& variant, Tree& T, double& bu
     BvhResult b2;
     build_bvh(lo.data(), hi.data(), (int64_t)n, 0, b2, 3, false, std::getenv("BINS") ? std::atoi(std::getenv("BINS")) : 32);
     Bvh4Result b4;
-    if (variant == "sah") collapse_bvh4_sah(b2, kStackMax, b4);
+    if (variant == "sah") collapse_bvh4_sah(b2, kStack4Budget, b4);
     else if (variant == "sah_nb") collapse_bvh4_sah(b2, 1000, b4);
     else if (variant == "greedy_nb") collapse_bvh4(b2, 1000, b4);
-    else collapse_bvh4(b2, kStackMax, b4);
+    else collapse_bvh4(b2, kStack4Budget, b4);
     build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     T.words = b4.words;
     T.order = b2.order;
@@ -495,12 +495,70 @@ static void cache_study(const Mesh& m, const Tree& T, long nrays) {
                 "deal by origin region %.3f\n", nrays, (double)acc / nrays, (double)hit_rr / acc, (double)hit_reg / acc);
 }
 
+// The library's 8-wide quantized tree (pt_bvh.cpp collapse_bvh8q) as a WideTree, decoded boxes.
+static void build_p8(const Mesh& m, WideTree& T, std::vector<uint32_t>& order, double& build_s, int& stack_need) {
+    const size_t n = (size_t)m.n;
+    std::vector<float> lo(n * 3), hi(n * 3);
+    for (size_t i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++) {
+            const float a = m.v1[3 * i + k], b = m.v2[3 * i + k], c = m.v3[3 * i + k];
+            float l = std::fmin(std::fmin(a, b), c), h = std::fmax(std::fmax(a, b), c);
+            const float e = std::fmax(std::fabs(l), std::fabs(h)) * 2.0e-6f + 1e-30f;
+            lo[3 * i + k] = l - e; hi[3 * i + k] = h + e;
+        }
+    const auto t0 = std::chrono::steady_clock::now();
+    BvhResult b2;
+    build_bvh(lo.data(), hi.data(), (int64_t)n, 0, b2, 3, false, std::getenv("BINS") ? std::atoi(std::getenv("BINS")) : 32);
+    Bvh8Result b8;
+    collapse_bvh8q(b2, std::getenv("BUDGET8") ? std::atoi(std::getenv("BUDGET8")) : 64, b8);
+    build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    stack_need = b8.stack_need;
+    T.W = 8;
+    T.Q = 11;
+    T.nodes.assign(b8.nodes(), WNode{});
+    size_t bad = 0, prims = 0;
+    for (size_t i = 0; i < b8.nodes(); i++) {
+        const uint32_t* w = &b8.words[i * kNode8Words];
+        const int nc = (int)(w[3] >> 28), nin = (int)((w[3] >> 24) & 15u);
+        for (int k = 0; k < nc; k++) {
+            WChild c;
+            bvh8_child_box(w, k, c.lo, c.hi);
+            if (k < nin) c.ref = w[4] + (uint32_t)k;
+            else {
+                const uint32_t ch = w[5] + (uint32_t)k;
+                c.ref = 0x80000000u | ((uint32_t)(b8.chunk_count[ch] - 1) << 29) | b8.chunk_first[ch];
+                prims += b8.chunk_count[ch];
+                T.leaves++;
+            }
+            T.nodes[i].c.push_back(c);
+        }
+    }
+    // containment: every leaf chunk's triangles inside the decoded boxes on its path is what the traversal
+    // needs; checked here on the leaves' own boxes
+    for (size_t i = 0; i < b8.nodes(); i++)
+        for (const WChild& c : T.nodes[i].c)
+            if (c.ref & 0x80000000u) {
+                const uint32_t f = c.ref & 0x1FFFFFFFu, cnt = ((c.ref >> 29) & 3u) + 1u;
+                for (uint32_t t = f; t < f + cnt; t++)
+                    for (int k = 0; k < 3; k++)
+                        if (lo[3 * b2.order[t] + k] < c.lo[k] || hi[3 * b2.order[t] + k] > c.hi[k]) bad++;
+            }
+    order = b2.order;
+    size_t used = 0;
+    for (const WNode& nd : T.nodes) used += nd.c.size();
+    T.fill = (double)used / (8.0 * (double)T.nodes.size());
+    std::printf("p8: %zu nodes, %zu chunks, %zu primitives in chunks (of %zu), %zu bounds outside their box, stack %d\n",
+                b8.nodes(), b8.chunk_first.size(), prims, n, bad, stack_need);
+}
+
 // The C4 ray mix (main's loop) through a wide tree: steps (lines) per ray by depth and for shadow rays.
 static void run_wide(const Mesh& m, int W, int Q, int stride) {
     WideTree T;
     std::vector<uint32_t> order;
     double bs = 0;
-    build_wide(m, W, Q, T, order, bs);
+    int sneed = 0;
+    if (W == 0) build_p8(m, T, order, bs, sneed);
+    else build_wide(m, W, Q, T, order, bs);
     WideTracer tr{m, T, order};
     const int Wd = 1920, H = 1080, kDepth = 4;
     const v3 lights[2] = {v3{0.f, 5.f, 0.f}, v3{4.f, 5.f, 4.f}};
@@ -578,7 +636,8 @@ int main(int argc, char** argv) {
     const v3 lights[2] = {v3{0.f, 5.f, 0.f}, v3{4.f, 5.f, 4.f}};
     for (const auto& var : variants) {
         int W = 0, Q = 0;
-        if (std::sscanf(var.c_str(), "w%dq%d", &W, &Q) == 2) {   // wide-node model: w8q8, w8q16, w4q0 ...
+        if (var == "p8" || std::sscanf(var.c_str(), "w%dq%d", &W, &Q) == 2) {   // wide-node model: w8q8, w8q16, w4q0 ...; p8: the library's
+            if (var == "p8") W = 0;
             run_wide(m, W, Q, stride);
             continue;
         }
