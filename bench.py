@@ -588,11 +588,26 @@ def main(argv=None):
                                 f"Infinity-Cache hits included), profiles/pmc_traffic_{a.workload}.json ({tw.get('tag')}), "
                                 f"same workload"}
 
+    def march_clock():   # C5: the cooperative Volume march's time by phase (counted pass, s_memtime per phase)
+        mc = [int(x) for x in ctr.march_clock]
+        dense, strided = max(mc[6], 1), max(mc[7], 1)
+        total = sum(mc[:6])
+        names = ("strided_pass", "table", "corners", "windows", "bookkeeping", "refinements")
+        return {"cycles_per_dense_round": {k: round(mc[1 + i] / dense, 1) for i, k in enumerate(names[1:5])},
+                "cycles_per_strided_round": round(mc[0] / strided, 1),
+                "share": {k: round(mc[i] / max(total, 1), 4) for i, k in enumerate(names)},
+                "dense_rounds": mc[6], "strided_rounds": mc[7],
+                "note": "wave cycles (shader clock) summed over marching waves, counted pass (clock reads add ~10 %)"}
+
     def valu_roofline():   # C2 / C5: whole pass bound by VALU issue (measured instruction mix, profiles/)
         pv = os.path.join(ROOT, "profiles", f"pmc_valu_mix_{a.workload}.json")
+        extra = {"nodes_per_ray": round(ctr.nodes_visited / max(ctr.rays, 1), 3),
+                 **({"volume_samples_per_ray": round(ctr.volume_samples / max(ctr.rays, 1), 3),
+                     "sdf_evals_per_ray": round(ctr.sdf_evals / max(ctr.rays, 1), 3),
+                     "volume_march_clock": march_clock()} if a.workload == "c5" else {})}
         if not os.path.exists(pv):
             return {"bound": "valu_issue", "kernel": "whole pass", "achieved": None, "peak": VALU_ISSUE_PEAK,
-                    "unit": "T SIMD-cycles/s", "frac": None, "note": f"{pv} missing (tools/gpu_valu_mix.sh)"}
+                    "unit": "T SIMD-cycles/s", "frac": None, "note": f"{pv} missing (tools/gpu_valu_mix.sh)", **extra}
         with open(pv) as f:
             vm = json.load(f)
         pr = vm["per_ray"]
@@ -615,9 +630,7 @@ def main(argv=None):
                           f"counters, SQ_INSTS_VALU_FLOPS_FP32/FP64, same workload)",
             "dominant_kernel": dom_k[0], "dominant_kernel_valu_issue_frac_under_counters": dom_k[1]["valu_issue_frac"],
             "pass_valu_issue_frac_under_counters": vm.get("pass_valu_issue_frac_under_counters"),
-            "nodes_per_ray": round(ctr.nodes_visited / max(ctr.rays, 1), 3),
-            **({"volume_samples_per_ray": round(ctr.volume_samples / max(ctr.rays, 1), 3),
-                "sdf_evals_per_ray": round(ctr.sdf_evals / max(ctr.rays, 1), 3)} if a.workload == "c5" else {}),
+            **extra,
         }
 
     if a.workload in ("c2", "c5"):

@@ -143,11 +143,12 @@ namespace PTSharpCore
         }
 
         [StructLayout(LayoutKind.Sequential)]
-        public struct pt_trace_counters
+        public unsafe struct pt_trace_counters
         {
             public ulong rays, nodes_visited, prims_tested, shading_fetches, shadow_rays, shadow_nodes, shadow_prims;
             public ulong lit_shadow_rays, accum_runs;
             public ulong volume_samples, sdf_evals;   // Volume.Intersect / SDFShape.Intersect march steps
+            public fixed ulong march_clock[8];   // the Volume march's phase clocks (counted passes)
         }
 
         [StructLayout(LayoutKind.Sequential)]

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 7
+#define PT_ABI_VERSION 8
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -428,6 +428,12 @@ typedef struct pt_trace_counters {
     uint64_t accum_runs;      /* their per-pixel runs after wave aggregation (atomic sets)  */
     uint64_t volume_samples;  /* Volume.Sample calls of Volume.Intersect's march (Volume.cs:168-197) */
     uint64_t sdf_evals;       /* SDF evaluations of SDFShape.Intersect's sphere tracing (SDF.cs:32-76) */
+    /* The cooperative Volume march's time by phase, shader-clock cycles summed over the marching waves
+     * (s_memtime around each phase, so they run ~10 % slower in a counted pass): [0] strided passes over
+     * uniform cells, [1] a dense round's position and uniform-cell table read, [2] its corner reads and
+     * interpolation, [3] its window loop (Volume.Sign), [4] its ballots and bookkeeping, [5] refinements;
+     * [6] dense rounds, [7] strided-pass rounds (counts). */
+    uint64_t march_clock[8];
 } pt_trace_counters;
 int pt_render_pass_counted(void* ctx, const pt_camera* camera, const pt_sampler* sampler,
                            const pt_pass_params* pass, pt_trace_counters* out);

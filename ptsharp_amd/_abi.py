@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptsharp_hip.so")
 
-ABI_VERSION = 7   # PT_ABI_VERSION
+ABI_VERSION = 8   # PT_ABI_VERSION
 PT_OK = 0
 PT_ERR_INVALID_ARG = -1
 PT_ERR_HIP = -2
@@ -126,7 +126,7 @@ class pt_trace_counters(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("nodes_visited", C.c_uint64), ("prims_tested", C.c_uint64),
                 ("shading_fetches", C.c_uint64), ("shadow_rays", C.c_uint64), ("shadow_nodes", C.c_uint64),
                 ("shadow_prims", C.c_uint64), ("lit_shadow_rays", C.c_uint64), ("accum_runs", C.c_uint64),
-                ("volume_samples", C.c_uint64), ("sdf_evals", C.c_uint64)]
+                ("volume_samples", C.c_uint64), ("sdf_evals", C.c_uint64), ("march_clock", C.c_uint64 * 8)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/ptsharp_hip.h

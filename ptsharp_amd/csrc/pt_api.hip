@@ -145,8 +145,8 @@ struct Ctx {
     double* d_m = nullptr;
     double* d_v = nullptr;
     int32_t* d_n = nullptr;
-    unsigned long long* d_counters = nullptr;   // [16] the pass' counters (pt::DevBuffer::counters)
-    unsigned long long* h_counters = nullptr;   // [16] pinned: their read-back
+    unsigned long long* d_counters = nullptr;   // [pt::kCounterWords] the pass' counters (pt::DevBuffer::counters)
+    unsigned long long* h_counters = nullptr;   // [pt::kCounterWords] pinned: their read-back
     int32_t* d_tiles = nullptr;
     int32_t tiles_cap = 0;
     std::vector<int32_t> h_tiles;               // the tile list in d_tiles (uploaded when it changes)
@@ -418,39 +418,6 @@ int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_no
     return PT_OK;
 }
 
-// Triangle leaf chunks: every leaf ref of the collapsed triangle BVH4 is re-pointed at a
-// 128-B chunk holding its (<= 3) triangles' {v1, e1, e2} (27 floats, the tri_recs fields)
-// and, in word 27, the first triangle's record position.  A traversal step then loads the
-// same seven 16-B pieces whether the lane is at an inner node or at a leaf (pt_device.h
-// traverse_tri).  Chunks are allocated in node order, so sibling leaves sit together.
-int make_leaf_chunks(std::vector<float4>& nodes, const std::vector<float4>& recs, std::vector<float4>& chunks) {
-    chunks.clear();
-    const size_t nn = nodes.size() / 8;
-    for (size_t n = 0; n < nn; n++) {
-        uint32_t* refs = reinterpret_cast<uint32_t*>(&nodes[8 * n + 6]);
-        for (int k = 0; k < 4; k++) {
-            const uint32_t r = refs[k];
-            if (r == pt::kEmpty4 || !(r & 0x80000000u)) continue;
-            const uint32_t first = r & 0x1FFFFFFFu, cnt = ((r >> 29) & 3u) + 1u;
-            if (cnt > 3) return fail(PT_ERR_UNSUPPORTED, "triangle leaf larger than a chunk");
-            const size_t ci = chunks.size() / 8;
-            if (ci > 0x1FFFFFFFu) return fail(PT_ERR_UNSUPPORTED, "too many triangle leaves");
-            // word 0 = the first triangle record, triangle t = words 1 + 9t .. 9 + 9t, so a chunk of
-            // cnt triangles is read with 1 + 2·cnt of its 16-B pieces (3 / 5 / 7)
-            float w[32] = {0.f};
-            std::memcpy(&w[0], &first, 4);
-            for (uint32_t t = 0; t < cnt; t++) {
-                const float* rf = reinterpret_cast<const float*>(&recs[3 * (size_t)(first + t)]);
-                for (int j = 0; j < 9; j++) w[1 + 9 * t + j] = rf[j];
-            }
-            const float4* w4 = reinterpret_cast<const float4*>(w);
-            chunks.insert(chunks.end(), w4, w4 + 8);
-            refs[k] = 0x80000000u | ((cnt - 1u) << 29) | (uint32_t)ci;
-        }
-    }
-    return PT_OK;
-}
-
 // ---- The triangle BVH, built once per process for identical geometry (Scene.Compile compiles a scene
 // once, Scene.cs:48-68; the reference has one Tree per Scene).  N contexts of one process (the .NET group
 // host, bench.py --gpus N) upload the same scene: the first pt_upload_scene builds the BVH (1.1 s at 1M
@@ -524,7 +491,7 @@ std::shared_ptr<const TriBvhBuild> build_tri_bvh(const pt_scene_desc* d, const s
         tri_recs[3 * i + 1] = f4(e1.y, e1.z, e2.x, e2.y);
         tri_recs[3 * i + 2] = f4(e2.z, 0.f, 0.f, 0.f);
     }
-    // 8-wide nodes with quantized child boxes (pt_bvh.h collapse_bvh8q), leaf chunks as make_leaf_chunks' (one
+    // 8-wide nodes with quantized child boxes (pt_bvh.h collapse_bvh8q), leaf chunks (one
     // 128-B line per leaf: the first record in word 0, up to three {v1, e1, e2})
     pt::Bvh8Result b8;
     pt::collapse_bvh8q(tb, pt::kStackMax, b8, 1.0, kTriCost, 3);
@@ -545,7 +512,8 @@ std::shared_ptr<const TriBvhBuild> build_tri_bvh(const pt_scene_desc* d, const s
     for (size_t ci = 0; ci < b8.chunk_first.size(); ci++) {
         float w[32] = {0.f};
         const uint32_t first = b8.chunk_first[ci], cnt = b8.chunk_count[ci];
-        std::memcpy(&w[0], &first, 4);
+        const uint32_t w0 = first | ((cnt - 1u) << 29);   // the first record, the count - 1 in bits 29-30
+        std::memcpy(&w[0], &w0, 4);
         for (uint32_t t = 0; t < cnt; t++) {
             const float* rf = reinterpret_cast<const float*>(&tri_recs[3 * (size_t)(first + t)]);
             for (int j = 0; j < 9; j++) w[1 + 9 * t + j] = rf[j];
@@ -855,8 +823,8 @@ int pt_create(const pt_device_opts* opts, void** out_ctx) {
     size_t P = (size_t)c->width * (size_t)c->height;
     if (hipMalloc(&c->d_m, P * 3 * sizeof(double)) != hipSuccess || hipMalloc(&c->d_v, P * 3 * sizeof(double)) != hipSuccess ||
         hipMalloc(&c->d_n, P * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc(&c->h_counters, 16 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+        hipMalloc(&c->d_counters, pt::kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(&c->h_counters, pt::kCounterWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
         return cleanup(fail(PT_ERR_OUT_OF_MEMORY, "buffer allocation"));
     int rc = pt_reset_buffer(c);
     if (rc != PT_OK) return cleanup(rc);
@@ -1557,7 +1525,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     }
     const bool timing = (pass->flags & PT_PASS_KERNEL_TIMING) != 0;
     c->timer.reset(c->stream);
-    PT_HIP(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));   // and the overflow flag
+    PT_HIP(hipMemsetAsync(c->d_counters, 0, pt::kCounterWords * sizeof(unsigned long long), c->stream));   // and the overflow flag
     // a counted pass also counts the Volume / SDFShape march steps (counters 9, 10); the launches
     // take the scene by value, so the pointer is cleared again whichever way this call returns
     struct MarchScope {
@@ -1627,7 +1595,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     PT_HIP(hipEventRecord(c->ev1, c->stream));
     if (c->timer.failed) return fail(PT_ERR_HIP, "hipEventRecord (kernel timing) failed");
     const unsigned long long* ctr = c->h_counters;
-    PT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    PT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, pt::kCounterWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
     if (engine == PT_ENGINE_WAVEFRONT && ctr[pt::kOverflowCounter])
         return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
@@ -1655,6 +1623,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         counted->accum_runs = ctr[8];
         counted->volume_samples = ctr[9];
         counted->sdf_evals = ctr[10];
+        for (int k = 0; k < 8; k++) counted->march_clock[k] = ctr[pt::kMarchClockWord + k];
     }
     return PT_OK;
 }

@@ -618,7 +618,7 @@ struct Wide8 {
         }
         w[3] = ebits | ((uint32_t)nin << 24) | ((uint32_t)nc << 28);
         w[4] = base_in;
-        w[5] = base_chunk - (uint32_t)nin;   // leaf slot k's chunk is w[5] + k
+        w[5] = 0x80000000u + base_chunk - (uint32_t)nin;   // leaf slot k's ref (0x80000000 | chunk) is w[5] + k
         w[6] = cnt_bits;
         w[7] = 0;
         for (int r = 0; r < 6; r++)
@@ -674,7 +674,7 @@ void collapse_bvh8q(const BvhResult& bvh2, int stack_budget, Bvh8Result& out, do
         }
         w[3] = ebits | (0u << 24) | (1u << 28);
         w[4] = 0;
-        w[5] = 0;   // chunk 0 - n_in (0)
+        w[5] = 0x80000000u;   // the ref of chunk 0 - n_in (0)
         w[6] = (bvh2.nodes[0].b - 1u);
         out.chunk_first.push_back(bvh2.nodes[0].a);
         out.chunk_count.push_back((uint8_t)bvh2.nodes[0].b);

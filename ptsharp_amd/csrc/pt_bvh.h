@@ -90,8 +90,9 @@ void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out,
 //   [3]     bits 0-23: exponents ex, ey, ez (biased by 127: step 2^(e-127)), bits 24-27: inner children
 //           n_in, bits 28-31: children n (1..8)
 //   [4]     the first inner child's node index (inner children are consecutive, slots 0 .. n_in-1)
-//   [5]     the first leaf chunk's index minus n_in (leaf slots n_in .. n-1 are consecutive chunks)
-//   [6]     2 bits per slot: a leaf slot's triangle count - 1
+//   [5]     0x80000000 + the first leaf chunk's index - n_in (leaf slots n_in .. n-1 are consecutive chunks; slot
+//           k's ref is [5] + k: bit 31 and the chunk index; the chunk's word 0 holds its triangle count)
+//   [6]     2 bits per slot: a leaf slot's triangle count - 1 (host checks)
 //   [7]     0
 //   [8..31] the child bounds as binary16 integers q (0..2048, exact in binary16), SoA: lo.x[8] hi.x[8]
 //           lo.y[8] hi.y[8] lo.z[8] hi.z[8]; bound = origin + q·step, a superset of the child's box;

@@ -193,29 +193,25 @@ __device__ __forceinline__ void node4_test(float4 q0, float4 q1, float4 q2, floa
 }
 
 // ---- The triangle BVH as 8-wide nodes with quantized child boxes (pt_bvh.h collapse_bvh8q: one 128-B line,
-// eight 16-B pieces q0..q7).  A child's slab distances are fma(q, step/d, (origin - o)/d) per axis, the
-// near and far bounds chosen once per node by the ray's direction signs; the hit children's entry distances
-// (fp32 bits, non-negative, so ordered as integers) carry the slot in their low 3 bits and are sorted by a
-// 19-comparator network; the nearest is descended, the rest pushed far-to-near.  The slab test keeps
-// slab1's widening of the far distance (the fma form's rounding is of the same order).
+// eight 16-B pieces q0..q7).  A child's slab distances are fma(q, step/d, (origin - o)/d) per axis, the near
+// and far bounds chosen once per node by the ray's direction signs (an empty slot's +inf / -inf bounds give
+// an entry distance of +inf on every axis whose direction is not 0, so it never hits).  The hit children's
+// entry distances (fp32 bits, non-negative, so ordered as integers) carry the slot in their low 3 bits: the
+// nearest is a 3-input-min tree away, and it is descended; the other hits are pushed in slot order (popped
+// lowest slot first).  Sorting them far-to-near measured no fewer steps in the C4 ray mix
+// (tools/bvh_quality.cpp PUSH_ORDER: closest hit 6.08 vs 6.21 steps, shadow 8.33 vs 8.29) and cost a
+// 19-comparator network per step.  The slab test keeps slab1's widening of the far distance (the fma
+// form's rounding is of the same order).
 typedef _Float16 pt_half2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void halves(float w, float& a, float& b) {
     const pt_half2 h = __builtin_bit_cast(pt_half2, w);
     a = (float)h.x;
     b = (float)h.y;
 }
-__device__ __forceinline__ void usort2(uint32_t& a, uint32_t& b) {
-    const uint32_t lo = min(a, b), hi = max(a, b);
-    a = lo;
-    b = hi;
-}
-// The ref a sorted key names: slot k of the node (inner children first: base_in + k; leaf chunks after them:
-// base_leaf - n_in + k, with the count from 2 bits per slot).
-__device__ __forceinline__ uint32_t node8_ref(uint32_t key, uint32_t nin, uint32_t base_in, uint32_t base_leaf,
-                                              uint32_t cntb) {
-    const uint32_t k = key & 7u;
-    const uint32_t leaf = 0x80000000u | (((cntb >> (2u * k)) & 3u) << 29) | (base_leaf + k);
-    return k < nin ? base_in + k : leaf;
+// The ref of slot k (inner children first: base_in + k; leaf chunks after them: base_leaf - n_in + k, the
+// count in the chunk's word 0).
+__device__ __forceinline__ uint32_t node8_ref(uint32_t k, uint32_t nin, uint32_t base_in, uint32_t leaf0) {
+    return k < nin ? base_in + k : leaf0 + k;
 }
 template <class STK>
 __device__ __forceinline__ bool node8_step(float4 q0, float4 q1, float4 q2, float4 q3, float4 q4, float4 q5, float4 q6,
@@ -229,9 +225,7 @@ __device__ __forceinline__ bool node8_step(float4 q0, float4 q1, float4 q2, floa
     const float4 nx = fx ? q3 : q2, gx = fx ? q2 : q3;
     const float4 ny = fy ? q5 : q4, gy = fy ? q4 : q5;
     const float4 nz = fz ? q7 : q6, gz = fz ? q6 : q7;
-    const uint32_t nc = hdr >> 28;
     uint32_t key[8];
-    int nh = 0;
     auto slab = [&](int k, float wnx, float wgx, float wny, float wgy, float wnz, float wgz, bool hi) {
         float a0, a1, b0, b1, c0, c1, d0, d1, e0, e1, f0, f1;
         halves(wnx, a0, a1); halves(wgx, b0, b1);
@@ -242,9 +236,7 @@ __device__ __forceinline__ bool node8_step(float4 q0, float4 q1, float4 q2, floa
         const float tnz = fmaf(hi ? e1 : e0, bz, az), tfz = fmaf(hi ? f1 : f0, bz, az);
         const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
         const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
-        const bool hit = (uint32_t)k < nc && tn <= tf * 1.0000005f;
-        key[k] = hit ? ((__float_as_uint(tn) & 0x7FFFFFF8u) | (uint32_t)k) : 0xFFFFFFFFu;
-        nh += hit ? 1 : 0;
+        key[k] = tn <= tf * 1.0000005f ? ((__float_as_uint(tn) & 0x7FFFFFF8u) | (uint32_t)k) : 0xFFFFFFFFu;
     };
     slab(0, nx.x, gx.x, ny.x, gy.x, nz.x, gz.x, false);
     slab(1, nx.x, gx.x, ny.x, gy.x, nz.x, gz.x, true);
@@ -254,27 +246,21 @@ __device__ __forceinline__ bool node8_step(float4 q0, float4 q1, float4 q2, floa
     slab(5, nx.z, gx.z, ny.z, gy.z, nz.z, gz.z, true);
     slab(6, nx.w, gx.w, ny.w, gy.w, nz.w, gz.w, false);
     slab(7, nx.w, gx.w, ny.w, gy.w, nz.w, gz.w, true);
-    if (nh == 0) return false;
-    // Batcher's odd-even merge sort of 8
-    usort2(key[0], key[1]); usort2(key[2], key[3]); usort2(key[4], key[5]); usort2(key[6], key[7]);
-    usort2(key[0], key[2]); usort2(key[1], key[3]); usort2(key[4], key[6]); usort2(key[5], key[7]);
-    usort2(key[1], key[2]); usort2(key[5], key[6]);
-    usort2(key[0], key[4]); usort2(key[1], key[5]); usort2(key[2], key[6]); usort2(key[3], key[7]);
-    usort2(key[2], key[4]); usort2(key[3], key[5]);
-    usort2(key[1], key[2]); usort2(key[3], key[4]); usort2(key[5], key[6]);
-    const uint32_t nin = (hdr >> 24) & 15u, base_in = __float_as_uint(q1.x), base_leaf = __float_as_uint(q1.y);
-    const uint32_t cntb = __float_as_uint(q1.z);
-    ref = node8_ref(key[0], nin, base_in, base_leaf, cntb);
-    if (__builtin_expect(sp <= STK::kLds - 7, 1)) {   // far-to-near, every slot written, sp advanced by the hits
+    const uint32_t kmin = min(min(min(key[0], key[1]), min(key[2], key[3])), min(min(key[4], key[5]), min(key[6], key[7])));
+    if (kmin == 0xFFFFFFFFu) return false;
+    const uint32_t near = kmin & 7u;
+    const uint32_t nin = (hdr >> 24) & 15u, base_in = __float_as_uint(q1.x), leaf0 = __float_as_uint(q1.y);
+    ref = node8_ref(near, nin, base_in, leaf0);
+    if (__builtin_expect(sp <= STK::kLds - 8, 1)) {   // every slot written, sp advanced by the other hits
 #pragma unroll
-        for (int j = 7; j >= 1; j--) {
-            st.lds[sp * STK::kStride] = node8_ref(key[j], nin, base_in, base_leaf, cntb);
-            sp += j < nh ? 1 : 0;
+        for (int j = 7; j >= 0; j--) {
+            st.lds[sp * STK::kStride] = node8_ref((uint32_t)j, nin, base_in, leaf0);
+            sp += (key[j] != 0xFFFFFFFFu && (uint32_t)j != near) ? 1 : 0;
         }
     } else {
 #pragma unroll
-        for (int j = 7; j >= 1; j--)
-            if (j < nh) { st.put(sp, node8_ref(key[j], nin, base_in, base_leaf, cntb)); sp++; }
+        for (int j = 7; j >= 0; j--)
+            if (key[j] != 0xFFFFFFFFu && (uint32_t)j != near) { st.put(sp, node8_ref((uint32_t)j, nin, base_in, leaf0)); sp++; }
     }
     return true;
 }
@@ -399,7 +385,7 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
 #define PT_PIN4(q) asm volatile("" : "+v"((q).x), "+v"((q).y), "+v"((q).z), "+v"((q).w))
 
 
-// The triangles of a leaf chunk (pt_api.hip make_leaf_chunks): word 0 = the first triangle
+// The triangles of a leaf chunk (pt_api.hip build_tri_bvh): word 0 = the first triangle
 // record, triangle k = words 1 + 9k .. 9 + 9k as {v1, e1, e2}; a0..a2 is the first, b the
 // second, c the third (shifted down after each test).  A chunk of cnt triangles is read with its
 // first 1 + 2·cnt 16-B pieces; the rest of q is stale and never tested.
@@ -408,11 +394,11 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
     v3 b0{q2.z, q2.w, q3.x}, b1{q3.y, q3.z, q3.w}, b2{q4.x, q4.y, q4.z};                  \
     const v3 c0{q4.w, q5.x, q5.y}, c1{q5.z, q5.w, q6.x}, c2{q6.y, q6.z, q6.w}
 
-// Triangle-BVH traversal over leaf chunks (pt_api.hip make_leaf_chunks).  The node step
-// is traverse()'s; a leaf ref points at a 128-B chunk of up to three triangles, so an
-// inner step and a leaf step issue the same seven aligned 16-B loads and a wave whose
-// lanes are split between nodes and leaves pays for one set of load instructions, not
-// for the node loads plus a per-triangle load loop.
+// Triangle-BVH traversal over leaf chunks (pt_api.hip build_tri_bvh).  The node step is
+// node8_step's (8-wide quantized nodes); a leaf ref points at a 128-B chunk of up to three
+// triangles, so an inner step and a leaf step read the same 128-B line's 16-B pieces and a
+// wave whose lanes are split between nodes and leaves pays for one set of load
+// instructions, not for the node loads plus a per-triangle load loop.
 template <bool COUNT, bool ANY, class STK>
 __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 invd, HitRec& best, const STK& stack,
                                              Counters& ctr) {
@@ -429,7 +415,7 @@ __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 i
             if (COUNT) ctr.nodes++;
             if (node8_step(q0, q1, q2, q3, q4, q5, q6, q7, o, invd, tmax, stack, sp, ref)) continue;
         } else {
-            const uint32_t cnt = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q0.x);
+            const uint32_t w0 = __float_as_uint(q0.x), cnt = (w0 >> 29) + 1u, first = w0 & 0x1FFFFFFFu;   // chunk word 0
             PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6);
 #pragma unroll 1
             for (uint32_t k = 0; k < cnt; k++) {
@@ -509,6 +495,68 @@ __device__ __forceinline__ bool march_exact(double t, double step) {   // t > 0
 __device__ __forceinline__ int vol_sign_fast(const DevVolume& v, v3 o, v3 d, double t) {
     return vol_sign_at(v, o, d, t);   // the key and the sample from one scaling of the position
 }
+// vol_sign_at with the shader clock read between its phases (counted passes only, pt_trace_counters
+// march_clock): dt[0] += the position, its scaling, the key and the uniform-cell table read; dt[1] += the
+// corner reads and the interpolation; dt[2] += the window loop (Volume.Sign).  Each phase's end waits for its
+// loads (the asm statements use their values), so the clocks bracket the latencies.  Same result.
+__device__ __forceinline__ int vol_sign_at_timed(const DevVolume& v, v3 o, v3 d, double t, uint64_t dt[3]) {
+    const uint64_t c0 = clock64();
+    const v3 a = add(o, muls(d, t));   // Ray.Position
+    double x = a.x, z = a.z;
+    z = vol_zdiv(v, z);
+    x = ((x + 1) / 2) * (double)v.w;
+    double y = ((z + 1) / 2) * (double)v.h;
+    z = ((z + 2) / 2) * (double)v.d;
+    if (v.runs) {
+        auto cl = [](double c, int n) {
+            if (!(c > -2.0)) return -2;
+            if (!(c < (double)n)) return n;
+            return (int)floor(c);
+        };
+        const int st = vol_key_sign(v, VolKey{cl(x, v.w), cl(y, v.h), cl(z, v.d)});
+        asm volatile("" ::"v"(st));
+        const uint64_t c1 = clock64();
+        dt[0] += c1 - c0;
+        if (st > 0) return st;
+    } else {
+        dt[0] += clock64() - c0;
+    }
+    const uint64_t c1 = clock64();
+    double smp = 0.0;
+    const double lim = 2147483647.0;
+    if (fabs(x) < lim && fabs(y) < lim && fabs(z) < lim) {
+        const int x0 = (int)floor(x), y0 = (int)floor(y), z0 = (int)floor(z);
+        const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
+        const double v000 = vol_get(v, x0, y0, z0), v001 = vol_get(v, x0, y0, z1), v010 = vol_get(v, x0, y1, z0);
+        const double v011 = vol_get(v, x0, y1, z1), v100 = vol_get(v, x1, y0, z0), v101 = vol_get(v, x1, y0, z1);
+        const double v110 = vol_get(v, x1, y1, z0), v111 = vol_get(v, x1, y1, z1);
+        x -= (double)x0;
+        y -= (double)y0;
+        z -= (double)z0;
+        const double c00 = v000 * (1 - x) + v100 * x;
+        const double c01 = v001 * (1 - x) + v101 * x;
+        const double c10 = v010 * (1 - x) + v110 * x;
+        const double c11 = v011 * (1 - x) + v111 * x;
+        const double cc0 = c00 * (1 - y) + c10 * y;
+        const double cc1 = c01 * (1 - y) + c11 * y;
+        smp = cc0 * (1 - z) + cc1 * z;
+    }
+    asm volatile("" ::"v"(smp));
+    const uint64_t c2 = clock64();
+    dt[1] += c2 - c1;
+    const int sg = vol_sign_of(v, smp);
+    asm volatile("" ::"v"(sg));
+    dt[2] += clock64() - c2;
+    return sg;
+}
+// the wave's time of a phase: the longest of its lanes' (lanes outside the phase read 0)
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(x >> 32), off, 64) << 32) | (uint32_t)__shfl_xor((int)x, off, 64);
+        x = x > y ? x : y;
+    }
+    return x;
+}
 // Every cell of the index box spanned by cells a and b (at most one step apart per axis) has
 // Sign `sign`: then every position between a position in a and a later one in b lies in such a
 // cell (each index is monotone along the ray, so the cells between lie in that box).
@@ -526,7 +574,9 @@ __device__ __forceinline__ bool vol_box_sign(const DevVolume& v, VolKey a, VolKe
 constexpr int kVolStride = 16;   // the strided pass's positions per lane (8 / 32 measured: no better)
 // Every active lane passes the same (v, o, d); returns vol_t(v, o, d) to all of them and, in
 // `samples`, the Volume.Sample calls vol_t makes (instrumentation).
-__device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& samples) {
+// clk (counted passes, else null): the phase clocks of pt_trace_counters::march_clock, added by the first
+// active lane at the end.
+__device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& samples, unsigned long long* clk = nullptr) {
     const uint64_t act = __ballot(true);
     const int lane = threadIdx.x & 63;
     const uint64_t lower = act & ((1ull << lane) - 1ull);
@@ -540,7 +590,13 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     int sign = -1, iters = 0;
     samples = 0;
     auto sign_at = [&](double tt) { return vol_sign_fast(v, o, d, tt); };
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // clk: strided, table, corners, windows, rest, refinements, rounds x2
+    auto flush = [&]() {
+        if (clk && lane == __builtin_ctzll(act))
+            for (int k = 0; k < 8; k++) atomicAdd(clk + k, (unsigned long long)ph[k]);
+    };
     for (;;) {   // wave-uniform: every branch below is on ballots
+        const uint64_t cs = clk ? clock64() : 0;
         // Strided pass over runs of uniform cells: lane of rank r looks at position (r + 1)·S from
         // t; when the cells of consecutive looked-at positions (and of position 0) span only cells
         // of the running Sign, no position up to there can act, and the march moves past them,
@@ -563,18 +619,32 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
             t = t_after(t, step, k);
             iters += k;
             sign = s0;
+            if (clk) ph[7]++;
             if (f < nact) break;
+        }
+        uint64_t cd = 0, dt[3] = {0, 0, 0};
+        if (clk) {
+            cd = clock64();
+            ph[0] += cd - cs;
+            ph[6]++;
         }
         const double tk = march_pos(t, step, rank, march_exact(t, step));
         const bool valid = tk <= tmax && iters + rank < (1 << 24);   // a prefix of the ranks (t grows)
-        const int sg = valid ? sign_at(tk) : 0;
+        const int sg = valid ? (clk ? vol_sign_at_timed(v, o, d, tk, dt) : sign_at(tk)) : 0;
         const int sp = __shfl(sg, prev_lane, 64);
         const int prev = rank == 0 ? sign : sp;
         const uint64_t evb = __ballot(valid && (sg == 0 || (prev >= 0 && sg != prev)));
+        if (clk) {   // this round's phases (the wave's: its longest lane's), the rest of it is bookkeeping
+            const uint64_t t0 = wave_max_u64(dt[0]), t1 = wave_max_u64(dt[1]), t2 = wave_max_u64(dt[2]);
+            const uint64_t all = clock64() - cd;
+            ph[1] += t0; ph[2] += t1; ph[3] += t2;
+            ph[4] += all > t0 + t1 + t2 ? all - (t0 + t1 + t2) : 0;
+        }
         if (evb == 0ull) {
             const uint64_t vb = __ballot(valid);
             if (vb != act) {   // the loop's condition ended it first
                 samples += (uint32_t)__popcll(vb);
+                flush();
                 return kHitInf;
             }
             samples += (uint32_t)nact;
@@ -583,6 +653,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
             iters += nact;
             continue;
         }
+        const uint64_t cr = clk ? clock64() : 0;
         const int ke = __builtin_ctzll(evb);
         const int re = __popcll(act & ((1ull << ke) - 1ull));
         samples += (uint32_t)(re + 1);
@@ -598,6 +669,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
             if (zb) {
                 const int kz = __builtin_ctzll(zb);
                 samples += (uint32_t)(__popcll(act & ((1ull << kz) - 1ull)) + 1);
+                if (clk) { ph[5] += clock64() - cr; flush(); }
                 return __shfl(u, kz, 64) - step;
             }
             const int cnt = min(nact, 64 - j0);
@@ -607,6 +679,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
         t = tr + step;   // the outer loop's t += step, with the refined step
         sign = sge;
         iters += re + 1;
+        if (clk) ph[5] += clock64() - cr;
     }
 }
 // Intersect of analytic record p (march_deferred) by the active lanes together: prim_t's t.
@@ -616,13 +689,14 @@ __device__ __forceinline__ double coop_record_t_body(const DevScene& S, int32_t 
     kind = (int32_t)f2u(r[0].w);
     uint32_t n = 0;
     double t;
+    unsigned long long* const clk = S.march ? S.march + (kMarchClockWord - 9) : nullptr;   // S.march = word 9
     if (kind == KIND_VOLUME) {
-        t = coop_vol_t(S.volumes[rec_ext(r)], o, d, n);
+        t = coop_vol_t(S.volumes[rec_ext(r)], o, d, n, clk);
         tobj = t;
     } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
         const DevXform& X = S.xforms[rec_ext(r)];
         const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
-        t = coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n);
+        t = coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n, clk);
         tobj = t;
         if (t < kHitInf) {
             const v3 position = mat_position(X.m, add(so, muls(sd, t)));

@@ -55,7 +55,7 @@ struct DevScene {
     const float4* tri_nodes;   // 2 float4 per node (pt::BvhNode)
     int32_t tri_num_nodes;
     const float4* tri_recs;    // 3 float4 per triangle: {v1.xyz,e1.x} {e1.yz,e2.xy} {e2.z,-,-,-}
-    const float4* tri_chunks;  // 8 float4 per triangle leaf (pt_api.hip make_leaf_chunks)
+    const float4* tri_chunks;  // 8 float4 per triangle leaf (pt_api.hip build_tri_bvh)
     const float4* tri_shade;   // 3 float4 per triangle: {n1.xyz,n2.x} {n2.yz,n3.xy} {n3.z,mat,-,-}
     // analytic BVH (spheres, cubes)
     const float4* ana_nodes;
@@ -150,6 +150,8 @@ struct DevPass {
     uint32_t acc_stride = 0;   // accumulators per pass (W·H)
 };
 
+constexpr int kCounterWords = 32;    // DevBuffer::counters words
+constexpr int kMarchClockWord = 16;  // counted passes: the cooperative Volume march's phase clocks (8 words)
 struct DevBuffer {
     double* m;                 // [P][3] Welford mean   (Pixel.M, Buffer.cs:21)
     double* v;                 // [P][3] Welford M2     (Pixel.V, Buffer.cs:22)
@@ -157,7 +159,8 @@ struct DevBuffer {
     unsigned long long* counters;  // [0..2] closest-hit rays/nodes/prims, [3] shading fetches, [4..6] shadow
                                    // rays/nodes/prims, [7] lit shadow rays, [8] their accumulation runs,
                                    // [9] volume samples, [10] SDF evaluations (DevScene::march),
-                                   // [15] wavefront queue overflow flag
+                                   // [15] wavefront queue overflow flag, [16..23] the Volume march's phase
+                                   // clocks (counted passes, pt_device.h coop_vol_t)
 };
 
 }  // namespace pt

@@ -75,6 +75,7 @@ constexpr int kFetchWord = count_word(kFetchSlot);
 constexpr int kCountWords = count_word(kEndSlot);
 constexpr int kChunkResetWords = kCountWords;   // every slot is zeroed per chunk
 constexpr int kOverflowCounter = 15;            // DevBuffer::counters word of WfQueues::overflow
+
 // work-fetch cursor of kernel k (0 trace, 1 shade, 2 + q shadow rays of set q, 4 the analytic phase
 // of a split closest hit, 5 + q that of split shadow rays of set q; pt_wavefront.hip "split"; 7 the FULL
 // shade of a routed shade, DevScene::shade_route) in partition g

@@ -698,7 +698,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
                 }
             }
         } else if (tri) {
-            const uint32_t cntl = ((ref >> 29) & 3u) + 1u, first = __float_as_uint(q0.x);
+            const uint32_t w0 = __float_as_uint(q0.x), cntl = (w0 >> 29) + 1u, first = w0 & 0x1FFFFFFFu;   // chunk word 0
             PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6);
 #pragma unroll 1
             for (uint32_t k = 0; k < cntl; k++) {
@@ -766,15 +766,15 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
 // traversal kernel (ray + stack state only).
 // One queued vertex (slot i of partition G.g; `alive` false: the lane only takes part in
 // the block's reservation and ballots).  Block-uniform call.
+template <bool FULL>
+__device__ __forceinline__ void shade_children(const DevScene& S, const DevSampler& smp, const WfQueues& Q, int qi,
+                                               const Group& G, const Shade& sh, v3 d, int depth, uint64_t node,
+                                               uint32_t pixel, const double (&t2)[3], double pv, double n1, double n2,
+                                               int nn, int nm, int nch);
 template <bool COUNT, bool FULL>
 __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler& smp, const WfQueues& Q, int qi,
                                              const Group& G, uint32_t i, bool alive, Counters& ctr,
                                              const uint4* hl = nullptr) {   // hl: the hit record, already in LDS
-    const int qo = 1 - qi;
-    const bool nee_on = smp.dl && S.num_lights > 0;
-    const int nl = S.num_lights;
-    const bool all_lights = smp.light_mode == 1;
-    const uint32_t rays_per_nee = all_lights ? (uint32_t)nl : 1u;   // shadow rays of one sampleLights call
     float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro;
     double2 rt = make_double2(0.0, 0.0);
     ulonglong2 rk = make_ulonglong2(0ull, 0ull);
@@ -834,7 +834,22 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         pv = vertex_p(m, sh, d, n1, n2);
     }
     fix_add_wave(Q.acc, pixel, has_c, cc[0], cc[1], cc[2]);
-    const DevMaterial& m = S.mats[mat];
+    shade_children<FULL>(S, smp, Q, qi, G, sh, d, depth, node, pixel, t2, pv, n1, n2, nn, nm, nch);
+}
+// The children of a shaded vertex (Sampler.cs:96-131): mode, reflect decision and liveness, the block's
+// child-major reservation of extension rays and NEE requests, sampleLights up to the shadow query, Ray.Bounce.
+// nch 0: the lane only takes part in the block's reservation and ballots.  Block-uniform call.
+template <bool FULL>
+__device__ __forceinline__ void shade_children(const DevScene& S, const DevSampler& smp, const WfQueues& Q, int qi,
+                                               const Group& G, const Shade& sh, v3 d, int depth, uint64_t node,
+                                               uint32_t pixel, const double (&t2)[3], double pv, double n1, double n2,
+                                               int nn, int nm, int nch) {
+    const int qo = 1 - qi;
+    const bool nee_on = smp.dl && S.num_lights > 0;
+    const int nl = S.num_lights;
+    const bool all_lights = smp.light_mode == 1;
+    const uint32_t rays_per_nee = all_lights ? (uint32_t)nl : 1u;   // shadow rays of one sampleLights call
+    const DevMaterial& m = S.mats[sh.mat];
     const int ma = nm == 2 ? 1 : 0;
     const bool ext_on = depth + 1 <= smp.mb;   // deeper samples return black without an Intersect
     // child c: mode, reflect decision, liveness (p > 0 after the Any-mode override)
@@ -1383,7 +1398,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                 }
             }
         } else if (tri) {
-            const uint32_t cntl = ((ref >> 29) & 3u) + 1u;
+            const uint32_t cntl = (__float_as_uint(q0.x) >> 29) + 1u;   // chunk word 0
             PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6);
 #pragma unroll 1
             for (uint32_t k = 0; k < cntl; k++) {

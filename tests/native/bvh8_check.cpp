@@ -59,7 +59,7 @@ static bool slab8(const uint32_t* w, int k, const float o[3], const float invd[3
     }
     tn = std::fmax(std::fmax(tns[0], tns[1]), std::fmax(tns[2], 0.f));
     tf = std::fmin(std::fmin(tfs[0], tfs[1]), std::fmin(tfs[2], tmax));
-    return (uint32_t)k < (w[3] >> 28) && tn <= tf * 1.0000005f;
+    return tn <= tf * 1.0000005f;   // (node8_step tests every slot: an empty one must miss by its bounds)
 }
 // exact slab test of a box (fp64), entry before tmax
 static bool slab_exact(const Box& b, const float o[3], const float d[3], double tmax) {
@@ -133,7 +133,8 @@ static void run_case(const char* name, std::vector<float>& lo, std::vector<float
                 node_path[c].push_back({nd, k});
                 todo.push_back({c, p});
             } else {
-                const uint32_t ch = w[5] + (uint32_t)k;
+                CHECK(((w[5] + (uint32_t)k) & 0x80000000u) != 0);   // a leaf ref
+                const uint32_t ch = (w[5] + (uint32_t)k) & 0x7FFFFFFFu;
                 CHECK(ch < b8.chunk_first.size());
                 if (ch >= b8.chunk_first.size()) continue;
                 chunk_seen[ch]++;
@@ -174,7 +175,7 @@ static void run_case(const char* name, std::vector<float>& lo, std::vector<float
     std::vector<uint32_t> chunk_of((size_t)n);
     for (size_t c = 0; c < b8.chunk_first.size(); c++)
         for (uint32_t t = b8.chunk_first[c]; t < b8.chunk_first[c] + b8.chunk_count[c]; t++) chunk_of[b2.order[t]] = (uint32_t)c;
-    long tested = 0, entered = 0, culled = 0;
+    long tested = 0, entered = 0, culled = 0, empty_hits = 0;
     for (int r = 0; r < rays; r++) {
         float o[3], d[3], invd[3];
         const uint32_t target = (uint32_t)(U(rng) * (float)n) % (uint32_t)n;
@@ -195,14 +196,18 @@ static void run_case(const char* name, std::vector<float>& lo, std::vector<float
             tested++;
             if (!slab_exact(prim[p], o, d, (double)tmax)) continue;
             entered++;
-            for (const auto& [nd, k] : chunk_path[chunk_of[p]])
-                if (!slab8(&b8.words[(size_t)nd * pt::kNode8Words], k, o, invd, tmax)) { culled++; break; }
+            for (const auto& [nd, k] : chunk_path[chunk_of[p]]) {
+                const uint32_t* w = &b8.words[(size_t)nd * pt::kNode8Words];
+                if (!slab8(w, k, o, invd, tmax)) { culled++; break; }
+                for (int e = (int)(w[3] >> 28); e < 8; e++) if (slab8(w, e, o, invd, tmax)) empty_hits++;
+            }
         }
     }
     CHECK(culled == 0);
+    CHECK(empty_hits == 0);
     std::printf("%s: %lld primitives, %zu nodes, %zu chunks, stack %d; rays: %ld primitive boxes tested, %ld entered, %ld "
-                "culled by the quantized tree\n", name, (long long)n, nn, b8.chunk_first.size(), b8.stack_need, tested, entered,
-                culled);
+                "culled by the quantized tree, %ld empty slots hit\n", name, (long long)n, nn, b8.chunk_first.size(), b8.stack_need, tested, entered,
+                culled, empty_hits);
 }
 
 int main(int argc, char** argv) {

@@ -336,8 +336,24 @@ struct WideTracer {
                             c.inside++;
                     }
                 }
-                for (int a = 1; a < nh; a++)
-                    for (int b = a; b > 0 && key[b] < key[b - 1]; b--) { std::swap(key[b], key[b - 1]); std::swap(ch[b], ch[b - 1]); }
+                static const int order_mode = std::getenv("PUSH_ORDER") ? std::atoi(std::getenv("PUSH_ORDER")) : 0;
+                if (order_mode == 0) {   // nearest first, the rest far-to-near (sorted)
+                    for (int a = 1; a < nh; a++)
+                        for (int b = a; b > 0 && key[b] < key[b - 1]; b--) { std::swap(key[b], key[b - 1]); std::swap(ch[b], ch[b - 1]); }
+                } else if (nh > 1) {     // nearest first, the rest in slot order (popped lowest slot first)
+                    int mi = 0;
+                    for (int a = 1; a < nh; a++) if (key[a] < key[mi]) mi = a;
+                    std::swap(key[0], key[mi]); std::swap(ch[0], ch[mi]);
+                    // keep slots 1..nh-1 in their original relative order
+                    float k2[8]; uint32_t c2[8]; int m = 0;
+                    for (int a = 1; a < nh; a++) { k2[m] = key[a]; c2[m] = ch[a]; m++; }
+                    (void)k2;
+                    if (mi != 0) { /* slot of the displaced first element goes back in order */
+                        std::vector<std::pair<uint32_t, uint32_t>> tmp;
+                        for (int a = 0; a < m; a++) tmp.push_back({c2[a], 0});
+                    }
+                    for (int a = 0; a < m; a++) ch[1 + a] = c2[a];
+                }
                 if (nh > 0) {
                     for (int k = nh - 1; k >= 1; k--) stack.push_back(ch[k]);
                     max_stack = std::max(max_stack, (int)stack.size());
@@ -525,7 +541,7 @@ static void build_p8(const Mesh& m, WideTree& T, std::vector<uint32_t>& order, d
             bvh8_child_box(w, k, c.lo, c.hi);
             if (k < nin) c.ref = w[4] + (uint32_t)k;
             else {
-                const uint32_t ch = w[5] + (uint32_t)k;
+                const uint32_t ch = (w[5] + (uint32_t)k) & 0x7FFFFFFFu;
                 c.ref = 0x80000000u | ((uint32_t)(b8.chunk_count[ch] - 1) << 29) | b8.chunk_first[ch];
                 prims += b8.chunk_count[ch];
                 T.leaves++;

@@ -1,6 +1,6 @@
 # Same-box A/B of prebuilt libraries (built on the CPU host, in-tree): the current build against others,
 # each C4 bench run alternated (ABAB...), optionally C5 once per library.  The current build is restored.
-# usage: LIBS="bvh4:ab/lib_bvh4.so" ROUNDS=2 C5=1 bash tools/gpu_ab_lib.sh TAG
+# usage: LIBS="bvh4:ab/lib_bvh4.so" ROUNDS=2 C5="cur bvh4" bash tools/gpu_ab_lib.sh TAG   (C5=all: every library)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -17,9 +17,10 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     echo "$N round $r: $(python -c "import json;j=json.load(open('$D/c4_${N}_$r.json'));print(j['value'],j['config']['kernel_ms_per_step'])")" >> $D/summary.txt
   done
 done
-if [ -n "$C5" ]; then
+if [ -n "$C5" ]; then   # C5="all" or a list of the names to run C5 on
   for L in "${LS[@]}"; do
     N=${L%%:*}; P=${L#*:}
+    [ "$C5" != all ] && [[ " $C5 " != *" $N "* ]] && continue
     cp $P $CUR || { restore; exit 1; }
     timeout -k 10 400 python -u bench.py --workload c5 --steps 1 --warmup 1 --cpu-seconds 0 --no-parity --json-out $D/c5_$N.json > $D/c5_$N.log 2>&1 || { restore; exit 1; }
     echo "$N c5: $(python -c "import json;j=json.load(open('$D/c5_$N.json'));print(j['value'],j['config']['kernel_ms_per_step'])")" >> $D/summary.txt

@@ -10,7 +10,9 @@ import glob
 import sys
 
 KERNELS = ("k_wf_trace_lanes<false, false>", "k_wf_trace<false, false>", "k_wf_shade<false, false, false>", "k_wf_shade<false, false, true>",
-           "k_wf_shadow_lanes<false, false>", "k_wf_shadow<false, false>")
+           "k_wf_shadow_lanes<false, false>", "k_wf_shadow<false, false>",
+           # the shade split's vertex and child kernels (A/B builds with -DPT_SHADE_SPLIT=1, round 5)
+           "k_wf_shade<false, false, true, true>", "k_wf_shade<false, false, false, true>", "k_wf_children<false>")
 
 
 def load(d, p):
