@@ -202,6 +202,9 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #ifndef PT_SDF_LDS_MAX
 #define PT_SDF_LDS_MAX 16384   // LDS bytes k_wf_sdf_* may stage the SDF programs in; 0: never
 #endif
+#ifndef PT_VOL_LDS_MAX
+#define PT_VOL_LDS_MAX 40960   // LDS bytes k_wf_vol_* may stage the scene's one Volume in (its uniform-cell table); 0: never
+#endif
 #ifndef PT_VOL_DEFER
 #define PT_VOL_DEFER 1   // split traversal: Volumes deferred to k_wf_vol_hits / k_wf_vol_shadow (0: marched in place)
 #endif
@@ -1280,6 +1283,12 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         vols.back().zero_sign = zero_sign[(size_t)i];
     }
     rc = upload(c, vols, &S.volumes); if (rc) return rc;
+    S.vol_lds = 0;
+    if (d->num_volumes == 1 && !vol_runs.empty()) {   // k_wf_vol_* stage it in LDS (pt_wavefront.hip stage_vol)
+        const size_t need = pt::kVolLdsHeader + (((size_t)d->volumes[0].num_windows * sizeof(pt::DevWindow) + 15) & ~(size_t)15) +
+                            ((vol_runs.size() + 15) & ~(size_t)15);
+        if (need <= (size_t)PT_VOL_LDS_MAX) S.vol_lds = (int32_t)need;
+    }
     rc = upload(c, xforms, &S.xforms); if (rc) return rc;
     rc = upload(c, ext_recs, &S.ext_recs); if (rc) return rc;
     rc = upload(c, blas, &S.blas); if (rc) return rc;

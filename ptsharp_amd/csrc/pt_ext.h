@@ -62,6 +62,7 @@ struct DevVolume {
     const int8_t* runs;
     int32_t zero_sign, _pad;
 };
+constexpr size_t kVolLdsHeader = 128;   // a DevVolume staged in LDS (pt_wavefront.hip stage_vol), padded
 struct DevBlas {          // object-space BVH4 of a mesh instanced by TransformedShape
     int32_t node_off;     // first node in blas_nodes
     int32_t num_nodes;

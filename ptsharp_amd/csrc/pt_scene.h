@@ -88,6 +88,8 @@ struct DevScene {
     const DevSdfIns* sdf_prog;
     const double* sdf_params;
     int32_t sdf_lds;           // LDS bytes k_wf_sdf_* stage sdf_prog and sdf_params in (8-B aligned halves); 0: none
+    int32_t vol_lds;           // LDS bytes k_wf_vol_* stage the scene's one Volume in (its DevVolume, windows and
+                               // uniform-cell table: pt_wavefront.hip stage_vol); 0: none
     int32_t sdf_prog_n;        // entries of sdf_prog
     const DevSdfShape* sdf_shapes;
     const DevVolume* volumes;

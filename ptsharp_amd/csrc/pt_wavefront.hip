@@ -394,7 +394,35 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
 // the traversal's order, the Volume's march before the SDF).  A wave takes 64 entries and marches their
 // Volumes one at a time with all its lanes (march_pending, the cooperative march), in a kernel that
 // holds nothing else and so runs more waves than the FULL kernel that found them.
-__global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, WfQueues Q, int qi) {
+// The scene's one Volume staged in this block's LDS (DevScene::vol_lds > 0): its DevVolume, its windows and its
+// uniform-cell table, so the march's table reads, window loop and the volume's fields are LDS reads (flat loads of
+// LDS addresses) instead of L1 / L2 round trips; the grid's corners stay in HBM.  Returns the scene view that reads
+// them there.  Block-uniform call.
+static_assert(sizeof(DevVolume) <= kVolLdsHeader, "stage_vol's header");
+__device__ __forceinline__ DevScene stage_vol(const DevScene& S) {
+    extern __shared__ __align__(16) unsigned char s_vol[];
+    DevScene V = S;
+    const DevVolume src = S.volumes[0];
+    DevVolume* hv = reinterpret_cast<DevVolume*>(s_vol);
+    DevWindow* win = reinterpret_cast<DevWindow*>(s_vol + kVolLdsHeader);
+    const uint32_t nwin_b = ((uint32_t)src.nwin * (uint32_t)sizeof(DevWindow) + 15u) & ~15u;
+    int8_t* runs = reinterpret_cast<int8_t*>(s_vol + kVolLdsHeader + nwin_b);
+    const uint32_t nr = (uint32_t)((src.w + 1) * (src.h + 1) * (src.d + 1));
+    for (uint32_t k = threadIdx.x; k < nr; k += blockDim.x) runs[k] = src.runs[k];
+    for (uint32_t k = threadIdx.x; k < (uint32_t)src.nwin; k += blockDim.x) win[k] = src.windows[k];
+    if (threadIdx.x == 0) {
+        DevVolume v = src;
+        v.windows = win;
+        v.runs = runs;
+        *hv = v;
+    }
+    __syncthreads();
+    V.volumes = hv;
+    return V;
+}
+template <bool STAGED>
+__global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S0, WfQueues Q, int qi) {
+    const DevScene S = STAGED ? stage_vol(S0) : S0;
     const uint32_t n = min(Q.counts[kSdfWord], Q.cap);
     const bool env_black = S.env_tex < 0 && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
     const uint32_t lane = threadIdx.x & 63;
@@ -432,7 +460,9 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S, W
 }
 // The Volume records split shadow rays deferred: blocked (unlit) when the march's t is nearer than
 // the light; k_wf_sdf_shadow then skips the ray.
-__global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S, WfQueues Q, int qo) {
+template <bool STAGED>
+__global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S0, WfQueues Q, int qo) {
+    const DevScene S = STAGED ? stage_vol(S0) : S0;
     const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
@@ -1663,7 +1693,10 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
-            if (Q.volq && S.num_vol > 0) hipLaunchKernelGGL(k_wf_vol_hits, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
+            if (Q.volq && S.num_vol > 0 && S.vol_lds > 0)
+                hipLaunchKernelGGL(k_wf_vol_hits<true>, dim3(grid_for(n, 256, 2048)), dim3(256), (size_t)S.vol_lds, stream, S, Q, qi);
+            else if (Q.volq && S.num_vol > 0)
+                hipLaunchKernelGGL(k_wf_vol_hits<false>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
             if (S.num_sdf > 0 && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_hits<true>, dim3(grid_for(n, 256, 8192)), dim3(256), (size_t)S.sdf_lds, stream, S, Q, qi);
             else if (S.num_sdf > 0)
@@ -1730,8 +1763,11 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
-            if (Q.volq_sh && S.num_vol > 0)   // (the queues outlive a re-upload of a scene without Volumes)
-                hipLaunchKernelGGL(k_wf_vol_shadow, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256), 0,
+            if (Q.volq_sh && S.num_vol > 0 && S.vol_lds > 0)   // (the queues outlive a re-upload of a scene without Volumes)
+                hipLaunchKernelGGL(k_wf_vol_shadow<true>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256),
+                                   (size_t)S.vol_lds, side, S, Q, 1 - qi);
+            else if (Q.volq_sh && S.num_vol > 0)
+                hipLaunchKernelGGL(k_wf_vol_shadow<false>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256), 0,
                                    side, S, Q, 1 - qi);
             if (sq && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_shadow<true>, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256),
