@@ -26,10 +26,10 @@ scene: both VALU-issue-bound (fp64 sampler math; fp64 marches), priced by the pa
 cycles per ray (PMC instruction mix by kind, profiles/pmc_valu_mix_<workload>.json) against 1024 SIMDs
 at 2.4 GHz, with the measured fp32 / fp64 FLOP rates beside it.
 
-Roofline: the closest-hit kernel's algorithmic bytes (per ray: 112 B per
-BVH4 node fetch, 36 B per primitive test, 44 B ray in + hit out) over its HIP-event time,
+Roofline: the closest-hit kernel's algorithmic bytes (per ray: 128 B per
+BVH8 node fetch, 36 B per primitive test, 44 B ray in + hit out) over its HIP-event time,
 against the L2 bandwidth (≈34.5 TB/s, MI355X_MICROARCH.md §L2).  The BVH nodes and leaf
-chunks (79 MB at 1M triangles) live in L2 and the 256 MB Infinity Cache, so HBM is not the
+chunks (~62 MB at 1M triangles) live in L2 and the 256 MB Infinity Cache, so HBM is not the
 binding bound (the same bytes over 8 TB/s gave a fraction above 1 in round 1).  `traffic`
 is the measured L2↔fabric bytes per launch (rocprofv3 FETCH_SIZE×2 + WRITE_SIZE, which
 count Infinity-Cache hits too; profiles/pmc_traffic.json), set beside the compulsory bytes
