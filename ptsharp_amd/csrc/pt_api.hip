@@ -145,8 +145,8 @@ struct Ctx {
     double* d_m = nullptr;
     double* d_v = nullptr;
     int32_t* d_n = nullptr;
-    unsigned long long* d_counters = nullptr;   // [pt::kCounterWords] the pass' counters (pt::DevBuffer::counters)
-    unsigned long long* h_counters = nullptr;   // [pt::kCounterWords] pinned: their read-back
+    unsigned long long* d_counters = nullptr;   // [pt::kCounterAllocWords] the pass' counters (pt::DevBuffer::counters)
+    unsigned long long* h_counters = nullptr;   // [pt::kCounterAllocWords] pinned: their read-back
     int32_t* d_tiles = nullptr;
     int32_t tiles_cap = 0;
     std::vector<int32_t> h_tiles;               // the tile list in d_tiles (uploaded when it changes)
@@ -204,6 +204,9 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #endif
 #ifndef PT_VOL_LDS_MAX
 #define PT_VOL_LDS_MAX 40960   // LDS bytes k_wf_vol_* may stage the scene's one Volume in (its uniform-cell table); 0: never
+#endif
+#ifndef PT_VOL_CELLS_MAX
+#define PT_VOL_CELLS_MAX (1ull << 30)   // bytes of cell-major Volume corners (8 per cell) a scene may hold; 0: none
 #endif
 #ifndef PT_VOL_DEFER
 #define PT_VOL_DEFER 1   // split traversal: Volumes deferred to k_wf_vol_hits / k_wf_vol_shadow (0: marched in place)
@@ -826,8 +829,8 @@ int pt_create(const pt_device_opts* opts, void** out_ctx) {
     size_t P = (size_t)c->width * (size_t)c->height;
     if (hipMalloc(&c->d_m, P * 3 * sizeof(double)) != hipSuccess || hipMalloc(&c->d_v, P * 3 * sizeof(double)) != hipSuccess ||
         hipMalloc(&c->d_n, P * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&c->d_counters, pt::kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc(&c->h_counters, pt::kCounterWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+        hipMalloc(&c->d_counters, pt::kCounterAllocWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(&c->h_counters, pt::kCounterAllocWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
         return cleanup(fail(PT_ERR_OUT_OF_MEMORY, "buffer allocation"));
     int rc = pt_reset_buffer(c);
     if (rc != PT_OK) return cleanup(rc);
@@ -953,6 +956,18 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
         runs_off.push_back(vol_runs.size());
         vol_runs.resize(vol_runs.size() + (size_t)(v.w + 1) * (v.h + 1) * (v.d + 1));
         pt::vol_build_runs(host_volume(i), vol_runs.data() + runs_off.back(), zero_sign[(size_t)i]);
+    }
+    // cell-major corners of the march (pt_ext.h vol_build_cells), per volume while they stay within
+    // PT_VOL_CELLS_MAX bytes in all; cells_off = -1: the march reads the grid
+    std::vector<double> vol_cells;
+    std::vector<int64_t> cells_off((size_t)std::max(d->num_volumes, 0), -1);
+    for (int i = 0; i < d->num_volumes; i++) {
+        const pt_volume& v = d->volumes[i];
+        const size_t n = 8 * (size_t)(v.w + 1) * (v.h + 1) * (v.d + 1);
+        if ((vol_cells.size() + n) * sizeof(double) > (size_t)PT_VOL_CELLS_MAX) continue;
+        cells_off[(size_t)i] = (int64_t)vol_cells.size();
+        vol_cells.resize(vol_cells.size() + n);
+        pt::vol_build_cells(host_volume(i), vol_cells.data() + cells_off[(size_t)i]);
     }
     const pt::v3 origin = pt::zero3();
     // IShape.BoundingBox of a shape that can be analytic or inner (exact, as the reference computes it)
@@ -1276,11 +1291,14 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, windows, &d_win); if (rc) return rc;
     const int8_t* d_runs = nullptr;
     rc = upload(c, vol_runs, &d_runs); if (rc) return rc;
+    const double* d_cells = nullptr;
+    rc = upload(c, vol_cells, &d_cells); if (rc) return rc;
     std::vector<pt::DevVolume> vols;
     for (int i = 0; i < d->num_volumes; i++) {
         vols.push_back(dev_volume(d->volumes[i], d_vox + vol_off[(size_t)i], d_win ? d_win + win_off[(size_t)i] : nullptr));
         vols.back().runs = d_runs ? d_runs + runs_off[(size_t)i] : nullptr;
         vols.back().zero_sign = zero_sign[(size_t)i];
+        vols.back().cells = cells_off[(size_t)i] >= 0 ? d_cells + cells_off[(size_t)i] : nullptr;
     }
     rc = upload(c, vols, &S.volumes); if (rc) return rc;
     S.vol_lds = 0;
@@ -1534,7 +1552,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     }
     const bool timing = (pass->flags & PT_PASS_KERNEL_TIMING) != 0;
     c->timer.reset(c->stream);
-    PT_HIP(hipMemsetAsync(c->d_counters, 0, pt::kCounterWords * sizeof(unsigned long long), c->stream));   // and the overflow flag
+    PT_HIP(hipMemsetAsync(c->d_counters, 0, (counted ? pt::kCounterAllocWords : pt::kCounterWords) * sizeof(unsigned long long),
+                          c->stream));   // and the overflow flag; a counted pass' march clock slots too
     // a counted pass also counts the Volume / SDFShape march steps (counters 9, 10); the launches
     // take the scene by value, so the pointer is cleared again whichever way this call returns
     struct MarchScope {
@@ -1604,7 +1623,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     PT_HIP(hipEventRecord(c->ev1, c->stream));
     if (c->timer.failed) return fail(PT_ERR_HIP, "hipEventRecord (kernel timing) failed");
     const unsigned long long* ctr = c->h_counters;
-    PT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, pt::kCounterWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    PT_HIP(hipMemcpyAsync(c->h_counters, c->d_counters, (counted ? pt::kCounterAllocWords : pt::kCounterWords) * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
     if (engine == PT_ENGINE_WAVEFRONT && ctr[pt::kOverflowCounter])
         return fail(PT_ERR_OUT_OF_MEMORY, "wavefront queue overflow (pass results are incomplete)");
@@ -1632,7 +1652,10 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         counted->accum_runs = ctr[8];
         counted->volume_samples = ctr[9];
         counted->sdf_evals = ctr[10];
-        for (int k = 0; k < 8; k++) counted->march_clock[k] = ctr[pt::kMarchClockWord + k];
+        for (int k = 0; k < 8; k++) {
+            counted->march_clock[k] = 0;
+            for (int j = 0; j < pt::kMarchSlots; j++) counted->march_clock[k] += ctr[pt::kMarchClockWord + 8 * j + k];
+        }
     }
     return PT_OK;
 }

@@ -526,17 +526,15 @@ __device__ __forceinline__ int vol_sign_at_timed(const DevVolume& v, v3 o, v3 d,
     const double lim = 2147483647.0;
     if (fabs(x) < lim && fabs(y) < lim && fabs(z) < lim) {
         const int x0 = (int)floor(x), y0 = (int)floor(y), z0 = (int)floor(z);
-        const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
-        const double v000 = vol_get(v, x0, y0, z0), v001 = vol_get(v, x0, y0, z1), v010 = vol_get(v, x0, y1, z0);
-        const double v011 = vol_get(v, x0, y1, z1), v100 = vol_get(v, x1, y0, z0), v101 = vol_get(v, x1, y0, z1);
-        const double v110 = vol_get(v, x1, y1, z0), v111 = vol_get(v, x1, y1, z1);
+        double k[8];
+        vol_corners(v, x0, y0, z0, k);
         x -= (double)x0;
         y -= (double)y0;
         z -= (double)z0;
-        const double c00 = v000 * (1 - x) + v100 * x;
-        const double c01 = v001 * (1 - x) + v101 * x;
-        const double c10 = v010 * (1 - x) + v110 * x;
-        const double c11 = v011 * (1 - x) + v111 * x;
+        const double c00 = k[0] * (1 - x) + k[4] * x;
+        const double c01 = k[1] * (1 - x) + k[5] * x;
+        const double c10 = k[2] * (1 - x) + k[6] * x;
+        const double c11 = k[3] * (1 - x) + k[7] * x;
         const double cc0 = c00 * (1 - y) + c10 * y;
         const double cc1 = c01 * (1 - y) + c11 * y;
         smp = cc0 * (1 - z) + cc1 * z;
@@ -689,7 +687,9 @@ __device__ __forceinline__ double coop_record_t_body(const DevScene& S, int32_t 
     kind = (int32_t)f2u(r[0].w);
     uint32_t n = 0;
     double t;
-    unsigned long long* const clk = S.march ? S.march + (kMarchClockWord - 9) : nullptr;   // S.march = word 9
+    // S.march = word 9; this wave's slot of the phase clocks
+    unsigned long long* const clk =
+        S.march ? S.march + (kMarchClockWord - 9) + 8 * (((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (kMarchSlots - 1)) : nullptr;
     if (kind == KIND_VOLUME) {
         t = coop_vol_t(S.volumes[rec_ext(r)], o, d, n, clk);
         tobj = t;

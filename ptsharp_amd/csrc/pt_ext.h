@@ -61,6 +61,10 @@ struct DevVolume {
     // for; null: no skipping.  zero_sign: the Sign of a cell with every corner outside the grid.
     const int8_t* runs;
     int32_t zero_sign, _pad;
+    // The eight corners of every cell of the runs table's lattice, cell-major (vol_build_cells: 64 B per cell,
+    // v000 v001 v010 v011 v100 v101 v110 v111, Volume.Get's values), so a march position's corners are one
+    // half-line read instead of eight reads on four lines; null: read data.
+    const double* cells;
 };
 constexpr size_t kVolLdsHeader = 128;   // a DevVolume staged in LDS (pt_wavefront.hip stage_vol), padded
 struct DevBlas {          // object-space BVH4 of a mesh instanced by TransformedShape
@@ -302,6 +306,23 @@ PT_HD double vol_get(const DevVolume& v, int x, int y, int z) {   // Volume.Get 
     if (x < 0 || y < 0 || z < 0 || x >= v.w || y >= v.h || z >= v.d) return 0;
     return v.data[(size_t)x + (size_t)y * (size_t)v.w + (size_t)z * (size_t)v.w * (size_t)v.h];
 }
+struct alignas(16) VolPair {
+    double lo, hi;
+};
+// The eight corners of cell (x0, y0, z0): Volume.Get's values, from the cell-major copy when the cell is on it.
+PT_HD void vol_corners(const DevVolume& v, int x0, int y0, int z0, double c[8]) {
+    if (v.cells && x0 >= -1 && y0 >= -1 && z0 >= -1 && x0 < v.w && y0 < v.h && z0 < v.d) {
+        const VolPair* p = reinterpret_cast<const VolPair*>(
+            v.cells + 8 * ((size_t)(x0 + 1) + (size_t)(y0 + 1) * (v.w + 1) + (size_t)(z0 + 1) * (v.w + 1) * (v.h + 1)));
+        const VolPair a = p[0], b = p[1], e = p[2], f = p[3];   // four 16-B loads of one half-line
+        c[0] = a.lo; c[1] = a.hi; c[2] = b.lo; c[3] = b.hi; c[4] = e.lo; c[5] = e.hi; c[6] = f.lo; c[7] = f.hi;
+        return;
+    }
+    c[0] = vol_get(v, x0, y0, z0); c[1] = vol_get(v, x0, y0, z0 + 1);
+    c[2] = vol_get(v, x0, y0 + 1, z0); c[3] = vol_get(v, x0, y0 + 1, z0 + 1);
+    c[4] = vol_get(v, x0 + 1, y0, z0); c[5] = vol_get(v, x0 + 1, y0, z0 + 1);
+    c[6] = vol_get(v, x0 + 1, y0 + 1, z0); c[7] = vol_get(v, x0 + 1, y0 + 1, z0 + 1);
+}
 // Volume.Sample (Volume.cs:73-105), with its y-from-z slip (:77).  Coordinates outside
 // the int range (an OverflowException in the reference) sample 0, as in the oracle.
 PT_HD double vol_sample(const DevVolume& v, double x, double y, double z) {
@@ -346,10 +367,7 @@ PT_HD double vol_sample_cell(const DevVolume& v, double x, double y, double z, V
     if (!(fabs(x) < lim && fabs(y) < lim && fabs(z) < lim)) return 0;
     const int x0 = (int)floor(x), y0 = (int)floor(y), z0 = (int)floor(z);
     if (x0 != k.x0 || y0 != k.y0 || z0 != k.z0) {
-        const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
-        k.c[0] = vol_get(v, x0, y0, z0); k.c[1] = vol_get(v, x0, y0, z1); k.c[2] = vol_get(v, x0, y1, z0);
-        k.c[3] = vol_get(v, x0, y1, z1); k.c[4] = vol_get(v, x1, y0, z0); k.c[5] = vol_get(v, x1, y0, z1);
-        k.c[6] = vol_get(v, x1, y1, z0); k.c[7] = vol_get(v, x1, y1, z1);
+        vol_corners(v, x0, y0, z0, k.c);
         k.x0 = x0; k.y0 = y0; k.z0 = z0;
     }
     x -= (double)x0;
@@ -482,6 +500,15 @@ PT_HD int vol_key_sign(const DevVolume& v, VolKey k) {
     if (k.x < -1 || k.y < -1 || k.z < -1 || k.x >= v.w || k.y >= v.h || k.z >= v.d) return v.zero_sign;
     return v.runs[(k.x + 1) + (size_t)(k.y + 1) * (v.w + 1) + (size_t)(k.z + 1) * (v.w + 1) * (v.h + 1)];
 }
+// Host: fill out[8·((x0+1) + (y0+1)(w+1) + (z0+1)(w+1)(h+1)) + c] = corner c of cell (x0, y0, z0), the runs table's
+// cells, c = 4·dx + 2·dy + dz (vol_sample's v000 v001 v010 v011 v100 v101 v110 v111).
+inline void vol_build_cells(const DevVolume& v, double* out) {
+    size_t i = 0;
+    for (int z0 = -1; z0 < v.d; z0++)
+        for (int y0 = -1; y0 < v.h; y0++)
+            for (int x0 = -1; x0 < v.w; x0++, i++)
+                for (int c = 0; c < 8; c++) out[8 * i + (size_t)c] = vol_get(v, x0 + (c >> 2), y0 + (c >> 1 & 1), z0 + (c & 1));
+}
 // The Sign of march position t (vol_key_sign of a uniform cell, else Volume.Sign of the sample) with the
 // lattice coordinates computed once: vol_key and Volume.Sample (vol_sample) scale the same position by
 // the same operations, so the key and the sample share them (one fp64 division by zscale, not two).
@@ -504,17 +531,15 @@ PT_HD int vol_sign_at(const DevVolume& v, v3 o, v3 d, double t) {
     const double lim = 2147483647.0;   // vol_sample from the scaled coordinates on
     if (!(fabs(x) < lim && fabs(y) < lim && fabs(z) < lim)) return vol_sign_of(v, 0.0);
     const int x0 = (int)floor(x), y0 = (int)floor(y), z0 = (int)floor(z);
-    const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
-    const double v000 = vol_get(v, x0, y0, z0), v001 = vol_get(v, x0, y0, z1), v010 = vol_get(v, x0, y1, z0);
-    const double v011 = vol_get(v, x0, y1, z1), v100 = vol_get(v, x1, y0, z0), v101 = vol_get(v, x1, y0, z1);
-    const double v110 = vol_get(v, x1, y1, z0), v111 = vol_get(v, x1, y1, z1);
+    double k[8];
+    vol_corners(v, x0, y0, z0, k);
     x -= (double)x0;
     y -= (double)y0;
     z -= (double)z0;
-    const double c00 = v000 * (1 - x) + v100 * x;
-    const double c01 = v001 * (1 - x) + v101 * x;
-    const double c10 = v010 * (1 - x) + v110 * x;
-    const double c11 = v011 * (1 - x) + v111 * x;
+    const double c00 = k[0] * (1 - x) + k[4] * x;
+    const double c01 = k[1] * (1 - x) + k[5] * x;
+    const double c10 = k[2] * (1 - x) + k[6] * x;
+    const double c11 = k[3] * (1 - x) + k[7] * x;
     const double c0 = c00 * (1 - y) + c10 * y;
     const double c1 = c01 * (1 - y) + c11 * y;
     return vol_sign_of(v, c0 * (1 - z) + c1 * z);

@@ -153,7 +153,12 @@ struct DevPass {
 };
 
 constexpr int kCounterWords = 32;    // DevBuffer::counters words
-constexpr int kMarchClockWord = 16;  // counted passes: the cooperative Volume march's phase clocks (8 words)
+// Counted passes: the cooperative Volume march's phase clocks, 8 words per slot, kMarchSlots slots after the
+// counters (a march adds its clocks to its wave's slot: one set of 8 words hit by every march serialised the
+// counted pass' march kernels on those lines, C5 13 s per counted pass); the host sums the slots.
+constexpr int kMarchClockWord = kCounterWords;
+constexpr int kMarchSlots = 2048;
+constexpr int kCounterAllocWords = kCounterWords + 8 * kMarchSlots;
 struct DevBuffer {
     double* m;                 // [P][3] Welford mean   (Pixel.M, Buffer.cs:21)
     double* v;                 // [P][3] Welford M2     (Pixel.V, Buffer.cs:22)

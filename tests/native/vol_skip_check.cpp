@@ -227,6 +227,11 @@ int main(int argc, char** argv) {
             std::vector<int8_t> runs((size_t)(w + 1) * (h + 1) * (dd + 1));
             vol_build_runs(v, runs.data(), v.zero_sign);
             v.runs = runs.data();
+            // the device's cell-major corners (vol_build_cells): vol_t, vol_sign_at and the emulated cooperative
+            // march read them, the loop as written (naive_t, vref) reads the grid
+            std::vector<double> cells(8 * runs.size());
+            vol_build_cells(v, cells.data());
+            v.cells = cells.data();
             long long uni = 0;
             for (int8_t r : runs) uni += r != 0;
             long long vbad = 0;
@@ -250,6 +255,7 @@ int main(int argc, char** argv) {
                 const auto c1 = std::chrono::steady_clock::now();
                 DevVolume vref = v;
                 vref.zinv = 0.0;
+                vref.cells = nullptr;
                 const double b = naive_t(vref, o, dir);
                 const auto c2 = std::chrono::steady_clock::now();
                 t_skip += std::chrono::duration<double>(c1 - c0).count();
