@@ -469,7 +469,8 @@ PT_HD double t_after(double t, double step, long long k) {
             break;
         }
         const double lim = ldexp(1.0, e);
-        const long long room = (long long)ceil((lim - t) / step) - 1;   // additions that stay below lim
+        // additions that stay below lim; step is a power of two, so multiplying by its reciprocal is the division
+        const long long room = (long long)ceil((lim - t) * (1.0 / step)) - 1;
         if (room >= k) return t + (double)k * step;
         t = t + (double)room * step;
         t += step;   // into the next binade: rounded, as the reference's
