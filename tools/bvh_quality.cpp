@@ -320,8 +320,8 @@ struct WideTracer {
             if (!(ref & 0x80000000u)) {
                 c.nodes++;
                 const WNode& nd = T.nodes[ref];
-                float key[8];
-                uint32_t ch[8];
+                float key[16];
+                uint32_t ch[16];
                 int nh = 0;
                 for (const WChild& w : nd.c) {
                     tests++;
@@ -345,13 +345,9 @@ struct WideTracer {
                     for (int a = 1; a < nh; a++) if (key[a] < key[mi]) mi = a;
                     std::swap(key[0], key[mi]); std::swap(ch[0], ch[mi]);
                     // keep slots 1..nh-1 in their original relative order
-                    float k2[8]; uint32_t c2[8]; int m = 0;
-                    for (int a = 1; a < nh; a++) { k2[m] = key[a]; c2[m] = ch[a]; m++; }
-                    (void)k2;
-                    if (mi != 0) { /* slot of the displaced first element goes back in order */
-                        std::vector<std::pair<uint32_t, uint32_t>> tmp;
-                        for (int a = 0; a < m; a++) tmp.push_back({c2[a], 0});
-                    }
+                    uint32_t c2[16];
+                    int m = 0;
+                    for (int a = 1; a < nh; a++) c2[m++] = ch[a];
                     for (int a = 0; a < m; a++) ch[1 + a] = c2[a];
                 }
                 if (nh > 0) {
