@@ -574,7 +574,8 @@ constexpr int kVolStride = 16;   // the strided pass's positions per lane (8 / 3
 // `samples`, the Volume.Sample calls vol_t makes (instrumentation).
 // clk (counted passes, else null): the phase clocks of pt_trace_counters::march_clock, added by the first
 // active lane at the end.
-__device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& samples, unsigned long long* clk = nullptr) {
+template <bool TIMED>
+__device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& samples, unsigned long long* clk) {
     const uint64_t act = __ballot(true);
     const int lane = threadIdx.x & 63;
     const uint64_t lower = act & ((1ull << lane) - 1ull);
@@ -590,11 +591,11 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
     auto sign_at = [&](double tt) { return vol_sign_fast(v, o, d, tt); };
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // clk: strided, table, corners, windows, rest, refinements, rounds x2
     auto flush = [&]() {
-        if (clk && lane == __builtin_ctzll(act))
+        if (TIMED && clk && lane == __builtin_ctzll(act))
             for (int k = 0; k < 8; k++) atomicAdd(clk + k, (unsigned long long)ph[k]);
     };
     for (;;) {   // wave-uniform: every branch below is on ballots
-        const uint64_t cs = clk ? clock64() : 0;
+        const uint64_t cs = TIMED ? clock64() : 0;
         // Strided pass over runs of uniform cells: lane of rank r looks at position (r + 1)·S from
         // t; when the cells of consecutive looked-at positions (and of position 0) span only cells
         // of the running Sign, no position up to there can act, and the march moves past them,
@@ -617,22 +618,22 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
             t = t_after(t, step, k);
             iters += k;
             sign = s0;
-            if (clk) ph[7]++;
+            if (TIMED) ph[7]++;
             if (f < nact) break;
         }
         uint64_t cd = 0, dt[3] = {0, 0, 0};
-        if (clk) {
+        if (TIMED) {
             cd = clock64();
             ph[0] += cd - cs;
             ph[6]++;
         }
         const double tk = march_pos(t, step, rank, march_exact(t, step));
         const bool valid = tk <= tmax && iters + rank < (1 << 24);   // a prefix of the ranks (t grows)
-        const int sg = valid ? (clk ? vol_sign_at_timed(v, o, d, tk, dt) : sign_at(tk)) : 0;
+        const int sg = valid ? (TIMED ? vol_sign_at_timed(v, o, d, tk, dt) : sign_at(tk)) : 0;
         const int sp = __shfl(sg, prev_lane, 64);
         const int prev = rank == 0 ? sign : sp;
         const uint64_t evb = __ballot(valid && (sg == 0 || (prev >= 0 && sg != prev)));
-        if (clk) {   // this round's phases (the wave's: its longest lane's), the rest of it is bookkeeping
+        if (TIMED) {   // this round's phases (the wave's: its longest lane's), the rest of it is bookkeeping
             const uint64_t t0 = wave_max_u64(dt[0]), t1 = wave_max_u64(dt[1]), t2 = wave_max_u64(dt[2]);
             const uint64_t all = clock64() - cd;
             ph[1] += t0; ph[2] += t1; ph[3] += t2;
@@ -651,7 +652,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
             iters += nact;
             continue;
         }
-        const uint64_t cr = clk ? clock64() : 0;
+        const uint64_t cr = TIMED ? clock64() : 0;
         const int ke = __builtin_ctzll(evb);
         const int re = __popcll(act & ((1ull << ke) - 1ull));
         samples += (uint32_t)(re + 1);
@@ -667,7 +668,7 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
             if (zb) {
                 const int kz = __builtin_ctzll(zb);
                 samples += (uint32_t)(__popcll(act & ((1ull << kz) - 1ull)) + 1);
-                if (clk) { ph[5] += clock64() - cr; flush(); }
+                if (TIMED) { ph[5] += clock64() - cr; flush(); }
                 return __shfl(u, kz, 64) - step;
             }
             const int cnt = min(nact, 64 - j0);
@@ -677,10 +678,13 @@ __device__ inline double coop_vol_t(const DevVolume& v, v3 o, v3 d, uint32_t& sa
         t = tr + step;   // the outer loop's t += step, with the refined step
         sign = sge;
         iters += re + 1;
-        if (clk) ph[5] += clock64() - cr;
+        if (TIMED) ph[5] += clock64() - cr;
     }
 }
 // Intersect of analytic record p (march_deferred) by the active lanes together: prim_t's t.
+// TIMED (counted passes): the march's phase clocks (pt_trace_counters::march_clock); the timed passes' kernels
+// are built without them (their registers: the FULL kernels spilled 31 more VGPRs with the clocks inline).
+template <bool TIMED>
 __device__ __forceinline__ double coop_record_t_body(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind,
                                                     double& tobj) {
     const float4* r = S.ana_recs + 3 * (size_t)p;
@@ -688,15 +692,15 @@ __device__ __forceinline__ double coop_record_t_body(const DevScene& S, int32_t 
     uint32_t n = 0;
     double t;
     // S.march = word 9; this wave's slot of the phase clocks
-    unsigned long long* const clk =
-        S.march ? S.march + (kMarchClockWord - 9) + 8 * (((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (kMarchSlots - 1)) : nullptr;
+    unsigned long long* const clk = TIMED && S.march
+        ? S.march + (kMarchClockWord - 9) + 8 * (((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (kMarchSlots - 1)) : nullptr;
     if (kind == KIND_VOLUME) {
-        t = coop_vol_t(S.volumes[rec_ext(r)], o, d, n, clk);
+        t = coop_vol_t<TIMED>(S.volumes[rec_ext(r)], o, d, n, clk);
         tobj = t;
     } else {   // xform_t over an inner Volume (TransformedShape.cs:43-73)
         const DevXform& X = S.xforms[rec_ext(r)];
         const v3 so = mat_position(X.inv, o), sd = mat_direction(X.inv, d);
-        t = coop_vol_t(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n, clk);
+        t = coop_vol_t<TIMED>(S.volumes[rec_ext(S.ext_recs + 3 * (size_t)X.rec)], so, sd, n, clk);
         tobj = t;
         if (t < kHitInf) {
             const v3 position = mat_position(X.m, add(so, muls(sd, t)));
@@ -707,12 +711,13 @@ __device__ __forceinline__ double coop_record_t_body(const DevScene& S, int32_t 
     return t;
 }
 // Out of line in the FULL traversal kernels (their registers), inlined in k_wf_vol_* (INL).
+template <bool TIMED>
 __device__ __noinline__ double coop_record_t(const DevScene& S, int32_t p, v3 o, v3 d, int32_t& kind, double& tobj) {
-    return coop_record_t_body(S, p, o, d, kind, tobj);
+    return coop_record_t_body<TIMED>(S, p, o, d, kind, tobj);
 }
 // The lanes' pending Volume records, one ray at a time by all active lanes (at least S.coop_min_lanes):
 // march_pending's merge, without its few-lanes fallback (k_wf_vol_hits / k_wf_vol_shadow run full waves).
-template <bool ANY, bool INL = false>
+template <bool ANY, bool INL, bool TIMED>
 __device__ inline void march_coop(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked) {
     const int lane = threadIdx.x & 63;
     for (uint64_t todo = __ballot(pend >= 0); todo; todo &= todo - 1ull) {   // wave-uniform
@@ -722,7 +727,7 @@ __device__ inline void march_coop(const DevScene& S, v3 o, v3 d, int32_t pend, H
         const v3 sd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
         int32_t kind;
         double tx = 0;
-        const double t = INL ? coop_record_t_body(S, p, so, sd, kind, tx) : coop_record_t(S, p, so, sd, kind, tx);
+        const double t = INL ? coop_record_t_body<TIMED>(S, p, so, sd, kind, tx) : coop_record_t<TIMED>(S, p, so, sd, kind, tx);
         if (lane == src) {
             if (ANY) {
                 if (t < best.t) *blocked = true;
@@ -736,7 +741,7 @@ __device__ inline void march_coop(const DevScene& S, v3 o, v3 d, int32_t pend, H
 // Closest hit: the march's t replaces the best when nearer, and on a tie with a triangle (the
 // analytic BVH is traversed before the triangles, which replace only a strictly farther best);
 // any-hit (ANY): *blocked when nearer than the light.
-template <bool ANY>
+template <bool ANY, bool TIMED>
 __device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend, HitRec& best, bool* blocked = nullptr) {
     auto merge = [&](double t, int32_t kind, int32_t p, double tx) {
         if (ANY) {
@@ -754,7 +759,7 @@ __device__ inline void march_pending(const DevScene& S, v3 o, v3 d, int32_t pend
         }
         return;
     }
-    march_coop<ANY>(S, o, d, pend, best, blocked);
+    march_coop<ANY, false, TIMED>(S, o, d, pend, best, blocked);
 }
 
 // Scene.Intersect (Scene.cs:75-79): closest hit over planes, analytic BVH, triangle BVH.
@@ -782,7 +787,7 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
                                             FULL ? &pend : nullptr);
     }
     traverse_tri<COUNT, false>(S, o, d, invd, best, stack, ctr);
-    if (FULL) march_pending<false>(S, o, d, pend, best);
+    if (FULL) march_pending<false, COUNT>(S, o, d, pend, best);
     return best;
 }
 
@@ -821,7 +826,7 @@ __device__ __forceinline__ bool any_nearer(const DevScene& S, v3 o, v3 d, double
     if (traverse_tri<COUNT, true>(S, o, d, invd, best, stack, ctr)) return true;
     if (FULL) {   // the lanes still unblocked march their pending Volume together
         bool blocked = false;
-        march_pending<true>(S, o, d, pend, best, &blocked);
+        march_pending<true, COUNT>(S, o, d, pend, best, &blocked);
         if (blocked) return true;
     }
     return false;
@@ -877,7 +882,7 @@ __device__ __forceinline__ void trace_ana(const DevScene& S, v3 o, v3 d, const S
                                             sdf_out ? &pend_sdf : nullptr);
     }
     if (vol_out) *vol_out = pend;
-    else march_pending<false>(S, o, d, pend, best);
+    else march_pending<false, COUNT>(S, o, d, pend, best);
     if (sdf_out) *sdf_out = pend_sdf;
     else sdf_pending<false>(S, o, d, pend_sdf, best);
     if (best.kind == KIND_TRI && tri_best) best.t = t_in;
@@ -910,7 +915,7 @@ __device__ __forceinline__ bool ana_blocked(const DevScene& S, const DevLight& L
         *vol_out = pend;
     } else {
         bool blocked = false;
-        march_pending<true>(S, o, d, pend, best, &blocked);
+        march_pending<true, COUNT>(S, o, d, pend, best, &blocked);
         if (blocked) return true;
     }
     if (sdf_out) {   // left for k_wf_sdf_shadow
@@ -960,7 +965,7 @@ __device__ __forceinline__ void trace_heavy(const DevScene& S, v3 o, v3 d, Count
         if (t < best.t) { best.t = t; best.kind = kind; best.idx = (int32_t)p; best.tx = tx; }
     }
     if (vol_out) *vol_out = pend;
-    else march_pending<false>(S, o, d, pend, best);
+    else march_pending<false, COUNT>(S, o, d, pend, best);
     if (sdf_out) *sdf_out = pend_sdf;
     else sdf_pending<false>(S, o, d, pend_sdf, best);
     if (best.kind == KIND_TRI && tri_best) best.t = t_in;
@@ -990,7 +995,7 @@ __device__ __forceinline__ bool heavy_blocked(const DevScene& S, const DevLight&
         *vol_out = pend;
     } else {
         bool blocked = false;
-        march_pending<true>(S, o, d, pend, best, &blocked);
+        march_pending<true, COUNT>(S, o, d, pend, best, &blocked);
         if (blocked) return true;
     }
     if (sdf_out) {

@@ -420,7 +420,7 @@ __device__ __forceinline__ DevScene stage_vol(const DevScene& S) {
     V.volumes = hv;
     return V;
 }
-template <bool STAGED>
+template <bool STAGED, bool COUNT>
 __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S0, WfQueues Q, int qi) {
     const DevScene S = STAGED ? stage_vol(S0) : S0;
     const uint32_t n = min(Q.counts[kSdfWord], Q.cap);
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S0, 
             d = v3{b.x, b.y, b.z};
         }
         const int32_t kind0 = best.kind;
-        march_coop<false, true>(S, o, d, pend, best, nullptr);
+        march_coop<false, true, COUNT>(S, o, d, pend, best, nullptr);
         if (pend >= 0 && best.idx == pend && (best.kind == KIND_VOLUME || best.kind == KIND_XFORM)) {   // nearer
             const unsigned long long tb = (unsigned long long)__double_as_longlong(best.kind == KIND_XFORM ? best.tx : best.t);
             hit_store(&Q.hits[e.x], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)best.kind, (uint32_t)pend));
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_hits(DevScene S0, 
 }
 // The Volume records split shadow rays deferred: blocked (unlit) when the march's t is nearer than
 // the light; k_wf_sdf_shadow then skips the ray.
-template <bool STAGED>
+template <bool STAGED, bool COUNT>
 __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S0, WfQueues Q, int qo) {
     const DevScene S = STAGED ? stage_vol(S0) : S0;
     const uint32_t n = min(Q.counts[sdf_sh_word(qo)], Q.s_cap);
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(256, PT_VOL_WAVES) void k_wf_vol_shadow(DevScene S0
             d = v3{b.x, b.y, b.z};
         }
         bool blocked = false;
-        march_coop<true, true>(S, o, d, pend, best, &blocked);
+        march_coop<true, true, COUNT>(S, o, d, pend, best, &blocked);
         if (pend >= 0 && blocked) Q.n_lit[qo][e.x] = 0;
     }
 }
@@ -1679,7 +1679,10 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     // the §8f row-4 shapes live) from that result (pt_device.h trace_ana / ana_blocked; routed:
     // trace_heavy / heavy_blocked for the rays that reach a heavy box).  Shadow rays split only when
     // every light's own t is a lean intersect (spheres, cubes, planes).
-    const bool split = plan.lanes < 0 && fullg && S.tri_num_nodes > kLanesMinNodes;
+#ifndef PT_SPLIT_VOL
+#define PT_SPLIT_VOL 0
+#endif
+    const bool split = plan.lanes < 0 && fullg && (S.tri_num_nodes > kLanesMinNodes || (PT_SPLIT_VOL && S.num_vol > 0));
     const bool split_sh = split && S.lights_lean;
     const hipStream_t side = plan.side ? plan.side : stream;
     auto trace = [&](int qi, uint64_t n) {
@@ -1693,10 +1696,14 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_trace_lanes<false, true>), dim3(tl), dim3(kTB), 0, stream, S, Q, qi, B.counters);
                 hipLaunchKernelGGL((k_wf_trace<false, true, true>), dim3(ta), dim3(kTB), 0, stream, S, Q, qi, B.counters);
             }
-            if (Q.volq && S.num_vol > 0 && S.vol_lds > 0)
-                hipLaunchKernelGGL(k_wf_vol_hits<true>, dim3(grid_for(n, 256, 2048)), dim3(256), (size_t)S.vol_lds, stream, S, Q, qi);
-            else if (Q.volq && S.num_vol > 0)
-                hipLaunchKernelGGL(k_wf_vol_hits<false>, dim3(grid_for(n, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
+            if (Q.volq && S.num_vol > 0) {   // the Volume staged in LDS when it fits (S.vol_lds); a counted pass times the march
+                const dim3 vg(grid_for(n, 256, 2048));
+                const size_t vl = (size_t)S.vol_lds;
+                if (vl > 0 && count) hipLaunchKernelGGL((k_wf_vol_hits<true, true>), vg, dim3(256), vl, stream, S, Q, qi);
+                else if (vl > 0) hipLaunchKernelGGL((k_wf_vol_hits<true, false>), vg, dim3(256), vl, stream, S, Q, qi);
+                else if (count) hipLaunchKernelGGL((k_wf_vol_hits<false, true>), vg, dim3(256), 0, stream, S, Q, qi);
+                else hipLaunchKernelGGL((k_wf_vol_hits<false, false>), vg, dim3(256), 0, stream, S, Q, qi);
+            }
             if (S.num_sdf > 0 && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_hits<true>, dim3(grid_for(n, 256, 8192)), dim3(256), (size_t)S.sdf_lds, stream, S, Q, qi);
             else if (S.num_sdf > 0)
@@ -1763,12 +1770,14 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
-            if (Q.volq_sh && S.num_vol > 0 && S.vol_lds > 0)   // (the queues outlive a re-upload of a scene without Volumes)
-                hipLaunchKernelGGL(k_wf_vol_shadow<true>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256),
-                                   (size_t)S.vol_lds, side, S, Q, 1 - qi);
-            else if (Q.volq_sh && S.num_vol > 0)
-                hipLaunchKernelGGL(k_wf_vol_shadow<false>, dim3(grid_for(children * plan.lights_per_child, 256, 2048)), dim3(256), 0,
-                                   side, S, Q, 1 - qi);
+            if (Q.volq_sh && S.num_vol > 0) {   // (the queues outlive a re-upload of a scene without Volumes)
+                const dim3 vg(grid_for(children * plan.lights_per_child, 256, 2048));
+                const size_t vl = (size_t)S.vol_lds;
+                if (vl > 0 && count) hipLaunchKernelGGL((k_wf_vol_shadow<true, true>), vg, dim3(256), vl, side, S, Q, 1 - qi);
+                else if (vl > 0) hipLaunchKernelGGL((k_wf_vol_shadow<true, false>), vg, dim3(256), vl, side, S, Q, 1 - qi);
+                else if (count) hipLaunchKernelGGL((k_wf_vol_shadow<false, true>), vg, dim3(256), 0, side, S, Q, 1 - qi);
+                else hipLaunchKernelGGL((k_wf_vol_shadow<false, false>), vg, dim3(256), 0, side, S, Q, 1 - qi);
+            }
             if (sq && S.sdf_lds > 0)
                 hipLaunchKernelGGL(k_wf_sdf_shadow<true>, dim3(grid_for(children * plan.lights_per_child, 256, 8192)), dim3(256),
                                    (size_t)S.sdf_lds, side, S, Q, 1 - qi);
