@@ -647,10 +647,10 @@ int main(int argc, char** argv) {
     const int W = 1920, H = 1080, kDepth = 4;
     const v3 lights[2] = {v3{0.f, 5.f, 0.f}, v3{4.f, 5.f, 4.f}};
     for (const auto& var : variants) {
-        int W = 0, Q = 0;
-        if (var == "p8" || std::sscanf(var.c_str(), "w%dq%d", &W, &Q) == 2) {   // wide-node model: w8q8, w8q16, w4q0 ...; p8: the library's
-            if (var == "p8") W = 0;
-            run_wide(m, W, Q, stride);
+        int wide = 0, qbits = 0;   // (not W: the image width below)
+        if (var == "p8" || std::sscanf(var.c_str(), "w%dq%d", &wide, &qbits) == 2) {   // wide-node model: w8q8, w8q16, w4q0 ...; p8: the library's
+            if (var == "p8") wide = 0;
+            run_wide(m, wide, qbits, stride);
             continue;
         }
         Tree T;
