@@ -9,10 +9,8 @@ import csv
 import glob
 import sys
 
-KERNELS = ("k_wf_trace_lanes<false, false>", "k_wf_trace<false, false>", "k_wf_shade<false, false, false>", "k_wf_shade<false, false, true>",
-           "k_wf_shadow_lanes<false, false>", "k_wf_shadow<false, false>",
-           # the shade split's vertex and child kernels (A/B builds with -DPT_SHADE_SPLIT=1, round 5)
-           "k_wf_shade<false, false, true, true>", "k_wf_shade<false, false, false, true>", "k_wf_children<false>")
+# every wavefront kernel of the run (the counted pass' instantiations included, under their own names),
+# listed by time; kernels under 1 ms in all are left out
 
 
 def load(d, p):
@@ -21,7 +19,7 @@ def load(d, p):
     dur = collections.defaultdict(dict)
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"].split("(")[0].replace("void pt::", "").replace("pt::", "")
-        if name not in KERNELS:
+        if not name.startswith("k_wf_"):
             continue
         by[name][r["Counter_Name"]] += float(r["Counter_Value"])
         dur[name][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
@@ -33,7 +31,9 @@ label = sys.argv[2] if len(sys.argv) > 2 else d
 p4, t4 = load(d, "p4")
 p5, t5 = load(d, "p5")
 p6, _ = load(d, "p6")
-print(f"# rocprofv3 --pmc passes (kernel-trace only) of `bench.py --steps 2 --warmup 1 --spp 16` (the bench configuration, tools/gpu_evidence.sh), {label}.")
+print(f"# rocprofv3 --pmc passes (kernel-trace only) of one bench command (tools/gpu_evidence.sh: `bench.py --steps 2 --warmup 1 --spp 16`, "
+      f"the bench configuration; tools/gpu_residency.sh: any workload), {label}.")
+KERNELS = [k for k in sorted(t4, key=lambda k: -t4[k]) if t4[k] >= 1e-3]
 print("# SQ_WAVE_CYCLES counts quad-cycles; cycles = GRBM_GUI_ACTIVE / 8 (sum over XCDs). Per-CU ratios divide by 256 CUs.")
 for k in KERNELS:
     if k not in p4 or t4.get(k, 0) <= 0:
