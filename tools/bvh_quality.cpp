@@ -522,7 +522,8 @@ static void build_p8(const Mesh& m, WideTree& T, std::vector<uint32_t>& order, d
     BvhResult b2;
     build_bvh(lo.data(), hi.data(), (int64_t)n, 0, b2, 3, false, std::getenv("BINS") ? std::atoi(std::getenv("BINS")) : 32);
     Bvh8Result b8;
-    collapse_bvh8q(b2, std::getenv("BUDGET8") ? std::atoi(std::getenv("BUDGET8")) : 64, b8);
+    collapse_bvh8q(b2, std::getenv("BUDGET8") ? std::atoi(std::getenv("BUDGET8")) : 64, b8, 1.0,
+                   std::getenv("C_TRI") ? std::atof(std::getenv("C_TRI")) : 0.5);
     build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     stack_need = b8.stack_need;
     T.W = 8;
