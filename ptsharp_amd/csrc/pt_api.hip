@@ -961,7 +961,8 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     // PT_VOL_CELLS_MAX bytes in all; cells_off = -1: the march reads the grid
     std::vector<double> vol_cells;
     std::vector<int64_t> cells_off((size_t)std::max(d->num_volumes, 0), -1);
-    for (int i = 0; i < d->num_volumes; i++) {
+    const char* cells_env = std::getenv("PT_VOL_CELLS");   // "0" at upload: the march reads the grid (tests)
+    for (int i = 0; i < d->num_volumes && !(cells_env && !std::strcmp(cells_env, "0")); i++) {
         const pt_volume& v = d->volumes[i];
         const size_t n = 8 * (size_t)(v.w + 1) * (v.h + 1) * (v.d + 1);
         if ((vol_cells.size() + n) * sizeof(double) > (size_t)PT_VOL_CELLS_MAX) continue;
@@ -1302,7 +1303,8 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     }
     rc = upload(c, vols, &S.volumes); if (rc) return rc;
     S.vol_lds = 0;
-    if (d->num_volumes == 1 && !vol_runs.empty()) {   // k_wf_vol_* stage it in LDS (pt_wavefront.hip stage_vol)
+    const char* lds_env = std::getenv("PT_VOL_LDS");   // "0" at upload: no staging (tests)
+    if (d->num_volumes == 1 && !vol_runs.empty() && !(lds_env && !std::strcmp(lds_env, "0"))) {   // k_wf_vol_* stage it in LDS (pt_wavefront.hip stage_vol)
         const size_t need = pt::kVolLdsHeader + (((size_t)d->volumes[0].num_windows * sizeof(pt::DevWindow) + 15) & ~(size_t)15) +
                             ((vol_runs.size() + 15) & ~(size_t)15);
         if (need <= (size_t)PT_VOL_LDS_MAX) S.vol_lds = (int32_t)need;

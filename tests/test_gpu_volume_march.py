@@ -125,3 +125,22 @@ def test_volume_march_forms_two_volumes(gpu):
     os_ = O.OracleScene(s)
     _, ok = oracle_hits(os_, o, d)
     assert int((ok == _abi.SHAPE_TRANSFORMED).sum()) >= 200
+
+
+def test_march_staging_and_cells_equal_plain_grid(gpu, monkeypatch):
+    """The Volume queue kernels' two layouts of the grid against the plain one: the Volume staged in LDS
+    (stage_vol: header, windows, uniform-cell table) and the corners read cell-major (vol_build_cells), each
+    switched off at upload (PT_VOL_LDS=0, PT_VOL_CELLS=0), must leave the same Buffer bits and ray counts as
+    both on, on the C5-kind mixed scene at test size (the split traversal, the deferred march)."""
+    from parity import render_gpu, same_buffer
+    s, c, smp = scenes.mixed(3000, seed=5)
+    smp.MaxBounces = 3
+    bufs = []
+    for lds, cells in (("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")):
+        monkeypatch.setenv("PT_VOL_LDS", lds)
+        monkeypatch.setenv("PT_VOL_CELLS", cells)
+        bufs.append(render_gpu(s, c, smp, 96, 64, 2, passes=1, seed=41, engine=_abi.ENGINE_WAVEFRONT, adaptive=2))
+    (a, ra) = bufs[0]
+    for b, rb in bufs[1:]:
+        assert ra == rb
+        same_buffer(a, b)
