@@ -1586,16 +1586,42 @@ __device__ __forceinline__ bool entry_pixel(const DevPass& P, const uint32_t* pl
     return x < P.width && y < P.height;
 }
 
+// The order of an extra-phase chunk's samples (ne entries, K samples each): entries in groups of kExtraGroup,
+// a group's slots sample-major (sample j of its w entries, then sample j + 1), the last group w = ne mod
+// kExtraGroup entries wide.  A wave of camera rays is then a few samples of neighbouring pixels (the ray
+// coherence of entry-major slots), and the finalize's lanes read whole runs of a group's accumulators.
+#ifndef PT_EXTRA_GROUP
+#define PT_EXTRA_GROUP 8
+#endif
+constexpr uint32_t kExtraGroup = PT_EXTRA_GROUP;
+static_assert(kExtraGroup >= 1, "kExtraGroup");
+// (slots are < ne · K, a uint32 count; a group's span kExtraGroup · K is taken in 64 bits)
+__device__ __forceinline__ uint32_t extra_slot(uint32_t el, uint32_t j, uint32_t ne, uint32_t K) {
+    const uint32_t b = el / kExtraGroup, w = min(kExtraGroup, ne - b * kExtraGroup);
+    return (uint32_t)((uint64_t)b * kExtraGroup * K) + j * w + (el - b * kExtraGroup);
+}
+__device__ __forceinline__ void extra_entry(uint32_t g, uint32_t ne, uint32_t K, uint32_t& el, uint32_t& j) {
+    const uint64_t span = (uint64_t)kExtraGroup * K;
+    const uint32_t b = (uint32_t)(g / span), w = min(kExtraGroup, ne - b * kExtraGroup);
+    const uint32_t off = (uint32_t)(g - b * span);
+    j = off / w;
+    el = b * kExtraGroup + (off - j * w);
+}
 __global__ __launch_bounds__(256) void k_wf_camera_extra(DevCamera cam, DevPass P, WfQueues Q, uint64_t begin,
                                                          uint32_t count, int32_t K, uint32_t sample_base,
                                                          const uint32_t* plist, int scaled) {
     // Camera samples are dealt to the XCD groups in interleaved 256-slot blocks
-    // (16 pixels' samples): every group gets an even share of sky, floor and mesh.
+    // (one sample of 256 pixels): every group gets an even share of sky, floor and mesh.
+    // Slot g of the chunk is sample j of entry e (extra_slot's order: groups of kExtraGroup entries, sample-major
+    // within a group), and it is the sample's accumulator too, so k_wf_finalize_extra's lanes, one entry each,
+    // read sample j of a group's entries together.
     const Group G = xcd_group();
+    const uint32_t ne = count / (uint32_t)K;
+    const uint64_t e0 = begin / (uint64_t)K;
     for (uint32_t g = (G.g + kParts * G.lb) * 256u + threadIdx.x; g < count; g += kParts * G.nb * 256u) {
-        const uint64_t slot = begin + g;
-        const uint64_t e = slot / (uint64_t)K;
-        const uint32_t j = (uint32_t)(slot % (uint64_t)K);
+        uint32_t el, j;
+        extra_entry(g, ne, (uint32_t)K, el, j);
+        const uint64_t e = e0 + el;
         int x, y;
         if (!entry_pixel(P, plist, e, x, y)) continue;
         const uint64_t pix = (uint64_t)y * (uint64_t)P.width + (uint64_t)x;
@@ -1618,7 +1644,9 @@ __global__ __launch_bounds__(256) void k_wf_camera_extra(DevCamera cam, DevPass 
 
 // One thread per entry: the K samples in order — AddSample each (adaptive), or stop
 // at the first IsFirefly sample (firefly; a pixel that did not stop goes on next_list for
-// the next round).  Clears the entry's accumulators.
+// the next round).  Clears the entry's accumulators (sample j of entry e at extra_slot's place,
+// k_wf_camera_extra).  The pixel's Welford state stays in registers across
+// the K samples (welford's arithmetic, in the same order) and is written once.
 __global__ __launch_bounds__(256) void k_wf_finalize_extra(DevPass P, DevBuffer B, FixAcc acc,
                                                            uint64_t begin_entry, uint32_t entries, int32_t K,
                                                            const uint32_t* plist, int firefly,
@@ -1629,13 +1657,33 @@ __global__ __launch_bounds__(256) void k_wf_finalize_extra(DevPass P, DevBuffer 
         const bool in = entry_pixel(P, plist, begin_entry + e, x, y);
         const size_t pix = (size_t)y * (size_t)P.width + (size_t)x;
         bool stop = !in;
+        int32_t n = 0;
+        double M[3] = {0.0, 0.0, 0.0}, V[3] = {0.0, 0.0, 0.0};
+        if (in) {
+            n = B.n[pix];
+            for (int k = 0; k < 3; k++) { M[k] = B.m[3 * pix + k]; V[k] = B.v[3 * pix + k]; }
+        }
+        const int32_t n0 = n;
         for (int j = 0; j < K; j++) {
             double c[3];
-            fix_take(acc, (size_t)e * (size_t)K + (size_t)j, c);
-            const double r = c[0], g = c[1], b = c[2];
+            fix_take(acc, extra_slot(e, (uint32_t)j, entries, (uint32_t)K), c);
             if (stop) continue;
-            if (firefly && is_firefly(r, g, b, x, y, P.width, P.height, snap, B.m + 3 * pix)) { stop = true; continue; }
-            welford(B, pix, r, g, b);
+            if (firefly && is_firefly(c[0], c[1], c[2], x, y, P.width, P.height, snap, M)) { stop = true; continue; }
+            n++;   // welford (pt_device.h), Buffer.AddSample
+            if (n == 1) {
+                M[0] = c[0]; M[1] = c[1]; M[2] = c[2];
+                continue;
+            }
+            for (int k = 0; k < 3; k++) {
+                const double mo = M[k];
+                const double mn = mo + (c[k] - mo) / (double)n;
+                V[k] = V[k] + (c[k] - mo) * (c[k] - mn);
+                M[k] = mn;
+            }
+        }
+        if (n != n0) {
+            B.n[pix] = n;
+            for (int k = 0; k < 3; k++) { B.m[3 * pix + k] = M[k]; B.v[3 * pix + k] = V[k]; }
         }
         if (next_list && !stop) next_list[atomicAdd(next_count, 1u)] = (uint32_t)pix;
     }
