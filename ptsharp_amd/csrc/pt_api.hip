@@ -208,6 +208,9 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
 #ifndef PT_VOL_CELLS_MAX
 #define PT_VOL_CELLS_MAX (1ull << 30)   // bytes of cell-major Volume corners (8 per cell) a scene may hold; 0: none
 #endif
+#ifndef PT_EXTRA_CHUNK_MAX
+#define PT_EXTRA_CHUNK_MAX (32ull << 20)   // camera samples per chunk of the adaptive / firefly phases, at most
+#endif
 #ifndef PT_VOL_DEFER
 #define PT_VOL_DEFER 1   // split traversal: Volumes deferred to k_wf_vol_hits / k_wf_vol_shadow (0: marched in place)
 #endif
@@ -1472,6 +1475,21 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         if (chunk < cam_samples && chunk >= tile) chunk = chunk / tile * tile;
     }
     if (pass->adaptive_samples < 0 || pass->firefly_samples < 0) return fail(PT_ERR_INVALID_ARG, "negative extra samples");
+    // The adaptive / firefly phases' chunks: as many of their camera samples as the queues may hold (the main
+    // loop's chunk is bounded by its own samples: C5's 1-spp pass at 4K gave the 32-sample adaptive phase 32
+    // chunks of 8.3M), up to PT_EXTRA_CHUNK_MAX samples, whole tiles' worth of entries.
+    uint64_t chunk_extra = chunk;
+    if (extra && !serial) {
+        const uint64_t k = (uint64_t)std::max(pass->adaptive_samples, 1);
+        const uint64_t all = (uint64_t)num_tiles * 1024u * k;
+        uint64_t ce = (uint64_t)std::min<double>((double)std::min<uint64_t>(all, (uint64_t)PT_EXTRA_CHUNK_MAX),
+                                                 std::floor(pmax / per_sample_nee / 256.0) * 256.0 * pt::kParts);
+        const uint64_t step = (uint64_t)pt::deal_run(spp_launch) * 256u * pt::kParts;
+        while (ce > step && group_max(ce) * std::max(1.0, per_sample_nee) > pmax) ce -= step;
+        while (ce > 256 && group_max(ce) * std::max(1.0, per_sample_nee) > pmax) ce -= 256;
+        ce = ce / (1024u * k) * (1024u * k);   // whole tiles of entries
+        if (ce > chunk_extra) chunk_extra = ce;
+    }
     int engine = pass->engine;
     if (engine == PT_ENGINE_AUTO)
         engine = extra || chunk >= 4096 || chunk >= cam_samples ? PT_ENGINE_WAVEFRONT : PT_ENGINE_MEGAKERNEL;
@@ -1508,6 +1526,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     }
     if (engine == PT_ENGINE_WAVEFRONT) {
         plan.chunk = chunk;
+        plan.chunk_extra = chunk_extra;
         // Shadow passes on the side stream, beside the next depth's closest-hit pass, when a
         // chunk's widest depth is small enough for the launches' fill and drain to matter (one
         // rank's 1/8 share of C4 passed one at a time, 33M rays: +6.5 %); a full C4 frame (265M)
@@ -1523,7 +1542,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
             plan.ev_side[0] = c->ev_side[0];
             plan.ev_side[1] = c->ev_side[1];
         }
-        const double group_samples = group_max(chunk);
+        const double group_samples = group_max(chunk_extra);   // (>= chunk's)
         const double need = group_samples * per_sample;   // a partition's widest depth
         const uint32_t pcap = (uint32_t)std::min(pmax, std::max(8192.0, std::max(group_samples, need)));
         const uint32_t spcap = (uint32_t)std::min(pmax, std::max(8192.0, group_samples * per_sample_nee));
@@ -1534,7 +1553,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
             return fail(PT_ERR_UNSUPPORTED, "adaptive samples exceed one wavefront chunk");
         if (serial && (uint64_t)pass->firefly_samples > chunk)
             return fail(PT_ERR_UNSUPPORTED, "firefly samples exceed one wavefront chunk");
-        if (extra && (rc = ensure_extra(c, chunk))) return rc;
+        if (extra && (rc = ensure_extra(c, chunk_extra))) return rc;
     }
     c->last_engine = engine;
     if (c->gathered || (c->loaded && c->comm)) {

@@ -110,6 +110,8 @@ constexpr uint32_t kWfMaxThreads = kWfMaxBlocks * 256;
 
 struct WfPlan {
     uint64_t chunk;            // camera samples per chunk
+    uint64_t chunk_extra;      // camera samples per chunk of the adaptive / firefly phases (>= chunk: their
+                               // queues and per-sample accumulators are sized for it)
     uint32_t root_children;    // ⌊√FH⌋² · modes at depth 0
     uint32_t children;         // modes at depth >= 1 (1, or 2 under SpecularModeAll)
     uint32_t lights_per_child; // shadow-ray slots per diffuse child: 1, or #lights under LightModeAll

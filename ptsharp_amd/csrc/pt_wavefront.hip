@@ -1899,7 +1899,7 @@ hipError_t wavefront_extra(const DevScene& S, const DevCamera& cam, const DevSam
     WfQueues Qx = Q;
     Qx.acc = Q.acc_s;  // per-sample accumulators
     // entries per chunk (whole pixels; smaller extra-phase chunks measured slower)
-    uint64_t per_chunk = plan.chunk / (uint64_t)K;
+    uint64_t per_chunk = std::max(plan.chunk, plan.chunk_extra) / (uint64_t)K;
     if (per_chunk < 1) per_chunk = 1;
     for (uint64_t e0 = 0; e0 < entries; e0 += per_chunk) {
         const uint64_t ne = (entries - e0) < per_chunk ? (entries - e0) : per_chunk;
