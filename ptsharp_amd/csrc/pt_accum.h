@@ -31,14 +31,20 @@ constexpr double kFixWave = 8192.0;                      // |x| < 2^13: |V| < 2^
 constexpr double kFixMagicLo = 4503599627370496.0;       // 2^52: round(y), y ∈ [0, 2^32], is the low mantissa of y + 2^52
 constexpr int kFixWords = 3;                             // words per accumulator in w (hi: its own array, the same stride)
 
-// Accumulators of n pixels (or samples): the low words w [n][3], the high words hi [n][3] (touched
-// only by a carry out of the low word, so the atomics' working set is w alone: 24 B per pixel or
-// sample), big [n][3] fp64.
+// Accumulators of n pixels (or samples), channel-planar: the low words w [3][n], the high words
+// hi [3][n] (touched only by a carry out of the low word, so the atomics' working set is w alone),
+// big [3][n] fp64.  Planar because integer atomics execute at the memory side, one request per
+// 64-B segment a wave instruction touches (MI355X_MICROARCH.md "Global float atomics": 64 rows ≈17×
+// slower than 256 contiguous bytes): a wave adding channel k for 64 consecutive accumulators touches
+// 512 contiguous bytes (8 segments) here, against 24 segments with the three channels interleaved
+// ([n][3], 24 B per accumulator).  `n` is the plane stride.
 struct FixAcc {
     unsigned long long* w;
     unsigned long long* hi;
     double* big;
+    uint64_t n;
 };
+__device__ __forceinline__ size_t fix_at(const FixAcc& A, size_t i, int k) { return (size_t)k * A.n + i; }
 
 __device__ __forceinline__ bool fix_ok(double x) { return fabs(x) < kFixBig; }   // false for NaN too
 
@@ -89,10 +95,10 @@ __device__ __forceinline__ double fixreg_value(const FixReg& a, int k) { return 
 // v (a fixed-point sum, as a signed 64-bit value) into channel k of accumulator i: one
 // returning atomic on the low word; the high word gets the carry (and v's sign extension).
 __device__ __forceinline__ void fix_atomic(const FixAcc& A, size_t i, int k, long long v) {
-    const unsigned long long old = atomicAdd(A.w + kFixWords * i + k, (unsigned long long)v);
+    const unsigned long long old = atomicAdd(A.w + fix_at(A, i, k), (unsigned long long)v);
     const unsigned long long now = old + (unsigned long long)v;
     const long long dh = (v < 0 ? -1 : 0) + (now < old ? 1 : 0);
-    if (dh) atomicAdd(A.hi + kFixWords * i + k, (unsigned long long)dh);
+    if (dh) atomicAdd(A.hi + fix_at(A, i, k), (unsigned long long)dh);
 }
 
 // One lane's term into accumulator i.
@@ -100,7 +106,7 @@ __device__ __forceinline__ void fix_add_lane(const FixAcc& A, size_t i, double r
     const double x[3] = {r, g, b};
     for (int k = 0; k < 3; k++) {
         if (x[k] == 0.0) continue;
-        if (!fix_ok(x[k])) { atomicAdd(A.big + 3 * i + k, x[k]); continue; }
+        if (!fix_ok(x[k])) { atomicAdd(A.big + fix_at(A, i, k), x[k]); continue; }
         fix_atomic(A, i, k, to_fix(x[k]));
     }
 }
@@ -155,7 +161,7 @@ __device__ __forceinline__ uint32_t fix_add_wave(const FixAcc& A, uint32_t idx, 
     if (alone) {   // rare: large (or side-sum) terms, added per lane
         for (int k = 0; k < 3; k++)
             if (x[k] != 0.0 && !(fabs(x[k]) < lim)) {
-                if (!fix_ok(x[k])) atomicAdd(A.big + 3 * (size_t)idx + k, x[k]);
+                if (!fix_ok(x[k])) atomicAdd(A.big + fix_at(A, idx, k), x[k]);
                 else fix_atomic(A, idx, k, to_fix(x[k]));
             }
     }
@@ -191,12 +197,10 @@ __device__ __forceinline__ uint32_t fix_add_wave(const FixAcc& A, uint32_t idx, 
 
 // Value of accumulator i (then cleared for the next pass).
 __device__ __forceinline__ void fix_take(const FixAcc& A, size_t i, double out[3]) {
-    unsigned long long* w = A.w + kFixWords * i;
-    unsigned long long* h = A.hi + kFixWords * i;
-    double* bg = A.big + 3 * i;
     for (int k = 0; k < 3; k++) {
-        out[k] = fix_value((long long)h[k], w[k]) + bg[k];
-        w[k] = 0ull; h[k] = 0ull; bg[k] = 0.0;
+        const size_t j = fix_at(A, i, k);
+        out[k] = fix_value((long long)A.hi[j], A.w[j]) + A.big[j];
+        A.w[j] = 0ull; A.hi[j] = 0ull; A.big[j] = 0.0;
     }
 }
 

@@ -311,6 +311,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     if ((rc = wf_alloc(c, &Q.acc.w, P * pt::kFixWords))) return rc;
     if ((rc = wf_alloc(c, &Q.acc.hi, P * pt::kFixWords))) return rc;
     if ((rc = wf_alloc(c, &Q.acc.big, P * 3))) return rc;
+    Q.acc.n = P;   // channel-planar (pt_accum.h FixAcc)
     PT_HIP(hipMemsetAsync(Q.acc.w, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
     PT_HIP(hipMemsetAsync(Q.acc.hi, 0, P * pt::kFixWords * sizeof(unsigned long long), c->stream));
     PT_HIP(hipMemsetAsync(Q.acc.big, 0, P * 3 * sizeof(double), c->stream));
@@ -353,6 +354,7 @@ int ensure_extra(Ctx* c, uint64_t chunk) {
         return fail(PT_ERR_OUT_OF_MEMORY, "hipMalloc per-sample accumulators");
     }
     c->acc_s_cap = chunk;
+    c->acc_s.n = chunk;
     PT_HIP(hipMemsetAsync(c->acc_s.w, 0, chunk * pt::kFixWords * sizeof(unsigned long long), c->stream));
     PT_HIP(hipMemsetAsync(c->acc_s.hi, 0, chunk * pt::kFixWords * sizeof(unsigned long long), c->stream));
     PT_HIP(hipMemsetAsync(c->acc_s.big, 0, chunk * 3 * sizeof(double), c->stream));
