@@ -1023,11 +1023,8 @@ __device__ inline void tex_bilinear(const DevTexture& T, double u, double v, dou
     c[0] = 0.0; c[1] = 0.0; c[2] = 0.0;
     if (!isfinite(uw) || !isfinite(vh)) return;
     const double X = trunc(uw), x = uw - X, Y = trunc(vh), y = vh - Y;
-    // global-segment loads (the texels live in hipMalloc memory): the generic pointer would make them
-    // flat loads, which also count against LDS's counter and wait on it
-    typedef const __attribute__((address_space(1))) double* gptr;
-    const gptr r0 = (gptr)(T.data + 3 * ((size_t)(int)Y * (size_t)T.w + (size_t)(int)X));
-    const gptr r1 = r0 + 3 * (size_t)T.w;
+    PT_GLOBAL(double) r0 = (PT_GLOBAL(double))(T.data + 3 * ((size_t)(int)Y * (size_t)T.w + (size_t)(int)X));
+    PT_GLOBAL(double) r1 = r0 + 3 * (size_t)T.w;
     const double w00 = (1 - x) * (1 - y), w10 = x * (1 - y), w01 = (1 - x) * y, w11 = x * y;
     for (int k = 0; k < 3; k++) {   // Black.Add(c00·w00).Add(c10·w10).Add(c01·w01).Add(c11·w11)
         double a = 0.0;

@@ -312,7 +312,7 @@ struct alignas(16) VolPair {
 // The eight corners of cell (x0, y0, z0): Volume.Get's values, from the cell-major copy when the cell is on it.
 PT_HD void vol_corners(const DevVolume& v, int x0, int y0, int z0, double c[8]) {
     if (v.cells && x0 >= -1 && y0 >= -1 && z0 >= -1 && x0 < v.w && y0 < v.h && z0 < v.d) {
-        const VolPair* p = reinterpret_cast<const VolPair*>(
+        PT_GLOBAL(VolPair) p = (PT_GLOBAL(VolPair))(
             v.cells + 8 * ((size_t)(x0 + 1) + (size_t)(y0 + 1) * (v.w + 1) + (size_t)(z0 + 1) * (v.w + 1) * (v.h + 1)));
         const VolPair a = p[0], b = p[1], e = p[2], f = p[3];   // four 16-B loads of one half-line
         c[0] = a.lo; c[1] = a.hi; c[2] = b.lo; c[3] = b.hi; c[4] = e.lo; c[5] = e.hi; c[6] = f.lo; c[7] = f.hi;

@@ -18,6 +18,14 @@
 #else
 #define PT_HD inline
 #endif
+// A pointer into hipMalloc memory, as a global-segment pointer in device code: its loads are global_load,
+// not the flat_load the compiler must use for a generic pointer (a flat load also waits on the LDS
+// counter); the plain pointer elsewhere.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_GLOBAL(T) const __attribute__((address_space(1))) T*
+#else
+#define PT_GLOBAL(T) const T*
+#endif
 
 #pragma clang fp contract(off)
 
