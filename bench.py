@@ -106,6 +106,38 @@ def _gloo_gather(r, dist, rank, world, mine):
 GATHER_WATCHDOG_S = 300.0
 
 
+def library_id(path=None):
+    """First 16 hex digits of the product library's SHA-256: bench lines and the stored counter profiles
+    (profiles/pmc_*.json) carry it, so a profile taken on another build is flagged, not silently reused."""
+    import hashlib
+    path = path or os.path.join(ROOT, "ptsharp_amd", "libptsharp_hip.so")
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def scale_block(contexts, gather_ms, elapsed_s):
+    """What an N-GPU line needs to explain itself: every context's rays, device time
+    of its passes (hipEvent) and wall time of its timed passes, the gather's wall time after the
+    last pass, the slowest context and its share of the timed region, and the imbalance (slowest
+    over mean wall).  contexts: [{"rank", "device", "rays", "kernel_ms", "render_ms"}]."""
+    render = [float(c["render_ms"]) for c in contexts]
+    slow = max(range(len(contexts)), key=lambda k: render[k]) if contexts else None
+    mean = sum(render) / len(render) if render else 0.0
+    return {
+        "contexts": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in c.items()} for c in contexts],
+        "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+        "render_ms_max": round(max(render), 3) if render else None,
+        "render_ms_mean": round(mean, 3) if render else None,
+        "slowest_rank": None if slow is None else contexts[slow]["rank"],
+        "slowest_share_of_elapsed": round(render[slow] / (elapsed_s * 1e3), 4) if render and elapsed_s > 0 else None,
+        "imbalance": round(max(render) / mean, 4) if render and mean > 0 else None,
+        "rays_total": int(sum(int(c["rays"]) for c in contexts)),
+    }
+
+
 def _watchdog(seconds, what):
     """Ends the process with status 3 if `what` has not finished within `seconds` (cancel() when it has)."""
     import threading
@@ -410,9 +442,15 @@ def main(argv=None):
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    per = _each(rs, lambda i, x: run_passes(x, a.steps, timed=True))
+
+    def timed_passes(i, x):   # this context's timed passes and their wall time (one host thread each)
+        tc = time.perf_counter()
+        res = run_passes(x, a.steps, timed=True)
+        return res + ((time.perf_counter() - tc) * 1e3,)
+    per = _each(rs, timed_passes)
+    t_rendered = time.perf_counter()
     rays_local = [p[0] for p in per]
-    rays, kernel_ms, kms, klaunch = per[0]   # rank 0's kernels for the roofline
+    rays, kernel_ms, kms, klaunch = per[0][:4]   # rank 0's kernels for the roofline
     gather = None
     if shared:   # no RCCL between ranks on one device: the same tile protocol over gloo
         _gloo_gather(r, dist, rank, world, tiles_for_rank(W, H, rank, world))
@@ -447,9 +485,18 @@ def main(argv=None):
         dog.cancel()
     _each(rs, lambda i, x: x.Synchronize())
     t1 = time.perf_counter()
+    gather_ms = (t1 - t_rendered) * 1e3 if gather else None
     if dist:
         dist.barrier()
     elapsed = t1 - t0
+    mine = [{"rank": rk, "device": dev, "rays": int(p[0]), "kernel_ms": float(p[1]), "render_ms": float(p[4]),
+             "gather_ms": None if gather_ms is None else float(gather_ms)} for rk, dev, p in zip(ranks, devices, per)]
+    if dist:
+        allc = [None] * world
+        dist.all_gather_object(allc, mine)
+        contexts = [c for lst in allc for c in lst]
+    else:
+        contexts = mine
     if dist:
         import torch
         tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -481,6 +528,7 @@ def main(argv=None):
         x.close()
 
     value = total_rays / elapsed / 1e6
+    lib_id = library_id()
     # camera samples traced per pixel per step: the pass' own, then AdaptiveSamples (Renderer.cs:355-372;
     # its second loop only fills pixelVariances, which nothing reads, and is not traced: DESIGN.md §1a)
     cam_spp = a.spp + a.adaptive
@@ -506,13 +554,15 @@ def main(argv=None):
     avg_launch_ms = kms[dom] / max(klaunch[dom], 1)
     achieved_gbs = dom_bytes / (kms[dom] * 1e-3) / 1e9
     rays_per_launch = rays * frac_rays / max(klaunch[dom], 1)
-    traffic = None
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if a.workload == "c4" else f"pmc_traffic_{a.workload}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             tj = json.load(f)
         if tj.get("kernel") == names[dom] and tj.get("workload_tris") == scene.Compile().num_triangles:
             traffic = round(tj["traffic_bytes_per_ray"] * rays_per_launch)
+            traffic_src = {"tag": tj.get("tag"), "library": tj.get("library"),
+                           "same_library": tj.get("library") is not None and tj.get("library") == library_id()}
     # compulsory bytes of one launch: each ray's queue entry (origin, direction: 32 B) read and its
     # hit (16 B) written once, the traversal footprint (BVH nodes + leaf chunks) read once
     compulsory = rays_per_launch * 48 + st.traversal_bytes
@@ -554,12 +604,17 @@ def main(argv=None):
             "bvh_bytes": int(bvh_bytes),
             "kernel_ms_per_step": {names[k]: round(kms[k] / a.steps, 3) for k in range(_abi.K_SLOTS) if klaunch[k]},
         },
+        # per-context rays / device time / wall time and the gather's own time (rank 0's clock for the gather)
+        "scale_detail": scale_block(contexts, gather_ms if mode != "dist" else
+                                    max((c["gather_ms"] or 0.0) for c in contexts) if gather else None, elapsed),
+        "library": lib_id,
         "roofline": {
             "bound": "l2", "kernel": names[dom],
             "achieved": round(achieved_gbs, 2), "peak": L2_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved_gbs / L2_PEAK_GBS, 5), "traffic": traffic,
             "traffic_kind": "L2-fabric bytes per launch (FETCH_SIZE x2 + WRITE_SIZE; Infinity-Cache hits included), "
                             "profiles/pmc_traffic.json, same workload",
+            "traffic_source": traffic_src,
             "compulsory_bytes_per_launch": round(compulsory),
             "traffic_over_compulsory": None if traffic is None else round(traffic / compulsory, 3),
             "traffic_frac_of_hbm_peak": None if traffic is None else
@@ -610,6 +665,13 @@ def main(argv=None):
                     "unit": "T SIMD-cycles/s", "frac": None, "note": f"{pv} missing (tools/gpu_valu_mix.sh)", **extra}
         with open(pv) as f:
             vm = json.load(f)
+        if vm.get("library") != lib_id:
+            # the stored instruction mix was measured on another build: not priced
+            return {"bound": "valu_issue", "kernel": "whole pass", "achieved": None, "peak": VALU_ISSUE_PEAK,
+                    "unit": "T SIMD-cycles/s", "frac": None, **whole_traffic(rays),
+                    "mix_stale": True, "mix_library": vm.get("library"), "library": lib_id,
+                    "note": f"{pv} ({vm.get('tag')}) was measured on library {vm.get('library')}, not this one "
+                            f"({lib_id}): re-run tools/gpu_valu_mix.sh", **extra}
         pr = vm["per_ray"]
         sec = kernel_ms * 1e-3
         achieved = pr["valu_issue_cycles"] * rays / sec / 1e12
@@ -636,7 +698,7 @@ def main(argv=None):
             "issue_model": "cycles per wave64 instruction: 2 (fp32 / int), 4 (fp64 add / mul / fma), 8 (fp32 transcendental), "
                            "16 (fp64 transcendental); peak = 1024 SIMDs x 2.4 GHz",
             "mix_source": f"profiles/pmc_valu_mix_{a.workload}.json ({vm.get('tag')}: SQ_INSTS_VALU and its per-kind "
-                          f"counters, SQ_INSTS_VALU_FLOPS_FP32/FP64, same workload)",
+                          f"counters, SQ_INSTS_VALU_FLOPS_FP32/FP64, same workload, same library {lib_id})",
             "dominant_kernel": dom_k[0], "dominant_kernel_valu_issue_frac_under_counters": dom_k[1]["valu_issue_frac"],
             "pass_valu_issue_frac_under_counters": vm.get("pass_valu_issue_frac_under_counters"),
             **extra,
@@ -654,47 +716,54 @@ def main(argv=None):
         if out["config"].get(k, 0) is None:
             del out["config"][k]
 
-    # ---------------- CPU baseline + parity sample (rank 0, N = 1 only)
+    # ---------------- CPU baseline + parity sample (rank 0, N = 1 only), at the timed configuration: the
+    # full frame at the bench's own spp per pass (one chunk, as each timed step runs it), pass index 1 (the
+    # first timed step's), against the oracle on a strided pixel set sized to ~cpu_seconds of CPU work
     if world == 1 and a.workload == "c4" and (a.cpu_seconds > 0 or not a.no_parity):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         osc = O.OracleScene(scene)
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-        # probe ~2k pixels, then size a strided pixel sample to ~cpu_seconds of CPU work at spp = 1
-        stride = max(1, (W * H) // 2048)
+        spp = a.spp
+        stride = max(1, (W * H) // 512)   # probe ~512 pixels, then size the sample to the budget
         tp = time.perf_counter()
-        _, prays = O.render_pixels(osc, camera, sampler, W, H, 1, 0, W * H, stride, seed=a.seed, pass_index=1,
+        _, prays = O.render_pixels(osc, camera, sampler, W, H, spp, 0, W * H, stride, seed=a.seed, pass_index=1,
                                    threads=threads)
         tp = time.perf_counter() - tp
         budget = max(a.cpu_seconds, 1.0)
         npx = max(64, min(W * H, int(((W * H + stride - 1) // stride) * budget / max(tp, 1e-3))))
         stride = max(1, (W * H) // npx)
         tc = time.perf_counter()
-        obuf, crays = O.render_pixels(osc, camera, sampler, W, H, 1, 0, W * H, stride, seed=a.seed, pass_index=1,
+        obuf, crays = O.render_pixels(osc, camera, sampler, W, H, spp, 0, W * H, stride, seed=a.seed, pass_index=1,
                                       threads=threads)
         tc = time.perf_counter() - tc
         sampled = (W * H + stride - 1) // stride
         out["cpu_baseline"] = {
             "value": round(crays / tc / 1e6, 5), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"oracle/pt_oracle.cpp (k-d tree, recursive sampler, fp64 colour) on {sampled} pixels "
-                      f"(every {stride}th of 1920x1080) x 1 spp, {crays} rays in {tc:.1f}s",
+                      f"(every {stride}th of {W}x{H}) x {spp} spp, pass 1, {crays} rays in {tc:.1f}s",
         }
         out["gpu_vs_cpu"] = round(value / (crays / tc / 1e6), 1)
         if not a.no_parity:
-            # same pixels, same seed and pass index on the GPU at spp = 1
+            # the GPU renders the whole frame at the same spp, seed and pass index: the timed step's chunking
             r.ResetBuffer()
-            r.SamplesPerPixel = 1
+            r.SamplesPerPixel = spp
             r._pass = 0
             r.RenderParallel()
             g = r.ReadBuffer()
             idx = np.arange(0, W * H, stride)
             gm = g.M.reshape(-1, 3)[idx]
             om = obuf.M.reshape(-1, 3)[idx]
+            gn, on = g.N.reshape(-1)[idx], obuf.N.reshape(-1)[idx]
             err = np.abs(gm - om)
             ok = (err <= 1e-3 * np.maximum(1.0, np.abs(om))).all(axis=1).mean()
+            ok9 = (err <= 1e-9 * np.maximum(1.0, np.abs(om))).all(axis=1).mean()
             from parity import psnr8
             out["parity"] = {"vs": "oracle (seeded CPU restatement; C# Random.Shared is unseedable)",
+                             "spp": spp, "pass_index": 1,
+                             "gpu_render": f"full {W}x{H} frame at {spp} spp in one pt_render_pass, as each timed step",
                              "pixels": int(len(idx)), "frac_within_1e-3": round(float(ok), 6),
+                             "frac_within_1e-9": round(float(ok9), 6), "n_equal": bool(np.array_equal(gn, on)),
                              "psnr_db": round(psnr8(gm[None], om[None]), 2), "max_abs_err": float(err.max())}
     r.close()
     line = json.dumps(out)

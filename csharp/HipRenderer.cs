@@ -140,6 +140,7 @@ namespace PTSharpCore
             public fixed double kernel_ms[8];       // PT_K_SLOTS
             public fixed uint kernel_launches[8];
             public ulong traversal_bytes;           // BVH nodes + leaf chunks (what traversal reads)
+            public ulong tail_handoffs;             // shadow refill kernel's tail hand-offs, last pass (ABI 9)
         }
 
         [StructLayout(LayoutKind.Sequential)]

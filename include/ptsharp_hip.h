@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 8
+#define PT_ABI_VERSION 9
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -310,6 +310,8 @@ typedef struct pt_stats {
     double kernel_ms[PT_K_SLOTS];     /* last pass, device time per pt_kernel_class (flag PT_PASS_KERNEL_TIMING) */
     uint32_t kernel_launches[PT_K_SLOTS];
     uint64_t traversal_bytes; /* of bvh_bytes: BVH nodes + leaf chunks, what the traversal kernels read */
+    uint64_t tail_handoffs;   /* last pass (ABI 9): stack entries the shadow refill kernel's idle lanes took from
+                               * busy lanes' rays in its tail (k_wf_shadow_lanes helpers; wavefront engine) */
 } pt_stats;
 
 int pt_get_version(void);

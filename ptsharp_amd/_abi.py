@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptsharp_hip.so")
 
-ABI_VERSION = 8   # PT_ABI_VERSION
+ABI_VERSION = 9   # PT_ABI_VERSION
 PT_OK = 0
 PT_ERR_INVALID_ARG = -1
 PT_ERR_HIP = -2
@@ -119,7 +119,7 @@ class pt_stats(C.Structure):
                 ("total_ms", C.c_double), ("bvh_nodes", C.c_uint64), ("bvh_bytes", C.c_uint64),
                 ("build_ms", C.c_double), ("passes", C.c_uint64), ("shadow_rays", C.c_uint64),
                 ("kernel_ms", C.c_double * K_SLOTS), ("kernel_launches", C.c_uint32 * K_SLOTS),
-                ("traversal_bytes", C.c_uint64)]
+                ("traversal_bytes", C.c_uint64), ("tail_handoffs", C.c_uint64)]
 
 
 class pt_trace_counters(C.Structure):

@@ -133,9 +133,16 @@ struct LdsFix {
 __device__ __forceinline__ bool lds_fix_add(const LdsFix& T, uint32_t idx, const long long v[3]) {
     // the index itself (linear probing): the flush walks the table in slot order, so neighbouring
     // accumulators' atomics leave in one wave instruction (8-B lanes on few 64-B segments; a
-    // multiplicative hash scattered them, one segment per lane: C5 nee_accum 115 -> 88 ms, r05nee)
+    // multiplicative hash scattered them, one segment per lane: C5 nee_accum 115 -> 88 ms, r05nee).
+    // Each 512-index block is shifted by 8 slots per block: pixels a row apart differ by W,
+    // and with idx alone rows 4 apart collided at W = 1920, 2 apart at 3840, every row at a power-of-two
+    // width; runs of one row stay contiguous.
+#ifndef PT_ACC_ROWSHIFT
+#define PT_ACC_ROWSHIFT 1   // 0: the index alone (round 5; A/B builds)
+#endif
+    const uint32_t home = PT_ACC_ROWSHIFT ? idx + (idx >> 9) * 8u : idx;
     for (uint32_t p = 0; p < 8u; p++) {
-        const uint32_t sl = (idx + p) & T.mask;
+        const uint32_t sl = (home + p) & T.mask;
         const uint32_t k = atomicCAS(T.key + sl, kLdsFree, idx);
         if (k == kLdsFree || k == idx) {
             for (int c = 0; c < 3; c++)

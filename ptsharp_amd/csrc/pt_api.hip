@@ -134,6 +134,7 @@ struct EventTimer : pt::LaunchTimer {
     void destroy() { for (auto e : pool) (void)hipEventDestroy(e); pool.clear(); }
 };
 
+struct TriBvhBuild;
 struct Ctx {
     int device = 0;
     int width = 0, height = 0;
@@ -188,6 +189,8 @@ struct Ctx {
     pt::WfPlan grids{};            // persistent grid sizes (pt::wavefront_grids), once per context
     EventTimer timer;
     double tri_build_ms = 0;       // last upload: host time to build (or wait for, or find) the triangle BVH
+    std::shared_ptr<const TriBvhBuild> tri_build;   // that build, shared with the other contexts of its geometry
+                                                    // (released at the next upload and at pt_destroy)
 };
 
 // Queue capacity bound (entries per queue).  A pass is rendered in chunks of camera
@@ -456,6 +459,14 @@ TriBvhCache& tri_bvh_cache() {
     static TriBvhCache c;
     return c;
 }
+// A finished build that no context holds (only the cache's own reference): evictable.  Builds held by live
+// contexts and builds in progress are never evicted, so neither a host-only pt_scene_bvh_digest nor another
+// scene's upload can push out the build a context of this process would reuse.
+bool tri_bvh_evictable(const std::shared_future<std::shared_ptr<const TriBvhBuild>>& f) {
+    if (f.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return false;
+    return f.get().use_count() <= 1;
+}
+constexpr size_t kTriBvhSpare = 2;   // unreferenced finished builds kept for a later upload of the same geometry
 TriBvhKey tri_bvh_key(const pt_scene_desc* d, const std::vector<int32_t>& tri_src) {
     TriBvhKey k;
     k.n = (uint64_t)tri_src.size() ^ ((uint64_t)kTriBins << 40) ^ ((uint64_t)(kTriCost * 1024) << 52);
@@ -561,7 +572,17 @@ std::shared_ptr<const TriBvhBuild> tri_bvh_shared(const pt_scene_desc* d, const 
         } else {
             C.builds++;
             C.entries.emplace_back(key, mine.get_future().share());
-            while (C.entries.size() > 2) C.entries.erase(C.entries.begin());
+            // oldest first, only the evictable ones, down to kTriBvhSpare of them
+            size_t spare = 0;
+            for (auto& e : C.entries) spare += tri_bvh_evictable(e.second) ? 1 : 0;
+            for (size_t i = 0; i < C.entries.size() && spare > kTriBvhSpare;) {
+                if (tri_bvh_evictable(C.entries[i].second)) {
+                    C.entries.erase(C.entries.begin() + (long)i);
+                    spare--;
+                } else {
+                    i++;
+                }
+            }
         }
     }
     if (theirs.valid()) {
@@ -577,6 +598,23 @@ std::shared_ptr<const TriBvhBuild> tri_bvh_shared(const pt_scene_desc* d, const 
             if (C.entries[i].first == key) { C.entries.erase(C.entries.begin() + (long)i); break; }
     }
     return r;
+}
+
+// A context lets go of its build (next upload, pt_destroy): the last context of a geometry takes its cache entry
+// along, so the host memory (tens of MB at 1M triangles) lives as long as a context uses it.
+void tri_bvh_release(Ctx* c) {
+    if (!c->tri_build) return;
+    TriBvhCache& C = tri_bvh_cache();
+    std::lock_guard<std::mutex> lk(C.mu);
+    for (size_t i = 0; i < C.entries.size(); i++) {
+        auto& f = C.entries[i].second;
+        if (f.wait_for(std::chrono::seconds(0)) == std::future_status::ready && f.get() == c->tri_build &&
+            f.get().use_count() <= 2) {   // the cache's reference and this context's
+            C.entries.erase(C.entries.begin() + (long)i);
+            break;
+        }
+    }
+    c->tri_build.reset();
 }
 
 // Box of a light shape as Box.Center / Box.OuterRadius compute it (Box.cs:316-324).
@@ -1114,6 +1152,8 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     const size_t nt = tri_src.size();
     const auto tbuild_t0 = std::chrono::steady_clock::now();
     const std::shared_ptr<const TriBvhBuild> tbv = tri_bvh_shared(d, tri_src);
+    tri_bvh_release(c);   // the previous upload's build
+    if (tbv->rc == PT_OK) c->tri_build = tbv;
     c->tri_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tbuild_t0).count();
     if (tbv->rc != PT_OK) return fail(tbv->rc, tbv->err);
     std::vector<float4> tri_recs(nt * 3), tri_shade(nt * 3);
@@ -1505,7 +1545,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         const int32_t step = (sub > 1 && engine == PT_ENGINE_WAVEFRONT) ? sub : 1;
         pt_pass_params one = *pass;
         pt_stats sum = c->stats;
-        uint64_t rays = 0, shadow = 0;
+        uint64_t rays = 0, shadow = 0, handoffs = 0;
         double ms = 0.0;
         for (int32_t k = 0; k < batch; k += step) {
             one.pass_index = pass->pass_index + (uint32_t)k;
@@ -1513,6 +1553,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
             if (int rc = render_pass_impl(c, camera, sampler, &one, nullptr)) return rc;
             rays += c->stats.rays;
             shadow += c->stats.shadow_rays;
+            handoffs += c->stats.tail_handoffs;
             ms += c->stats.last_pass_ms;
             for (int j = 0; j < PT_K_SLOTS; j++) {
                 sum.kernel_ms[j] = (k ? sum.kernel_ms[j] : 0.0) + c->stats.kernel_ms[j];
@@ -1523,6 +1564,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         std::memcpy(c->stats.kernel_launches, sum.kernel_launches, sizeof sum.kernel_launches);
         c->stats.rays = rays;
         c->stats.shadow_rays = shadow;
+        c->stats.tail_handoffs = handoffs;
         c->stats.last_pass_ms = ms;
         return PT_OK;
     }
@@ -1587,6 +1629,10 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     PT_HIP(hipEventRecord(c->ev0, c->stream));
     if (engine == PT_ENGINE_WAVEFRONT) {
         pt::LaunchTimer* tm = timing ? &c->timer : nullptr;
+        // PT_SHADOW_TAIL=early (environment; tests): k_wf_shadow_lanes hands stack entries to idle lanes from
+        // the first claim on, so the tail protocol runs all pass long (pt_stats.tail_handoffs counts it)
+        const char* tail_env = std::getenv("PT_SHADOW_TAIL");
+        c->Q.tail_early = (tail_env && !std::strcmp(tail_env, "early")) ? 1 : 0;
         PT_HIP(pt::wavefront_pass(c->S, cam, smp, P, B, c->Q, plan, counted != nullptr, c->stream, tm));
         if (serial) {
             // Renderer.Render (Renderer.cs:80-198): after a pixel's main samples, AdaptiveSamples
@@ -1657,6 +1703,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     const uint64_t rays = ctr[0] + ctr[4];
     c->stats.rays = rays;
     c->stats.shadow_rays = ctr[4];
+    c->stats.tail_handoffs = engine == PT_ENGINE_WAVEFRONT ? ctr[11] : 0;
     c->stats.rays_total += rays;
     c->stats.last_pass_ms = ms;
     c->stats.total_ms += ms;
@@ -1865,6 +1912,7 @@ void pt_destroy(void* ctx) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    tri_bvh_release(c);
     free_scene(c);
     free_wavefront(c);
     if (c->d_m) (void)hipFree(c->d_m);

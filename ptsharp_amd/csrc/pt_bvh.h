@@ -94,7 +94,7 @@ void collapse_bvh4_sah(const BvhResult& bvh2, int stack_budget, Bvh4Result& out,
 //           k's ref is [5] + k: bit 31 and the chunk index; the chunk's word 0 holds its triangle count)
 //   [6]     2 bits per slot: a leaf slot's triangle count - 1 (host checks)
 //   [7]     0
-//   [8..31] the child bounds as binary16 integers q (0..2048, exact in binary16), SoA: lo.x[8] hi.x[8]
+//   [8..31] the child bounds as binary16 integers q (0..kQMax = 2047, exact in binary16; pt_bvh.cpp), SoA: lo.x[8] hi.x[8]
 //           lo.y[8] hi.y[8] lo.z[8] hi.z[8]; bound = origin + q·step, a superset of the child's box;
 //           an empty slot has lo = +inf, hi = -inf.
 // A traversal computes a slab distance as fma(q, step/d, (origin - o)/d).

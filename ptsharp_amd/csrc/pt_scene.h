@@ -166,8 +166,10 @@ struct DevBuffer {
     unsigned long long* counters;  // [0..2] closest-hit rays/nodes/prims, [3] shading fetches, [4..6] shadow
                                    // rays/nodes/prims, [7] lit shadow rays, [8] their accumulation runs,
                                    // [9] volume samples, [10] SDF evaluations (DevScene::march),
-                                   // [15] wavefront queue overflow flag, [16..23] the Volume march's phase
-                                   // clocks (counted passes, pt_device.h coop_vol_t)
+                                   // [11] shadow-ray tail hand-offs (k_wf_shadow_lanes helpers, uncounted
+                                   // passes), [15] wavefront queue overflow flag; counted passes also hold
+                                   // the Volume march's phase clocks from word kMarchClockWord on, kMarchSlots
+                                   // slots of 8 words (pt_device.h coop_vol_t)
 };
 
 }  // namespace pt

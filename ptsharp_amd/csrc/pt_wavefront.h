@@ -56,6 +56,10 @@ struct WfQueues {
     uint32_t* ovf;       // closest-hit traversal stack entries beyond kLdsStack: [kStackMax - kLdsStack][kWfMaxThreads]
     uint32_t* ovf_sh;    // the same for the shadow kernels, which may run beside a closest-hit kernel (side stream)
     FixAcc acc_s;        // [chunk] per-sample accumulators of the adaptive / firefly phases
+    // k_wf_shadow_lanes' tail (helper hand-off): 0 as in a render, from the queue's drain on; 1 (PT_SHADOW_TAIL=early,
+    // tests) a wave refills only when all its lanes are idle and its idle lanes help from the first claim on, so
+    // the hand-off protocol runs throughout the pass instead of in each wave's last rays
+    int32_t tail_early;
 };
 
 // Every counter sits on a line of its own: returning atomics execute at the memory side,

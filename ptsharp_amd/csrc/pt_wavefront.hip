@@ -1240,7 +1240,11 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // subtrees (any-hit: the ray is blocked iff some subtree holds a blocker, in any order).
 // s_help[root]: helpers still running on root's ray, bit 31 = blocked.  A root that ends its own
 // traversal waits for its helpers before it reports the ray lit.
-template <bool COUNT, bool SPLIT = false>
+// EARLY (Q.tail_early, tests; its own instantiation: a runtime flag cost the render kernel 22 SGPR spills): a
+// wave refills only when every lane is idle — then no helper and no waiting root is
+// left, so the refill may reset s_help — and hands stack entries to idle lanes from its first claim on.
+// Uncounted passes add the hand-offs to counters[11].
+template <bool COUNT, bool SPLIT = false, bool EARLY = false>
 __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters) {
     constexpr bool split = SPLIT;
     __shared__ uint32_t s_stack[kLdsStack * kTB];
@@ -1262,10 +1266,14 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     bool waiting = false;   // a root whose traversal is done, waiting for its tail helpers
     __shared__ uint32_t s_help[kTB];
     __shared__ uint32_t s_map[kTB];   // per wave: donor lane by rank
+    __shared__ uint32_t s_handoffs[kTB / 64];   // per wave: tail hand-offs
+    if (lane == 0) s_handoffs[threadIdx.x >> 6] = 0u;
     bool helper = false;
     uint32_t root = threadIdx.x;
     const uint32_t wbase = threadIdx.x & ~63u;
     const bool route = split && S.route;   // routed split: lit rays that reach a heavy box go on (hq_sh)
+    constexpr bool early = EARLY && !COUNT;
+    constexpr uint32_t refill_at = early ? 64u : (uint32_t)PT_SHADOW_REFILL_IDLE;
     bool hpend = false;
     // a root ray found nothing nearer than its light: lit (a phantom light never is); under the routed
     // split, provisionally when the ray reaches a heavy box (the FULL half decides: k_wf_shadow<.., SPLIT>)
@@ -1292,7 +1300,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
         }
         const uint64_t idle = __ballot(!has);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (more && (nidle >= PT_SHADOW_REFILL_IDLE || nidle == 64u)) {   // wave-uniform
+        if (more && (nidle >= refill_at || nidle == 64u)) {   // wave-uniform
             uint32_t kc = 0;
             if (lane == 0) kc = atomicAdd(cursor, nidle);
             kc = __builtin_amdgcn_readfirstlane(kc);   // every lane is active here: lane 0's claim, in an SGPR
@@ -1300,6 +1308,11 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
             if (kc + nidle >= n) more = false;
             if (!has && k < n) {
                 i = base + k;
+                if (early) {   // a former helper is a root again (without EARLY no lane refills after the tail began)
+                    root = threadIdx.x;
+                    helper = false;
+                    waiting = false;
+                }
                 const float4 b = nt_load(&Q.n_n[qo][i]);
                 const float4 a = nt_load(&Q.n_o[qo][i]);
                 const uint32_t li = __float_as_uint(b.w);
@@ -1348,7 +1361,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
             }
         }
         if (!more && __ballot(has || hpend) == 0ull) break;   // (a ray finished at refill may wait for the append)
-        if (!COUNT && !more) {   // wave-uniform: the tail (not in the counting pass: its node counts stay sequential)
+        if (!COUNT && (!more || early)) {   // wave-uniform: the tail (not in the counting pass: its node counts stay sequential)
             if (has) {
                 const uint32_t st = s_help[root];
                 if (st & 0x80000000u) {   // a helper found a blocker: the root ends unlit, its helpers stop
@@ -1373,6 +1386,8 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                 __builtin_amdgcn_s_waitcnt(0xC07F);
                 __builtin_amdgcn_wave_barrier();
                 const bool take = !has && ri < nd;
+                if (lane == 0) s_handoffs[threadIdx.x >> 6] += nd;   // (to counters[11] at the end: the pointer
+                                                                     // live in the loop cost 26 SGPR spills)
                 const int src = take ? (int)s_map[wbase + ri] : (int)lane;
                 const float ox = __shfl(o.x, src, 64), oy = __shfl(o.y, src, 64), oz = __shfl(o.z, src, 64);
                 const float dx = __shfl(d.x, src, 64), dy = __shfl(d.y, src, 64), dz = __shfl(d.z, src, 64);
@@ -1450,7 +1465,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
             if (helper) atomicOr(&s_help[root], 0x80000000u);
             else {
                 Q.n_lit[qo][i] = 0;
-                if (!more) atomicOr(&s_help[root], 0x80000000u);   // its helpers stop
+                if (!more || early) atomicOr(&s_help[root], 0x80000000u);   // its helpers stop
             }
         } else if (pop) {
             if (sp > 0) {
@@ -1472,6 +1487,8 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     }
     uint32_t rays = wave_sum(ctr.rays);
     if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
+    if (!COUNT && lane == 0 && s_handoffs[threadIdx.x >> 6])
+        atomicAdd(&counters[11], (unsigned long long)s_handoffs[threadIdx.x >> 6]);
     if (COUNT) {
         uint32_t nodes = wave_sum(ctr.nodes), prims = wave_sum(ctr.prims);
         if (lane == 0) {
@@ -1480,9 +1497,9 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
         }
     }
 }
-template <bool COUNT, bool SPLIT = false>
+template <bool COUNT, bool SPLIT = false, bool EARLY = false>
 __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
-    shadow_lanes<COUNT, SPLIT>(S, Q, qo, counters);
+    shadow_lanes<COUNT, SPLIT, EARLY>(S, Q, qo, counters);
 }
 
 // ---------------------------------------------------------------- direct-light terms
@@ -1817,7 +1834,8 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
                 hipLaunchKernelGGL((k_wf_shadow_lanes<true, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<true, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             } else {
-                hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+                if (Q.tail_early) hipLaunchKernelGGL((k_wf_shadow_lanes<false, true, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+                else hipLaunchKernelGGL((k_wf_shadow_lanes<false, true>), dim3(hl), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
                 hipLaunchKernelGGL((k_wf_shadow<false, true, true>), dim3(ha), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
             }
             if (Q.volq_sh && S.num_vol > 0) {   // (the queues outlive a re-upload of a scene without Volumes)
@@ -1837,6 +1855,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
         } else if (count && fullg) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (lanes && Q.tail_early) hipLaunchKernelGGL((k_wf_shadow_lanes<false, false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (lanes) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);

@@ -88,3 +88,18 @@ def test_c5_mixed_4k_tiles_adaptive32(gpu):
                                 engine=_abi.ENGINE_WAVEFRONT, adaptive=32)
     assert (g.N[g.N > 0] == 33).all() and (g.N > 0).sum() == len(tiles) * 1024
     check(g, gr, o, orr)
+
+
+def test_c4_mesh1m_16spp_one_full_chunk(gpu, monkeypatch):
+    """C4 at the bench's own pass: 16 spp per RenderParallel on the 1M-triangle frame, as ONE queue chunk
+    whose widest depth fills the queues to their cap (the timed full frame is one 33.2M-sample chunk in
+    2^28-entry queues, 99 % full).  Here 16 tiles × 1024 pixels × 16 spp = 262,144 camera samples with
+    PT_WF_MAX_CAP = 2^21 entries: 8 first-bounce children per sample fill each partition's 2^18 entries
+    exactly.  Against the oracle at 16 spp, pass index 1."""
+    monkeypatch.setenv("PT_WF_MAX_CAP", str(1 << 21))
+    s, c, smp = scenes.bunny_frame(1_000_000)
+    tiles = tiles_for_rank(1920, 1080, 3, 128)
+    g, gr, o, orr = render_both(s, c, smp, 1920, 1080, spp=16, passes=1, seed=1234, tiles=tiles,
+                                engine=_abi.ENGINE_WAVEFRONT)
+    assert (g.N > 0).sum() == 16 * 1024
+    check(g, gr, o, orr)

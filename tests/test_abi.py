@@ -48,7 +48,7 @@ def test_struct_layouts_match_header():
     assert C.sizeof(_abi.pt_camera) == 12 * 4 + 3 * 8
     assert C.sizeof(_abi.pt_sampler) == 24
     assert C.sizeof(_abi.pt_pass_params) == 4 + 4 + 8 + 4 + 4 + 8 + 8 + 8 + 4 + 4   # passes, tail padding
-    assert C.sizeof(_abi.pt_stats) == 9 * 8 + 8 * 8 + 8 * 4 + 8
+    assert C.sizeof(_abi.pt_stats) == 9 * 8 + 8 * 8 + 8 * 4 + 8 + 8   # + tail_handoffs (ABI 9)
     assert C.sizeof(_abi.pt_trace_counters) == 88 + 8 * 8   # + march_clock[8] (ABI 8)
     assert _abi.pt_scene_desc.env_color.offset % 8 == 0
 

@@ -65,3 +65,28 @@ def test_group_refuses_more_gpus_than_devices():
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 2
     assert "HIP device" in p.stderr
+
+
+def test_scale_block_keys():
+    """The per-context record of an N-GPU line (`scale_detail`): each context's rays, device and wall
+    time, the gather's time, the slowest context and its share, the imbalance (VERDICT r05 #5)."""
+    ctx = [{"rank": 0, "device": 0, "rays": 100, "kernel_ms": 9.0, "render_ms": 10.0, "gather_ms": 1.5},
+           {"rank": 1, "device": 1, "rays": 120, "kernel_ms": 11.0, "render_ms": 12.0, "gather_ms": 1.5}]
+    b = bench.scale_block(ctx, 1.5, 0.0135)
+    for k in ("contexts", "gather_ms", "render_ms_max", "render_ms_mean", "slowest_rank",
+              "slowest_share_of_elapsed", "imbalance", "rays_total"):
+        assert k in b
+    assert b["slowest_rank"] == 1 and b["rays_total"] == 220 and b["gather_ms"] == 1.5
+    assert b["imbalance"] == round(12.0 / 11.0, 4)
+    assert b["slowest_share_of_elapsed"] == round(12.0 / 13.5, 4)
+    assert [c["rank"] for c in b["contexts"]] == [0, 1]
+    one = bench.scale_block(ctx[:1], None, 0.011)
+    assert one["gather_ms"] is None and one["imbalance"] == 1.0
+
+
+def test_library_id_matches_file():
+    import hashlib
+    p = os.path.join(ROOT, "ptsharp_amd", "libptsharp_hip.so")
+    if not os.path.exists(p):
+        pytest.skip("library not built")
+    assert bench.library_id() == hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]

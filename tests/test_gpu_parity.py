@@ -388,3 +388,51 @@ def test_pass_batch_fallbacks(gpu, case):
     else:
         kw = {"FireflySamples": 3}
     _batched_vs_separate(s, c, smp, 64, 48, spp, 3, engine=engine, **kw)
+
+
+def _render_stats(s, c, smp, w, h, spp, seed, tiles=None):
+    """One wavefront RenderParallel: (Buffer copy, rays, tail hand-offs of the pass)."""
+    from ptsharp_amd import Renderer
+    from ptsharp_amd.renderer import Buffer
+    r = Renderer.NewRenderer(s, c, smp, w, h, True, device=0)
+    try:
+        r.SamplesPerPixel, r.Seed, r.Tiles, r.Engine = spp, seed, tiles, _abi.ENGINE_WAVEFRONT
+        r.RenderParallel()
+        st = r.Stats()
+        b = r.ReadBuffer()
+        out = Buffer(w, h)
+        out.M, out.V, out.N = b.M.copy(), b.V.copy(), b.N.copy()
+        return out, int(st.rays), int(st.tail_handoffs)
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("name", ["mesh1m", "mixed4k"])
+def test_shadow_tail_handoffs_forced(gpu, monkeypatch, name):
+    """The shadow refill kernel's tail (idle lanes take stack entries of busy lanes' rays) forced to run
+    all pass long (PT_SHADOW_TAIL=early: a wave refills only when every lane is idle and hands off from
+    its first claim on).  mixed4k is the routed split (C5's 1M-triangle mesh + SDF + Volume at 4K, the
+    scene where round 4's helper read the borrowed ray for the heavy-box test): the hand-off count is
+    non-zero, and the Buffer equals the default tail's and the lockstep kernels' (PT_LANES=0) bit for
+    bit and the oracle's within the parity bar.  mesh1m: the lean instantiation on the C4 frame."""
+    if name == "mixed4k":
+        s, c, smp = scenes.mixed(1_000_000)
+        w, h, tiles = 3840, 2160, tiles_for_rank(3840, 2160, 5, 1024)
+    else:
+        s, c, smp = scenes.bunny_frame(1_000_000)
+        w, h, tiles = 1920, 1080, tiles_for_rank(1920, 1080, 9, 256)
+    monkeypatch.setenv("PT_SHADOW_TAIL", "early")
+    e, re_, he = _render_stats(s, c, smp, w, h, 2, 4242, tiles)
+    assert he > 0, "the forced tail handed nothing off"
+    monkeypatch.delenv("PT_SHADOW_TAIL")
+    d, rd, hd = _render_stats(s, c, smp, w, h, 2, 4242, tiles)
+    assert re_ == rd
+    same_buffer(e, d)
+    if name == "mixed4k":
+        monkeypatch.setenv("PT_LANES", "0")
+        l, rl, _ = _render_stats(s, c, smp, w, h, 2, 4242, tiles)
+        monkeypatch.delenv("PT_LANES")
+        assert rl == re_
+        same_buffer(e, l)
+        o, orr = O.render(O.OracleScene(s), c, smp, w, h, 2, passes=1, seed=4242, tiles=tiles)
+        check(e, re_, o, orr)

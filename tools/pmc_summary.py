@@ -34,7 +34,7 @@ rays_per_step = bench["value"] * 1e6 * bench["ms_per_step"] / 1e3
 kind_frac = (1 - cfg["shadow_ray_fraction"]) if "trace" in kernel else (cfg["shadow_ray_fraction"] if "shadow" in kernel else 1.0)
 rays_in_kernel = rays_per_step * kind_frac * (bench["steps"] + bench["warmup"])
 out = {
-    "kernel": kernel, "workload_tris": cfg["triangles"], "source": src, "tag": tag,
+    "kernel": kernel, "workload_tris": cfg["triangles"], "source": src, "tag": tag, "library": bench.get("library"),
     "fetch_kb": fetch, "write_kb": write, "launches": [nf, nw],
     "traffic_bytes_total": (2 * fetch + write) * 1024,
     "traffic_bytes_per_ray": (2 * fetch + write) * 1024 / rays_in_kernel,

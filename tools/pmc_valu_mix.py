@@ -82,6 +82,7 @@ for w in wls:
     lanes = 64 if (cal64 or cal32 or 64) < 8 else 1   # counters per wave-instruction -> per lane
     out = {
         "tag": tag, "source": src, "workload": w, "bench_line": f"{src}/bench_{w}.json",
+        "library": bench.get("library"),   # bench.py flags the mix when the library it prices differs
         "rays_per_pass": rays_per_pass, "passes_profiled": passes, "rays_profiled": rays,
         "issue_cycles_model": ISSUE,
         "flops_per_counted_op": {"fp32": cal32, "fp64": cal64}, "flop_counter_lane_factor": lanes,

@@ -25,7 +25,7 @@ bench = json.load(open(os.path.join(src, f"bench_{wl}_fetch.json")))
 rays_per_pass = bench["value"] * 1e6 * bench["ms_per_step"] * 1e-3
 passes = bench["warmup"] + 1 + bench["steps"]   # warm-up, the counted pass, the timed steps
 out = {
-    "workload": wl, "tag": tag, "source": src,
+    "workload": wl, "tag": tag, "source": src, "library": bench.get("library"),
     "fetch_kb": fetch_kb, "write_kb": write_kb,
     "traffic_bytes_total": (2 * fetch_kb + write_kb) * 1024,
     "passes": passes, "rays_per_pass": round(rays_per_pass),
