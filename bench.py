@@ -725,7 +725,7 @@ def main(argv=None):
         osc = O.OracleScene(scene)
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
         spp = a.spp
-        stride = max(1, (W * H) // 512)   # probe ~512 pixels, then size the sample to the budget
+        stride = max(1, (W * H) // 2048)   # probe ~2048 pixels (~3 s), then size the sample to the budget
         tp = time.perf_counter()
         _, prays = O.render_pixels(osc, camera, sampler, W, H, spp, 0, W * H, stride, seed=a.seed, pass_index=1,
                                    threads=threads)

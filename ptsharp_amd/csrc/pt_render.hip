@@ -25,12 +25,11 @@
 namespace pt {
 
 constexpr int kBlock = 256;
-// The megakernel's per-lane traversal stack: the first kMegaLds entries in LDS (a column per lane), the rest
-// of kStackMax in the lane's scratch.  kStackMax grew to 64 with the 8-wide BVH (it bounds the collapse), but
-// the deepest stack the CPU model saw on C4 is 17 entries: all 64 in LDS would take 64 KiB per 256-thread
-// block, 2 blocks per CU.  24 entries: 24 KiB per block.
-constexpr int kMegaLds = 24;
-using MStack = SpillStack<kBlock, kMegaLds>;
+// The megakernel's per-lane traversal stack: all kStackMax entries in LDS (64 KiB per 256-thread block).  The
+// deepest stack the CPU model saw on C4 is 17 entries, but 24 entries in LDS and the rest in the lane's scratch
+// ran 3 % slower (C4 960x540, 1 spp: 589 -> 571 Mrays/s, gpurun_out/r06a/mega.txt): the kernel's registers,
+// not its LDS, bound its occupancy, and the scratch column cost the difference.
+using MStack = LdsStack<kBlock>;
 constexpr int kMaxFrames = 34;   // MaxBounces <= 32 under SpecularModeAll (checked on the host)
 
 // Sampler.sampleLight (Sampler.cs:212-296): the megakernel keeps the reference's
@@ -206,9 +205,8 @@ __device__ void sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3 d
 template <bool COUNT, bool FULL>
 __global__ __launch_bounds__(kBlock) void k_render_pass(DevScene S, DevCamera cam, DevSampler smp, DevPass P,
                                                         DevBuffer B) {
-    __shared__ uint32_t s_stack[kMegaLds * kBlock];
-    uint32_t deep[kStackMax - kMegaLds];   // scratch
-    const MStack stack{s_stack + threadIdx.x, deep, 1u};
+    __shared__ uint32_t s_stack[kStackMax * kBlock];
+    const MStack stack{s_stack + threadIdx.x};
     const int tile_slot = blockIdx.x >> 2;
     const int quarter = blockIdx.x & 3;
     const int tile = P.tiles ? P.tiles[tile_slot] : tile_slot;
@@ -267,9 +265,8 @@ template <bool FULL, bool ANY>
 __global__ __launch_bounds__(kBlock) void k_intersect(DevScene S, uint32_t n, const float* __restrict__ o3,
                                                       const float* __restrict__ d3, const double* __restrict__ tl,
                                                       double* __restrict__ out_t, int32_t* __restrict__ out_kind) {
-    __shared__ uint32_t s_stack[kMegaLds * kBlock];
-    uint32_t deep[kStackMax - kMegaLds];   // scratch
-    const MStack stack{s_stack + threadIdx.x, deep, 1u};
+    __shared__ uint32_t s_stack[kStackMax * kBlock];
+    const MStack stack{s_stack + threadIdx.x};
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const v3 o{o3[3 * (size_t)i], o3[3 * (size_t)i + 1], o3[3 * (size_t)i + 2]};
