@@ -466,6 +466,9 @@ struct Lru {
     }
 };
 static void cache_study(const Mesh& m, const Tree& T, long nrays) {
+    // Round 6: also the work of each origin region (lines per ray summed by region, 64 fine
+    // ranges of BVH order), the imbalance of the 8-way deal by equal ray counts and by equal work (8 contiguous
+    // runs of the fine ranges cut at equal cumulative lines), and the L2 hit rate of the work-balanced deal.
     Tracer tr{m, T};
     std::vector<uint32_t> pos_of(m.n);
     for (size_t p = 0; p < T.order.size(); p++) pos_of[T.order[p]] = (uint32_t)p;
@@ -474,11 +477,12 @@ static void cache_study(const Mesh& m, const Tree& T, long nrays) {
     cx /= m.n; cy /= m.n; cz /= m.n;
     std::mt19937_64 rng(777);
     std::uniform_real_distribution<double> U(0.0, 1.0);
-    std::vector<Lru> rr, reg;
-    for (int k = 0; k < 8; k++) { rr.emplace_back(32768); reg.emplace_back(32768); }
-    long acc = 0, hit_rr = 0, hit_reg = 0;
+    constexpr int kFine = 64;
     Count c;
     std::vector<uint32_t> lines;
+    std::vector<std::vector<uint32_t>> ray_lines(nrays);
+    std::vector<int> ray_fine(nrays);
+    double fine_lines[kFine] = {0}, fine_rays[kFine] = {0};
     for (long r = 0; r < nrays; r++) {
         const int tri = (int)(U(rng) * m.n) % m.n;
         const v3 a{m.v1[3 * tri], m.v1[3 * tri + 1], m.v1[3 * tri + 2]}, b{m.v2[3 * tri], m.v2[3 * tri + 1], m.v2[3 * tri + 2]};
@@ -496,15 +500,105 @@ static void cache_study(const Mesh& m, const Tree& T, long nrays) {
         tr.lines = &lines;
         int32_t prim;
         tr.trace(p, d, false, 0, c, prim);
-        const int xr = (int)(r % 8), xg = (int)((uint64_t)pos_of[tri] * 8 / (uint64_t)m.n);
-        for (uint32_t l : lines) {
-            acc++;
-            hit_rr += rr[xr].access(l);
-            hit_reg += reg[xg].access(l);
+        ray_lines[r] = lines;
+        const int f = (int)((uint64_t)pos_of[tri] * kFine / (uint64_t)m.n);
+        ray_fine[r] = f;
+        fine_lines[f] += (double)lines.size();
+        fine_rays[f] += 1.0;
+    }
+    // deals: 0 round-robin, 1 equal-count regions (8 ranges of BVH order), 2 equal-work regions
+    int cut[9];
+    {
+        double total = 0, accw = 0;
+        for (int f = 0; f < kFine; f++) total += fine_lines[f];
+        int g = 1;
+        cut[0] = 0;
+        for (int f = 0; f < kFine && g < 8; f++) {
+            accw += fine_lines[f];
+            if (accw >= total * g / 8.0) cut[g++] = f + 1;
+        }
+        while (g < 8) { cut[g] = cut[g - 1]; g++; }
+        cut[8] = kFine;
+    }
+    auto region_of = [&](int deal, long r) {
+        if (deal == 0) return (int)(r % 8);
+        if (deal == 1) return ray_fine[r] * 8 / kFine;
+        int g = 0;
+        while (g < 7 && ray_fine[r] >= cut[g + 1]) g++;
+        return g;
+    };
+    const char* names[3] = {"round-robin", "equal-count regions", "equal-work regions"};
+    std::printf("equal-work cuts (of %d fine ranges):", kFine);
+    for (int g = 0; g <= 8; g++) std::printf(" %d", cut[g]);
+    std::printf("\n");
+    for (int deal = 0; deal < 3; deal++) {
+        std::vector<Lru> l2;
+        for (int k = 0; k < 8; k++) l2.emplace_back(32768);
+        double work[8] = {0}, rays[8] = {0};
+        long acc = 0, hit = 0;
+        for (long r = 0; r < nrays; r++) {
+            const int g = region_of(deal, r);
+            work[g] += (double)ray_lines[r].size();
+            rays[g] += 1;
+            for (uint32_t l : ray_lines[r]) { acc++; hit += l2[g].access(l); }
+        }
+        double mx = 0, mean = 0;
+        for (int g = 0; g < 8; g++) { mx = std::max(mx, work[g]); mean += work[g] / 8; }
+        std::printf("cache study, %s: L2 (8 x 4 MB LRU) hit rate %.3f, lines per XCD max/mean %.3f, rays per XCD:", names[deal],
+                    (double)hit / acc, mx / mean);
+        for (int g = 0; g < 8; g++) std::printf(" %.0f", rays[g]);
+        std::printf(", lines per XCD:");
+        for (int g = 0; g < 8; g++) std::printf(" %.0f", work[g]);
+        std::printf("\n");
+    }
+    // Concurrency (INFLIGHT rays per XCD stepping together, one line per ray per round, a finished ray replaced
+    // by the XCD's next): the GPU keeps ~49k rays in flight per XCD (32 CUs x 24 waves x 64 lanes), so a line is
+    // reused only while the rays near it are in flight.  Deals: round-robin; 8 equal-count regions; 64 fine
+    // regions, XCD g taking regions g, g + 8, ... one after another (its in-flight rays share one fine region).
+    if (const char* inf_env = std::getenv("INFLIGHT")) {
+        const size_t K = (size_t)std::atol(inf_env);
+        for (int deal = 0; deal < 3; deal++) {
+            std::vector<std::vector<long>> order(8);
+            if (deal == 2) {
+                for (int g = 0; g < 8; g++)
+                    for (int f = g; f < kFine; f += 8)
+                        for (long r = 0; r < nrays; r++) if (ray_fine[r] == f) order[g].push_back(r);
+            } else {
+                for (long r = 0; r < nrays; r++) order[deal == 0 ? (int)(r % 8) : ray_fine[r] * 8 / kFine].push_back(r);
+            }
+            long acc = 0, hit = 0;
+            double rounds_max = 0;
+            for (int g = 0; g < 8; g++) {
+                Lru l2(32768);
+                std::vector<long> slot_ray(K, -1);
+                std::vector<size_t> slot_pos(K, 0);
+                size_t next = 0, active = 0;
+                for (size_t k = 0; k < K && next < order[g].size(); k++) { slot_ray[k] = order[g][next++]; active++; }
+                double rounds = 0;
+                while (active) {
+                    rounds++;
+                    for (size_t k = 0; k < K; k++) {
+                        if (slot_ray[k] < 0) continue;
+                        const std::vector<uint32_t>& L = ray_lines[slot_ray[k]];
+                        if (slot_pos[k] < L.size()) { acc++; hit += l2.access(L[slot_pos[k]++]); }
+                        if (slot_pos[k] >= L.size()) {
+                            slot_pos[k] = 0;
+                            if (next < order[g].size()) slot_ray[k] = order[g][next++];
+                            else { slot_ray[k] = -1; active--; }
+                        }
+                    }
+                }
+                rounds_max = std::max(rounds_max, rounds);
+            }
+            std::printf("cache study, %zu rays in flight per XCD, %s: L2 hit rate %.3f, rounds of the slowest XCD %.0f\n", K,
+                        deal == 0 ? "round-robin" : deal == 1 ? "8 equal-count regions" : "64 regions, 8 per XCD in turn",
+                        (double)hit / acc, rounds_max);
         }
     }
-    std::printf("cache study: %ld surface rays, %.2f lines/ray; L2 (8 x 4 MB LRU) hit rate: round-robin deal %.3f, "
-                "deal by origin region %.3f\n", nrays, (double)acc / nrays, (double)hit_rr / acc, (double)hit_reg / acc);
+    std::printf("cache study: %ld surface rays, %.2f lines/ray; lines per ray by fine region (64 ranges of BVH order):", nrays,
+                (double)c.nodes / std::max(c.rays, 1.0) + (double)c.leaves / std::max(c.rays, 1.0));
+    for (int f = 0; f < kFine; f++) std::printf(" %.1f", fine_rays[f] ? fine_lines[f] / fine_rays[f] : 0.0);
+    std::printf("\n");
 }
 
 // The library's 8-wide quantized tree (pt_bvh.cpp collapse_bvh8q) as a WideTree, decoded boxes.

@@ -12,6 +12,6 @@ for r in $(seq 1 ${ROUNDS:-1}); do
     NAME=${V%%:*}; ENVS=${V#*:}
     echo "== $NAME ($ENVS) round $r" >> $D/progress.log
     env $ENVS timeout -k 10 400 python -u bench.py $A --cpu-seconds 0 --no-parity --json-out $D/${W}_${NAME}_$r.json > $D/${W}_${NAME}_$r.log 2>&1 || exit 1
-    echo "$NAME round $r: $(python -c "import json;print(json.load(open('$D/${W}_${NAME}_$r.json'))['value'])")" >> $D/summary.txt
+    echo "$NAME round $r: $(python -c "import json;j=json.load(open('$D/${W}_${NAME}_$r.json'));print(j['value'],j['config']['kernel_ms_per_step'])")" >> $D/summary.txt
   done
 done
