@@ -536,7 +536,7 @@ def main(argv=None):
     # class times both of its forms <COUNT, FULL, SCAN>, one of which returns at once; the
     # closest-hit class is k_wf_trace_lanes<COUNT> on triangle scenes)
     names = ["k_wf_camera", trace_name, shade_name, shadow_name,
-             "k_wf_finalize", "k_render_pass<false, false>", "k_wf_nee_accum", "k_wf_region_sort"]
+             "k_wf_finalize", "k_render_pass<false, false>", "k_wf_nee_accum", "-"]
     # the closest-hit kernel is the dominant one by design (on a multi-GPU shard the shadow
     # passes run beside it on a second stream, so their event spans overlap it)
     # (C3 / C2: the kernel with the most time)

@@ -280,8 +280,7 @@ typedef struct pt_pass_params {
 typedef enum pt_kernel_class {
     PT_K_CAMERA = 0, PT_K_TRACE = 1, PT_K_SHADE = 2, PT_K_SHADOW = 3, PT_K_FINALIZE = 4, PT_K_MEGAKERNEL = 5,
     PT_K_ACCUM = 6,            /* k_wf_nee_accum: the visible shadow rays' light terms into the pixel sums */
-    PT_K_REGION_SORT = 7,      /* k_wf_region_*: the deep ray queues sorted by origin region (PT_REGION_SORT=1) */
-    PT_K_COUNT = 8
+    PT_K_COUNT = 7
 } pt_kernel_class;
 #define PT_K_SLOTS 8           /* length of pt_stats.kernel_ms / kernel_launches */
 

@@ -243,13 +243,6 @@ uint32_t wf_max_cap(Ctx* c) {
     return cap;
 }
 
-// PT_REGION_SORT=1|2 (environment): the deep ray queues are region-sorted before they are traced (pt_wavefront.h)
-int region_sort_mode() {
-    const char* e = std::getenv("PT_REGION_SORT");
-    return e && !std::strcmp(e, "1") ? 1 : e && !std::strcmp(e, "2") ? 2 : 0;
-}
-bool region_sort_wanted() { return region_sort_mode() != 0; }
-
 void free_wavefront(Ctx* c) {
     for (auto& a : c->wf_arrays) a.release();
     c->wf_arrays.clear();
@@ -281,9 +274,8 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     const bool want_sdf = c->S.num_sdf > 0 || (PT_VOL_DEFER && c->S.num_vol > 0);
     const bool want_vol = PT_VOL_DEFER && c->S.num_vol > 0;
     const bool want_heavy = c->S.route != 0;  // the routed split's queues of rays that reach a row-4 shape's box
-    const bool want_sort = region_sort_wanted();  // the region sort's spare ray-queue arrays
     if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes && (!want_sdf || c->Q.sdfq) && (!want_vol || c->Q.volq) &&
-        (!want_heavy || c->Q.hq) && (!want_sort || c->Q.sq_o))
+        (!want_heavy || c->Q.hq))
         return PT_OK;
     cap = std::max(cap, c->wf_cap);
     scap = std::max(scap, c->wf_scap);
@@ -311,14 +303,6 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     if (want_heavy && (rc = wf_alloc(c, &Q.hq, cap))) return rc;
     if (want_heavy && (rc = wf_alloc(c, &Q.hq_sh, scap))) return rc;   // one shadow pass at a time uses it
     if ((rc = wf_alloc(c, &Q.counts, pt::kCountWords))) return rc;
-    if (want_sort) {   // outside the queue budget (64 B per entry: 17 GB at 2^28 entries)
-        if ((rc = wf_alloc(c, &Q.sq_o, cap))) return rc;
-        if ((rc = wf_alloc(c, &Q.sq_d, cap))) return rc;
-        if ((rc = wf_alloc(c, &Q.sq_t, cap))) return rc;
-        if ((rc = wf_alloc(c, &Q.sq_k, cap))) return rc;
-        if ((rc = wf_alloc(c, &Q.regions, pt::kRegionTabWords))) return rc;
-        PT_HIP(hipMemsetAsync(Q.regions, 0, pt::kRegionTabWords * sizeof(uint32_t), c->stream));
-    }
     Q.overflow = c->d_counters + pt::kOverflowCounter;
     // spill columns: one region for the closest-hit kernels, one for the shadow kernels (they
     // can run at the same time on the side stream)
@@ -1485,7 +1469,6 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     if (const char* f = std::getenv("PT_SHADE_FORM")) plan.shade_form = !std::strcmp(f, "direct") ? 1 : !std::strcmp(f, "scan") ? 2 : 0;
     plan.lanes = -1;
     if (const char* f = std::getenv("PT_LANES")) plan.lanes = !std::strcmp(f, "0") ? 0 : !std::strcmp(f, "1") ? 1 : -1;
-    plan.region_sort = region_sort_mode();
     plan.root_children = (uint32_t)std::max(1, n_root * n_root * nm_root);
     plan.children = (uint32_t)nm;
     plan.lights_per_child = (uint32_t)(sampler->light_mode == PT_LIGHT_ALL ? std::max(1, c->S.num_lights) : 1);

@@ -20,9 +20,11 @@ struct HitRec {
     double tx = 0;  // KIND_XFORM (FULL): the inner shape's object-space t, so Hit.Info need not intersect again
 };
 
-// A whole traversal stack in a private array (scratch): the nested traversal of an instanced mesh.
+// A whole traversal stack in a private array (scratch): the nested traversal of an instanced mesh, whose
+// object-space BVH4 keeps every path within kStack4Budget pushes (pack_nodes checks it).  Sized by that bound,
+// not by the triangle BVH8's kStackMax (64 since round 5: 128 B more scratch per lane for no use).
 struct LocalStack {
-    static constexpr int kLds = kStackMax;
+    static constexpr int kLds = kStack4Budget;
     static constexpr int kStride = 1;
     uint32_t* lds;
     __device__ __forceinline__ void put(int i, uint32_t v) const { lds[i] = v; }
@@ -441,7 +443,7 @@ __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 i
 // idx is the triangle's position in the mesh's BLAS records.
 __device__ __noinline__ HitRec blas_hit(const DevScene& S, int b, v3 o, v3 d) {
     const DevBlas B = S.blas[b];
-    uint32_t st[kStackMax];
+    uint32_t st[kStack4Budget];
     const LocalStack stack{st};
     HitRec best{kHitInf, -1, -1};
     Counters ctr{0, 0, 0, 0};

@@ -60,25 +60,7 @@ struct WfQueues {
     // tests) a wave refills only when all its lanes are idle and its idle lanes help from the first claim on, so
     // the hand-off protocol runs throughout the pass instead of in each wave's last rays
     int32_t tail_early;
-    // Region sort (WfPlan::region_sort): a spare set of ray-queue arrays (cap entries) the deep queues are
-    // reordered into, and the region table (kRegionTabWords words; pt_wavefront.hip k_wf_region_*)
-    float4* sq_o;
-    float4* sq_d;
-    double2* sq_t;
-    ulonglong2* sq_k;
-    uint32_t* regions;
 };
-
-// Region sort of the deep ray queues (rays of depth >= 2, whose origins lie on the scene): the rays of a
-// queue are reordered by origin region — a Morton cell of a 4x4x4 grid over the triangle BVH's root box —
-// into partitions of whole regions (LPT-balanced by ray count), so each XCD's persistent grid traces one
-// region at a time and its L2 holds that region's BVH lines (tools/bvh_quality.cpp INFLIGHT study).
-constexpr int kRegions = 64;
-constexpr int kRegionStride = 16;   // words between a region's counters (own 64-B line)
-constexpr int kRegCount = 0, kRegCursor = kRegions * kRegionStride, kRegBase = 2 * kRegions * kRegionStride;
-constexpr int kRegOrig = kRegBase + kRegions, kRegFlag = kRegOrig + kParts;
-constexpr int kRegSpread = kRegFlag + 1;   // mode 2: [kRegions][kParts] bases of each region's share of each partition
-constexpr int kRegionTabWords = kRegSpread + kRegions * kParts;
 
 // Every counter sits on a line of its own: returning atomics execute at the memory side,
 // one line at a time, so cursors packed into one 128-B line serialise every partition's
@@ -145,8 +127,6 @@ struct WfPlan {
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
     int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always
                                // (PT_LANES=0|1 in the environment; tests)
-    int32_t region_sort;       // the deep queues region-sorted before they are traced (PT_REGION_SORT=1 | 2): 1 whole
-                               // regions per partition (LPT), 2 every region spread evenly over the partitions
     // Optional second stream: each depth's shadow pass runs there, beside the next depth's
     // closest-hit pass (independent queues), so one fills the other's ramp and tail.
     // ev_main orders shade(d) → shadow(d); ev_side[q], recorded after the light terms of

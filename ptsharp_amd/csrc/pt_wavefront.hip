@@ -704,15 +704,7 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
             const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
                                           : (leaf ? 0u : ref));
             q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
-#ifdef PT_PROBE_HALF   // timing probe only (wrong boxes): inner triangle-BVH nodes read 4 pieces
-            if (leaf || !tri) {
-                q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; q7 = S.lines[at + 7u];
-            } else {
-                q4 = q2; q5 = q3; q6 = q2; q7 = q3;
-            }
-#else
             q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; q7 = S.lines[at + 7u];
-#endif
         }
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6); PT_PIN4(q7);
         bool pop = true;
@@ -1427,15 +1419,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
             const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
                                           : (leaf ? 0u : ref));
             q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
-#ifdef PT_PROBE_HALF   // timing probe only (wrong boxes): inner triangle-BVH nodes read 4 pieces
-            if (leaf || !tri) {
-                q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; q7 = S.lines[at + 7u];
-            } else {
-                q4 = q2; q5 = q3; q6 = q2; q7 = q3;
-            }
-#else
             q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; q7 = S.lines[at + 7u];
-#endif
         }
         PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6); PT_PIN4(q7);
         bool pop = true, blocked = false;
@@ -1735,135 +1719,6 @@ __global__ __launch_bounds__(256) void k_wf_select(DevPass P, DevBuffer B, int k
     }
 }
 
-// ---------------------------------------------------------------- region sort (deep queues)
-// The region of a ray origin: the Morton index of its cell in a 4x4x4 grid over the triangle BVH's root box
-// (origins outside it, e.g. on the floor, fall in the boundary cells).
-__device__ __forceinline__ uint32_t ray_region(const DevScene& S, float x, float y, float z) {
-    auto cell = [](float v, float lo, float hi) -> uint32_t {
-        const float t = (v - lo) * (4.0f / (hi - lo));
-        return t >= 3.f ? 3u : t >= 2.f ? 2u : t >= 1.f ? 1u : 0u;   // (NaN: 0)
-    };
-    const uint32_t cx = cell(x, S.tri_box[0], S.tri_box[3]), cy = cell(y, S.tri_box[1], S.tri_box[4]);
-    const uint32_t cz = cell(z, S.tri_box[2], S.tri_box[5]);
-    return (cx & 1u) | ((cy & 1u) << 1) | ((cz & 1u) << 2) | ((cx & 2u) << 2) | ((cy & 2u) << 3) | ((cz & 2u) << 4);
-}
-// Rays per region of queue q (every partition).  The table's counters are zero (allocation, k_wf_region_plan).
-__global__ __launch_bounds__(256) void k_wf_region_hist(DevScene S, WfQueues Q, int q) {
-    __shared__ uint32_t h[kRegions];
-    if (threadIdx.x < kRegions) h[threadIdx.x] = 0u;
-    __syncthreads();
-    for (int g = 0; g < kParts; g++) {
-        const uint32_t n = min(*ray_count(Q, q, g), Q.pcap), base = (uint32_t)g * Q.pcap;
-        for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < n; k += gridDim.x * 256u) {
-            const float4 a = Q.q_o[q][base + k];
-            atomicAdd(&h[ray_region(S, a.x, a.y, a.z)], 1u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < kRegions && h[threadIdx.x]) atomicAdd(Q.regions + kRegCount + threadIdx.x * kRegionStride, h[threadIdx.x]);
-}
-// One thread: regions to partitions, largest first to the least loaded (LPT), each partition's regions in
-// Morton order; the sorted queue's partition counts replace queue q's (the originals kept for the scatter).
-// A partition past pcap (a queue near capacity) leaves the order as it is (kRegFlag: identity scatter).
-__global__ void k_wf_region_plan(WfQueues Q, int q, int mode) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint32_t* R = Q.regions;
-    uint32_t cnt[kRegions];
-    uint8_t ord[kRegions], part[kRegions];
-    for (int r = 0; r < kRegions; r++) {
-        cnt[r] = R[kRegCount + r * kRegionStride];
-        R[kRegCount + r * kRegionStride] = 0u;    // for the next sort's histogram
-        R[kRegCursor + r * kRegionStride] = 0u;   // for this sort's scatter
-        ord[r] = (uint8_t)r;
-    }
-    for (int i = 1; i < kRegions; i++)   // insertion sort, count descending
-        for (int j = i; j > 0 && cnt[ord[j]] > cnt[ord[j - 1]]; j--) { const uint8_t t = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = t; }
-    if (mode == 2) {   // every region's rays dealt evenly to the partitions, regions in Morton order in each
-        uint32_t offg[kParts] = {0};
-        for (int r = 0; r < kRegions; r++)
-            for (int g = 0; g < kParts; g++) {
-                R[kRegSpread + r * kParts + g] = (uint32_t)g * Q.pcap + offg[g];
-                offg[g] += cnt[r] / kParts + ((uint32_t)g < cnt[r] % kParts ? 1u : 0u);
-            }
-        bool fits = true;
-        for (int g = 0; g < kParts; g++) fits = fits && offg[g] <= Q.pcap;
-        for (int g = 0; g < kParts; g++) {
-            R[kRegOrig + g] = min(*ray_count(Q, q, g), Q.pcap);
-            if (fits) *ray_count(Q, q, g) = offg[g];
-        }
-        R[kRegFlag] = fits ? 2u : 1u;
-        return;
-    }
-    uint64_t load[kParts] = {0};
-    for (int i = 0; i < kRegions; i++) {
-        int best = 0;
-        for (int g = 1; g < kParts; g++) if (load[g] < load[best]) best = g;
-        part[ord[i]] = (uint8_t)best;
-        load[best] += cnt[ord[i]];
-    }
-    bool ok = true;
-    for (int g = 0; g < kParts; g++) ok = ok && load[g] <= (uint64_t)Q.pcap;
-    uint32_t off[kParts] = {0};
-    for (int r = 0; r < kRegions; r++) {
-        R[kRegBase + r] = (uint32_t)part[r] * Q.pcap + off[part[r]];
-        off[part[r]] += cnt[r];
-    }
-    for (int g = 0; g < kParts; g++) {
-        R[kRegOrig + g] = min(*ray_count(Q, q, g), Q.pcap);
-        if (ok) *ray_count(Q, q, g) = off[g];   // the low half of the pair word: the NEE count stays
-    }
-    R[kRegFlag] = ok ? 0u : 1u;
-}
-// Every ray of queue q to its region's run in the spare arrays (a block's rays of one region reserved with
-// one atomic per region; the order inside a region is free: results do not depend on queue order).
-__global__ __launch_bounds__(256) void k_wf_region_scatter(DevScene S, WfQueues Q, int q) {
-    const uint32_t* R = Q.regions;
-    __shared__ uint32_t lh[kRegions], lb[kRegions];
-    const bool ident = R[kRegFlag] == 1u, spread = R[kRegFlag] == 2u;
-    uint32_t tiles = 0;
-    for (int g = 0; g < kParts; g++) tiles += (R[kRegOrig + g] + 255u) / 256u;
-    for (uint32_t t = blockIdx.x; t < tiles; t += gridDim.x) {   // block-uniform
-        int g = 0;
-        uint32_t tt = t;
-        for (; g < kParts; g++) {
-            const uint32_t tg = (R[kRegOrig + g] + 255u) / 256u;
-            if (tt < tg) break;
-            tt -= tg;
-        }
-        const uint32_t k = tt * 256u + threadIdx.x;
-        const bool has = k < R[kRegOrig + g];
-        const uint32_t src = (uint32_t)g * Q.pcap + k;
-        if (threadIdx.x < kRegions) lh[threadIdx.x] = 0u;
-        __syncthreads();
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-        double2 th = make_double2(0.0, 0.0);
-        ulonglong2 kk = make_ulonglong2(0ull, 0ull);
-        uint32_t r = 0, rank = 0;
-        if (has) {
-            a = nt_load(&Q.q_o[q][src]);
-            b = nt_load(&Q.q_d[q][src]);
-            th = nt_load(&Q.q_t[q][src]);
-            kk = nt_load(&Q.q_k[q][src]);
-            r = ray_region(S, a.x, a.y, a.z);
-            if (!ident) rank = atomicAdd(&lh[r], 1u);
-        }
-        __syncthreads();
-        if (!ident && threadIdx.x < kRegions && lh[threadIdx.x])
-            lb[threadIdx.x] = (spread ? 0u : R[kRegBase + threadIdx.x]) +
-                              atomicAdd(Q.regions + kRegCursor + threadIdx.x * kRegionStride, lh[threadIdx.x]);
-        __syncthreads();
-        if (has) {
-            uint32_t dst = ident ? src : lb[r] + rank;
-            if (spread) dst = R[kRegSpread + r * kParts + dst % kParts] + dst / kParts;   // j-th ray of region r
-            q_store_next(&Q.sq_o[dst], a);
-            q_store_next(&Q.sq_d[dst], b);
-            q_store_late(&Q.sq_t[dst], th);
-            q_store_late(&Q.sq_k[dst], kk);
-        }
-        __syncthreads();
-    }
-}
-
 // ---------------------------------------------------------------- host driver
 // Grid for `items` work items; a multiple of kParts (XCD groups), at most cap_blocks.
 static unsigned grid_for(uint64_t items, unsigned block, unsigned cap_blocks) {
@@ -1875,9 +1730,8 @@ static unsigned grid_for(uint64_t items, unsigned block, unsigned cap_blocks) {
 }
 
 // Trace / shade / shadow for every depth of one chunk whose camera rays are queued.
-static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer& B, const WfQueues& Q0,
+static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const DevBuffer& B, const WfQueues& Q,
                        const WfPlan& plan, bool count, hipStream_t stream, LaunchTimer* timer, uint64_t bound) {
-    WfQueues Q = Q0;   // the region sort swaps a ray queue's arrays with the spare set (this chunk's launches see the swap)
     auto begin_k = [&](int cls, hipStream_t s) { if (timer) timer->begin(cls, s); };
     auto end_k = [&](int cls, hipStream_t s) { if (timer) timer->end(cls, s); };
     const bool full = S.full != 0;        // shade: textures or row-4 shapes
@@ -2014,19 +1868,6 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
         if (plan.side) (void)hipEventRecord(plan.ev_side[1 - qi], side);
         bound = children < Q.cap ? children : Q.cap;
         qi = 1 - qi;
-        // rays of depth >= 2 (their origins on the scene): region-sorted into the spare arrays, which then become
-        // queue qi (the arrays they came from are the next spare)
-        if (plan.region_sort && depth >= 1 && depth < smp.mb && Q.sq_o && S.tri_num_nodes > 0) {
-            begin_k(7, stream);   // (the counters are zero: at allocation, then after each plan read them)
-            hipLaunchKernelGGL(k_wf_region_hist, dim3(grid_for(bound, 256, 2048)), dim3(256), 0, stream, S, Q, qi);
-            hipLaunchKernelGGL(k_wf_region_plan, dim3(1), dim3(64), 0, stream, Q, qi, plan.region_sort);
-            hipLaunchKernelGGL(k_wf_region_scatter, dim3(grid_for(bound, 256, 8192)), dim3(256), 0, stream, S, Q, qi);
-            end_k(7, stream);
-            std::swap(Q.q_o[qi], Q.sq_o);
-            std::swap(Q.q_d[qi], Q.sq_d);
-            std::swap(Q.q_t[qi], Q.sq_t);
-            std::swap(Q.q_k[qi], Q.sq_k);
-        }
         // trace(d + 1) frees pair word 1 - qi and shade(d + 1) rewrites shadow set 1 - qi: the
         // shadow pass and the light-term accumulation of depth d - 1 read both
         if (plan.side && depth >= 1) (void)hipStreamWaitEvent(stream, plan.ev_side[1 - qi], 0);

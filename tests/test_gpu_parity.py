@@ -436,21 +436,3 @@ def test_shadow_tail_handoffs_forced(gpu, monkeypatch, name):
         same_buffer(e, l)
         o, orr = O.render(O.OracleScene(s), c, smp, w, h, 2, passes=1, seed=4242, tiles=tiles)
         check(e, re_, o, orr)
-
-
-@pytest.mark.parametrize("mode", ["1", "2"])
-@pytest.mark.parametrize("cap", [None, 1 << 20])
-def test_region_sort_bit_identical(gpu, monkeypatch, cap, mode):
-    """The deep queues sorted by origin region before they are traced (PT_REGION_SORT=1: whole regions per
-    partition; 2: every region spread over the partitions): the same rays and
-    the same Buffer bits as the unsorted queues (queue order never reaches the results: keys are per path
-    node, sums fixed-point).  The 1M-triangle frame at 480x270, 4 spp; with PT_WF_MAX_CAP = 2^20 the pass
-    runs in several chunks."""
-    if cap:
-        monkeypatch.setenv("PT_WF_MAX_CAP", str(cap))
-    s, c, smp = scenes.bunny_frame(1_000_000)
-    a, ra = render_gpu(s, c, smp, 480, 270, spp=4, seed=61, engine=_abi.ENGINE_WAVEFRONT)
-    monkeypatch.setenv("PT_REGION_SORT", mode)
-    b, rb = render_gpu(s, c, smp, 480, 270, spp=4, seed=61, engine=_abi.ENGINE_WAVEFRONT)
-    assert ra == rb
-    same_buffer(a, b)

@@ -169,7 +169,7 @@ static void run(uint4* buf, size_t bytes, int waves_per_simd, int active, uint32
     CK(hipEventDestroy(a)); CK(hipEventDestroy(b));
 }
 
-int main() {
+int main(int argc, char** argv) {
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int cus = prop.multiProcessorCount;
@@ -181,6 +181,19 @@ int main() {
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint32_t*)buf, maxb / 4);
     CK(hipDeviceSynchronize());
     printf("CUs %d\n", cus);
+    if (argc > 1) {   // "chase": K of a 128-B record's eight 16-B pieces per dependent step, 6 waves per SIMD
+        for (size_t w : {(size_t)96 << 20, maxb}) {
+            run<1, 8>(buf, w, 6, 64, out, cus);
+            run<2, 8>(buf, w, 6, 64, out, cus);
+            run<4, 8>(buf, w, 6, 64, out, cus);
+            run<6, 8>(buf, w, 6, 64, out, cus);
+            run<7, 8>(buf, w, 6, 64, out, cus);
+            run<8, 8>(buf, w, 6, 64, out, cus);
+            run<4, 4>(buf, w, 6, 64, out, cus);
+        }
+        CK(hipDeviceSynchronize());
+        return 0;
+    }
     const size_t ws[3] = {(size_t)2 << 20, (size_t)96 << 20, maxb};
     for (size_t w : ws) {
         run_group_tp<1, 8>(buf, w, out, cus);
