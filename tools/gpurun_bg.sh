@@ -7,5 +7,6 @@ for k in $(seq 1 12); do
   timeout $((TO + 900)) /usr/local/graft/bin/gpurun --timeout $TO -- "$CMD" > $LOG 2>&1
   rc=$?
   if grep -q "status=transient rc=None" $LOG; then sleep 150; continue; fi
+  if [ $rc = 3 ]; then sleep 180; continue; fi   # no box or slot free right now (nothing charged)
   exit $rc
 done
