@@ -440,7 +440,7 @@ int pack_nodes(const pt::BvhResult& b, std::vector<float4>& out, int32_t& num_no
 // upload's order; the last two builds are kept.
 struct TriBvhBuild {
     std::vector<uint32_t> order;      // BVH position -> index into tri_src
-    std::vector<float4> nodes;        // the traversal units (pt_bvh.h Bvh8UnitResult): nodes and leaf chunks
+    std::vector<float4> nodes, chunks;
     int32_t num_nodes = 0;
     float box[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int rc = PT_OK;
@@ -527,13 +527,10 @@ std::shared_ptr<const TriBvhBuild> build_tri_bvh(const pt_scene_desc* d, const s
         out->err = g_last_error;
         return out;
     }
-    // the traversal format: 64-B units, a node in one, a leaf chunk in two (pt_bvh.h pack_bvh8_units)
-    pt::Bvh8UnitResult bu;
-    if (!pt::pack_bvh8_units(b8, bu)) {
-        out->rc = fail(PT_ERR_UNSUPPORTED, "triangle BVH beyond 2^27 64-B units");
-        out->err = g_last_error;
-        return out;
-    }
+    out->nodes.resize(b8.words.size() / 4);
+    std::memcpy(out->nodes.data(), b8.words.data(), b8.words.size() * sizeof(uint32_t));
+    out->num_nodes = (int32_t)b8.nodes();
+    out->chunks.resize(8 * b8.chunk_first.size());
     for (size_t ci = 0; ci < b8.chunk_first.size(); ci++) {
         float w[32] = {0.f};
         const uint32_t first = b8.chunk_first[ci], cnt = b8.chunk_count[ci];
@@ -543,17 +540,14 @@ std::shared_ptr<const TriBvhBuild> build_tri_bvh(const pt_scene_desc* d, const s
             const float* rf = reinterpret_cast<const float*>(&tri_recs[3 * (size_t)(first + t)]);
             for (int j = 0; j < 9; j++) w[1 + 9 * t + j] = rf[j];
         }
-        std::memcpy(&bu.units[(size_t)bu.chunk_unit[ci] * pt::kUnitWords], w, sizeof w);
+        std::memcpy(&out->chunks[8 * ci], w, sizeof w);
     }
-    out->nodes.resize(bu.units.size() / 4);
-    std::memcpy(out->nodes.data(), bu.units.data(), bu.units.size() * sizeof(uint32_t));
-    out->num_nodes = (int32_t)b8.nodes();
-    if (!bu.units.empty()) {   // root box = union of the root node's children (their quantized boxes)
-        const uint32_t* w = bu.units.data();
+    if (!out->nodes.empty()) {   // root box = union of the root node's children (their quantized boxes)
+        const uint32_t* w = b8.words.data();
         for (int ax = 0; ax < 3; ax++) { out->box[ax] = INFINITY; out->box[3 + ax] = -INFINITY; }
         for (int k = 0; k < (int)(w[3] >> 28); k++) {
             float lo[3], hi[3];
-            pt::bvh8u_child_box(w, k, lo, hi);
+            pt::bvh8_child_box(w, k, lo, hi);
             for (int ax = 0; ax < 3; ax++) {
                 out->box[ax] = std::min(out->box[ax], lo[ax]);
                 out->box[3 + ax] = std::max(out->box[3 + ax], hi[ax]);
@@ -1185,8 +1179,9 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
             tri_uv[2 * i + 1] = f4(t3[0], t3[1], 0.f, 0.f);
         }
     }
-    const std::vector<float4>& tri_units = tbv->nodes;
+    const std::vector<float4>& tri_nodes = tbv->nodes;
     const int32_t tri_num_nodes = tbv->num_nodes;
+    const std::vector<float4>& tri_chunks = tbv->chunks;
     float tri_box[6];
     std::memcpy(tri_box, tbv->box, sizeof tri_box);
 
@@ -1285,17 +1280,20 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
 
     pt::DevScene S{};
     std::memcpy(S.tri_box, tri_box, sizeof tri_box);
-    {   // the traversal lines: [ana_nodes (128-B BVH4 lines) | tri_units (64-B units)], one allocation
+    {   // the traversal lines: [ana_nodes | tri_nodes | tri_chunks], 8 float4 per node / chunk
         std::vector<float4> lines;
-        lines.reserve(ana_nodes.size() + tri_units.size());
+        lines.reserve(ana_nodes.size() + tri_nodes.size() + tri_chunks.size());
         lines.insert(lines.end(), ana_nodes.begin(), ana_nodes.end());
-        lines.insert(lines.end(), tri_units.begin(), tri_units.end());
-        if (lines.size() >= 0xFFFFFFFFull) return fail(PT_ERR_UNSUPPORTED, "more than 2^32 BVH pieces");   // 32-bit piece offsets
+        lines.insert(lines.end(), tri_nodes.begin(), tri_nodes.end());
+        lines.insert(lines.end(), tri_chunks.begin(), tri_chunks.end());
+        if (lines.size() >= 0xFFFFFFFFull) return fail(PT_ERR_UNSUPPORTED, "more than 2^29 BVH lines");   // 32-bit piece offsets
         rc = upload(c, lines, &S.lines); if (rc) return rc;
         S.lines_n = (uint32_t)(lines.size() / 8);
-        S.tri_unit0 = (uint32_t)(ana_nodes.size() / 4);
+        S.tri_node_line0 = (uint32_t)(ana_nodes.size() / 8);
+        S.tri_chunk_line0 = (uint32_t)((ana_nodes.size() + tri_nodes.size()) / 8);
         S.ana_nodes = ana_nodes.empty() ? nullptr : S.lines;
-        S.tri_units = tri_units.empty() ? nullptr : S.lines + 4 * (size_t)S.tri_unit0;
+        S.tri_nodes = tri_nodes.empty() ? nullptr : S.lines + 8 * (size_t)S.tri_node_line0;
+        S.tri_chunks = tri_chunks.empty() ? nullptr : S.lines + 8 * (size_t)S.tri_chunk_line0;
     }
     // one 128-B shading record per triangle (pt_scene.h tri_rstride): what k_wf_shade reads
     // for a triangle hit is one line instead of two or three
@@ -1397,8 +1395,8 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     c->S = S;
     c->has_scene = true;
     c->stats.bvh_nodes = (uint64_t)tri_num_nodes + (uint64_t)ana_num_nodes;
-    c->stats.traversal_bytes = (tri_units.size() + ana_nodes.size() + ana_recs.size()) * sizeof(float4);
-    c->stats.bvh_bytes = (tri_units.size() + ana_nodes.size()) * sizeof(float4) +
+    c->stats.traversal_bytes = (tri_nodes.size() + tri_chunks.size() + ana_nodes.size() + ana_recs.size()) * sizeof(float4);
+    c->stats.bvh_bytes = (tri_nodes.size() + tri_chunks.size() + ana_nodes.size()) * sizeof(float4) +
                          (tri_sh.size() + ana_recs.size()) * sizeof(float4);
     c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return PT_OK;
@@ -1891,8 +1889,9 @@ int pt_scene_bvh_digest(const pt_scene_desc* d, uint64_t out[4]) {
     };
     eat(b->order.data(), b->order.size() * sizeof(uint32_t));
     eat(b->nodes.data(), b->nodes.size() * sizeof(float4));
+    eat(b->chunks.data(), b->chunks.size() * sizeof(float4));
     out[0] = h;
-    out[1] = (uint64_t)b->nodes.size() * sizeof(float4);
+    out[1] = (uint64_t)(b->nodes.size() + b->chunks.size()) * sizeof(float4);
     TriBvhCache& C = tri_bvh_cache();
     std::lock_guard<std::mutex> lk(C.mu);
     out[2] = (uint64_t)C.builds;

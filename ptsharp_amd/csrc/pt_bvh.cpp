@@ -646,105 +646,6 @@ void bvh8_child_box(const uint32_t* w, int slot, float lo[3], float hi[3]) {
     }
 }
 
-namespace {
-// x rounded down to a float whose low 9 mantissa bits are 0 (toward -inf: the quantized origin never exceeds x)
-float clear9_down(float x) {
-    uint32_t b;
-    std::memcpy(&b, &x, 4);
-    if (b & 0x1FFu) {
-        if (b & 0x80000000u) b = (b & ~0x1FFu) + 0x200u;   // negative: one step further from zero
-        else b &= ~0x1FFu;                                  // positive (or +0): toward zero
-    }
-    float r;
-    std::memcpy(&r, &b, 4);
-    return r;
-}
-}  // namespace
-
-bool pack_bvh8_units(const Bvh8Result& b8, Bvh8UnitResult& out) {
-    out = Bvh8UnitResult{};
-    const size_t nn = b8.nodes();
-    if (nn == 0) return true;
-    out.chunk_unit.assign(b8.chunk_first.size(), 0u);
-    // unit of every bvh8 node, blocks laid breadth-first (root at 0, its block from 2)
-    std::vector<uint32_t> unit_of(nn, 0u), base_of(nn, 0u);
-    uint64_t next = 2;
-    std::vector<uint32_t> queue{0u};
-    for (size_t qi = 0; qi < queue.size(); qi++) {
-        const uint32_t nd = queue[qi];
-        const uint32_t* w = &b8.words[(size_t)nd * kNode8Words];
-        const uint32_t nc = w[3] >> 28, nin = (w[3] >> 24) & 15u, pad = (nin + 1u) & ~1u;
-        base_of[nd] = (uint32_t)next;
-        for (uint32_t k = 0; k < nin; k++) {
-            unit_of[w[4] + k] = (uint32_t)(next + k);
-            queue.push_back(w[4] + k);
-        }
-        for (uint32_t k = nin; k < nc; k++) out.chunk_unit[(w[5] + k) & 0x7FFFFFFFu] = (uint32_t)(next + pad + 2u * (k - nin));
-        next += pad + 2u * (nc - nin);
-        if (next > kUnitMax) return false;
-    }
-    out.units.assign((size_t)next * kUnitWords, 0u);
-    out.nodes = nn;
-    for (size_t nd = 0; nd < nn; nd++) {
-        const uint32_t* w = &b8.words[nd * kNode8Words];
-        const uint32_t nc = w[3] >> 28, nin = (w[3] >> 24) & 15u, base = base_of[nd];
-        uint32_t* u = &out.units[(size_t)unit_of[nd] * kUnitWords];
-        float clo[8][3], chi[8][3];
-        for (uint32_t k = 0; k < nc; k++) bvh8_child_box(w, (int)k, clo[k], chi[k]);
-        uint32_t ebits = 0;
-        uint8_t qb[6][8];
-        for (int ax = 0; ax < 3; ax++) {
-            float o = INFINITY, top = -INFINITY;
-            for (uint32_t k = 0; k < nc; k++) { o = std::min(o, clo[k][ax]); top = std::max(top, chi[k][ax]); }
-            o = clear9_down(o);
-            const double ext = (double)top - (double)o;
-            int e = -126;
-            while (e < 127 && std::ldexp(255.0, e) < ext) e++;
-            for (;;) {   // the outward rounding can need one more step
-                bool ok = true;
-                for (uint32_t k = 0; k < nc && ok; k++) ok = std::ceil(((double)chi[k][ax] - (double)o) / std::ldexp(1.0, e)) <= 255.0;
-                if (ok || e >= 127) break;
-                e++;
-            }
-            uint32_t ob;
-            std::memcpy(&ob, &o, 4);
-            u[ax] = ob | ((base >> (9 * ax)) & 0x1FFu);
-            ebits |= (uint32_t)(e + 127) << (8 * ax);
-            for (int k = 0; k < 8; k++) {
-                if ((uint32_t)k >= nc) { qb[2 * ax][k] = 255; qb[2 * ax + 1][k] = 0; continue; }
-                const double step = std::ldexp(1.0, e);
-                const double lo = std::floor(((double)clo[k][ax] - (double)o) / step);
-                const double hi = std::ceil(((double)chi[k][ax] - (double)o) / step);
-                qb[2 * ax][k] = (uint8_t)std::min(255.0, std::max(0.0, lo));
-                qb[2 * ax + 1][k] = (uint8_t)std::min(255.0, std::max(0.0, hi));
-            }
-        }
-        u[3] = ebits | (nin << 24) | (nc << 28);
-        for (int r = 0; r < 6; r++)
-            for (int j = 0; j < 2; j++)
-                u[4 + 2 * r + j] = (uint32_t)qb[r][4 * j] | ((uint32_t)qb[r][4 * j + 1] << 8) | ((uint32_t)qb[r][4 * j + 2] << 16) |
-                                   ((uint32_t)qb[r][4 * j + 3] << 24);
-    }
-    return true;
-}
-
-void bvh8u_child_box(const uint32_t* u, int slot, float lo[3], float hi[3]) {
-    for (int ax = 0; ax < 3; ax++) {
-        const uint32_t ob = u[ax] & ~0x1FFu;
-        float o;
-        std::memcpy(&o, &ob, 4);
-        const int e = (int)((u[3] >> (8 * ax)) & 0xFFu) - 127;
-        const uint32_t ql = (u[4 + 4 * ax + slot / 4] >> (8 * (slot & 3))) & 0xFFu;
-        const uint32_t qh = (u[6 + 4 * ax + slot / 4] >> (8 * (slot & 3))) & 0xFFu;
-        const double l = (double)o + std::ldexp((double)ql, e), h = (double)o + std::ldexp((double)qh, e);
-        float fl = (float)l, fh = (float)h;
-        if ((double)fl > l) fl = std::nextafter(fl, -INFINITY);
-        if ((double)fh < h) fh = std::nextafter(fh, INFINITY);
-        lo[ax] = fl;
-        hi[ax] = fh;
-    }
-}
-
 void collapse_bvh8q(const BvhResult& bvh2, int stack_budget, Bvh8Result& out, double c_step, double c_tri, int max_leaf) {
     out = Bvh8Result{};
     if (bvh2.nodes.empty()) return;

@@ -116,32 +116,4 @@ void collapse_bvh8q(const BvhResult& bvh2, int stack_budget, Bvh8Result& out, do
 // The box a slot's quantized bounds describe, in exact arithmetic rounded outward to fp32 (host checks).
 void bvh8_child_box(const uint32_t* node, int slot, float lo[3], float hi[3]);
 
-// The traversal format (round 6): the 8-wide tree above re-laid in 64-byte units, a node in ONE unit (four 16-B
-// pieces: a node step issues four loads, a leaf step seven), a leaf chunk in two (128-B aligned, the chunk format
-// of pt_api.hip build_tri_bvh).  The children of a node are one block: its inner children's nodes (units base ..
-// base + n_in - 1, the block padded to an even count) then its leaf chunks (base + pad + 2j).  Node = 16 words:
-//   [0..2]  origin x, y, z: fp32 rounded down to a multiple of 2^9 ulps; their low 9 bits hold bits 0-8, 9-17,
-//           18-26 of base (the block's first unit)
-//   [3]     bits 0-23: exponents ex, ey, ez (biased by 127: step 2^(e-127)), bits 24-27: inner children n_in,
-//           bits 28-31: children n (1..8; slots n..7 are empty and never tested)
-//   [4..15] the child bounds as bytes q (0..255), lo.x[8] hi.x[8] lo.y[8] hi.y[8] lo.z[8] hi.z[8] (slot k: byte k%4
-//           of word 2j + k/4); bound = origin + q·step, a superset of the child's (decoded bvh8) box
-// A traversal computes a slab distance as fma(q, step/d, (origin - o)/d), as with the 128-B node.
-constexpr int kUnitWords = 16;
-constexpr uint32_t kUnitMax = 1u << 27;   // base: 27 bits of units (8 GiB of nodes and chunks)
-struct Bvh8UnitResult {
-    std::vector<uint32_t> units;        // kUnitWords per 64-B unit; unit 0 is the root node
-    std::vector<uint32_t> chunk_unit;   // per leaf chunk of the Bvh8Result: its first unit (the caller fills the two)
-    size_t nodes = 0;                   // node units
-    size_t count() const { return units.size() / kUnitWords; }
-};
-// Re-lay and re-quantize (8-bit, on the bvh8_child_box boxes: conservative).  false: more than kUnitMax units.
-bool pack_bvh8_units(const Bvh8Result& b8, Bvh8UnitResult& out);
-// The box slot `slot` of a node unit describes, exact arithmetic rounded outward to fp32 (host checks).
-void bvh8u_child_box(const uint32_t* unit, int slot, float lo[3], float hi[3]);
-// The node's origin component (low 9 bits cleared), its base and children.
-inline uint32_t bvh8u_base(const uint32_t* w) {
-    return (w[0] & 0x1FFu) | ((w[1] & 0x1FFu) << 9) | ((w[2] & 0x1FFu) << 18);
-}
-
 }  // namespace pt

@@ -267,67 +267,6 @@ __device__ __forceinline__ bool node8_step(float4 q0, float4 q1, float4 q2, floa
     return true;
 }
 
-// The same 8-wide step over a 64-B node unit (pt_bvh.h Bvh8UnitResult; round 6): four 16-B pieces instead of eight.
-// The bounds are bytes (v_cvt_f32_ubyte*), the slots past the node's child count are masked (their bytes are not
-// a box that always misses at 8 bits: a ray thousands of node extents away could pass the widened far test), and
-// a child's unit follows from the block base: inner child k at base + k, leaf chunk k at base + pad + 2(k - n_in).
-// The gather microbenchmark (tools/microbench_gather.hip chase, 96 MB, 6 waves) steps 4 pieces in 0.61 of the
-// time of 8.
-__device__ __forceinline__ float ubyte_f(uint32_t w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
-template <class STK>
-__device__ __forceinline__ bool node8u_step(float4 q0, float4 q1, float4 q2, float4 q3, v3 o, v3 invd, float tmax,
-                                            const STK& st, int& sp, uint32_t& ref) {
-    const uint32_t wx = __float_as_uint(q0.x), wy = __float_as_uint(q0.y), wz = __float_as_uint(q0.z);
-    const uint32_t hdr = __float_as_uint(q0.w);
-    const float sx = __uint_as_float((hdr & 0xFFu) << 23), sy = __uint_as_float(((hdr >> 8) & 0xFFu) << 23);
-    const float sz = __uint_as_float(((hdr >> 16) & 0xFFu) << 23);
-    const float ax = (__uint_as_float(wx & ~0x1FFu) - o.x) * invd.x, ay = (__uint_as_float(wy & ~0x1FFu) - o.y) * invd.y;
-    const float az = (__uint_as_float(wz & ~0x1FFu) - o.z) * invd.z;
-    const float bx = sx * invd.x, by = sy * invd.y, bz = sz * invd.z;
-    const bool fx = invd.x < 0.f, fy = invd.y < 0.f, fz = invd.z < 0.f;   // the near bound is hi on that axis
-    // q1 = {lo.x[0..3], lo.x[4..7], hi.x[0..3], hi.x[4..7]} as bytes; q2 the same for y, q3 for z
-    const uint32_t nx0 = __float_as_uint(fx ? q1.z : q1.x), nx1 = __float_as_uint(fx ? q1.w : q1.y);
-    const uint32_t gx0 = __float_as_uint(fx ? q1.x : q1.z), gx1 = __float_as_uint(fx ? q1.y : q1.w);
-    const uint32_t ny0 = __float_as_uint(fy ? q2.z : q2.x), ny1 = __float_as_uint(fy ? q2.w : q2.y);
-    const uint32_t gy0 = __float_as_uint(fy ? q2.x : q2.z), gy1 = __float_as_uint(fy ? q2.y : q2.w);
-    const uint32_t nz0 = __float_as_uint(fz ? q3.z : q3.x), nz1 = __float_as_uint(fz ? q3.w : q3.y);
-    const uint32_t gz0 = __float_as_uint(fz ? q3.x : q3.z), gz1 = __float_as_uint(fz ? q3.y : q3.w);
-    const uint32_t nc = hdr >> 28;
-    uint32_t key[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const int b = k & 3;
-        const bool h = k >= 4;
-        const float tnx = fmaf(ubyte_f(h ? nx1 : nx0, b), bx, ax), tfx = fmaf(ubyte_f(h ? gx1 : gx0, b), bx, ax);
-        const float tny = fmaf(ubyte_f(h ? ny1 : ny0, b), by, ay), tfy = fmaf(ubyte_f(h ? gy1 : gy0, b), by, ay);
-        const float tnz = fmaf(ubyte_f(h ? nz1 : nz0, b), bz, az), tfz = fmaf(ubyte_f(h ? gz1 : gz0, b), bz, az);
-        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
-        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tmax));
-        key[k] = ((uint32_t)k < nc && tn <= tf * 1.0000005f) ? ((__float_as_uint(tn) & 0x7FFFFFF8u) | (uint32_t)k)
-                                                             : 0xFFFFFFFFu;
-    }
-    const uint32_t kmin = min(min(min(key[0], key[1]), min(key[2], key[3])), min(min(key[4], key[5]), min(key[6], key[7])));
-    if (kmin == 0xFFFFFFFFu) return false;
-    const uint32_t near = kmin & 7u;
-    const uint32_t nin = (hdr >> 24) & 15u;
-    const uint32_t base = (wx & 0x1FFu) | ((wy & 0x1FFu) << 9) | ((wz & 0x1FFu) << 18);
-    const uint32_t lbase = 0x80000000u + base + ((nin + 1u) & ~1u) - 2u * nin;   // leaf slot k: lbase + 2k (wraps to bit 31 set)
-    auto refk = [&](uint32_t k) { return k < nin ? base + k : lbase + 2u * k; };
-    ref = refk(near);
-    if (__builtin_expect(sp <= STK::kLds - 8, 1)) {   // every slot written, sp advanced by the other hits
-#pragma unroll
-        for (int j = 7; j >= 0; j--) {
-            st.lds[sp * STK::kStride] = refk((uint32_t)j);
-            sp += (key[j] != 0xFFFFFFFFu && (uint32_t)j != near) ? 1 : 0;
-        }
-    } else {
-#pragma unroll
-        for (int j = 7; j >= 0; j--)
-            if (key[j] != 0xFFFFFFFFu && (uint32_t)j != near) { st.put(sp, refk((uint32_t)j)); sp++; }
-    }
-    return true;
-}
-
 // SDF records (an SDFShape, or a TransformedShape of one): their sphere tracing runs up to 1000
 // dependent steps, taken by the lane whose traversal meets the leaf.  The analytic half of a split
 // closest hit (k_wf_trace<.., SPLIT>) and of split shadow rays leaves the first SDF record of a ray in a
@@ -458,8 +397,10 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
     const v3 c0{q4.w, q5.x, q5.y}, c1{q5.z, q5.w, q6.x}, c2{q6.y, q6.z, q6.w}
 
 // Triangle-BVH traversal over leaf chunks (pt_api.hip build_tri_bvh).  The node step is
-// node8u_step's (8-wide quantized nodes in 64-B units); a leaf ref (bit 31) points at a 128-B chunk of up to
-// three triangles: a node step reads four 16-B pieces, a leaf step seven.
+// node8_step's (8-wide quantized nodes); a leaf ref points at a 128-B chunk of up to three
+// triangles, so an inner step and a leaf step read the same 128-B line's 16-B pieces and a
+// wave whose lanes are split between nodes and leaves pays for one set of load
+// instructions, not for the node loads plus a per-triangle load loop.
 template <bool COUNT, bool ANY, class STK>
 __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 invd, HitRec& best, const STK& stack,
                                              Counters& ctr) {
@@ -469,15 +410,13 @@ __device__ __forceinline__ bool traverse_tri(const DevScene& S, v3 o, v3 d, v3 i
     float tmax = tmax_bound(best.t);
     for (;;) {
         const bool leaf = (ref & 0x80000000u) != 0;
-        const float4* c = S.tri_units + 4 * (size_t)(ref & 0x7FFFFFFFu);
-        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3];
-        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3);
+        const float4* c = (leaf ? S.tri_chunks : S.tri_nodes) + 8 * (size_t)(ref & 0x1FFFFFFFu);
+        float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3], q4 = c[4], q5 = c[5], q6 = c[6], q7 = c[7];
+        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6); PT_PIN4(q7);
         if (!leaf) {
             if (COUNT) ctr.nodes++;
-            if (node8u_step(q0, q1, q2, q3, o, invd, tmax, stack, sp, ref)) continue;
+            if (node8_step(q0, q1, q2, q3, q4, q5, q6, q7, o, invd, tmax, stack, sp, ref)) continue;
         } else {
-            float4 q4 = c[4], q5 = c[5], q6 = c[6];   // a leaf chunk: two units
-            PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
             const uint32_t w0 = __float_as_uint(q0.x), cnt = (w0 >> 29) + 1u, first = w0 & 0x1FFFFFFFu;   // chunk word 0
             PT_CHUNK_TRIS(q0, q1, q2, q3, q4, q5, q6);
 #pragma unroll 1

@@ -52,19 +52,19 @@ struct DevLight {
 
 struct DevScene {
     // triangle BVH (world-space mesh + directly-added triangles)
-    const float4* tri_units;   // the 8-wide BVH's 64-B units (pt_bvh.h Bvh8UnitResult): a node in one (4 float4), a
-                               // leaf chunk of up to three triangles in two (8 float4; pt_api.hip build_tri_bvh)
+    const float4* tri_nodes;   // 2 float4 per node (pt::BvhNode)
     int32_t tri_num_nodes;
     const float4* tri_recs;    // 3 float4 per triangle: {v1.xyz,e1.x} {e1.yz,e2.xy} {e2.z,-,-,-}
+    const float4* tri_chunks;  // 8 float4 per triangle leaf (pt_api.hip build_tri_bvh)
     const float4* tri_shade;   // 3 float4 per triangle: {n1.xyz,n2.x} {n2.yz,n3.xy} {n3.z,mat,-,-}
     // analytic BVH (spheres, cubes)
     const float4* ana_nodes;
     int32_t ana_num_nodes;
     const float4* ana_recs;    // 3 float4: {a.xyz,kind} {b.xyz,scene index} {mat, radius(double) | ext index, -}
-    // ana_nodes (128-B BVH4 lines) and tri_units (64-B units) are one allocation, so a traversal step names
-    // its piece by a 32-bit float4 offset: 8·line for an analytic node, 4·(tri_unit0 + unit) for the triangles
+    // ana_nodes, tri_nodes and tri_chunks are one allocation of 128-B lines (in that order), so
+    // the cooperative fetch (pt_wavefront.hip coop_line) names any traversal line by a 32-bit index
     const float4* lines;
-    uint32_t tri_unit0, lines_n;   // lines_n: 128-B lines in `lines`
+    uint32_t tri_node_line0, tri_chunk_line0, lines_n;   // lines_n: 128-B lines in `lines`
     // the triangle BVH's root box (the union of the root node's child boxes): a refill traversal
     // whose ray misses it skips the triangle phase instead of spending a step on the root node
     float tri_box[6];          // lo.xyz, hi.xyz

@@ -699,22 +699,19 @@ __device__ __forceinline__ void trace_lanes(const DevScene& S, const WfQueues& Q
         // step loop then holds its state without spilling).  An analytic leaf reads its records in
         // prim_t; its line is not used.
         const bool leaf = (ref & 0x80000000u) != 0;
-        // a triangle node: one 64-B unit, four pieces; a leaf chunk or an analytic BVH4 node: seven pieces of its line
-        float4 q0, q1, q2, q3, q4 = make_float4(0.f, 0.f, 0.f, 0.f), q5 = q4, q6 = q4;
+        float4 q0, q1, q2, q3, q4, q5, q6, q7;
         {
-            const uint32_t at = tri ? 4u * (S.tri_unit0 + (ref & 0x7FFFFFFFu)) : (leaf ? 0u : 8u * ref);
+            const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
+                                          : (leaf ? 0u : ref));
             q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
-            PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3);
-            if (leaf || !tri) {
-                q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u];
-                PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
-            }
+            q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; q7 = S.lines[at + 7u];
         }
+        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6); PT_PIN4(q7);
         bool pop = true;
         if (!leaf) {
             if (COUNT) ctr.nodes++;
             if (tri) {   // the triangle BVH: 8-wide quantized nodes (pt_device.h node8_step)
-                pop = !node8u_step(q0, q1, q2, q3, o, invd, tmax, stack, sp, ref);
+                pop = !node8_step(q0, q1, q2, q3, q4, q5, q6, q7, o, invd, tmax, stack, sp, ref);
             } else {     // the analytic BVH4
                 float k0, k1, k2, k3;
                 uint32_t v0, v1, v2, v3r;
@@ -1417,22 +1414,19 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
         if (!has || waiting) continue;
         // one step: inner node or leaf of the current BVH (one 128-B line; see k_wf_trace_lanes)
         const bool leaf = (ref & 0x80000000u) != 0;
-        // a triangle node: one 64-B unit, four pieces; a leaf chunk or an analytic BVH4 node: seven pieces of its line
-        float4 q0, q1, q2, q3, q4 = make_float4(0.f, 0.f, 0.f, 0.f), q5 = q4, q6 = q4;
+        float4 q0, q1, q2, q3, q4, q5, q6, q7;
         {
-            const uint32_t at = tri ? 4u * (S.tri_unit0 + (ref & 0x7FFFFFFFu)) : (leaf ? 0u : 8u * ref);
+            const uint32_t at = 8u * (tri ? (leaf ? S.tri_chunk_line0 : S.tri_node_line0) + (ref & 0x1FFFFFFFu)
+                                          : (leaf ? 0u : ref));
             q0 = S.lines[at]; q1 = S.lines[at + 1u]; q2 = S.lines[at + 2u]; q3 = S.lines[at + 3u];
-            PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3);
-            if (leaf || !tri) {
-                q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u];
-                PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6);
-            }
+            q4 = S.lines[at + 4u]; q5 = S.lines[at + 5u]; q6 = S.lines[at + 6u]; q7 = S.lines[at + 7u];
         }
+        PT_PIN4(q0); PT_PIN4(q1); PT_PIN4(q2); PT_PIN4(q3); PT_PIN4(q4); PT_PIN4(q5); PT_PIN4(q6); PT_PIN4(q7);
         bool pop = true, blocked = false;
         if (!leaf) {
             if (COUNT) ctr.nodes++;
             if (tri) {   // the triangle BVH: 8-wide quantized nodes (pt_device.h node8_step)
-                pop = !node8u_step(q0, q1, q2, q3, o, invd, tmax, stack, sp, ref);
+                pop = !node8_step(q0, q1, q2, q3, q4, q5, q6, q7, o, invd, tmax, stack, sp, ref);
             } else {     // the analytic BVH4
                 float k0, k1, k2, k3;
                 uint32_t v0, v1, v2, v3r;

@@ -61,28 +61,6 @@ static bool slab8(const uint32_t* w, int k, const float o[3], const float invd[3
     tf = std::fmin(std::fmin(tfs[0], tfs[1]), std::fmin(tfs[2], tmax));
     return tn <= tf * 1.0000005f;   // (node8_step tests every slot: an empty one must miss by its bounds)
 }
-// node8u_step's slab test of slot k of a 64-B unit (fp32, fma, byte bounds), on the host
-static bool slab8u(const uint32_t* u, int k, const float o[3], const float invd[3], float tmax) {
-    if ((uint32_t)k >= (u[3] >> 28)) return false;   // the device masks slots past the child count
-    float tns[3], tfs[3];
-    for (int ax = 0; ax < 3; ax++) {
-        const uint32_t ob = u[ax] & ~0x1FFu;
-        float org;
-        std::memcpy(&org, &ob, 4);
-        const uint32_t sb = ((u[3] >> (8 * ax)) & 0xFFu) << 23;
-        float s;
-        std::memcpy(&s, &sb, 4);
-        const float a = (org - o[ax]) * invd[ax], b = s * invd[ax];
-        const bool flip = invd[ax] < 0.f;
-        const float ql = (float)((u[4 + 4 * ax + k / 4] >> (8 * (k & 3))) & 0xFFu);
-        const float qh = (float)((u[6 + 4 * ax + k / 4] >> (8 * (k & 3))) & 0xFFu);
-        tns[ax] = std::fmaf(flip ? qh : ql, b, a);
-        tfs[ax] = std::fmaf(flip ? ql : qh, b, a);
-    }
-    const float tn = std::fmax(std::fmax(tns[0], tns[1]), std::fmax(tns[2], 0.f));
-    const float tf = std::fmin(std::fmin(tfs[0], tfs[1]), std::fmin(tfs[2], tmax));
-    return tn <= tf * 1.0000005f;
-}
 // exact slab test of a box (fp64), entry before tmax
 static bool slab_exact(const Box& b, const float o[3], const float d[3], double tmax) {
     double tn = 0.0, tf = tmax;
@@ -230,94 +208,6 @@ static void run_case(const char* name, std::vector<float>& lo, std::vector<float
     std::printf("%s: %lld primitives, %zu nodes, %zu chunks, stack %d; rays: %ld primitive boxes tested, %ld entered, %ld "
                 "culled by the quantized tree, %ld empty slots hit\n", name, (long long)n, nn, b8.chunk_first.size(), b8.stack_need, tested, entered,
                 culled, empty_hits);
-
-    // ---- the 64-B unit format (pt_bvh.h pack_bvh8_units): the same tree re-laid, bounds re-quantized to bytes
-    pt::Bvh8UnitResult bu;
-    CHECK(pt::pack_bvh8_units(b8, bu));
-    const size_t nu = bu.count();
-    // walk the units from the root: every node and chunk unit reached once, each chunk's primitives inside every
-    // unit box on its path, every unit box a superset of the bvh8 box it re-quantizes
-    std::vector<int> unit_seen(nu, 0);
-    std::vector<std::vector<std::pair<uint32_t, int>>> upath(b8.chunk_first.size());
-    std::vector<std::pair<uint32_t, uint32_t>> utodo{{0u, 0u}};   // (unit, bvh8 node)
-    std::vector<std::vector<std::pair<uint32_t, int>>> unode_path(nn);
-    long u_outside = 0;
-    while (!utodo.empty()) {
-        const auto [un, nd] = utodo.back();
-        utodo.pop_back();
-        CHECK(un < nu && nd < nn);
-        if (un >= nu || nd >= nn) continue;
-        unit_seen[un]++;
-        const uint32_t* u = &bu.units[(size_t)un * pt::kUnitWords];
-        const uint32_t* w = &b8.words[(size_t)nd * pt::kNode8Words];
-        CHECK((u[3] >> 24) == (w[3] >> 24));   // the same n_in and n
-        const uint32_t nc = u[3] >> 28, nin = (u[3] >> 24) & 15u, base = pt::bvh8u_base(u);
-        CHECK(base % 2 == 0);   // chunks 128-B aligned
-        for (uint32_t k = 0; k < nc; k++) {
-            Box ub, wb;
-            pt::bvh8u_child_box(u, (int)k, ub.lo, ub.hi);
-            pt::bvh8_child_box(w, (int)k, wb.lo, wb.hi);
-            for (int ax = 0; ax < 3; ax++) CHECK(ub.lo[ax] <= wb.lo[ax] && ub.hi[ax] >= wb.hi[ax]);
-            if (k < nin) {
-                unode_path[w[4] + k] = unode_path[nd];
-                unode_path[w[4] + k].push_back({un, (int)k});
-                utodo.push_back({base + k, w[4] + k});
-            } else {
-                const uint32_t ch = (w[5] + k) & 0x7FFFFFFFu, cu = base + ((nin + 1u) & ~1u) + 2u * (k - nin);
-                CHECK(ch < bu.chunk_unit.size() && bu.chunk_unit[ch] == cu && cu + 1 < nu);
-                if (ch >= bu.chunk_unit.size() || cu + 1 >= nu) continue;
-                unit_seen[cu]++;
-                unit_seen[cu + 1]++;
-                upath[ch] = unode_path[nd];
-                upath[ch].push_back({un, (int)k});
-            }
-        }
-    }
-    for (size_t c = 0; c < upath.size(); c++)
-        for (const auto& [un, k] : upath[c]) {
-            Box sb;
-            pt::bvh8u_child_box(&bu.units[(size_t)un * pt::kUnitWords], k, sb.lo, sb.hi);
-            for (uint32_t t = b8.chunk_first[c]; t < b8.chunk_first[c] + b8.chunk_count[c]; t++)
-                for (int ax = 0; ax < 3; ax++)
-                    if (plo[3 * (size_t)b2.order[t] + ax] < sb.lo[ax] || phi[3 * (size_t)b2.order[t] + ax] > sb.hi[ax]) u_outside++;
-        }
-    CHECK(u_outside == 0);
-    long unused = 0;
-    for (size_t i = 0; i < nu; i++) { CHECK(unit_seen[i] <= 1); unused += unit_seen[i] == 0; }
-    CHECK(unused <= (long)nn + 1);   // padding units only (at most one per block, and the root's pair)
-    // rays: the fp32 byte-bound test never culls a box the exact test enters, and never enters a masked slot
-    std::mt19937 rng2(seed + 7);
-    long utested = 0, uentered = 0, uculled = 0, masked_hits = 0;
-    for (int r = 0; r < rays; r++) {
-        float o[3], d[3], invd[3];
-        const uint32_t target = (uint32_t)(U(rng2) * (float)n) % (uint32_t)n;
-        for (int k = 0; k < 3; k++) {
-            const float ext = ghi[k] - glo[k];
-            o[k] = (r % 3 == 0) ? glo[k] - ext * (r % 5 == 0 ? 1000.f : 1.f) + 3.f * ext * U(rng2)   // far away too
-                              : prim[target].lo[k] + (prim[target].hi[k] - prim[target].lo[k]) * U(rng2);
-            d[k] = U(rng2) * 2.f - 1.f;
-        }
-        if (r % 7 == 0) d[r % 3] = 0.f;
-        const float len = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-        if (len == 0.f) continue;
-        for (int k = 0; k < 3; k++) { d[k] /= len; invd[k] = 1.f / d[k]; }
-        const float tmax = (r % 2) ? INFINITY : (float)(0.1 + 3.0 * U(rng2));
-        for (int j = 0; j < 65; j++) {
-            const uint32_t p = j == 0 ? target : (uint32_t)(U(rng2) * (float)n) % (uint32_t)n;
-            utested++;
-            if (!slab_exact(prim[p], o, d, (double)tmax)) continue;
-            uentered++;
-            for (const auto& [un, k] : upath[chunk_of[p]]) {
-                const uint32_t* u = &bu.units[(size_t)un * pt::kUnitWords];
-                if (!slab8u(u, k, o, invd, tmax)) { uculled++; break; }
-                for (int e = (int)(u[3] >> 28); e < 8; e++) if (slab8u(u, e, o, invd, tmax)) masked_hits++;
-            }
-        }
-    }
-    CHECK(uculled == 0);
-    CHECK(masked_hits == 0);
-    std::printf("%s (64-B units): %zu units, %ld unused; rays: %ld primitive boxes tested, %ld entered, %ld culled\n", name, nu,
-                unused, utested, uentered, uculled);
 }
 
 int main(int argc, char** argv) {
