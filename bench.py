@@ -210,6 +210,9 @@ def parse(argv=None):
     p.add_argument("--height", type=int, default=None, help="default 1080 (c5: 2160)")
     p.add_argument("--adaptive", type=int, default=None,
                    help="Renderer.AdaptiveSamples (Renderer.cs:340-410; default 0, c5: 32 as Example.cs:355,412)")
+    p.add_argument("--firefly", type=int, default=0,
+                   help="Renderer.FireflySamples (Renderer.cs:412-470; Example.bunny sets 32, Example.cs:1100): per pass, "
+                        "pixels whose deviation exceeds 1 take up to N more samples, stopping at the first firefly")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     p.add_argument("--tris", type=int, default=None, help="mesh triangles (default: 1,000,000 for c4, 69,451 for c3)")
     p.add_argument("--seed", type=int, default=1234)
@@ -345,6 +348,7 @@ def main(argv=None):
         r = Renderer.NewRenderer(scene, camera, sampler, W, H, True, device=dev)
         r.SamplesPerPixel = a.spp
         r.AdaptiveSamples = a.adaptive
+        r.FireflySamples = a.firefly
         r.Seed = a.seed
         r.Engine = {"auto": 0, "mega": 1, "wave": 2}[a.engine]
         if a.shard:
@@ -588,7 +592,7 @@ def main(argv=None):
         "config": {
             "workload": WORKLOADS[a.workload],
             "width": W, "height": H, "spp_per_step": a.spp, "total_spp": a.spp * a.steps,
-            "adaptive_samples": a.adaptive,
+            "adaptive_samples": a.adaptive, **({"firefly_samples": a.firefly} if a.firefly else {}),
             "triangles": scene.Compile().num_triangles, "parallelism": f"tiles{world}" + (f" shard {a.shard}" if a.shard else "")
             + (f" (rehearsal: {world} ranks on {ndev.value} GPU(s))" if shared else "")
             + (f", gather {gather}" if gather else ""),
@@ -748,6 +752,7 @@ def main(argv=None):
             # the GPU renders the whole frame at the same spp, seed and pass index: the timed step's chunking
             r.ResetBuffer()
             r.SamplesPerPixel = spp
+            r.FireflySamples = 0   # (render_pixels runs the main samples; --firefly's phase is checked by the GPU tests)
             r._pass = 0
             r.RenderParallel()
             g = r.ReadBuffer()
