@@ -708,6 +708,45 @@ def main(argv=None):
             **extra,
         }
 
+    def shade_roofline():   # C4: the shade kernel beside the closest-hit roofline (VALU issue and bytes per vertex)
+        # algorithmic bytes per step: each vertex's queue entry (o, d, throughput, key: 64 B) and hit (16 B)
+        # read, the closest hit's triangle record and shading normals (96 B) per shading fetch, each child
+        # ray written (64 B: every closest-hit ray after the camera's) and each shadow request written
+        # (o, n, two fp64 weight pairs: 64 B); scaled from the counted pass to the timed region's rays
+        if not klaunch[_abi.K_SHADE]:
+            return None
+        cam_rays = W * H * cam_spp
+        per_pass = (ext_rays * (64 + 16) + ctr.shading_fetches * 96 + max(ext_rays - cam_rays, 0) * 64
+                    + ctr.shadow_rays * 64)
+        scale = rays / max(ctr.rays, 1)   # timed rays over the counted pass' rays (same ray mix)
+        sec = kms[_abi.K_SHADE] * 1e-3
+        gbs = per_pass * scale / max(sec, 1e-12) / 1e9
+        blk = {"kernel": names[_abi.K_SHADE], "ms_per_step": round(kms[_abi.K_SHADE] / a.steps, 3),
+               "launches": int(klaunch[_abi.K_SHADE]),
+               "bytes_per_vertex": round(per_pass / max(ext_rays, 1), 2), "vertices_per_step": round(ext_rays * scale / a.steps),
+               "achieved": round(gbs, 2), "unit": "GB/s", "frac_of_l2_peak": round(gbs / L2_PEAK_GBS, 5),
+               "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 5), "valu_issue_frac": None}
+        pv = os.path.join(ROOT, "profiles", "pmc_valu_mix_c4.json")
+        if os.path.exists(pv):
+            with open(pv) as f:
+                vm = json.load(f)
+            ks = {k: v for k, v in vm.get("kernels", {}).items() if k.startswith("k_wf_shade") and "miss" not in k}
+            if vm.get("library") == lib_id and ks:
+                issue = sum(v["valu_issue_cycles"] for v in ks.values())
+                busy = sum(v["busy_cycles_per_xcd"] for v in ks.values())
+                blk["valu_issue_frac"] = round(issue / max(1024 * busy, 1.0), 4)
+                # the mix's rays are all rays (closest hit + shadow) of the profiled passes: the same mix here
+                blk["valu_issue_cycles_per_vertex"] = round(issue / max(vm.get("rays_profiled", 1), 1)
+                                                            * ctr.rays / max(ext_rays, 1), 2)
+                blk["mix_source"] = f"profiles/pmc_valu_mix_c4.json ({vm.get('tag')}), same library"
+            else:
+                blk["mix_stale"] = True
+                blk["mix_library"] = vm.get("library")
+        return blk
+
+    if a.workload == "c4":
+        out["roofline"]["shade"] = shade_roofline()
+
     if a.workload in ("c2", "c5"):
         # C2 (fp64 sampler math, 16 children per camera hit) and C5 (the fp64 Volume / SDF marches) are
         # bound by VALU issue, not by bytes: the pass' measured VALU issue cycles per ray (instruction mix
