@@ -104,6 +104,12 @@ PT_HD uint64_t light_key(uint64_t k, uint32_t i) { return mix64(k ^ ((uint64_t)i
 PT_HD double draw(uint64_t k, uint32_t dim) {
     return (double)(mix64(k + (uint64_t)(dim + 1) * 0x9E3779B97F4A7C15ull) >> 11) * (1.0 / 9007199254740992.0);
 }
+// x / n for the sampler's stratum counts (n = FirstHitSamples' square root or its square, >= 1): when n
+// is a power of two its reciprocal is exact, and x · (1/n) is the same correctly rounded value as x / n
+// (fp64 division is a ~10-instruction sequence at the fp64 rate; C2's 16 children per camera hit
+// take two each).  strata_recip gives 1/n, or 0 for other n (then div_strata divides).
+PT_HD double strata_recip(int n) { return n > 0 && (n & (n - 1)) == 0 ? ldexp(1.0, -__builtin_ctz((unsigned)n)) : 0.0; }
+PT_HD double div_strata(double x, int n, double rn) { return rn != 0.0 ? x * rn : x / (double)n; }
 enum : uint32_t { D_STRATUM_U = 0, D_STRATUM_V = 1, D_REFLECT = 2, D_RUV_Z = 3, D_RUV_A = 4,
                   D_LIGHT = 5, D_SS_RUV_Z = 6, D_SS_RUV_A = 7, D_SS_XY = 8 };
 enum : uint32_t { D_JX = 0, D_JY = 1, D_LENS_ANGLE = 2, D_LENS_RADIUS = 3 };

@@ -89,8 +89,9 @@ __device__ __forceinline__ bool child_step(const DevScene& S, const DevSampler& 
     int stratum = c / nm;
     int u = stratum / n, v = stratum % n;
     uint64_t E = child_key(node, (uint32_t)c);
-    double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)n;
-    double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)n;
+    const double rn = strata_recip(n);   // pt_math.h div_strata
+    double fu = div_strata((double)u + draw(E, D_STRATUM_U), n, rn);
+    double fv = div_strata((double)(float)v + draw(E, D_STRATUM_V), n, rn);
     bool reflected;
     double p;
     bounce(m, sh, indir, fu, fv, mode, E, no, nd, reflected, p);
@@ -138,20 +139,21 @@ __device__ void sample_path(const DevScene& S, const DevSampler& smp, v3 o, v3 d
                     Shade sh = hit_info<COUNT, FULL>(S, h, o, d, ctr);
                     const DevMaterial& m = S.mats[sh.mat];
                     int n = (int)sqrt((double)samples);
-                    const double nsq = (double)(n * n);
+                    const double rsq = strata_recip(n * n);   // pt_math.h div_strata
                     bool alive = true;
                     if (m.emittance > 0) {
                         if (smp.dl && !emission) {
                             alive = false;
                         } else {
                             const double e = m.emittance * samples;
-                            fixreg_add3(acc, thr[0] * ((sh.col[0] * e) / nsq), thr[1] * ((sh.col[1] * e) / nsq),
-                                        thr[2] * ((sh.col[2] * e) / nsq));
+                            fixreg_add3(acc, thr[0] * div_strata(sh.col[0] * e, n * n, rsq),
+                                        thr[1] * div_strata(sh.col[1] * e, n * n, rsq),
+                                        thr[2] * div_strata(sh.col[2] * e, n * n, rsq));
                         }
                     }
                     if (alive) {
                         int nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
-                        double t2[3] = {thr[0] / nsq, thr[1] / nsq, thr[2] / nsq};
+                        double t2[3] = {div_strata(thr[0], n * n, rsq), div_strata(thr[1], n * n, rsq), div_strata(thr[2], n * n, rsq)};
                         if (n * n * nm == 1) {
                             // chain vertex: its only child is processed inline
                             double nthr[3];

@@ -848,19 +848,19 @@ __device__ __forceinline__ void shade_vertex(const DevScene& S, const DevSampler
         const DevMaterial& m = S.mats[mat];
         const int samples = depth == 0 ? smp.fh : 1;
         nn = (int)sqrt((double)samples);
-        const double nsq = (double)(nn * nn);   // result.DivScalar(n * n) (Sampler.cs:144)
+        const double rsq = strata_recip(nn * nn);   // result.DivScalar(n * n) (Sampler.cs:144): 1 / (n·n) when exact
         if (m.emittance > 0) {
             if (smp.dl && !emission) {
                 alive = false;  // Sampler.cs:75-78
             } else {
                 const double e = m.emittance * samples;   // Color.MulScalar(Emittance * samples) (Sampler.cs:79)
-                for (int k = 0; k < 3; k++) cc[k] = thr[k] * ((sh.col[k] * e) / nsq);
+                for (int k = 0; k < 3; k++) cc[k] = thr[k] * div_strata(sh.col[k] * e, nn * nn, rsq);
                 has_c = true;
             }
         }
         nm = (smp.spec_mode == 2 || (depth == 0 && smp.spec_mode == 1)) ? 2 : 1;
         nch = alive ? nn * nn * nm : 0;
-        for (int k = 0; k < 3; k++) t2[k] = thr[k] / nsq;
+        for (int k = 0; k < 3; k++) t2[k] = div_strata(thr[k], nn * nn, rsq);
         pv = vertex_p(m, sh, d, n1, n2);
     }
     fix_add_wave(Q.acc, pixel, has_c, cc[0], cc[1], cc[2]);
@@ -882,6 +882,8 @@ __device__ __forceinline__ void shade_children(const DevScene& S, const DevSampl
     const DevMaterial& m = S.mats[sh.mat];
     const int ma = nm == 2 ? 1 : 0;
     const bool ext_on = depth + 1 <= smp.mb;   // deeper samples return black without an Intersect
+    const double rn = strata_recip(nn);        // 1 / nn when exact (pt_math.h div_strata)
+    const int lg = rn != 0.0 ? __builtin_ctz((unsigned)nn) : 0;
     // child c: mode, reflect decision, liveness (p > 0 after the Any-mode override)
     // Block-wide child-major slots (below): each wave's count of child c's extension rays
     // and NEE requests goes to LDS here, ahead of the reservation's barriers.
@@ -892,9 +894,11 @@ __device__ __forceinline__ void shade_children(const DevScene& S, const DevSampl
     __shared__ uint32_t s_cc[kBlockMajorChildren][4][2];
     const bool block_major = smp.fh <= kBlockMajorFH;   // kernel-uniform: every depth's children fit s_cc
     uint32_t n_ext = 0, n_nee = 0;
+    uint64_t rbits = 0;   // the reflect decisions of children 0..63, kept for the second loop (one draw each)
     for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
-        const int mode = ma + c % nm;
+        const int mode = ma + (nm == 2 ? c & 1 : 0);   // nm is 1 or 2
         const bool refl = mode == 2 || (mode == 0 && c < nch && draw(child_key(node, (uint32_t)c), D_REFLECT) < pv);
+        rbits |= refl && c < 64 ? 1ull << c : 0ull;
         const bool live = c < nch && (mode == 0 || (refl ? pv > 0 : (1 - pv) > 0));
         const bool ee = live && ext_on, en = live && !refl && !m.transparent && nee_on;
         n_ext += ee ? 1u : 0u;
@@ -918,9 +922,10 @@ __device__ __forceinline__ void shade_children(const DevScene& S, const DevSampl
     // more children per vertex than s_cc holds, each wave fills its own share that way.
     uint32_t ej = block_major ? blk_e : __shfl(ebase, 0, 64), nj = block_major ? blk_n : __shfl(nbase, 0, 64);
     for (int c = 0; c < cmax; c++) {   // wave-uniform trip count: the ballots need every lane
-        const int mode = ma + c % nm;
+        const int mode = ma + (nm == 2 ? c & 1 : 0);
         const uint64_t E = child_key(node, (uint32_t)c);
-        const bool refl = mode == 2 || (mode == 0 && c < nch && draw(E, D_REFLECT) < pv);
+        const bool refl = c < 64 ? ((rbits >> c) & 1ull) != 0
+                                 : mode == 2 || (mode == 0 && c < nch && draw(E, D_REFLECT) < pv);
         const bool live = c < nch && (mode == 0 || (refl ? pv > 0 : (1 - pv) > 0));
         const bool reflected = refl || m.transparent;                 // specular branch (Sampler.cs:109-115)
         const bool emit_nee = live && !reflected && nee_on;
@@ -973,10 +978,10 @@ __device__ __forceinline__ void shade_children(const DevScene& S, const DevSampl
             }
         }
         if (!ext_on) continue;
-        const int stratum = c / nm;
-        const int u = stratum / nn, v = stratum % nn;
-        const double fu = ((double)u + draw(E, D_STRATUM_U)) / (double)nn;
-        const double fv = ((double)(float)v + draw(E, D_STRATUM_V)) / (double)nn;
+        const int stratum = nm == 2 ? c >> 1 : c;
+        const int u = rn != 0.0 ? stratum >> lg : stratum / nn, v = rn != 0.0 ? stratum & (nn - 1) : stratum % nn;
+        const double fu = div_strata((double)u + draw(E, D_STRATUM_U), nn, rn);
+        const double fv = div_strata((double)(float)v + draw(E, D_STRATUM_V), nn, rn);
         v3 no, nd;
         bounce_dir(m, sh, d, fu, fv, refl, n1, n2, E, no, nd);
         if (my_e < Q.pcap) {
