@@ -1390,6 +1390,7 @@ int pt_upload_scene(void* ctx, const pt_scene_desc* d) {
     rc = upload(c, heavy, &S.heavy); if (rc) return rc;
     S.num_planes = (int32_t)plane_scene.size();
     S.num_lights = (int32_t)lights.size();
+    S.num_mats = (int32_t)mats.size();
     for (int k = 0; k < 3; k++) S.env[k] = d->env_color[k];
     PT_HIP(hipStreamSynchronize(c->stream));
     c->S = S;

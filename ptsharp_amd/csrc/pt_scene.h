@@ -74,6 +74,7 @@ struct DevScene {
     const DevMaterial* mats;
     const DevLight* lights;
     int32_t num_lights;
+    int32_t num_mats;          // entries of mats (k_wf_shade stages a small table in LDS)
     double env[3];              // Scene.Color (fp64 Colour)
     // textures (§8f row 3)
     const DevTexture* texs;

@@ -128,6 +128,9 @@ constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera sl
 #ifndef PT_SHADE_MISS
 #define PT_SHADE_MISS 1   // routed shade: a textured environment's misses in k_wf_shade_miss (0: in the FULL shade)
 #endif
+#ifndef PT_SHADE_LDS
+#define PT_SHADE_LDS 1     // k_wf_shade reads a small scene's materials and lights from LDS (stage_shading)
+#endif
 #ifndef PT_SHADE_SCAN
 #define PT_SHADE_SCAN 8    // rows of 256 per SCAN claim: 16 best before claims carried their partial round, 8 since
                            // (C4 5836 / 5885 / 5743 for 16 / 8 / 32; the 1/8 share 5099 / 5208 / 4735)
@@ -1000,9 +1003,33 @@ __device__ __forceinline__ void shade_children(const DevScene& S, const DevSampl
 // at a time: each round trip of the chain (claim, queue loads, triangle record,
 // reservation) serves four times as many vertices.  Otherwise the block shades every
 // claimed slot (no extra read of the hit records, fewer live registers).
+// A scene's materials and lights, when few, staged in the shade block's LDS: a vertex' material (after its
+// triangle record), its light (after the light draw) and that light's material are dependent loads of the
+// shading chain; from LDS each costs an LDS round trip instead of an L1 / L2 one.  Returns the scene view
+// that reads them there (flat loads).  Block-uniform call.
+constexpr int kLdsMats = 32, kLdsLights = 16;
+static_assert(sizeof(DevMaterial) % 8 == 0 && sizeof(DevLight) % 8 == 0, "stage_shading copies 8-B words");
+__device__ __forceinline__ DevScene stage_shading(const DevScene& S0) {
+    __shared__ unsigned long long s_mats[kLdsMats * sizeof(DevMaterial) / 8];
+    __shared__ unsigned long long s_lights[kLdsLights * sizeof(DevLight) / 8];
+    DevScene S = S0;
+    if (S0.num_mats > kLdsMats || S0.num_lights > kLdsLights) return S;
+    const uint32_t nm = (uint32_t)S0.num_mats * (uint32_t)(sizeof(DevMaterial) / 8);
+    const uint32_t nl = (uint32_t)S0.num_lights * (uint32_t)(sizeof(DevLight) / 8);
+    const unsigned long long* gm = reinterpret_cast<const unsigned long long*>(S0.mats);
+    const unsigned long long* gl = reinterpret_cast<const unsigned long long*>(S0.lights);
+    for (uint32_t k = threadIdx.x; k < nm; k += blockDim.x) s_mats[k] = gm[k];
+    for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) s_lights[k] = gl[k];
+    __syncthreads();
+    S.mats = reinterpret_cast<const DevMaterial*>(s_mats);
+    S.lights = reinterpret_cast<const DevLight*>(s_lights);
+    return S;
+}
+
 template <bool COUNT, bool FULL, bool SCAN>
-__global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) void k_wf_shade(DevScene S, DevSampler smp, WfQueues Q, int qi,
+__global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) void k_wf_shade(DevScene S0, DevSampler smp, WfQueues Q, int qi,
                                                                   unsigned long long* counters, int form) {
+    const DevScene& S = S0;   // the kernel argument until the block knows it runs (stage_shading below)
     uint32_t queued = 0;
     for (int g = 0; g < kParts; g++) queued += min(*ray_count(Q, qi, g), Q.pcap);
     // SCAN unless (nearly) every queued ray has work: with its partial rounds carried over it
@@ -1016,6 +1043,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
                            : FULL ? 2ull * kept < (unsigned long long)queued
                                                      : 32ull * kept < 31ull * (unsigned long long)queued;
     if (scan != SCAN) return;
+    const DevScene Sv = PT_SHADE_LDS ? stage_shading(S0) : S0;
     if (blockIdx.x == 0 && threadIdx.x < kParts) {
         Q.counts[fetch_word(2 + (1 - qi), threadIdx.x)] = 0u;   // the fetch cursors of the shadow rays it writes
         Q.counts[fetch_word(0, threadIdx.x)] = 0u;              // the next k_wf_trace's (it may run beside k_wf_shadow)
@@ -1038,7 +1066,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             __syncthreads();
             const uint32_t k0 = s_k0;  // thread 0 rewrites it only after block_reserve2's barriers
             if (k0 >= n) break;
-            shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + k0 + threadIdx.x, k0 + threadIdx.x < n, ctr);
+            shade_vertex<COUNT, FULL>(Sv, smp, Q, qi, G, base + k0 + threadIdx.x, k0 + threadIdx.x < n, ctr);
         }
     } else {
         const bool env_black = (!FULL || S.env_tex < 0) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
@@ -1103,7 +1131,7 @@ __global__ __launch_bounds__(256, FULL ? PT_FULL_SHADE_WAVES : PT_SHADE_WAVES) v
             const uint32_t full = last ? total : total & ~255u;
             for (uint32_t r = 0; r < full; r += 256u) {   // block-uniform
                 const bool listed = r + threadIdx.x < full;
-                shade_vertex<COUNT, FULL>(S, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed, ctr,
+                shade_vertex<COUNT, FULL>(Sv, smp, Q, qi, G, base + (listed ? s_list[r + threadIdx.x] : 0u), listed, ctr,
                                           &s_hit[r + threadIdx.x]);
                 __syncthreads();   // the next round rewrites shade_vertex's LDS child counts
             }
