@@ -795,12 +795,14 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
 
 // t of the light's own primitive along (o, d), exactly as the closest-hit query computes it.
 template <bool FULL>
-__device__ __forceinline__ double light_t(const DevScene& S, const DevLight& L, v3 o, v3 d) {
+// lrec (may be null): the light's own record (3 float4), staged in LDS by the shadow kernels
+__device__ __forceinline__ double light_t(const DevScene& S, const DevLight& L, v3 o, v3 d, const float4* lrec = nullptr) {
     if (L.kind == KIND_PLANE) {
         float4 a = S.planes[2 * L.index], b = S.planes[2 * L.index + 1];
         return isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
     }
     int32_t kind;
+    if (lrec) return prim_t<false, FULL>(S, lrec, 0u, o, d, kind);
     return prim_t<false, FULL>(S, S.ana_recs, (uint32_t)L.index, o, d, kind);
 }
 
@@ -839,7 +841,7 @@ __device__ __forceinline__ bool any_nearer(const DevScene& S, v3 o, v3 d, double
 // then "is any primitive strictly nearer" (any-hit, early exit).  Counts one ray.
 template <bool COUNT, bool FULL, class STK>
 __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight& L, v3 o, v3 d, const STK& stack,
-                                              Counters& ctr) {
+                                              Counters& ctr, const float4* lrec = nullptr) {
     ctr.rays++;
     if (L.phantom) {
         // a struct Triangle light never equals the re-boxed hit shape; the reference still
@@ -849,7 +851,7 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
         traverse_tri<COUNT, true>(S, o, d, invd, h, stack, ctr);
         return false;
     }
-    const double tl = light_t<FULL>(S, L, o, d);
+    const double tl = light_t<FULL>(S, L, o, d, lrec);
     if (!(tl < kHitInf)) return false;
     return !any_nearer<COUNT, FULL>(S, o, d, tl, stack, ctr);
 }

@@ -131,6 +131,9 @@ constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera sl
 #ifndef PT_SHADE_LDS
 #define PT_SHADE_LDS 1     // k_wf_shade reads a small scene's materials and lights from LDS (stage_shading)
 #endif
+#ifndef PT_SHADOW_LDS
+#define PT_SHADOW_LDS 1    // the lean shadow kernels read a small scene's lights and their records from LDS (stage_lights)
+#endif
 #ifndef PT_SHADE_SCAN
 #define PT_SHADE_SCAN 8    // rows of 256 per SCAN claim: 16 best before claims carried their partial round, 8 since
                            // (C4 5836 / 5885 / 5743 for 16 / 8 / 32; the 1/8 share 5099 / 5208 / 4735)
@@ -1189,11 +1192,40 @@ __global__ __launch_bounds__(256) void k_wf_shade_miss(DevScene S, WfQueues Q, i
 #ifndef PT_SHADOW_WAVES
 #define PT_SHADOW_WAVES 7   // lockstep shadow kernel; the refill one runs PT_LANES_WAVES
 #endif
+// The lean shadow kernels' lights in LDS (LDSL: the scene has at most kLdsLights lights; the kernels
+// run their LDSL = false form otherwise): each light and its own record, the one light_t intersects.  A
+// shadow ray's light index comes from its queue entry, so the light and then its record were two dependent
+// loads ahead of the ray's first traversal step.
+template <bool LDSL>
+struct LightLds {
+    const DevLight* l;   // LDSL: kLdsLights lights in LDS
+    const float4* r;     // LDSL: 3 float4 per light, its ana_recs record
+    __device__ __forceinline__ const DevLight& light(const DevScene& S, uint32_t li) const { return LDSL ? l[li] : S.lights[li]; }
+    __device__ __forceinline__ const float4* rec(uint32_t li) const { return LDSL ? r + 3 * li : nullptr; }   // null: ana_recs
+};
+template <bool LDSL>
+__device__ __forceinline__ LightLds<LDSL> stage_lights(const DevScene& S) {   // block-uniform call
+    if constexpr (!LDSL) {
+        return LightLds<false>{nullptr, nullptr};
+    } else {
+        __shared__ DevLight s_l[kLdsLights];
+        __shared__ float4 s_r[kLdsLights * 3];
+        for (uint32_t k = threadIdx.x; k < (uint32_t)S.num_lights; k += blockDim.x) {
+            const DevLight L = S.lights[k];
+            s_l[k] = L;
+            if (L.kind != KIND_PLANE && !L.phantom)
+                for (int j = 0; j < 3; j++) s_r[3 * k + j] = S.ana_recs[3 * (size_t)L.index + j];
+        }
+        __syncthreads();
+        return LightLds<true>{s_l, s_r};
+    }
+}
+
 // One thread per shadow ray that k_wf_shade set up (light, direction, the colour the
 // light adds if it is the nearest hit): the visibility query of Sampler.cs:261-265.
 // SPLIT (FULL only): the analytic half of split shadow rays: the rays the refill kernel left lit.
-template <bool COUNT, bool FULL, bool SPLIT = false>
-__global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+template <bool COUNT, bool FULL, bool SPLIT, bool LDSL>
+__device__ __forceinline__ void shadow_rays(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters) {
     __shared__ uint32_t s_stack[kLdsStack * kTB];
     const WStack stack{s_stack + threadIdx.x, Q.ovf_sh + blockIdx.x * kTB + threadIdx.x, gridDim.x * kTB};
     const Group G = xcd_group();
@@ -1203,6 +1235,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
     uint32_t* cursor = Q.counts + fetch_word(SPLIT ? 5 + qo : 2 + qo, G.g);
     const uint32_t lane = threadIdx.x & 63;
     Counters ctr{0, 0, 0, 0};
+    const LightLds<LDSL> LL = stage_lights<LDSL>(S);
     for (;;) {  // kFetchBatches × 64 rays per claim, 64 at a time (see k_wf_trace)
         uint32_t kc = 0;
         if (lane == 0) kc = atomicAdd(cursor, 64u * kFetchBatches);
@@ -1245,8 +1278,9 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
                 if (!blocked) continue;
             } else if (li != kDead) {
                 const float4 a = nt_load(&Q.n_o[qo][i]);
-                const DevLight L = S.lights[li];
-                lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr);
+                const DevLight L = LL.light(S, li);
+                lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr,
+                                                 LL.rec(li));
             }
             Q.n_lit[qo][i] = lit ? 1 : 0;   // k_wf_nee_accum adds the lit rays' terms
         }
@@ -1260,6 +1294,11 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
             atomicAdd(&counters[6], (unsigned long long)prims);
         }
     }
+}
+// LDSL (lean, at most kLdsLights lights; the launch decides): the lights in LDS (stage_lights)
+template <bool COUNT, bool FULL, bool SPLIT = false, bool LDSL = false>
+__global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES) void k_wf_shadow(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+    shadow_rays<COUNT, FULL, SPLIT, LDSL && !FULL>(S, Q, qo, counters);
 }
 
 // Shadow visibility with per-lane refill (triangle scenes; see k_wf_trace_lanes): the
@@ -1277,7 +1316,7 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
 // wave refills only when every lane is idle — then no helper and no waiting root is
 // left, so the refill may reset s_help — and hands stack entries to idle lanes from its first claim on.
 // Uncounted passes add the hand-offs to counters[11].
-template <bool COUNT, bool SPLIT = false, bool EARLY = false>
+template <bool COUNT, bool SPLIT, bool EARLY, bool LDSL>
 __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& Q, int qo, unsigned long long* counters) {
     constexpr bool split = SPLIT;
     __shared__ uint32_t s_stack[kLdsStack * kTB];
@@ -1301,6 +1340,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
     __shared__ uint32_t s_map[kTB];   // per wave: donor lane by rank
     __shared__ uint32_t s_handoffs[kTB / 64];   // per wave: tail hand-offs
     if (lane == 0) s_handoffs[threadIdx.x >> 6] = 0u;
+    const LightLds<LDSL> LL = stage_lights<LDSL>(S);
     bool helper = false;
     uint32_t root = threadIdx.x;
     const uint32_t wbase = threadIdx.x & ~63u;
@@ -1353,7 +1393,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                     Q.n_lit[qo][i] = 0;
                 } else {   // light_visible (pt_device.h), head part
                     ctr.rays++;
-                    const DevLight L = S.lights[li];
+                    const DevLight L = LL.light(S, li);
                     o = v3{a.x, a.y, a.z};
                     d = v3{b.x, b.y, b.z};
                     invd = v3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
@@ -1364,7 +1404,7 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
                         run = S.tri_num_nodes > 0;
                         tri = true;
                     } else {
-                        tl = light_t<false>(S, L, o, d);
+                        tl = light_t<false>(S, L, o, d, LL.rec(li));
                         run = tl < kHitInf;
                         for (int p = 0; run && p < S.num_planes; p++) {
                             const float4 pa = S.planes[2 * p], pb = S.planes[2 * p + 1];
@@ -1530,9 +1570,10 @@ __device__ __forceinline__ void shadow_lanes(const DevScene& S, const WfQueues& 
         }
     }
 }
-template <bool COUNT, bool SPLIT = false, bool EARLY = false>
+// LDSL (at most kLdsLights lights; the launch decides): the lights in LDS (stage_lights)
+template <bool COUNT, bool SPLIT = false, bool EARLY = false, bool LDSL = false>
 __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr(PT_LANES_VGPRS))) void k_wf_shadow_lanes(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
-    shadow_lanes<COUNT, SPLIT, EARLY>(S, Q, qo, counters);
+    shadow_lanes<COUNT, SPLIT, EARLY, LDSL>(S, Q, qo, counters);
 }
 
 // ---------------------------------------------------------------- direct-light terms
@@ -1552,21 +1593,24 @@ __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsign
     const size_t base = (size_t)G.g * Q.spcap;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lit_n = 0, runs = 0;
-    auto row = [&](uint32_t j, const LdsFix* T) {   // slots j .. j + 63 of this wave (wave-uniform)
-        bool lit = false;
-        uint32_t pixel = 0;
-        double2 w01 = make_double2(0.0, 0.0), w2 = w01;
+    // One slot's flag and weights.  The weights are loaded with the flag, not after it (an unlit slot's are
+    // read and dropped: one round trip per row instead of two), and the window's next row is loaded before
+    // this row's sums run.
+    struct Slot { bool lit; double2 w01, w2; };
+    auto fetch = [&](uint32_t j) {
+        Slot x{false, make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
         if (j < n) {
             const size_t i = base + j;
-            lit = Q.n_lit[qo][i] != 0;
-            if (lit) {
-                w01 = nt_load(&Q.n_w[qo][2 * i]);
-                w2 = nt_load(&Q.n_w[qo][2 * i + 1]);
-                pixel = (uint32_t)__double_as_longlong(w2.y);
-            }
+            x.lit = Q.n_lit[qo][i] != 0;
+            x.w01 = nt_load(&Q.n_w[qo][2 * i]);
+            x.w2 = nt_load(&Q.n_w[qo][2 * i + 1]);
         }
-        const uint32_t r = fix_add_wave(Q.acc, pixel, lit, w01.x, w01.y, w2.x, T);
-        if (COUNT) { runs += r; lit_n += (uint32_t)__popcll(__ballot(lit)); }
+        return x;
+    };
+    auto row = [&](const Slot& x, const LdsFix* T) {   // one row of 64 slots of this wave (wave-uniform)
+        const uint32_t pixel = x.lit ? (uint32_t)__double_as_longlong(x.w2.y) : 0u;
+        const uint32_t r = fix_add_wave(Q.acc, pixel, x.lit, x.w01.x, x.w01.y, x.w2.x, T);
+        if (COUNT) { runs += r; lit_n += (uint32_t)__popcll(__ballot(x.lit)); }
     };
     // A pixel's light terms of one depth sit in runs of consecutive slots, one run per child index
     // of its vertex (the child-major fill): a block takes windows of kAccWin·256 slots, sums the
@@ -1581,7 +1625,12 @@ __global__ __launch_bounds__(256) void k_wf_nee_accum(WfQueues Q, int qo, unsign
     }
     __syncthreads();
     for (uint32_t w0 = G.lb * 256u * kAccWin; w0 < n; w0 += G.nb * 256u * kAccWin) {   // block-uniform
-        for (uint32_t r = 0; r < kAccWin; r++) row(w0 + r * 256u + threadIdx.x, &T);
+        Slot cur = fetch(w0 + threadIdx.x);
+        for (uint32_t r = 0; r < kAccWin; r++) {
+            const Slot nxt = r + 1 < kAccWin ? fetch(w0 + (r + 1) * 256u + threadIdx.x) : Slot{false, {0.0, 0.0}, {0.0, 0.0}};
+            row(cur, &T);
+            cur = nxt;
+        }
         __syncthreads();
         for (uint32_t e = threadIdx.x; e < kAccTable; e += 256u) {
             const uint32_t k = s_key[e];
@@ -1772,6 +1821,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     // Per-lane refill traversal (k_wf_trace_lanes, k_wf_shadow_lanes) where rays are long
     // enough to pay for it: lean scenes with a triangle BVH of more than kLanesMinNodes nodes.
     const bool lanes = !fullg && (plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes);
+    const bool ldsl = PT_SHADOW_LDS && S.num_lights <= kLdsLights;   // the lean shadow kernels' lights in LDS
     // Split traversal (row-4 scenes with a triangle BVH): the lean refill kernels take the planes and
     // the triangles at their occupancy, then the FULL lockstep kernels add the analytic BVH (where
     // the §8f row-4 shapes live) from that result (pt_device.h trace_ana / ana_blocked; routed:
@@ -1889,8 +1939,10 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
         else if (fullg) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (lanes && count) hipLaunchKernelGGL((k_wf_shadow_lanes<true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (lanes && Q.tail_early) hipLaunchKernelGGL((k_wf_shadow_lanes<false, false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (lanes && ldsl) hipLaunchKernelGGL((k_wf_shadow_lanes<false, false, false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (lanes) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (ldsl) hipLaunchKernelGGL((k_wf_shadow<false, false, false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         end_k(3, side);
         begin_k(6, side);   // PT_K_ACCUM
