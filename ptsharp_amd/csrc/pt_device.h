@@ -385,6 +385,10 @@ __device__ __forceinline__ bool traverse(const DevScene& S, const float4* __rest
 // Pin loaded values so the compiler keeps each aligned 16-B load whole (left alone it
 // re-splits them along the consumers' 12-B vertex fields into unaligned pieces).
 #define PT_PIN4(q) asm volatile("" : "+v"((q).x), "+v"((q).y), "+v"((q).z), "+v"((q).w))
+// Two loads pinned together: both are issued before the one wait the pin needs (a pin of one value
+// after its load makes the compiler wait for it before it issues the next)
+#define PT_PIN44(p, q) asm volatile("" : "+v"((p).x), "+v"((p).y), "+v"((p).z), "+v"((p).w), \
+                                         "+v"((q).x), "+v"((q).y), "+v"((q).z), "+v"((q).w))
 
 
 // The triangles of a leaf chunk (pt_api.hip build_tri_bvh): word 0 = the first triangle

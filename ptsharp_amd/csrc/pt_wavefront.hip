@@ -326,12 +326,15 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
         for (uint32_t k0 = kc; k0 < kc + 64u * kFetchBatches && k0 < n; k0 += 64u) {
             if (k0 + lane >= n) continue;
             const uint32_t i = route ? Q.hq[base + k0 + lane] : base + k0 + lane;
+            // both queue loads before the dead test: one round trip per ray, not two (the pin keeps the
+            // compiler from sinking the origin's load behind the test)
             float4 b = nt_load(&Q.q_d[qi][i]);
+            float4 a = nt_load(&Q.q_o[qi][i]);
+            PT_PIN44(b, a);
             if (__float_as_uint(b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
                 hit_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
                 continue;
             }
-            float4 a = nt_load(&Q.q_o[qi][i]);
             HitRec h;
             if constexpr (SPLIT) {
                 const uint4 r = Q.hits[i];   // the planes' and triangles' hit (k_wf_trace_lanes, split)
@@ -1246,10 +1249,11 @@ __device__ __forceinline__ void shadow_rays(const DevScene& S, const WfQueues& Q
             const uint32_t i = route ? Q.hq_sh[base + k0 + lane] : base + k0 + lane;
             if (SPLIT && Q.n_lit[qo][i] == 0) continue;   // blocked (or dead) in the refill half
             bool lit = false;
-            const float4 b = nt_load(&Q.n_n[qo][i]);
+            float4 b = nt_load(&Q.n_n[qo][i]);
+            float4 a = nt_load(&Q.n_o[qo][i]);   // with n_n, before the dead test: one round trip per ray
+            PT_PIN44(b, a);
             const uint32_t li = __float_as_uint(b.w);
             if (SPLIT) {
-                const float4 a = nt_load(&Q.n_o[qo][i]);
                 int32_t sdf = -1, vol = -1;
                 int32_t* const vol_out = Q.volq_sh ? &vol : nullptr;   // Volumes deferred to k_wf_vol_shadow
                 double tl = 0;
@@ -1277,7 +1281,6 @@ __device__ __forceinline__ void shadow_rays(const DevScene& S, const WfQueues& Q
                 }
                 if (!blocked) continue;
             } else if (li != kDead) {
-                const float4 a = nt_load(&Q.n_o[qo][i]);
                 const DevLight L = LL.light(S, li);
                 lit = light_visible<COUNT, FULL>(S, L, v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, stack, ctr,
                                                  LL.rec(li));
