@@ -394,12 +394,23 @@ def main(argv=None):
     # kernel <false, true, true> on the rays that reach a row-4 box, then the deferred Volume and SDF
     # records' kernels; the class times them together)
     split = fullg and lanes
+    # a few spheres / cubes (at most 8) and planes (at most 8), no triangles: the linear kernels
+    # (pt_wavefront.hip k_wf_trace_linear / k_wf_shadow_linear); lean shadow kernels read a scene's lights
+    # from LDS (their <.., true> forms) when it has at most 16
+    n_ana = len(fl.sphere_radius) + len(fl.cube_min)
+    linear = not fullg and not lanes and fl.num_triangles == 0 and 0 < n_ana <= 8 and len(fl.plane_point) <= 8
+    emits = np.array([m.emittance > 0 for m in fl.materials] + [False])
+    n_lights = sum(int(emits[np.asarray(arr, dtype=np.int64)].sum()) for arr in
+                   (fl.sphere_material, fl.cube_material, fl.plane_material, fl.tri_material) if len(arr))
+    ldsl = ", true" if n_lights <= 16 else ""
     trace_name = ("k_wf_trace_lanes<false, true> + k_wf_trace<false, true, true> + k_wf_vol_hits + k_wf_sdf_hits"
                   if split else "k_wf_trace<false, true>" if fullg else "k_wf_trace_lanes<false, false>" if lanes
-                  else "k_wf_trace<false, false>")
+                  else "k_wf_trace_linear<false>" if linear else "k_wf_trace<false, false>")
     shadow_name = ("k_wf_shadow_lanes<false, true> + k_wf_shadow<false, true, true> + k_wf_vol_shadow + k_wf_sdf_shadow"
-                   if split else "k_wf_shadow<false, true>" if fullg else "k_wf_shadow_lanes<false, false>" if lanes
-                   else "k_wf_shadow<false, false>")
+                   if split else "k_wf_shadow<false, true>" if fullg
+                   else f"k_wf_shadow_lanes<false, false{', false' + ldsl if ldsl else ''}>" if lanes
+                   else f"k_wf_shadow_linear<false{ldsl or ', false'}>" if linear
+                   else f"k_wf_shadow<false, false{', false' + ldsl if ldsl else ''}>")
     shade_name = "k_wf_shade<false, true, *>" if full else "k_wf_shade<false, false, *>"
 
     # Passes per call: a rank's 1/N share of the frame is batched N passes per call (the Buffer is

@@ -1481,6 +1481,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     plan.lanes_shadow_blocks = c->grids.lanes_shadow_blocks;
     plan.full_trace_blocks = c->grids.full_trace_blocks;
     plan.full_shadow_blocks = c->grids.full_shadow_blocks;
+    plan.linear_trace_blocks = c->grids.linear_trace_blocks;
+    plan.linear_shadow_blocks = c->grids.linear_shadow_blocks;
     const bool extra = pass->adaptive_samples > 0 || pass->firefly_samples > 0;
     const bool serial = (pass->flags & PT_PASS_SERIAL) != 0;   // Renderer.Render's extra phases (NumCPU == 1)
     // pt_pass_params.passes: K consecutive passes.  Plain RenderParallel passes run as one batch

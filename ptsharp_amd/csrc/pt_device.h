@@ -797,6 +797,29 @@ __device__ __forceinline__ HitRec trace(const DevScene& S, v3 o, v3 d, const STK
     return best;
 }
 
+// trace() for the scenes whose shapes are a few analytic records and planes, and no triangle BVH (lean, ana_linear,
+// tri_num_nodes 0): the same tests in the same order, so the same hit; for k_wf_trace_linear, which holds no
+// traversal state.
+// recs / planes: S.ana_recs / S.planes or copies of them (k_wf_trace_linear stages them in LDS).
+template <bool COUNT>
+__device__ __forceinline__ HitRec trace_linear(const DevScene& S, const float4* recs, const float4* planes, v3 o, v3 d,
+                                               Counters& ctr) {
+    ctr.rays++;
+    HitRec best{kHitInf, -1, -1};
+    for (int i = 0; i < S.num_planes; i++) {
+        float4 a = planes[2 * i], b = planes[2 * i + 1];
+        double t = isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+        if (t < best.t) { best.t = t; best.kind = KIND_PLANE; best.idx = i; }
+    }
+    for (int p = 0; p < S.ana_count; p++) {
+        if (COUNT) ctr.prims++;
+        int32_t kind;
+        const double t = prim_t<false, false>(S, recs, (uint32_t)p, o, d, kind);
+        if (t < best.t) { best.t = t; best.kind = kind; best.idx = p; }
+    }
+    return best;
+}
+
 // t of the light's own primitive along (o, d), exactly as the closest-hit query computes it.
 template <bool FULL>
 // lrec (may be null): the light's own record (3 float4), staged in LDS by the shadow kernels
@@ -858,6 +881,33 @@ __device__ __forceinline__ bool light_visible(const DevScene& S, const DevLight&
     const double tl = light_t<FULL>(S, L, o, d, lrec);
     if (!(tl < kHitInf)) return false;
     return !any_nearer<COUNT, FULL>(S, o, d, tl, stack, ctr);
+}
+// light_visible() for the same scenes as trace_linear (no triangles: a phantom light's ray has nothing to
+// trace); k_wf_shadow_linear.
+template <bool COUNT>
+__device__ __forceinline__ bool light_visible_linear(const DevScene& S, const float4* recs, const float4* planes,
+                                                     const DevLight& L, v3 o, v3 d, Counters& ctr, const float4* lrec) {
+    ctr.rays++;
+    if (L.phantom) return false;
+    double tl;
+    if (L.kind == KIND_PLANE) {   // light_t
+        const float4 a = planes[2 * L.index], b = planes[2 * L.index + 1];
+        tl = isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d);
+    } else {
+        int32_t kind;
+        tl = prim_t<false, false>(S, lrec ? lrec : recs + 3 * (size_t)L.index, 0u, o, d, kind);
+    }
+    if (!(tl < kHitInf)) return false;
+    for (int i = 0; i < S.num_planes; i++) {
+        float4 a = planes[2 * i], b = planes[2 * i + 1];
+        if (isect_plane(v3{a.x, a.y, a.z}, v3{b.x, b.y, b.z}, o, d) < tl) return false;
+    }
+    for (int p = 0; p < S.ana_count; p++) {
+        if (COUNT) ctr.prims++;
+        int32_t kind;
+        if (prim_t<false, false>(S, recs, (uint32_t)p, o, d, kind) < tl) return false;
+    }
+    return true;
 }
 // Split traversal (scenes with §8f row 4 shapes and a large triangle BVH, pt_wavefront.hip
 // "split"): the lean refill kernels take the planes and the triangle BVH, then the FULL kernel

@@ -123,6 +123,7 @@ struct WfPlan {
     uint32_t shade_blocks;     // shade, lockstep shadow; the refill and FULL traversal kernels below)
     uint32_t shadow_blocks;
     uint32_t lanes_trace_blocks, lanes_shadow_blocks, full_trace_blocks, full_shadow_blocks;
+    uint32_t linear_trace_blocks, linear_shadow_blocks;   // k_wf_trace_linear / k_wf_shadow_linear (resident)
     int32_t shade_form;        // k_wf_shade form: 0 chosen per depth from the kept count, 1 direct, 2 SCAN
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
     int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always

@@ -131,6 +131,9 @@ constexpr int32_t kDeadKind = -2;         // hit-record kind of a dead camera sl
 #ifndef PT_SHADE_LDS
 #define PT_SHADE_LDS 1     // k_wf_shade reads a small scene's materials and lights from LDS (stage_shading)
 #endif
+#ifndef PT_LINEAR
+#define PT_LINEAR 1        // k_wf_trace_linear / k_wf_shadow_linear for a few analytic records and no triangles
+#endif
 #ifndef PT_SHADOW_LDS
 #define PT_SHADOW_LDS 1    // the lean shadow kernels read a small scene's lights and their records from LDS (stage_lights)
 #endif
@@ -382,6 +385,81 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_TRACE_WAVES : PT_TRACE_WAVES) v
             atomicAdd(&counters[1], (unsigned long long)nodes);
             atomicAdd(&counters[2], (unsigned long long)prims);
         }
+    }
+}
+
+// Closest hit and shadow visibility of the scenes whose shapes are a few analytic records and planes with no
+// triangle BVH (lean, DevScene::ana_linear, tri_num_nodes 0: C2's gopher3).  k_wf_trace / k_wf_shadow ran them
+// through the general lockstep traversal, whose registers (stack, BVH state) held them at 7 waves, parked on
+// their queue loads 72 % of their wave time (profiles/r06q_wave_states.txt).  Here a ray is its queue entry
+// and the record tests (trace_linear / light_visible_linear: the same tests in the same order, so the same
+// results), and each wave loads its next row of 64 entries before it tests the current one.  Static deal:
+// wave w of the partition's group takes rows w, w + W, ... (every ray costs the same tests).
+struct LinRay { float4 b, a; };   // the queue entry: q_d / n_n and q_o / n_o
+// The records and planes in LDS (at most kLinRecs / kLinPlanes: the launch checks), read by every ray's tests:
+// from global memory the compiler issued them as vector loads per ray (it cannot prove them unwritten).
+constexpr int kLinRecs = 8, kLinPlanes = 8;
+struct LinScene { const float4* recs; const float4* planes; };
+__device__ __forceinline__ LinScene stage_linear(const DevScene& S) {   // block-uniform call
+    __shared__ float4 s_rec[3 * kLinRecs];
+    __shared__ float4 s_pl[2 * kLinPlanes];
+    for (uint32_t k = threadIdx.x; k < 3u * (uint32_t)S.ana_count; k += blockDim.x) s_rec[k] = S.ana_recs[k];
+    for (uint32_t k = threadIdx.x; k < 2u * (uint32_t)S.num_planes; k += blockDim.x) s_pl[k] = S.planes[k];
+    __syncthreads();
+    return LinScene{s_rec, s_pl};
+}
+__device__ __forceinline__ LinRay lin_fetch(const float4* qb, const float4* qa, uint32_t base, uint32_t k, uint32_t n) {
+    LinRay x;
+    if (k < n) {
+        x.b = nt_load(qb + base + k);
+        x.a = nt_load(qa + base + k);
+    } else {
+        x.b = make_float4(0.f, 0.f, 0.f, __uint_as_float(kDead));
+        x.a = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    return x;
+}
+template <bool COUNT>
+__global__ __launch_bounds__(256, 8) void k_wf_trace_linear(DevScene S, WfQueues Q, int qi, unsigned long long* counters) {
+    if (blockIdx.x == 0 && threadIdx.x < kParts) {   // as k_wf_trace
+        *pair_word(Q, 1 - qi, threadIdx.x) = 0ull;
+        Q.counts[fetch_word(1, threadIdx.x)] = 0u;
+        Q.counts[fetch_word(7, threadIdx.x)] = 0u;
+    }
+    const Group G = xcd_group();
+    const uint32_t n = min(*ray_count(Q, qi, G.g), Q.pcap), base = G.g * Q.pcap;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t W = G.nb * 4u;
+    Counters ctr{0, 0, 0, 0};
+    const bool env_black = (!FULL_SHADE_ENV(S)) && S.env[0] == 0.f && S.env[1] == 0.f && S.env[2] == 0.f;
+    uint32_t kept = 0;
+    const LinScene L = stage_linear(S);
+    uint32_t r = G.lb * 4u + (threadIdx.x >> 6);
+    LinRay cur = lin_fetch(Q.q_d[qi], Q.q_o[qi], base, r * 64u + lane, n);
+    for (; r * 64u < n; r += W) {   // wave-uniform
+        const LinRay nxt = lin_fetch(Q.q_d[qi], Q.q_o[qi], base, (r + W) * 64u + lane, n);
+        const uint32_t k = r * 64u + lane;
+        if (k < n) {
+            const uint32_t i = base + k;
+            if (__float_as_uint(cur.b.w) == kDead) {   // a camera slot outside the image: k_wf_shade skips it
+                hit_store(&Q.hits[i], make_uint4(0u, 0u, (uint32_t)kDeadKind, 0u));
+            } else {
+                const HitRec h = trace_linear<COUNT>(S, L.recs, L.planes, v3{cur.a.x, cur.a.y, cur.a.z},
+                                                     v3{cur.b.x, cur.b.y, cur.b.z}, ctr);
+                kept += (h.kind >= 0 || !env_black) ? 1u : 0u;
+                const unsigned long long tb = (unsigned long long)__double_as_longlong(h.t);
+                hit_store(&Q.hits[i], make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h.kind, (uint32_t)h.idx));
+            }
+        }
+        cur = nxt;
+    }
+    uint32_t rays = wave_sum(ctr.rays);
+    if (lane == 0 && rays) atomicAdd(&counters[0], (unsigned long long)rays);
+    kept = wave_sum(kept);
+    if (lane == 0 && kept) atomicAdd(Q.counts + kept_word(qi), kept);
+    if (COUNT) {
+        const uint32_t prims = wave_sum(ctr.prims);
+        if (lane == 0) atomicAdd(&counters[2], (unsigned long long)prims);
     }
 }
 
@@ -1304,6 +1382,39 @@ __global__ __launch_bounds__(kTB, FULL ? PT_FULL_SHADOW_WAVES : PT_SHADOW_WAVES)
     shadow_rays<COUNT, FULL, SPLIT, LDSL && !FULL>(S, Q, qo, counters);
 }
 
+// The shadow rays of the same scenes (see k_wf_trace_linear).
+template <bool COUNT, bool LDSL>
+__global__ __launch_bounds__(256, 8) void k_wf_shadow_linear(DevScene S, WfQueues Q, int qo, unsigned long long* counters) {
+    const Group G = xcd_group();
+    const uint32_t n = min(*nee_count(Q, qo, G.g), Q.spcap), base = G.g * Q.spcap;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t W = G.nb * 4u;
+    Counters ctr{0, 0, 0, 0};
+    const LightLds<LDSL> LL = stage_lights<LDSL>(S);
+    const LinScene L = stage_linear(S);
+    uint32_t r = G.lb * 4u + (threadIdx.x >> 6);
+    LinRay cur = lin_fetch(Q.n_n[qo], Q.n_o[qo], base, r * 64u + lane, n);
+    for (; r * 64u < n; r += W) {   // wave-uniform
+        const LinRay nxt = lin_fetch(Q.n_n[qo], Q.n_o[qo], base, (r + W) * 64u + lane, n);
+        const uint32_t k = r * 64u + lane;
+        if (k < n) {
+            const uint32_t li = __float_as_uint(cur.b.w);
+            bool lit = false;
+            if (li != kDead)
+                lit = light_visible_linear<COUNT>(S, L.recs, L.planes, LL.light(S, li), v3{cur.a.x, cur.a.y, cur.a.z},
+                                                  v3{cur.b.x, cur.b.y, cur.b.z}, ctr, LL.rec(li));
+            Q.n_lit[qo][base + k] = lit ? 1 : 0;   // k_wf_nee_accum adds the lit rays' terms
+        }
+        cur = nxt;
+    }
+    uint32_t rays = wave_sum(ctr.rays);
+    if (lane == 0 && rays) atomicAdd(&counters[4], (unsigned long long)rays);
+    if (COUNT) {
+        const uint32_t prims = wave_sum(ctr.prims);
+        if (lane == 0) atomicAdd(&counters[6], (unsigned long long)prims);
+    }
+}
+
 // Shadow visibility with per-lane refill (triangle scenes; see k_wf_trace_lanes): the
 // light's own t and the planes at refill, then one step loop over the analytic BVH and
 // the triangle BVH, any-hit (a primitive strictly nearer than the light ends the ray
@@ -1825,6 +1936,9 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     // enough to pay for it: lean scenes with a triangle BVH of more than kLanesMinNodes nodes.
     const bool lanes = !fullg && (plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes);
     const bool ldsl = PT_SHADOW_LDS && S.num_lights <= kLdsLights;   // the lean shadow kernels' lights in LDS
+    // a few analytic records and planes, no triangles: k_wf_trace_linear / k_wf_shadow_linear
+    const bool linear = PT_LINEAR && !fullg && !lanes && S.ana_linear && S.tri_num_nodes <= 0 && S.num_sdf <= 0 &&
+                        S.num_vol <= 0 && S.ana_count <= kLinRecs && S.num_planes <= kLinPlanes;
     // Split traversal (row-4 scenes with a triangle BVH): the lean refill kernels take the planes and
     // the triangles at their occupancy, then the FULL lockstep kernels add the analytic BVH (where
     // the §8f row-4 shapes live) from that result (pt_device.h trace_ana / ana_blocked; routed:
@@ -1869,6 +1983,8 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
         else if (fullg) hipLaunchKernelGGL((k_wf_trace<false, true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (lanes && count) hipLaunchKernelGGL((k_wf_trace_lanes<true>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else if (lanes) hipLaunchKernelGGL((k_wf_trace_lanes<false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
+        else if (linear && count) hipLaunchKernelGGL((k_wf_trace_linear<true>), dim3(plan.linear_trace_blocks), dim3(256), 0, stream, S, Q, qi, B.counters);
+        else if (linear) hipLaunchKernelGGL((k_wf_trace_linear<false>), dim3(plan.linear_trace_blocks), dim3(256), 0, stream, S, Q, qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_trace<true, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         else hipLaunchKernelGGL((k_wf_trace<false, false>), dim3(tg), dim3(kTB), 0, stream, S, Q, qi, B.counters);
         end_k(1, stream);
@@ -1944,6 +2060,9 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
         else if (lanes && Q.tail_early) hipLaunchKernelGGL((k_wf_shadow_lanes<false, false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (lanes && ldsl) hipLaunchKernelGGL((k_wf_shadow_lanes<false, false, false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (lanes) hipLaunchKernelGGL((k_wf_shadow_lanes<false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
+        else if (linear && count) hipLaunchKernelGGL((k_wf_shadow_linear<true, false>), dim3(plan.linear_shadow_blocks), dim3(256), 0, side, S, Q, 1 - qi, B.counters);
+        else if (linear && ldsl) hipLaunchKernelGGL((k_wf_shadow_linear<false, true>), dim3(plan.linear_shadow_blocks), dim3(256), 0, side, S, Q, 1 - qi, B.counters);
+        else if (linear) hipLaunchKernelGGL((k_wf_shadow_linear<false, false>), dim3(plan.linear_shadow_blocks), dim3(256), 0, side, S, Q, 1 - qi, B.counters);
         else if (count) hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else if (ldsl) hipLaunchKernelGGL((k_wf_shadow<false, false, false, true>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
         else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(hg), dim3(kTB), 0, side, S, Q, 1 - qi, B.counters);
@@ -1974,6 +2093,7 @@ hipError_t wavefront_pass(const DevScene& S, const DevCamera& cam, const DevSamp
     // Every persistent grid is launched as planned: a zero grid (a kernel whose occupancy query was never made)
     // would fail only at its launch, as "invalid configuration argument" with no kernel named (VERDICT r05 #7a)
     if (!plan.trace_blocks || !plan.shade_blocks || !plan.shadow_blocks || !plan.lanes_trace_blocks ||
+        !plan.linear_trace_blocks || !plan.linear_shadow_blocks ||
         !plan.lanes_shadow_blocks || !plan.full_trace_blocks || !plan.full_shadow_blocks || !plan.chunk)
         return hipErrorInvalidConfiguration;
     const uint64_t pix_slots = (uint64_t)P.num_tiles * 1024u;
@@ -2055,6 +2175,10 @@ hipError_t wavefront_grids(WfPlan& plan) {
     if (e == hipSuccess) plan.full_trace_blocks = resident(nb, kWfMaxBlocks);
     if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow<false, true>, kTB, 0);
     if (e == hipSuccess) plan.full_shadow_blocks = resident(nb, kWfMaxBlocks);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_trace_linear<false>, 256, 0);
+    if (e == hipSuccess) plan.linear_trace_blocks = resident(nb, 1u << 20);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_wf_shadow_linear<false, true>, 256, 0);
+    if (e == hipSuccess) plan.linear_shadow_blocks = resident(nb, 1u << 20);
     return e;
 }
 
