@@ -1087,7 +1087,8 @@ __device__ __forceinline__ void shade_children(const DevScene& S, const DevSampl
 // at a time: each round trip of the chain (claim, queue loads, triangle record,
 // reservation) serves four times as many vertices.  Otherwise the block shades every
 // claimed slot (no extra read of the hit records, fewer live registers).
-// A scene's materials and lights, when few, staged in the shade block's LDS: a vertex' material (after its
+// A scene's materials and lights, when few, staged in the shade block's LDS (and its analytic records and planes,
+// when few): a vertex' material (after its
 // triangle record), its light (after the light draw) and that light's material are dependent loads of the
 // shading chain; from LDS each costs an LDS round trip instead of an L1 / L2 one.  Returns the scene view
 // that reads them there (flat loads).  Block-uniform call.
@@ -1096,8 +1097,15 @@ static_assert(sizeof(DevMaterial) % 8 == 0 && sizeof(DevLight) % 8 == 0, "stage_
 __device__ __forceinline__ DevScene stage_shading(const DevScene& S0) {
     __shared__ unsigned long long s_mats[kLdsMats * sizeof(DevMaterial) / 8];
     __shared__ unsigned long long s_lights[kLdsLights * sizeof(DevLight) / 8];
+    __shared__ float4 s_ana[3 * kLinRecs];     // a few analytic records (a sphere or cube hit's record in hit_info)
+    __shared__ float4 s_pln[2 * kLinPlanes];   // and planes
     DevScene S = S0;
     if (S0.num_mats > kLdsMats || S0.num_lights > kLdsLights) return S;
+    const bool ana = S0.ana_count > 0 && S0.ana_count <= kLinRecs, pln = S0.num_planes > 0 && S0.num_planes <= kLinPlanes;
+    if (ana)
+        for (uint32_t k = threadIdx.x; k < 3u * (uint32_t)S0.ana_count; k += blockDim.x) s_ana[k] = S0.ana_recs[k];
+    if (pln)
+        for (uint32_t k = threadIdx.x; k < 2u * (uint32_t)S0.num_planes; k += blockDim.x) s_pln[k] = S0.planes[k];
     const uint32_t nm = (uint32_t)S0.num_mats * (uint32_t)(sizeof(DevMaterial) / 8);
     const uint32_t nl = (uint32_t)S0.num_lights * (uint32_t)(sizeof(DevLight) / 8);
     const unsigned long long* gm = reinterpret_cast<const unsigned long long*>(S0.mats);
@@ -1107,6 +1115,8 @@ __device__ __forceinline__ DevScene stage_shading(const DevScene& S0) {
     __syncthreads();
     S.mats = reinterpret_cast<const DevMaterial*>(s_mats);
     S.lights = reinterpret_cast<const DevLight*>(s_lights);
+    if (ana) S.ana_recs = s_ana;
+    if (pln) S.planes = s_pln;
     return S;
 }
 
