@@ -757,6 +757,13 @@ def main(argv=None):
 
     if a.workload == "c4":
         out["roofline"]["shade"] = shade_roofline()
+        # the same pass priced by VALU issue (the C2 / C5 lines' bound): the closest-hit kernel is bound by its
+        # dependent loads and by VALU issue together (profiles/r06q_wave_states.txt), so both fractions are shown
+        vi = valu_roofline()
+        out["roofline"]["valu_issue"] = {k: vi[k] for k in (
+            "achieved", "peak", "unit", "frac", "valu_issue_cycles_per_ray", "dominant_kernel",
+            "dominant_kernel_valu_issue_frac_under_counters", "pass_valu_issue_frac_under_counters", "mix_source",
+            "mix_stale", "note") if k in vi}
 
     if a.workload in ("c2", "c5"):
         # C2 (fp64 sampler math, 16 children per camera hit) and C5 (the fp64 Volume / SDF marches) are
