@@ -1470,6 +1470,8 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
     if (const char* f = std::getenv("PT_SHADE_FORM")) plan.shade_form = !std::strcmp(f, "direct") ? 1 : !std::strcmp(f, "scan") ? 2 : 0;
     plan.lanes = -1;
     if (const char* f = std::getenv("PT_LANES")) plan.lanes = !std::strcmp(f, "0") ? 0 : !std::strcmp(f, "1") ? 1 : -1;
+    plan.linear = -1;
+    if (const char* f = std::getenv("PT_LINEAR")) plan.linear = !std::strcmp(f, "0") ? 0 : -1;
     plan.root_children = (uint32_t)std::max(1, n_root * n_root * nm_root);
     plan.children = (uint32_t)nm;
     plan.lights_per_child = (uint32_t)(sampler->light_mode == PT_LIGHT_ALL ? std::max(1, c->S.num_lights) : 1);

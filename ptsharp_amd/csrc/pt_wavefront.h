@@ -128,6 +128,8 @@ struct WfPlan {
                                // (PT_SHADE_FORM=direct|scan in the environment; tests)
     int32_t lanes;             // refill traversal kernels: -1 by BVH size, 0 never, 1 always
                                // (PT_LANES=0|1 in the environment; tests)
+    int32_t linear;            // linear kernels (few analytic records, no triangles): -1 where they apply, 0 never
+                               // (PT_LINEAR=0 in the environment; tests)
     // Optional second stream: each depth's shadow pass runs there, beside the next depth's
     // closest-hit pass (independent queues), so one fills the other's ramp and tail.
     // ev_main orders shade(d) → shadow(d); ev_side[q], recorded after the light terms of

@@ -1947,7 +1947,7 @@ static hipError_t depth_loop(const DevScene& S, const DevSampler& smp, const Dev
     const bool lanes = !fullg && (plan.lanes >= 0 ? plan.lanes == 1 : S.tri_num_nodes > kLanesMinNodes);
     const bool ldsl = PT_SHADOW_LDS && S.num_lights <= kLdsLights;   // the lean shadow kernels' lights in LDS
     // a few analytic records and planes, no triangles: k_wf_trace_linear / k_wf_shadow_linear
-    const bool linear = PT_LINEAR && !fullg && !lanes && S.ana_linear && S.tri_num_nodes <= 0 && S.num_sdf <= 0 &&
+    const bool linear = PT_LINEAR && plan.linear != 0 && !fullg && !lanes && S.ana_linear && S.tri_num_nodes <= 0 && S.num_sdf <= 0 &&
                         S.num_vol <= 0 && S.ana_count <= kLinRecs && S.num_planes <= kLinPlanes;
     // Split traversal (row-4 scenes with a triangle BVH): the lean refill kernels take the planes and
     // the triangles at their occupancy, then the FULL lockstep kernels add the analytic BVH (where

@@ -436,3 +436,35 @@ def test_shadow_tail_handoffs_forced(gpu, monkeypatch, name):
         same_buffer(e, l)
         o, orr = O.render(O.OracleScene(s), c, smp, w, h, 2, passes=1, seed=4242, tiles=tiles)
         check(e, re_, o, orr)
+
+
+@pytest.mark.parametrize("name", ["gopher3", "materialspheres", "simplesphere", "example1"])
+def test_linear_kernels_match_lockstep(gpu, monkeypatch, name):
+    """The linear kernels (k_wf_trace_linear / k_wf_shadow_linear: a few analytic records and planes, no
+    triangles) test the same records in the same order as the lockstep traversal kernels (PT_LINEAR=0): the
+    same rays, the same counted-pass counters and the same Buffer bits.  The four scenes cover planes,
+    refraction (transparent / clear spheres), a cube light's neighbours, a thin-lens camera and
+    SpecularModeFirst."""
+    from ptsharp_amd import Renderer
+    out = {}
+    for lin in ("0", "1"):
+        if lin == "0":
+            monkeypatch.setenv("PT_LINEAR", "0")
+        else:
+            monkeypatch.delenv("PT_LINEAR", raising=False)
+        s, c, smp = getattr(scenes, name)()
+        smp.MaxBounces = min(smp.MaxBounces, 6)
+        b, rays, _ = _render_stats(s, c, smp, 64, 48, 2, 41)
+        r = Renderer.NewRenderer(s, c, smp, 32, 24, True, device=0)
+        try:
+            r.SamplesPerPixel, r.Seed, r.Engine = 1, 5, _abi.ENGINE_WAVEFRONT
+            ctr = r.RenderCounted()
+            counts = (int(ctr.rays), int(ctr.prims_tested), int(ctr.shadow_rays), int(ctr.shadow_prims),
+                      int(ctr.lit_shadow_rays))
+        finally:
+            r.close()
+        out[lin] = (b, rays, counts)
+    (a, ra, ca), (b, rb, cb) = out["0"], out["1"]
+    assert ra == rb and ra > 0
+    assert ca == cb
+    same_buffer(a, b)
