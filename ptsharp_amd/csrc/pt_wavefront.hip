@@ -1706,7 +1706,10 @@ __global__ __launch_bounds__(kTB, PT_LANES_WAVES) __attribute__((amdgpu_num_vgpr
 // (a pixel's rays sit in runs of consecutive slots, so fix_add_wave sums most of them in
 // registers).  Keeping the accumulation out of the traversal kernels keeps their refill path
 // and registers lean.  Group g takes partition g (written on its XCD by k_wf_shade).
-constexpr uint32_t kAccWin = 16;      // 256-slot rows per block window (one shade block's child-major region
+#ifndef PT_ACC_WIN
+#define PT_ACC_WIN 16
+#endif
+constexpr uint32_t kAccWin = PT_ACC_WIN;   // 256-slot rows per block window (one shade block's child-major region
                                       // of FirstHitSamples 16 children)
 constexpr uint32_t kAccTable = 512;   // LDS table entries (a power of two)
 template <bool COUNT>
