@@ -780,17 +780,22 @@ def main(argv=None):
     # ---------------- CPU baseline + parity sample (rank 0, N = 1 only), at the timed configuration: the
     # full frame at the bench's own spp per pass (one chunk, as each timed step runs it), pass index 1 (the
     # first timed step's), against the oracle on a strided pixel set sized to ~cpu_seconds of CPU work
-    if world == 1 and a.workload == "c4" and (a.cpu_seconds > 0 or not a.no_parity):
+    # (C3 and C2 too: the same leg on their frames; C5's adaptive phase is checked by the GPU tests)
+    if world == 1 and a.workload in ("c4", "c3", "c2") and a.adaptive == 0 and (a.cpu_seconds > 0 or not a.no_parity):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         osc = O.OracleScene(scene)
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
         spp = a.spp
-        stride = max(1, (W * H) // 2048)   # probe ~2048 pixels (~3 s), then size the sample to the budget
+        # probe ~2048 pixels (~3 s on C4; C2's 16 children per camera hit and 16 bounces: 256), then size the
+        # sample to the budget
+        stride = max(1, (W * H) // (256 if a.workload == "c2" else 2048))
         tp = time.perf_counter()
         _, prays = O.render_pixels(osc, camera, sampler, W, H, spp, 0, W * H, stride, seed=a.seed, pass_index=1,
                                    threads=threads)
         tp = time.perf_counter() - tp
+        print(f"cpu baseline probe: {(W * H + stride - 1) // stride} pixels x {spp} spp, {prays} rays in {tp:.1f}s",
+              file=sys.stderr, flush=True)   # (progress: a long oracle leg is not a hung run)
         budget = max(a.cpu_seconds, 1.0)
         npx = max(64, min(W * H, int(((W * H + stride - 1) // stride) * budget / max(tp, 1e-3))))
         stride = max(1, (W * H) // npx)
