@@ -176,6 +176,7 @@ struct Ctx {
     pt::WfQueues Q{};
     std::vector<DeviceArray> wf_arrays;
     uint32_t wf_cap = 0, wf_scap = 0;
+    bool wf_two_sets = false;      // a second shadow-ray set allocated (the side stream's shadow passes need it)
     int32_t acc_passes = 0;        // passes of per-pixel accumulators allocated (a batch needs one set per pass)
     uint32_t wf_max_cap = 0;       // queue capacity bound (wf_max_cap()), once per context
     // adaptive / firefly phases (allocated on first use, with the queues)
@@ -197,11 +198,12 @@ struct Ctx {
 // samples whose widest depth fits the queues; every chunk pays the fill and drain of
 // 16 persistent launches, so fewer, larger chunks are faster (C4, 16 spp per pass: 8
 // chunks of 32M-entry queues 2574 Mrays/s, 2 chunks 2809, one chunk 2853).  The bound is
-// the largest power of two whose queues (274 B per entry: two extension queues of
-// o, d, throughput r g, key + throughput b + hits + two shadow sets) fit a quarter of the device's memory
-// and half of its free memory, clamped to [2^20, 2^28] entries (2^28: 47 GB of the
-// MI355X's 288 GB).
-constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 28;
+// the largest power of two whose queues (209 B per entry: two extension queues of o, d, throughput r g,
+// key + throughput b, the hits, one shadow set) fit half of the device's memory and half of its free memory,
+// clamped to [2^20, 2^29] entries (2^29: 112 GB of the MI355X's 288 GB: C2's 33M camera samples × 16 children
+// in one chunk).  A chunk small enough for the side stream (kSideStreamMaxRays) keeps a second shadow set
+// (ensure_wavefront), within the same budget.
+constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 29;
 #ifndef PT_SDF_LDS_MAX
 #define PT_SDF_LDS_MAX 16384   // LDS bytes k_wf_sdf_* may stage the SDF programs in; 0: never
 #endif
@@ -223,7 +225,7 @@ constexpr double kSideStreamMaxRays = (double)(64ull << 20);   // a chunk's wide
 // shapes or Volumes (sdfq, sdfq_sh: 32 B per entry), with Volumes their record words (volq, volq_sh: 8 B),
 // and under the routed split the heavy queues (hq, hq_sh: 8 B).  At most 48 B per entry, 17 % over the
 // 274 B: 12.9 GB at 2^28 entries, inside the three quarters of the device the budget leaves free.
-constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + 2 * (64 + 1);
+constexpr size_t kWfBytesPerEntry = 2 * (16 + 16 + 16 + 16) + 16 + (64 + 1);
 
 // PT_WF_MAX_CAP (entries, environment) lowers the bound: tests use it to force many chunks.
 uint32_t wf_max_cap(Ctx* c) {
@@ -236,7 +238,7 @@ uint32_t wf_max_cap(Ctx* c) {
     }
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = total_b = (size_t)kWfMinCapLimit * kWfBytesPerEntry * 4;
-    const size_t budget = std::min(total_b / 4, free_b / 2);   // and at most half of what is free now
+    const size_t budget = std::min(total_b / 2, free_b / 2);   // and at most half of what is free now
     uint32_t cap = kWfMaxCapLimit;
     while (cap > kWfMinCapLimit && (size_t)cap * kWfBytesPerEntry > budget) cap >>= 1;
     c->wf_max_cap = cap;
@@ -248,6 +250,7 @@ void free_wavefront(Ctx* c) {
     c->wf_arrays.clear();
     c->Q = pt::WfQueues{};
     c->wf_cap = c->wf_scap = 0;
+    c->wf_two_sets = false;
     c->acc_passes = 0;
     c->d_plist = nullptr;
     c->d_plist2 = nullptr;
@@ -269,17 +272,22 @@ int wf_alloc(Ctx* c, T** out, size_t n) {
     return PT_OK;
 }
 
-int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
+// two_sets: the shadow passes run on the side stream beside the next depth (pt::WfPlan::side), so the shadow rays
+// of depth d and d + 1 live at once, in sets by depth parity; on one stream a depth's shadow rays are consumed
+// before the next depth's shade writes its own, and both sets are the same memory.
+int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes, bool two_sets) {
     // the split traversal's deferred-record queues (pt_wavefront.hip k_wf_vol_* / k_wf_sdf_*)
     const bool want_sdf = c->S.num_sdf > 0 || (PT_VOL_DEFER && c->S.num_vol > 0);
     const bool want_vol = PT_VOL_DEFER && c->S.num_vol > 0;
     const bool want_heavy = c->S.route != 0;  // the routed split's queues of rays that reach a row-4 shape's box
-    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes && (!want_sdf || c->Q.sdfq) && (!want_vol || c->Q.volq) &&
+    if (c->wf_cap >= cap && c->wf_scap >= scap && c->Q.acc.w && c->acc_passes >= acc_passes && (!two_sets || c->wf_two_sets) &&
+        (!want_sdf || c->Q.sdfq) && (!want_vol || c->Q.volq) &&
         (!want_heavy || c->Q.hq))
         return PT_OK;
     cap = std::max(cap, c->wf_cap);
     scap = std::max(scap, c->wf_scap);
     acc_passes = std::max(acc_passes, c->acc_passes);
+    two_sets = two_sets || c->wf_two_sets;
     free_wavefront(c);
     pt::WfQueues Q{};
     int rc;
@@ -292,11 +300,17 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     if ((rc = wf_alloc(c, &Q.hits, cap))) return rc;
     if (want_sdf && (rc = wf_alloc(c, &Q.sdfq, cap))) return rc;
     if (want_vol && (rc = wf_alloc(c, &Q.volq, cap))) return rc;
-    for (int q = 0; q < 2; q++) {   // shadow-ray sets by depth parity
+    for (int q = 0; q < (two_sets ? 2 : 1); q++) {   // shadow-ray sets by depth parity
         if ((rc = wf_alloc(c, &Q.n_o[q], scap))) return rc;
         if ((rc = wf_alloc(c, &Q.n_n[q], scap))) return rc;
         if ((rc = wf_alloc(c, &Q.n_w[q], 2 * (size_t)scap))) return rc;
         if ((rc = wf_alloc(c, &Q.n_lit[q], scap))) return rc;
+    }
+    if (!two_sets) {   // one stream: set 1 is set 0's memory
+        Q.n_o[1] = Q.n_o[0];
+        Q.n_n[1] = Q.n_n[0];
+        Q.n_w[1] = Q.n_w[0];
+        Q.n_lit[1] = Q.n_lit[0];
     }
     if (want_sdf && (rc = wf_alloc(c, &Q.sdfq_sh, scap))) return rc;   // one shadow pass at a time uses it
     if (want_vol && (rc = wf_alloc(c, &Q.volq_sh, scap))) return rc;
@@ -326,6 +340,7 @@ int ensure_wavefront(Ctx* c, uint32_t cap, uint32_t scap, int32_t acc_passes) {
     c->Q = Q;
     c->wf_cap = cap;
     c->wf_scap = scap;
+    c->wf_two_sets = two_sets;
     c->acc_passes = acc_passes;
     return PT_OK;
 }
@@ -1596,7 +1611,7 @@ static int render_pass_impl(Ctx* c, const pt_camera* camera, const pt_sampler* s
         const uint32_t pcap = (uint32_t)std::min(pmax, std::max(8192.0, std::max(group_samples, need)));
         const uint32_t spcap = (uint32_t)std::min(pmax, std::max(8192.0, group_samples * per_sample_nee));
         uint32_t cap = pcap * pt::kParts, scap = spcap * pt::kParts;
-        int rc = ensure_wavefront(c, cap, scap, P.passes);
+        int rc = ensure_wavefront(c, cap, scap, P.passes, side);
         if (rc) return rc;
         if ((uint64_t)pass->adaptive_samples > chunk)
             return fail(PT_ERR_UNSUPPORTED, "adaptive samples exceed one wavefront chunk");
