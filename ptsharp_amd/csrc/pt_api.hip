@@ -214,7 +214,7 @@ constexpr uint32_t kWfMinCapLimit = 1u << 20, kWfMaxCapLimit = 1u << 29;
 #define PT_VOL_CELLS_MAX (1ull << 30)   // bytes of cell-major Volume corners (8 per cell) a scene may hold; 0: none
 #endif
 #ifndef PT_EXTRA_CHUNK_MAX
-#define PT_EXTRA_CHUNK_MAX (32ull << 20)   // camera samples per chunk of the adaptive / firefly phases, at most
+#define PT_EXTRA_CHUNK_MAX (64ull << 20)   // camera samples per chunk of the adaptive / firefly phases, at most (round 6: 32M → 64M with the 2^29-entry queues, C5 +1.8 %, profiles/r06ec_ab_extra_chunk.txt)
 #endif
 #ifndef PT_VOL_DEFER
 #define PT_VOL_DEFER 1   // split traversal: Volumes deferred to k_wf_vol_hits / k_wf_vol_shadow (0: marched in place)
